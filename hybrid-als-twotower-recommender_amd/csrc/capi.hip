@@ -1,0 +1,30 @@
+// Error plumbing and version of the C-ABI (include/hrec.h).
+#include <stdarg.h>
+
+#include "common.h"
+
+namespace hrec {
+
+static thread_local char g_last_error[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return HREC_E_LAUNCH;
+  }
+  return HREC_OK;
+}
+
+}  // namespace hrec
+
+extern "C" int hrec_abi_version(void) { return HREC_ABI_VERSION; }
+
+extern "C" const char* hrec_last_error(void) { return hrec::g_last_error; }

@@ -1,0 +1,42 @@
+// Shared helpers for the libhrec HIP sources (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/hrec.h"
+
+namespace hrec {
+
+// Thread-local message of the last failure (hrec_last_error()).
+void set_error(const char* fmt, ...);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// After a launch: map the HIP status to an HREC code.
+int check_launch(const char* what);
+
+constexpr int kWave = 64;
+
+// splitmix64 finaliser; host and device identical (integer only).
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// h64(seed, u, i) of BASELINE.md §3 (u, i < 2^32).
+__host__ __device__ inline uint64_t pair_hash(uint64_t seed, uint64_t u, uint64_t i) {
+  return mix64(seed * 0x9E3779B97F4A7C15ull + ((u << 32) | (i & 0xffffffffull)));
+}
+
+}  // namespace hrec
+
+#define HREC_REQUIRE(cond, ...)          \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::hrec::set_error(__VA_ARGS__);    \
+      return HREC_E_INVALID;             \
+    }                                    \
+  } while (0)

@@ -1,0 +1,383 @@
+// K2: ALS scoring (Spark ALSModel.transform, JVM-exact f32 chain),
+// generic stable top-k (the reference's sorted(..., reverse=True)[:k]),
+// K9: hybrid min-max fusion (src/hybrid_system.py:57-75) + top-k (:108).
+#include <float.h>
+
+#include "common.h"
+
+namespace hrec {
+
+// --------------------------------------------------------------- ALS score
+// One thread per item; UB users per block row held in LDS (broadcast reads).
+// The item matrix is stored transposed [kp][ld] so every c-step is one
+// coalesced 1-KiB read per wave. Sequential c order, product rounded, sum
+// rounded: Spark's `dotProduct += featuresA(i) * featuresB(i)` on floats.
+template <int UB>
+__global__ __launch_bounds__(256) void als_score_kernel(const float* __restrict__ U,
+                                                        const int64_t* __restrict__ user_rows, int n_users,
+                                                        const float* __restrict__ Vt, int64_t ld,
+                                                        const int64_t* __restrict__ item_rows,
+                                                        int64_t n_items, int k, int kp,
+                                                        float* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ float ush[UB][64];
+  __shared__ int uok[UB];
+  const int b0 = blockIdx.y * UB;
+  for (int t = threadIdx.x; t < UB * 64; t += blockDim.x) {
+    const int b = t >> 6, c = t & 63;
+    const int64_t ur = (b0 + b < n_users) ? user_rows[b0 + b] : -1;
+    ush[b][c] = (ur >= 0 && c < kp) ? U[ur * kp + c] : 0.f;
+    if (c == 0) uok[b] = ur >= 0;
+  }
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_items) return;
+  const int64_t ir = item_rows ? item_rows[j] : j;
+  float acc[UB];
+#pragma unroll
+  for (int b = 0; b < UB; ++b) acc[b] = 0.f;
+  if (ir >= 0) {
+    const float* __restrict__ v = Vt + ir;
+    for (int c = 0; c < k; ++c) {
+      const float vc = v[(int64_t)c * ld];
+#pragma unroll
+      for (int b = 0; b < UB; ++b) {
+        const float prod = ush[b][c] * vc;
+        acc[b] = acc[b] + prod;
+      }
+    }
+  }
+  const float qnan = __builtin_nanf("");
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+    if (b0 + b < n_users) out[(int64_t)(b0 + b) * n_items + j] = (ir >= 0 && uok[b]) ? acc[b] : qnan;
+  }
+}
+
+// ----------------------------------------------------------------- top-k
+// Order: larger value first; equal values -> smaller index first (a stable
+// descending sort of the input order). NaN sorts last.
+template <typename T>
+__device__ __forceinline__ bool better(T va, int64_t ia, T vb, int64_t ib) {
+  const bool na = va != va, nb = vb != vb;
+  if (na || nb) return !na && nb ? true : (na && nb ? ia < ib : false);
+  return va > vb || (va == vb && ia < ib);
+}
+
+template <typename T>
+struct KV {
+  T v;
+  int64_t i;
+};
+
+template <typename T>
+__device__ __forceinline__ KV<T> wave_best(KV<T> x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    KV<T> y;
+    y.v = __shfl_xor(x.v, off, kWave);
+    y.i = __shfl_xor(x.i, off, kWave);
+    // lanes without a candidate carry i = INT64_MAX and lose every comparison
+    const bool take = (x.i == INT64_MAX) ? (y.i != INT64_MAX)
+                                         : (y.i != INT64_MAX && better(y.v, y.i, x.v, x.i));
+    if (take) x = y;
+  }
+  return x;
+}
+
+constexpr int kTopkBlock = 256;
+constexpr int kTopkPer = 16;  // elements per thread per segment
+constexpr int kTopkSeg = kTopkBlock * kTopkPer;
+
+// Stage 1: rows x segments; each block selects the top `kk` of its segment
+// of one row by kk rounds of block arg-best over elements held in registers.
+// `src_idx` (optional) maps positions to original indices (stage 2 input).
+template <typename T>
+__global__ __launch_bounds__(kTopkBlock) void topk_segment_kernel(const T* __restrict__ vals,
+                                                                  const int64_t* __restrict__ src_idx,
+                                                                  int64_t n, int64_t row_stride, int kk,
+                                                                  T* __restrict__ out_v,
+                                                                  int64_t* __restrict__ out_i,
+                                                                  int64_t out_row_stride) {
+  __shared__ KV<T> red[kTopkBlock / 64];
+  __shared__ int64_t win;
+  const int64_t row = blockIdx.y;
+  const int64_t seg0 = (int64_t)blockIdx.x * kTopkSeg;
+  const T* __restrict__ rv = vals + row * row_stride;
+  const int64_t* __restrict__ ri = src_idx ? src_idx + row * row_stride : nullptr;
+  T v[kTopkPer];
+  int64_t id[kTopkPer];
+#pragma unroll
+  for (int e = 0; e < kTopkPer; ++e) {
+    const int64_t p = seg0 + (int64_t)e * kTopkBlock + threadIdx.x;
+    if (p < n) {
+      v[e] = rv[p];
+      id[e] = ri ? ri[p] : p;
+    } else {
+      v[e] = 0;
+      id[e] = -1;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r = 0; r < kk; ++r) {
+    KV<T> best{(T)0, -1};
+#pragma unroll
+    for (int e = 0; e < kTopkPer; ++e) {
+      if (id[e] >= 0 && (best.i < 0 || better(v[e], id[e], best.v, best.i))) best = KV<T>{v[e], id[e]};
+    }
+    if (best.i < 0) best.i = INT64_MAX;
+    KV<T> wb = wave_best(best);
+    if (lane == 0) red[w] = wb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      KV<T> b = red[0];
+      for (int q = 1; q < kTopkBlock / 64; ++q) {
+        if (red[q].i == INT64_MAX) continue;
+        if (b.i == INT64_MAX || better(red[q].v, red[q].i, b.v, b.i)) b = red[q];
+      }
+      const int64_t o = row * out_row_stride + (int64_t)blockIdx.x * kk + r;
+      out_v[o] = b.v;
+      out_i[o] = b.i == INT64_MAX ? -1 : b.i;
+      win = b.i;
+    }
+    __syncthreads();
+    const int64_t wi = win;
+#pragma unroll
+    for (int e = 0; e < kTopkPer; ++e)
+      if (id[e] == wi) id[e] = -1;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- fusion
+// sklearn MinMaxScaler.fit_transform (container sklearn _data.py:518-522,
+// 261-262): scale = 1/range (range < 10*eps -> 1), min_ = 0 - min*scale,
+// y = x*scale + min_ ; two roundings each, in the input dtype.
+__global__ __launch_bounds__(256) void minmax_partial_kernel(const double* __restrict__ als,
+                                                             const void* __restrict__ tt, int tt_f32,
+                                                             int64_t n, double* __restrict__ part) {
+  __shared__ double sh[4][256];
+  double amin = DBL_MAX, amax = -DBL_MAX, tmin = DBL_MAX, tmax = -DBL_MAX;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+    const double a = als[p];
+    const double t = tt_f32 ? (double)((const float*)tt)[p] : ((const double*)tt)[p];
+    amin = fmin(amin, a);
+    amax = fmax(amax, a);
+    tmin = fmin(tmin, t);
+    tmax = fmax(tmax, t);
+  }
+  sh[0][threadIdx.x] = amin;
+  sh[1][threadIdx.x] = amax;
+  sh[2][threadIdx.x] = tmin;
+  sh[3][threadIdx.x] = tmax;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      sh[0][threadIdx.x] = fmin(sh[0][threadIdx.x], sh[0][threadIdx.x + s]);
+      sh[1][threadIdx.x] = fmax(sh[1][threadIdx.x], sh[1][threadIdx.x + s]);
+      sh[2][threadIdx.x] = fmin(sh[2][threadIdx.x], sh[2][threadIdx.x + s]);
+      sh[3][threadIdx.x] = fmax(sh[3][threadIdx.x], sh[3][threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) part[blockIdx.x * 4 + threadIdx.x] = sh[threadIdx.x][0];
+}
+
+// coef = {als_scale, als_min_, tt_scale, tt_min_} as doubles (the tt pair is
+// the exact f32 values widened when tt_f32).
+__global__ void minmax_final_kernel(const double* __restrict__ part, int nparts, int tt_f32,
+                                    double* __restrict__ coef) {
+  if (threadIdx.x != 0) return;
+  double amin = DBL_MAX, amax = -DBL_MAX, tmin = DBL_MAX, tmax = -DBL_MAX;
+  for (int q = 0; q < nparts; ++q) {
+    amin = fmin(amin, part[4 * q + 0]);
+    amax = fmax(amax, part[4 * q + 1]);
+    tmin = fmin(tmin, part[4 * q + 2]);
+    tmax = fmax(tmax, part[4 * q + 3]);
+  }
+  double arange = amax - amin;
+  if (arange < 10.0 * DBL_EPSILON) arange = 1.0;
+  const double ascale = 1.0 / arange;
+  coef[0] = ascale;
+  coef[1] = 0.0 - amin * ascale;
+  if (tt_f32) {
+    const float fmin_ = (float)tmin, fmax_ = (float)tmax;
+    float frange = fmax_ - fmin_;
+    if (frange < 10.0f * FLT_EPSILON) frange = 1.0f;
+    const float fscale = 1.0f / frange;
+    const float fmin2 = 0.0f - fmin_ * fscale;
+    coef[2] = (double)fscale;
+    coef[3] = (double)fmin2;
+  } else {
+    double trange = tmax - tmin;
+    if (trange < 10.0 * DBL_EPSILON) trange = 1.0;
+    const double tscale = 1.0 / trange;
+    coef[2] = tscale;
+    coef[3] = 0.0 - tmin * tscale;
+  }
+}
+
+// fused = w0*als_norm + w1*tt_norm, f64 (numpy 1.21 scalar promotion: the
+// f32 tt_norm element is widened before the multiply — SURVEY App. A.3).
+__global__ __launch_bounds__(256) void fuse_kernel(const double* __restrict__ als, const void* __restrict__ tt,
+                                                   int tt_f32, int64_t n, const double* __restrict__ coef,
+                                                   double w0, double w1, double* __restrict__ fused) {
+#pragma clang fp contract(off)
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const double an = als[p] * coef[0] + coef[1];
+  double tn;
+  if (tt_f32) {
+    const float x = ((const float*)tt)[p];
+    const float y = x * (float)coef[2] + (float)coef[3];
+    tn = (double)y;
+  } else {
+    tn = ((const double*)tt)[p] * coef[2] + coef[3];
+  }
+  fused[p] = w0 * an + w1 * tn;
+}
+
+template <typename T>
+int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s);
+
+}  // namespace hrec
+
+using namespace hrec;
+
+// Workspace for a stable top-k of n_rows rows of n elements (bytes).
+static size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
+  size_t total = 0;
+  int64_t m = n;
+  while (true) {
+    const int64_t segs = (m + kTopkSeg - 1) / kTopkSeg;
+    if (segs <= 1) break;
+    const int64_t cand = segs * kk;
+    total += (size_t)n_rows * (size_t)cand * (elem + 8);
+    m = cand;
+  }
+  return total + 256;
+}
+
+namespace hrec {
+template <typename T>
+int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s) {
+  // Multi-pass: segments -> candidates (kk per segment) -> ... -> one segment.
+  const T* cur_v = vals;
+  const int64_t* cur_i = nullptr;
+  int64_t m = n, stride = row_stride;
+  char* w = (char*)ws;
+  size_t used = 0;
+  while (true) {
+    const int64_t segs = (m + kTopkSeg - 1) / kTopkSeg;
+    if (segs <= 1) {
+      hipLaunchKernelGGL((topk_segment_kernel<T>), dim3(1, (unsigned)n_rows), dim3(kTopkBlock), 0, s, cur_v,
+                         cur_i, m, stride, kk, out_val, out_idx, (int64_t)kk);
+      return check_launch("topk_segment_kernel");
+    }
+    const int64_t cand = segs * kk;
+    const size_t vb = (size_t)n_rows * cand * sizeof(T), ib = (size_t)n_rows * cand * 8;
+    if (used + vb + ib > ws_bytes) {
+      set_error("topk: workspace too small");
+      return HREC_E_INVALID;
+    }
+    int64_t* ni = (int64_t*)(w + used);
+    T* nv = (T*)(w + used + ib);
+    used += vb + ib;
+    hipLaunchKernelGGL((topk_segment_kernel<T>), dim3((unsigned)segs, (unsigned)n_rows), dim3(kTopkBlock), 0, s,
+                       cur_v, cur_i, m, stride, kk, nv, ni, cand);
+    int rc = check_launch("topk_segment_kernel");
+    if (rc) return rc;
+    cur_v = nv;
+    cur_i = ni;
+    m = cand;
+    stride = cand;
+  }
+}
+}  // namespace hrec
+
+extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_rows, int n_users,
+                              const float* item_factors_t, int64_t ld_items, const int64_t* item_rows,
+                              int64_t n_items, int k, int kp, float* out, void* stream) {
+  HREC_REQUIRE(kp == 16 || kp == 32 || kp == 64, "als_score: kp must be 16, 32 or 64");
+  HREC_REQUIRE(k >= 1 && k <= kp, "als_score: need 1 <= k <= kp");
+  HREC_REQUIRE(n_users >= 0 && n_items >= 0 && ld_items >= 0, "als_score: negative size");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(user_factors && user_rows && item_factors_t && out, "als_score: null pointer");
+  HREC_REQUIRE(item_rows != nullptr || n_items <= ld_items, "als_score: n_items > ld_items");
+  constexpr int UB = 16;
+  const dim3 grid((unsigned)((n_items + 255) / 256), (unsigned)((n_users + UB - 1) / UB));
+  hipLaunchKernelGGL((als_score_kernel<UB>), grid, dim3(256), 0, as_stream(stream), user_factors, user_rows,
+                     n_users, item_factors_t, ld_items, item_rows, n_items, k, kp, out);
+  return check_launch("als_score_kernel");
+}
+
+extern "C" size_t hrec_topk_workspace_bytes(int64_t n_rows, int64_t n, int top_k, int is_f64) {
+  return topk_ws_bytes(n_rows, n, top_k, is_f64 ? 8 : 4);
+}
+
+extern "C" int hrec_topk_f32(const float* vals, int64_t n_rows, int64_t n, int64_t row_stride, int top_k,
+                             int64_t* out_idx, float* out_val, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+  HREC_REQUIRE(n_rows >= 0 && n >= 0 && row_stride >= n, "topk_f32: bad shape");
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "topk_f32: top_k must be in [1, 1024]");
+  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(n_rows < 65536, "topk_f32: at most 65535 rows per call");
+  HREC_REQUIRE(vals && out_idx && out_val, "topk_f32: null pointer");
+  return topk_rows<float>(vals, n_rows, n, row_stride, top_k, out_idx, out_val, workspace, workspace_bytes,
+                          as_stream(stream));
+}
+
+extern "C" int hrec_topk_f64(const double* vals, int64_t n_rows, int64_t n, int64_t row_stride, int top_k,
+                             int64_t* out_idx, double* out_val, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+  HREC_REQUIRE(n_rows >= 0 && n >= 0 && row_stride >= n, "topk_f64: bad shape");
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "topk_f64: top_k must be in [1, 1024]");
+  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(n_rows < 65536, "topk_f64: at most 65535 rows per call");
+  HREC_REQUIRE(vals && out_idx && out_val, "topk_f64: null pointer");
+  return topk_rows<double>(vals, n_rows, n, row_stride, top_k, out_idx, out_val, workspace, workspace_bytes,
+                           as_stream(stream));
+}
+
+static constexpr int kMinmaxParts = 256;
+
+extern "C" size_t hrec_fuse_workspace_bytes(int64_t n, int top_k) {
+  return (size_t)kMinmaxParts * 4 * 8 + 64 + (size_t)n * 8 + topk_ws_bytes(1, n, top_k, 8);
+}
+
+extern "C" int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, int64_t n, int als_wins,
+                              int top_k, int64_t* out_idx, double* out_score, double* out_fused,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  HREC_REQUIRE(n >= 0, "fuse_topk: negative n");
+  HREC_REQUIRE(top_k >= 0 && top_k <= 1024, "fuse_topk: top_k must be in [0, 1024]");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(als && tt, "fuse_topk: null input");
+  HREC_REQUIRE(top_k == 0 || (out_idx && out_score), "fuse_topk: null output");
+  const size_t need = hrec_fuse_workspace_bytes(n, top_k);
+  HREC_REQUIRE(workspace && workspace_bytes >= need, "fuse_topk: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t s = as_stream(stream);
+  char* w = (char*)workspace;
+  double* part = (double*)w;
+  double* coef = (double*)(w + kMinmaxParts * 4 * 8);
+  double* fused = out_fused ? out_fused : (double*)(w + kMinmaxParts * 4 * 8 + 64);
+  char* tws = w + kMinmaxParts * 4 * 8 + 64 + (size_t)n * 8;
+  const size_t tws_bytes = workspace_bytes - (kMinmaxParts * 4 * 8 + 64 + (size_t)n * 8);
+  const int parts = (int)((n + 255) / 256 < kMinmaxParts ? (n + 255) / 256 : kMinmaxParts);
+  hipLaunchKernelGGL(minmax_partial_kernel, dim3(parts), dim3(256), 0, s, als, tt, tt_is_f32, n, part);
+  int rc = check_launch("minmax_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(minmax_final_kernel, dim3(1), dim3(64), 0, s, part, parts, tt_is_f32, coef);
+  rc = check_launch("minmax_final_kernel");
+  if (rc) return rc;
+  // src/hybrid_system.py:69 — strict '>' picks (0.8, 0.2), else (0.2, 0.8).
+  const double w0 = als_wins ? 0.8 : 0.2, w1 = als_wins ? 0.2 : 0.8;
+  hipLaunchKernelGGL(fuse_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, als, tt, tt_is_f32, n,
+                     coef, w0, w1, fused);
+  rc = check_launch("fuse_kernel");
+  if (rc || top_k == 0) return rc;
+  const int kk = (int)(top_k < n ? top_k : n);
+  rc = topk_rows<double>(fused, 1, n, n, kk, out_idx, out_score, tws, tws_bytes, s);
+  return rc;
+}

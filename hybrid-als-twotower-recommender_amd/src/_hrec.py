@@ -1,0 +1,210 @@
+"""ctypes binding of libhrec.so (the C-ABI declared in include/hrec.h).
+
+Every wrapper takes torch tensors that already live on the current HIP
+device and launches on torch's current stream; nothing here computes on the
+host. If the library is missing the wrappers raise HrecError — there is no
+CPU fallback on the product path.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libhrec.so")
+
+_c_i32 = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_u64 = ctypes.c_uint64
+_c_dbl = ctypes.c_double
+_c_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "hrec_abi_version": (_c_i32, []),
+    "hrec_last_error": (ctypes.c_char_p, []),
+    "hrec_synth_row_counts": (_c_i32, [_c_u64, _c_u64, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp]),
+    "hrec_synth_fill": (_c_i32, [_c_u64, _c_u64, _c_u64, _c_i64, _c_i64, _c_i64, _c_i32, _c_i32,
+                                 _vp, _vp, _vp, _vp]),
+    "hrec_scan_workspace_bytes": (_c_sz, [_c_i64]),
+    "hrec_exclusive_scan_i64": (_c_i32, [_vp, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "hrec_als_init_factors": (_c_i32, [_c_u64, _c_i64, _c_i64, _c_i32, _c_i32, _vp, _vp]),
+    "hrec_als_half_sweep": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl,
+                                     _c_i32, _vp, _vp]),
+    "hrec_transpose_f32": (_c_i32, [_vp, _c_i64, _c_i64, _vp, _vp]),
+    "hrec_als_score": (_c_i32, [_vp, _vp, _c_i32, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp,
+                                _vp]),
+    "hrec_topk_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i32]),
+    "hrec_topk_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_topk_f64": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_fuse_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
+    "hrec_fuse_topk": (_c_i32, [_vp, _vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_sz,
+                                _vp]),
+}
+
+ABI_VERSION = 1
+_LIB = None
+
+
+class HrecError(RuntimeError):
+    """A libhrec call failed (or the library is not built)."""
+
+
+def lib():
+    """Load libhrec.so once. torch is imported first so the library binds to
+    the HIP runtime torch already loaded (same soname libamdhip64.so.7)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise HrecError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                " (no CPU fallback exists for the HIP hot path)")
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.hrec_abi_version() != ABI_VERSION:
+            raise HrecError("libhrec ABI version mismatch; rebuild the library")
+        _LIB = handle
+    return _LIB
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def _check(name, rc):
+    if rc != 0:
+        msg = lib().hrec_last_error().decode(errors="replace")
+        raise HrecError(f"{name} failed ({rc}): {msg}")
+
+
+def _stream():
+    return _vp(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(t, dtype, name):
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise HrecError(f"{name}: expected a device tensor")
+    if t.dtype != dtype:
+        raise HrecError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise HrecError(f"{name}: tensor must be contiguous")
+    return _vp(t.data_ptr())
+
+
+def require_device():
+    if not torch.cuda.is_available():
+        raise HrecError("no HIP device visible: the MI355X hot path needs a GPU")
+
+
+# ------------------------------------------------------------------ synth
+def synth_row_counts(seed, threshold, row_begin, n_rows, n_cols, transposed, counts):
+    _check("hrec_synth_row_counts", lib().hrec_synth_row_counts(
+        seed, threshold, row_begin, n_rows, n_cols, int(transposed),
+        _dev(counts, torch.int64, "counts"), _stream()))
+
+
+def synth_fill(seed, seed2, threshold, row_begin, n_rows, n_cols, transposed, n_levels, indptr,
+               indices, values):
+    _check("hrec_synth_fill", lib().hrec_synth_fill(
+        seed, seed2, threshold, row_begin, n_rows, n_cols, int(transposed), n_levels,
+        _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
+        _dev(values, torch.float32, "values"), _stream()))
+
+
+def exclusive_scan(counts):
+    """indptr[n+1] from counts[n] on the device."""
+    n = counts.numel()
+    out = torch.empty(n + 1, dtype=torch.int64, device=counts.device)
+    ws_bytes = int(lib().hrec_scan_workspace_bytes(n))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=counts.device)
+    _check("hrec_exclusive_scan_i64", lib().hrec_exclusive_scan_i64(
+        _dev(counts, torch.int64, "counts"), n, _dev(out, torch.int64, "out"),
+        _dev(ws, torch.uint8, "ws"), ws.numel(), _stream()))
+    return out
+
+
+# -------------------------------------------------------------------- ALS
+def als_init_factors(seed, row_begin, n_rows, k, kp, out):
+    _check("hrec_als_init_factors", lib().hrec_als_init_factors(
+        seed, row_begin, n_rows, k, kp, _dev(out, torch.float32, "out"), _stream()))
+
+
+def als_half_sweep(indptr, indices, values, src_factors, k, reg_param, dst_factors, accum_mode=0):
+    n_rows = indptr.numel() - 1
+    kp = dst_factors.shape[1]
+    if src_factors.shape[1] != kp or dst_factors.shape[0] < n_rows:
+        raise HrecError("als_half_sweep: factor shapes do not match")
+    _check("hrec_als_half_sweep", lib().hrec_als_half_sweep(
+        _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
+        _dev(values, torch.float32, "values"), n_rows,
+        _dev(src_factors, torch.float32, "src_factors"), src_factors.shape[0], k, kp,
+        float(reg_param), int(accum_mode), _dev(dst_factors, torch.float32, "dst_factors"),
+        _stream()))
+
+
+def transpose(x):
+    rows, cols = x.shape
+    out = torch.empty((cols, rows), dtype=torch.float32, device=x.device)
+    _check("hrec_transpose_f32", lib().hrec_transpose_f32(
+        _dev(x, torch.float32, "in"), rows, cols, _dev(out, torch.float32, "out"), _stream()))
+    return out
+
+
+def als_score(user_factors, user_rows, item_factors_t, item_rows, n_items, k, out=None):
+    kp = user_factors.shape[1]
+    n_users = user_rows.numel()
+    if out is None:
+        out = torch.empty((n_users, n_items), dtype=torch.float32, device=user_factors.device)
+    _check("hrec_als_score", lib().hrec_als_score(
+        _dev(user_factors, torch.float32, "user_factors"), _dev(user_rows, torch.int64, "user_rows"),
+        n_users, _dev(item_factors_t, torch.float32, "item_factors_t"), item_factors_t.shape[1],
+        _dev(item_rows, torch.int64, "item_rows"), n_items, k, kp,
+        _dev(out, torch.float32, "out"), _stream()))
+    return out
+
+
+# ------------------------------------------------------------------ top-k
+def topk(vals, top_k):
+    """Stable descending top-k of each row of a 2-D f32/f64 device tensor."""
+    if vals.dim() == 1:
+        vals = vals.unsqueeze(0)
+    n_rows, n = vals.shape
+    kk = min(int(top_k), n)
+    dev = vals.device
+    is64 = vals.dtype == torch.float64
+    out_i = torch.empty((n_rows, kk), dtype=torch.int64, device=dev)
+    out_v = torch.empty((n_rows, kk), dtype=vals.dtype, device=dev)
+    if kk == 0:
+        return out_i, out_v
+    ws_bytes = int(lib().hrec_topk_workspace_bytes(n_rows, n, kk, int(is64)))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    fn = lib().hrec_topk_f64 if is64 else lib().hrec_topk_f32
+    _check("hrec_topk", fn(_dev(vals, vals.dtype, "vals"), n_rows, n, vals.stride(0), kk,
+                           _dev(out_i, torch.int64, "out_idx"), _dev(out_v, vals.dtype, "out_val"),
+                           _dev(ws, torch.uint8, "ws"), ws_bytes, _stream()))
+    return out_i, out_v
+
+
+# ----------------------------------------------------------------- fusion
+def fuse_topk(als, tt, als_wins, top_k, want_fused=True):
+    """als: f64 [n]; tt: f32 or f64 [n] (device). Returns (idx, score, fused)."""
+    n = als.numel()
+    dev = als.device
+    tt_f32 = tt.dtype == torch.float32
+    kk = min(int(top_k), n)
+    out_i = torch.empty(max(kk, 1), dtype=torch.int64, device=dev)
+    out_s = torch.empty(max(kk, 1), dtype=torch.float64, device=dev)
+    fused = torch.empty(n, dtype=torch.float64, device=dev) if want_fused else None
+    ws_bytes = int(lib().hrec_fuse_workspace_bytes(n, kk))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    _check("hrec_fuse_topk", lib().hrec_fuse_topk(
+        _dev(als, torch.float64, "als"), _dev(tt, tt.dtype, "tt"), int(tt_f32), n, int(bool(als_wins)),
+        kk, _dev(out_i, torch.int64, "out_idx"), _dev(out_s, torch.float64, "out_score"),
+        _dev(fused, torch.float64, "out_fused"), _dev(ws, torch.uint8, "ws"), ws_bytes, _stream()))
+    return out_i[:kk], out_s[:kk], fused

@@ -1,0 +1,76 @@
+"""Synthetic interaction matrices generated on the device (K10).
+
+Replaces the Amazon CSV the reference downloads (src/data_preprocessing.py:22-35)
+for the perf configurations of BASELINE.json. The matrix is defined by a
+counter-based hash predicate:
+
+    (u, i) in R  <=>  h64(seed, u, i) < threshold(density)
+    rating(u, i)  =   h64(seed2, u, i) mod 19      (label-encoded 0..18,
+                                                     src/data_preprocessing.py:79-80)
+
+so CSR rows (users) and CSC columns (items) are generated independently and
+every shard of every world size sees the same matrix.
+"""
+from dataclasses import dataclass
+
+import torch
+
+from . import _hrec
+
+SEED = 20250620
+SEED2 = 20250621
+SEED_INIT = 7
+N_LEVELS = 19
+
+
+def threshold(density):
+    """uint64 acceptance threshold: int(density * 2**64) (double product)."""
+    if not 0.0 <= density < 1.0:
+        raise ValueError("density must be in [0, 1)")
+    return int(float(density) * 18446744073709551616.0)
+
+
+@dataclass
+class DeviceCSR:
+    """One shard of a compressed-row matrix on the device.
+
+    Rows are global rows row_begin .. row_begin + n_rows - 1; indptr is local
+    (starts at 0). For the item side (CSC of R) rows are items and column
+    indices are user ids."""
+    indptr: torch.Tensor   # int64 [n_rows + 1]
+    indices: torch.Tensor  # int32 [nnz]
+    values: torch.Tensor   # f32   [nnz]
+    row_begin: int
+    n_rows: int
+    n_cols: int
+
+    @property
+    def nnz(self):
+        return int(self.indices.numel())
+
+
+def generate(n_users, n_items, density, transposed, row_begin=0, n_rows=None, seed=SEED,
+             seed2=SEED2, n_levels=N_LEVELS, device=None):
+    """Generate rows [row_begin, row_begin+n_rows) of R (transposed=False:
+    user rows over items) or of R^T (transposed=True: item rows over users).
+    Rows past the end of the matrix are empty (shard padding)."""
+    _hrec.require_device()
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    total_rows = n_items if transposed else n_users
+    n_cols = n_users if transposed else n_items
+    if n_rows is None:
+        n_rows = total_rows - row_begin
+    real = max(0, min(n_rows, total_rows - row_begin))
+    thr = threshold(density)
+    counts = torch.zeros(n_rows, dtype=torch.int64, device=device)
+    if real > 0:
+        _hrec.synth_row_counts(seed, thr, row_begin, real, n_cols, transposed, counts)
+    indptr = _hrec.exclusive_scan(counts)
+    nnz = int(indptr[-1].item())
+    indices = torch.empty(max(nnz, 1), dtype=torch.int32, device=device)[:nnz]
+    values = torch.empty(max(nnz, 1), dtype=torch.float32, device=device)[:nnz]
+    if real > 0 and nnz > 0:
+        _hrec.synth_fill(seed, seed2, thr, row_begin, real, n_cols, transposed, n_levels, indptr,
+                         indices, values)
+    del counts
+    return DeviceCSR(indptr, indices, values, row_begin, n_rows, n_cols)

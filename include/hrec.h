@@ -1,0 +1,142 @@
+/*
+ * hrec.h — C-ABI of libhrec.so, the MI355X (gfx950) hot path of the hybrid
+ * ALS + two-tower recommender.
+ *
+ * The reference (HSoumi/hybrid-als-twotower-recommender) has no FFI of its
+ * own: its hot path sits behind two third-party engines that its Python
+ * wrappers call. Each entry point below replaces one of those downward calls
+ * (file:line into the reference tree):
+ *
+ *   Spark  ALS.fit            src/als_model.py:52-62   -> hrec_synth_* (data),
+ *                                                          hrec_als_init_factors,
+ *                                                          hrec_als_half_sweep
+ *   Spark  ALSModel.transform src/als_model.py:71-76   -> hrec_als_score
+ *   Python/sklearn fusion     src/hybrid_system.py:57-75,108 -> hrec_fuse_topk
+ *   Keras  two-tower graph    src/two_tower_model.py:38-89 -> hrec_tt_*
+ *
+ * Conventions (all functions):
+ *   - every pointer is a DEVICE pointer owned by the caller, except where a
+ *     parameter is documented as host memory;
+ *   - row-major storage; factor matrices have a leading dimension `kp`
+ *     (16, 32 or 64) >= k whose padding columns are kept at zero;
+ *   - CSR: int64 indptr[n_rows+1] (local, starts at 0), int32 indices,
+ *     f32 values;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *     calls are asynchronous on it and never allocate or synchronise;
+ *   - return 0 on success, a negative HREC_E* code on failure; the message
+ *     of the last failure on the calling thread is hrec_last_error().
+ */
+#ifndef HREC_H
+#define HREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HREC_ABI_VERSION 1
+
+#define HREC_OK 0
+#define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
+#define HREC_E_LAUNCH (-2)  /* HIP launch/runtime error                  */
+#define HREC_E_UNSUPPORTED (-3)
+
+int hrec_abi_version(void);
+const char* hrec_last_error(void);
+
+/* ---------------------------------------------------------------- synth --
+ * Synthetic interaction matrix R: (u,i) in R  <=>
+ *   h64(seed,u,i) < threshold,  rating(u,i) = h64(seed2,u,i) mod n_levels,
+ * h64(s,u,i) = mix64(s*0x9E3779B97F4A7C15 + (u<<32 | i)), mix64 = splitmix64
+ * finaliser. The same predicate generates CSR rows (users, transposed=0) and
+ * CSC columns (items, transposed=1) independently, so shards agree.
+ * Rows are row_begin .. row_begin+n_rows-1 of the chosen orientation; the
+ * other dimension has n_cols entries. Replaces the dataset the reference
+ * reads at src/data_preprocessing.py:22-35 for the perf configurations. */
+int hrec_synth_row_counts(uint64_t seed, uint64_t threshold, int64_t row_begin,
+                          int64_t n_rows, int64_t n_cols, int transposed,
+                          int64_t* counts, void* stream);
+int hrec_synth_fill(uint64_t seed, uint64_t seed2, uint64_t threshold,
+                    int64_t row_begin, int64_t n_rows, int64_t n_cols,
+                    int transposed, int n_levels, const int64_t* indptr,
+                    int32_t* indices, float* values, void* stream);
+
+/* Exclusive prefix sum of counts[n] into out[n+1] (out[n] = total).
+ * Workspace: hrec_scan_workspace_bytes(n) bytes of device memory. */
+size_t hrec_scan_workspace_bytes(int64_t n);
+int hrec_exclusive_scan_i64(const int64_t* counts, int64_t n, int64_t* out,
+                            void* workspace, size_t workspace_bytes,
+                            void* stream);
+
+/* ------------------------------------------------------------------ ALS --
+ * Initial factors (Spark ALS.initialize [ext: pyspark 3.5.1 ALS.scala]:
+ * per row a Gaussian-like vector, L2-normalised, f32). Counter-based on
+ * (seed, global row) so every shard layout yields the same matrix. */
+int hrec_als_init_factors(uint64_t seed, int64_t row_begin, int64_t n_rows,
+                          int k, int kp, float* out, void* stream);
+
+/* One ALS half-sweep (Spark computeFactors + NormalEquation.add +
+ * CholeskySolver.solve [ext]; called from src/als_model.py:62):
+ * for every local dst row r with n_r = indptr[r+1]-indptr[r] ratings,
+ *   (sum_j v_j v_j^T + reg_param*n_r*I) x_r = sum_j rating_j v_j,
+ * v_j = src_factors[indices[j]], accumulated in f64 (accum_mode 0), solved
+ * by Cholesky in f64, stored as f32 in dst_factors[r*kp .. +kp).
+ * Rows with n_r == 0 get a zero vector (Spark has no factor for them).
+ * accum_mode: 0 = f64 Gramian (Spark-exact semantics). */
+int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices,
+                        const float* values, int64_t n_rows,
+                        const float* src_factors, int64_t n_src, int k, int kp,
+                        double reg_param, int accum_mode, float* dst_factors,
+                        void* stream);
+
+/* out[c*rows + r] = in[r*cols + c] (f32). */
+int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, float* out,
+                       void* stream);
+
+/* ALS scoring (Spark ALSModel.transform predict UDF [ext], reached from
+ * src/als_model.py:75): out[b*n_items + j] = sum_{c<k} U[u_b][c]*V[i_j][c]
+ * as a sequential f32 chain, product rounded then sum rounded (no FMA),
+ * exactly the JVM loop. NaN where u_b < 0 or i_j < 0 (unknown id).
+ * user_factors is [*, kp] row-major; item_factors_t is the TRANSPOSED item
+ * matrix [kp, ld_items]; item_rows == NULL means i_j = j. */
+int hrec_als_score(const float* user_factors, const int64_t* user_rows,
+                   int n_users, const float* item_factors_t, int64_t ld_items,
+                   const int64_t* item_rows, int64_t n_items, int k, int kp,
+                   float* out, void* stream);
+
+/* ---------------------------------------------------------------- top-k --
+ * Stable descending top-k of each of n_rows rows (row i starts at
+ * vals + i*row_stride, n elements): larger value first, equal values keep
+ * input order (smaller index first), NaN last — Python's
+ * sorted(..., key=score, reverse=True)[:k] as used at
+ * src/hybrid_system.py:108 and src/als_model.py:173. */
+size_t hrec_topk_workspace_bytes(int64_t n_rows, int64_t n, int top_k, int is_f64);
+int hrec_topk_f32(const float* vals, int64_t n_rows, int64_t n, int64_t row_stride,
+                  int top_k, int64_t* out_idx, float* out_val, void* workspace,
+                  size_t workspace_bytes, void* stream);
+int hrec_topk_f64(const double* vals, int64_t n_rows, int64_t n, int64_t row_stride,
+                  int top_k, int64_t* out_idx, double* out_val, void* workspace,
+                  size_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------- fusion --
+ * HybridRecommendationSystem.adaptive_fusion + top-k
+ * (src/hybrid_system.py:57-75 and :108): both score vectors (aligned to the
+ * same item order) are min-max scaled with sklearn MinMaxScaler arithmetic
+ * in their own dtype (als f64; tt f32 when tt_is_f32, else f64), then
+ * fused = w0*als_norm + w1*tt_norm in f64 with (w0,w1) = (0.8,0.2) when
+ * als_wins (the strict als_f1 > tt_f1 of :69) else (0.2,0.8).
+ * out_fused (optional, n doubles) receives every fused score; out_idx /
+ * out_score receive the stable top min(top_k, n). */
+size_t hrec_fuse_workspace_bytes(int64_t n, int top_k);
+int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, int64_t n,
+                   int als_wins, int top_k, int64_t* out_idx, double* out_score,
+                   double* out_fused, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HREC_H */

@@ -1,0 +1,174 @@
+"""CPU: pin the oracle against the reference's golden vectors and cross-check
+its numpy / C restatements (no GPU)."""
+import numpy as np
+import pytest
+from conftest import dec_pairs, dec_score, load_golden
+
+from oracle import als as oals
+from oracle import build as obuild
+from oracle import fusion as ofus
+from oracle import synth as osyn
+from oracle import two_tower as ott
+
+
+def _same(a, b):
+    """Bit-exact scalar equality that also checks the numpy scalar kind."""
+    return float(a) == float(b) and type(a) is type(b)
+
+
+# ------------------------------------------------------------ fusion golden
+@pytest.mark.parametrize("case", load_golden("fusion.json")["cases"], ids=lambda c: c["name"])
+def test_fusion_oracle_matches_reference(case):
+    meta = load_golden("fusion.json")["meta"]
+    legacy = int(meta["numpy"].split(".")[0]) < 2  # fixtures record the numpy they ran under
+    als = dec_pairs(case["als"])
+    tt = dec_pairs(case["tt"])
+    combined = ofus.adaptive_fusion(als, tt, case["als_f1"], case["tt_f1"], legacy=legacy)
+    exp = dec_pairs(case["combined"])
+    assert [i for i, _ in combined] == [i for i, _ in exp]
+    for (_, a), (_, b) in zip(combined, exp):
+        assert float(a) == float(b)
+    top = ofus.top_k(combined, case["top_k"])
+    assert [(i, float(s)) for i, s in top] == [(i, float(s)) for i, s in dec_pairs(case["top"])]
+
+
+def test_f1_oracle_matches_reference():
+    for rec in load_golden("f1.json")["cases"]:
+        actual = {int(i): s for i, s in rec["actual"]}
+        pred = {int(i): s for i, s in rec["pred"]}
+        got = ofus.compute_f1_score(actual, pred, k=rec["k"])  # TT copy: guarded k > 0
+        assert float(got) == rec["tt"]
+        if rec["als"] != "ZeroDivisionError":
+            assert float(got) == rec["als"]
+
+
+def test_similar_items_oracle_matches_reference():
+    for case in load_golden("similar_items.json")["cases"]:
+        feats = {int(i): {"features": np.asarray(f, dtype=np.float64), "rating": r}
+                 for i, f, r in case["item_features"]}
+        for q in case["queries"]:
+            assert ofus.find_similar_items(feats, q) == case["similar"][str(q)]
+
+
+def test_als_fallback_oracle_matches_reference():
+    for case in load_golden("als_fallback.json")["cases"]:
+        feats = {int(i): {"features": np.asarray(f, dtype=np.float64), "rating": r}
+                 for i, f, r in case["item_features"]}
+        spark = {int(i): (np.nan if p is None else p) for i, p in case["spark_predictions"]}
+        got = ofus.als_predict_with_fallback(spark, feats, case["global_mean"], case["query"])
+        exp = dec_pairs(case["result"])
+        assert len(got) == len(exp)
+        for (gi, gs), (ei, es) in zip(got, exp):
+            assert gi == ei and _same(gs, es)
+
+
+def test_tt_numeric_inputs_oracle_matches_reference():
+    for case in load_golden("tt_inputs.json")["cases"]:
+        tr = np.column_stack([case["train"]["price"], case["train"]["average_review_rating"]])
+        scale, min_, dmin, dmax = ott.scaler_fit(tr)
+        assert dmin.tolist() == case["scaler_min"] and dmax.tolist() == case["scaler_max"]
+        assert ott.scaler_transform(tr, scale, min_).tolist() == case["prepare_numeric_in"]
+        cand = np.column_stack([case["candidates"]["price"], case["candidates"]["average_review_rating"]])
+        assert ott.scaler_transform(cand, scale, min_).tolist() == case["inputs"]["numeric_in"]
+        assert case["inputs"]["user_in"] == [31] * len(case["candidates"]["itemId"])
+        assert case["inputs"]["item_id_in"] == case["candidates"]["itemId"]
+
+
+def test_utils_known_answers():
+    u = load_golden("utils.json")["cases"]
+    assert u["scale_ratings_to_5"][0][1] == [1.0, 2.0, 3.0, 4.0, 5.0]
+    items, exp = u["normalize_predictions"][0]
+    got = ofus.minmax(np.array([s for _, s in items]))
+    assert got.tolist() == [s for _, s in exp]
+
+
+# ------------------------------------------------------------------ synth
+def test_synth_numpy_matches_c():
+    for transposed in (0, 1):
+        a = osyn.csr_rows(300, 200, 0.05, transposed, 7, 40, 11, 12)
+        b = obuild.synth_csr(300, 200, 0.05, transposed, 7, 40, 11, 12)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_synth_csr_csc_are_transposes():
+    U, I = 120, 90
+    csr = obuild.synth_csr(U, I, 0.08, 0, 0, U, 3, 4)
+    csc = obuild.synth_csr(U, I, 0.08, 1, 0, I, 3, 4)
+    dense_r = np.zeros((U, I), np.float32)
+    mask_r = np.zeros((U, I), bool)
+    for u in range(U):
+        c = csr[1][csr[0][u]:csr[0][u + 1]]
+        dense_r[u, c] = csr[2][csr[0][u]:csr[0][u + 1]]
+        mask_r[u, c] = True
+    mask_c = np.zeros((U, I), bool)
+    dense_c = np.zeros((U, I), np.float32)
+    for i in range(I):
+        c = csc[1][csc[0][i]:csc[0][i + 1]]
+        dense_c[c, i] = csc[2][csc[0][i]:csc[0][i + 1]]
+        mask_c[c, i] = True
+    assert (mask_r == mask_c).all() and (dense_r == dense_c).all()
+    assert 0.04 < mask_r.mean() < 0.12
+    assert set(np.unique(csr[2])) <= set(range(19))
+
+
+def test_init_factors_unit_norm():
+    f = osyn.init_factors(7, 5, 6, 10)
+    np.testing.assert_allclose(np.linalg.norm(f.astype(np.float64), axis=1), 1.0, rtol=1e-6)
+
+
+# -------------------------------------------------------------------- ALS
+def _small_problem(seed=0, n_rows=25, n_src=30, k=8):
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(0, 12, n_rows)
+    indptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    indices = rng.integers(0, n_src, indptr[-1]).astype(np.int32)
+    values = rng.integers(0, 19, indptr[-1]).astype(np.float32)
+    src = rng.normal(size=(n_src, k)).astype(np.float32)
+    return indptr, indices, values, src
+
+
+def test_als_spark_restatement_variants_agree():
+    indptr, indices, values, src = _small_problem()
+    a = oals.half_sweep_spark(indptr, indices, values, src, 8, 0.1)
+    b = oals.half_sweep_blas(indptr, indices, values, src, 8, 0.1)
+    c = obuild.half_sweep(indptr, indices, values, src, 8, 0.1)
+    np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(a, c, rtol=1e-5, atol=1e-6)
+    empty = np.diff(indptr) == 0
+    assert (a[empty] == 0).all() and (c[empty] == 0).all()
+
+
+def test_als_rank1_known_answer():
+    # k = 1: x = sum(r v) / (sum(v^2) + reg * n), in closed form.
+    indptr = np.array([0, 3], np.int64)
+    indices = np.array([0, 1, 1], np.int32)  # duplicate rating counts twice (Spark keeps both)
+    values = np.array([4.0, 0.0, 2.0], np.float32)
+    src = np.array([[0.5], [2.0]], np.float32)
+    x = oals.half_sweep_spark(indptr, indices, values, src, 1, 0.1)
+    expect = (4 * 0.5 + 0 * 2.0 + 2 * 2.0) / (0.25 + 4 + 4 + 0.1 * 3)
+    assert abs(float(x[0, 0]) - expect) < 1e-7
+    assert float(obuild.half_sweep(indptr, indices, values, src, 1, 0.1)[0, 0]) == float(x[0, 0])
+
+
+def test_als_normal_equation_residual():
+    indptr, indices, values, src = _small_problem(seed=3, k=16)
+    x = obuild.half_sweep(indptr, indices, values, src, 16, 0.05)
+    for r in range(len(indptr) - 1):
+        b, e = indptr[r], indptr[r + 1]
+        if b == e:
+            continue
+        V = src[indices[b:e]].astype(np.float64)
+        A = V.T @ V + 0.05 * (e - b) * np.eye(16)
+        rhs = V.T @ values[b:e].astype(np.float64)
+        np.testing.assert_allclose(A @ x[r].astype(np.float64), rhs, rtol=1e-5, atol=1e-5)
+
+
+def test_als_score_matrix_matches_scalar_predict():
+    rng = np.random.default_rng(1)
+    U = rng.normal(size=(4, 12)).astype(np.float32)
+    V = rng.normal(size=(9, 12)).astype(np.float32)
+    m = oals.score_matrix(U, V)
+    users = np.repeat(np.arange(4), 9)
+    items = np.tile(np.arange(9), 4)
+    np.testing.assert_array_equal(m.reshape(-1), oals.predict(U, V, users, items))
