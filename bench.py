@@ -1,0 +1,233 @@
+"""Headline benchmark: ALS epochs/sec (+ scored user-item pairs/sec) at rank 64.
+
+Workload (BASELINE.json configs[1], SURVEY §8d "c2"): synthetic 1,000,000 users
+x 100,000 items at 0.5 % density (nnz ~ 5.0e8, ratings 0..18), rank 64,
+reg 0.1. One step = one ALS epoch = item half-sweep + user half-sweep
+(Spark's iteration order), generated and kept on the device (inputs resident
+in HBM before the timed region). With N ranks (torchrun), users and items are
+row-sharded and the factors replicated by RCCL all-gathers after each
+half-sweep; the total work is fixed (scaling "strong").
+
+Also measured in the same run (not the headline value):
+  * scoring: B users x all items, JVM-exact ALS dot + stable top-5 on the
+    device (pairs scored and consumed by top-k per second);
+  * roofline of the dominant kernel (als_half_sweep_f64_kernel), timed with
+    HIP events on the stream it is launched on;
+  * cpu_baseline: the C oracle (Spark ALS restated, OpenMP) on rank 0 over a
+    bounded row sample of the same matrix, extrapolated to one epoch.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hybrid-als-twotower-recommender_amd"))
+sys.path.insert(0, ROOT)
+
+from src import _hrec, synthetic  # noqa: E402
+from src.als_engine import DeviceALS, shard_range  # noqa: E402
+
+METRIC = "ALS epochs/sec + scored user-item pairs/sec at rank=64, 1/2/4/8 MI355X"
+F64_MFMA_PEAK_TFLOPS = 78.6  # AMD MI355X spec (FP64 matrix); not in MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    "c2": dict(users=1_000_000, items=100_000, density=0.005, rank=64),
+    "c2s": dict(users=100_000, items=20_000, density=0.005, rank=64),  # quick check
+}
+
+
+def algo_flops(nnz, n_dst, k):
+    """symmetric rank-1 Gramian + rhs per rating, Cholesky + 2 solves per row."""
+    return nnz * (k * (k + 1) + 2 * k) + n_dst * (k ** 3 / 3 + 2 * k * k)
+
+
+def algo_bytes(nnz, n_dst, k):
+    """index + value + one gathered f32 factor row per rating, indptr, dst write."""
+    return nnz * (4 + 4 + 4 * k) + (n_dst + 1) * 8 + n_dst * k * 4
+
+
+def cpu_baseline(eng, cfg, n_user_rows, n_item_rows):
+    """C oracle on a bounded sample of the same matrix (rank 0, N=1)."""
+    import numpy as np
+
+    from oracle import build as obuild
+
+    obuild.build()
+    k = cfg["rank"]
+
+    def sample(csr, rows):
+        ip = csr.indptr[: rows + 1].cpu().numpy()
+        return ip, csr.indices[: int(ip[-1])].cpu().numpy(), csr.values[: int(ip[-1])].cpu().numpy()
+
+    ucsr = sample(eng.user_csr, n_user_rows)
+    icsc = sample(eng.item_csc, n_item_rows)
+    U = eng.U[: cfg["users"], :k].cpu().numpy()
+    V = eng.V[: cfg["items"], :k].cpu().numpy()
+    t0 = time.perf_counter()
+    obuild.half_sweep(*icsc, U, k, 0.1)
+    t_item = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    obuild.half_sweep(*ucsr, V, k, 0.1)
+    t_user = time.perf_counter() - t0
+    epoch_s = t_item * cfg["items"] / n_item_rows + t_user * cfg["users"] / n_user_rows
+    return {
+        "value": 1.0 / epoch_s, "unit": "epochs/s", "cores": int(obuild.load().oracle_max_threads()),
+        "kind": "port",
+        "sample": (f"C oracle (Spark 3.5.1 ALS restated: f64 dspr Gramian + dpptrf/dpptrs, OpenMP) on "
+                   f"{n_item_rows} item rows + {n_user_rows} user rows of the same c2 matrix, "
+                   f"{t_item + t_user:.1f} s measured, extrapolated to one full epoch"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--score-users", type=int, default=1024)
+    ap.add_argument("--cpu-user-rows", type=int, default=12000)
+    ap.add_argument("--cpu-item-rows", type=int, default=1200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        group = dist.group.WORLD
+
+    cfg = CONFIGS[args.config]
+    k = cfg["rank"]
+    n_users, n_items = cfg["users"], cfg["items"]
+    u0, u_per = shard_range(n_users, world, rank)
+    i0, i_per = shard_range(n_items, world, rank)
+    csr = synthetic.generate(n_users, n_items, cfg["density"], False, u0, u_per)
+    csc = synthetic.generate(n_users, n_items, cfg["density"], True, i0, i_per)
+    eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group)
+    eng.init_user_factors(synthetic.SEED_INIT)
+    torch.cuda.synchronize()
+
+    nnz_local = torch.tensor([csr.nnz, csc.nnz], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(nnz_local)
+    nnz_user, nnz_item = (int(x) for x in nnz_local.tolist())
+
+    for _ in range(args.warmup):
+        eng.epoch()
+
+    # Timed region: K epochs, barrier + synchronize on both sides.
+    stream = torch.cuda.current_stream()
+    ev = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        e[0].record(stream)
+        _hrec.als_half_sweep(csc.indptr, csc.indices, csc.values, eng.U, k, eng.reg, eng.V_local)
+        e[1].record(stream)
+        eng._gather(eng.V, eng.V_local)
+        e[2].record(stream)
+        _hrec.als_half_sweep(csr.indptr, csr.indices, csr.values, eng.V, k, eng.reg, eng.U_local)
+        e[3].record(stream)
+        eng._gather(eng.U, eng.U_local)
+        ev.append(e)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    item_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+    user_ms = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev)
+    # per-rank algorithmic work of one epoch (both launches of the kernel)
+    flops = algo_flops(csc.nnz, i_per, k) + algo_flops(csr.nnz, u_per, k)
+    bytes_ = algo_bytes(csc.nnz, i_per, k) + algo_bytes(csr.nnz, u_per, k)
+    kern_s = (item_ms + user_ms) / 1e3
+    achieved_tf = flops / kern_s / 1e12
+
+    # Scoring: B users x all items, JVM-exact dot + stable top-5, rank 0's GPU.
+    scoring = None
+    if rank == 0 and args.score_users > 0:
+        Vt = _hrec.transpose(eng.V[:n_items].contiguous())
+        B = args.score_users
+        users = torch.arange(B, dtype=torch.int64, device="cuda") * (n_users // B)
+        out = torch.empty((B, n_items), dtype=torch.float32, device="cuda")
+        for _ in range(2):
+            _hrec.als_score(eng.U, users, Vt, None, n_items, k, out=out)
+            _hrec.topk(out, 5)
+        torch.cuda.synchronize()
+        reps = 3
+        s0 = time.perf_counter()
+        for _ in range(reps):
+            _hrec.als_score(eng.U, users, Vt, None, n_items, k, out=out)
+            _hrec.topk(out, 5)
+        torch.cuda.synchronize()
+        sc_s = (time.perf_counter() - s0) / reps
+        scoring = {"pairs_per_s": B * n_items / sc_s, "ms_per_batch": sc_s * 1e3, "users": B,
+                   "items": n_items, "top_k": 5, "dtype": "f32 (JVM-exact, no FMA)"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(eng, cfg, min(args.cpu_user_rows, n_users), min(args.cpu_item_rows, n_items))
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        line = {
+            "metric": METRIC,
+            "value": args.steps / elapsed,
+            "unit": "epochs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (hash-defined interaction matrix generated on device, BASELINE.md §3)",
+            "config": {
+                "workload": (f"{args.config}: {n_users} users x {n_items} items, density {cfg['density']}, "
+                             f"rank {k}, reg 0.1; step = one ALS epoch (item + user half-sweep)"),
+                "users": n_users, "items": n_items, "density": cfg["density"], "rank": k,
+                "nnz": nnz_user, "nnz_check_csc": nnz_item,
+                "parallelism": f"dp{world} (row-sharded users/items, RCCL all-gather of factors)",
+            },
+            "roofline": {
+                "kernel": "als_half_sweep_f64_kernel (item + user launches)",
+                "bound": "mfma",
+                "achieved": achieved_tf,
+                "peak": F64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved_tf / F64_MFMA_PEAK_TFLOPS,
+                "traffic": None,
+                "kernel_ms_per_epoch": {"item": item_ms, "user": user_ms},
+                "gather_view": {"algorithmic_GBps": bytes_ / kern_s / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
+                                "frac": bytes_ / kern_s / 1e9 / HBM_PEAK_GBS},
+            },
+            "cpu_baseline": cpu,
+            "scoring": scoring,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

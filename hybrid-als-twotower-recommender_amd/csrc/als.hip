@@ -45,6 +45,68 @@ struct Vec<1> {
 
 __device__ __forceinline__ int tri(int i) { return (i * (i + 1)) >> 1; }
 
+// Wave-uniform broadcast of lane `src`'s double (two v_readlane_b32).
+__device__ __forceinline__ double bcast(double v, int src) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, src);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Solve (L L^T) x = b for the SPD matrix held as a packed lower triangle in
+// LDS (row i at tri(i)), b_i in lane i. Right-looking Cholesky with the
+// matrix in REGISTERS: lane i owns row i (a[c] = A[i][c]); every column
+// broadcast is a v_readlane, so the O(k^3/6) update is pure VALU with static
+// register indices (fully unrolled) and no LDS traffic. Entries right of the
+// diagonal are never read, so lanes update them unmasked. The packed LDS
+// array is reused once to transpose L for the back substitution.
+template <int KP>
+__device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, double bi, int lane) {
+  const int i = lane < KP ? lane : KP - 1;
+  double a[KP];
+#pragma unroll
+  for (int c = 0; c < KP; ++c) {
+    const int hi = i > c ? i : c, lo = i > c ? c : i;
+    a[c] = A[tri(hi) + lo];
+  }
+  double myrd = 0.0;  // lane j keeps 1 / L[j][j]
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    const double d = sqrt(bcast(a[j], j));
+    const double rd = 1.0 / d;
+    const double l = (lane == j) ? d : a[j] * rd;
+    a[j] = l;
+    myrd = (lane == j) ? rd : myrd;
+#pragma unroll
+    for (int c = j + 1; c < KP; ++c) a[c] = fma(-l, bcast(l, c), a[c]);
+  }
+  // forward: L y = b
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    const double yj = bcast(bi, j) * bcast(myrd, j);
+    const double upd = fma(-a[j], yj, bi);
+    bi = (lane == j) ? yj : ((lane > j) ? upd : bi);
+  }
+  // transpose L through LDS: lane i stores row i, then reads column i.
+  __syncthreads();
+  if (lane < KP) {
+#pragma unroll
+    for (int c = 0; c < KP; ++c)
+      if (c <= lane) A[tri(lane) + c] = a[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < KP; ++c) a[c] = (c >= i) ? A[tri(c) + i] : 0.0;  // a[c] = L[c][i]
+  // backward: L^T x = y
+#pragma unroll
+  for (int j = KP - 1; j >= 0; --j) {
+    const double xj = bcast(bi, j) * bcast(myrd, j);
+    const double upd = fma(-a[j], xj, bi);
+    bi = (lane == j) ? xj : ((lane < j) ? upd : bi);
+  }
+  return bi;
+}
+
 // NT floats per lane (kp = 16*NT), CH steps of 4 nnz per pipeline chunk.
 template <int NT, int CH>
 __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
@@ -176,41 +238,11 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
 
   // Spark CholeskySolver: ata[diag] += numExplicits * regParam.
   const double lambda = (double)n * reg;
-  const bool live = lane < KP;
-  if (live) A[tri(lane) + lane] += (lane < k) ? lambda : 1.0;
-  double bi = live ? bsh[lane] : 0.0;
+  if (lane < KP) A[tri(lane) + lane] += (lane < k) ? lambda : 1.0;
+  const double b_in = lane < KP ? bsh[lane] : 0.0;
   __syncthreads();
-
-  // Right-looking Cholesky A = L L^T, lane i owns row i of the packed lower
-  // triangle.
-  for (int j = 0; j < KP; ++j) {
-    const double d = sqrt(A[tri(j) + j]);
-    double l = 0.0;
-    if (live && lane > j) {
-      l = A[tri(lane) + j] / d;
-      A[tri(lane) + j] = l;
-    }
-    __syncthreads();
-    if (lane == j) A[tri(j) + j] = d;
-    if (live && lane > j) {
-      const int base = tri(lane);
-      for (int c = j + 1; c <= lane; ++c) A[base + c] -= l * A[tri(c) + j];
-    }
-    __syncthreads();
-  }
-  // L y = b
-  for (int j = 0; j < KP; ++j) {
-    const double yj = __shfl(bi, j, kWave) / A[tri(j) + j];
-    if (lane == j) bi = yj;
-    if (live && lane > j) bi -= A[tri(lane) + j] * yj;
-  }
-  // L^T x = y
-  for (int j = KP - 1; j >= 0; --j) {
-    const double xj = __shfl(bi, j, kWave) / A[tri(j) + j];
-    if (lane == j) bi = xj;
-    if (lane < j) bi -= A[tri(j) + lane] * xj;
-  }
-  if (live) out[lane] = (float)bi;
+  const double x = solve_spd_rows_impl<KP>(A, b_in, lane);
+  if (lane < KP) out[lane] = (float)x;
 }
 
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int64_t rows,

@@ -237,6 +237,40 @@ __global__ __launch_bounds__(256) void fuse_kernel(const double* __restrict__ al
   fused[p] = w0 * an + w1 * tn;
 }
 
+
+// ------------------------------------------------------- cold-start cosine
+// ALSModel._find_similar_items (src/als_model.py:93-104): sklearn
+// cosine_similarity([target], [other]) = dot(a/|a|, b/|b|) with a zero norm
+// replaced by 1. One thread per (query, item); the query's own row -> -inf so
+// it never ranks (the reference skips it).
+__global__ __launch_bounds__(256) void cosine_kernel(const double* __restrict__ feats, int64_t n_items, int dim,
+                                                     const int64_t* __restrict__ qrows, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int64_t q = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n_items) return;
+  const int64_t qr = qrows[q];
+  double* o = out + q * n_items;
+  if (j == qr) {
+    o[j] = -__builtin_inf();
+    return;
+  }
+  const double* a = feats + qr * dim;
+  const double* b = feats + j * dim;
+  double na = 0.0, nb = 0.0;
+  for (int c = 0; c < dim; ++c) {
+    na = na + a[c] * a[c];
+    nb = nb + b[c] * b[c];
+  }
+  na = sqrt(na);
+  nb = sqrt(nb);
+  if (na == 0.0) na = 1.0;
+  if (nb == 0.0) nb = 1.0;
+  double dot = 0.0;
+  for (int c = 0; c < dim; ++c) dot = dot + (a[c] / na) * (b[c] / nb);
+  o[j] = dot;
+}
+
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
               T* out_val, void* ws, size_t ws_bytes, hipStream_t s);
@@ -380,4 +414,15 @@ extern "C" int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, 
   const int kk = (int)(top_k < n ? top_k : n);
   rc = topk_rows<double>(fused, 1, n, n, kk, out_idx, out_score, tws, tws_bytes, s);
   return rc;
+}
+
+extern "C" int hrec_cosine_sim(const double* feats, int64_t n_items, int dim, const int64_t* query_rows,
+                               int64_t n_query, double* out, void* stream) {
+  HREC_REQUIRE(n_items >= 0 && n_query >= 0 && dim >= 1, "cosine_sim: bad shape");
+  if (n_items == 0 || n_query == 0) return HREC_OK;
+  HREC_REQUIRE(n_query < 65536, "cosine_sim: at most 65535 queries per call");
+  HREC_REQUIRE(feats && query_rows && out, "cosine_sim: null pointer");
+  const dim3 grid((unsigned)((n_items + 255) / 256), (unsigned)n_query);
+  hipLaunchKernelGGL(cosine_kernel, grid, dim3(256), 0, as_stream(stream), feats, n_items, dim, query_rows, out);
+  return check_launch("cosine_kernel");
 }

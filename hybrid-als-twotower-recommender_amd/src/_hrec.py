@@ -38,6 +38,7 @@ _SIGNATURES = {
     "hrec_topk_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "hrec_topk_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_topk_f64": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_cosine_sim": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp]),
     "hrec_fuse_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
     "hrec_fuse_topk": (_c_i32, [_vp, _vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_sz,
                                 _vp]),
@@ -208,3 +209,14 @@ def fuse_topk(als, tt, als_wins, top_k, want_fused=True):
         kk, _dev(out_i, torch.int64, "out_idx"), _dev(out_s, torch.float64, "out_score"),
         _dev(fused, torch.float64, "out_fused"), _dev(ws, torch.uint8, "ws"), ws_bytes, _stream()))
     return out_i[:kk], out_s[:kk], fused
+
+
+# ------------------------------------------------------------ cold start
+def cosine_sim(feats, query_rows):
+    """[n_query, n_items] f64 cosine similarities (self = -inf)."""
+    n_items, dim = feats.shape
+    out = torch.empty((query_rows.numel(), n_items), dtype=torch.float64, device=feats.device)
+    _check("hrec_cosine_sim", lib().hrec_cosine_sim(
+        _dev(feats, torch.float64, "feats"), n_items, dim, _dev(query_rows, torch.int64, "query_rows"),
+        query_rows.numel(), _dev(out, torch.float64, "out"), _stream()))
+    return out

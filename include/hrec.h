@@ -135,6 +135,15 @@ int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, int64_t n,
                    double* out_fused, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* ------------------------------------------------------ cold-start sim --
+ * ALSModel._find_similar_items (src/als_model.py:93-104): out[q*n_items+j] =
+ * cosine(feats[query_rows[q]], feats[j]) with sklearn's normalise-then-dot
+ * (zero norm -> 1); the query's own entry is -inf (the reference skips it).
+ * feats: [n_items, dim] f64 row-major in item_features dict order. */
+int hrec_cosine_sim(const double* feats, int64_t n_items, int dim,
+                    const int64_t* query_rows, int64_t n_query, double* out,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif
