@@ -1,0 +1,546 @@
+// K4-K7: the two-tower model of src/two_tower_model.py:38-89 on gfx950.
+//
+//   user_vec = LN_u(E_user[u])                                   (:71-74)
+//   h        = relu(numeric @ W1 + b1)        Dense(16, relu)    (:56-57)
+//   z        = [E_item[i] | E_man[m] | E_cat[c] | h]  (d+32)      (:60)
+//   item_vec = LN_i(z @ W2 + b2)              Dense(d) + LN      (:63-64)
+//   score    = <user_vec, item_vec>           Dot(axes=1)        (:80)
+// LayerNormalization: Keras 2.8 (epsilon 1e-3, biased variance over the
+// last axis, y = xhat*gamma + beta). Loss MSE, optimiser Adam (:84-88) with
+// TF 2.8's dense ResourceApplyAdam and sparse (IndexedSlices) update rules.
+// f32 throughout (the reference's Keras dtype).
+#include "common.h"
+
+namespace hrec {
+
+constexpr int kTR = 32;     // rows (samples / candidates) per workgroup
+constexpr int kBlock = 256;
+constexpr float kLnEps = 1e-3f;
+
+struct TTDev {
+  int d;
+  const float *ue, *ie, *me, *ce, *w1, *b1, *w2, *b2, *gu, *bu, *gi, *bi;
+};
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+  return x;
+}
+
+// LayerNorm of one row held in LDS (length d), one wave. Writes y (and the
+// normalised row + 1/std when save != nullptr).
+__device__ __forceinline__ void ln_row(const float* __restrict__ x, int d, const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float* __restrict__ y,
+                                       float* __restrict__ xhat_out, float* __restrict__ rstd_out, int lane) {
+  float s = 0.f;
+  for (int c = lane; c < d; c += kWave) s += x[c];
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+  for (int c = lane; c < d; c += kWave) {
+    const float t = x[c] - mean;
+    q += t * t;
+  }
+  const float var = wave_sum(q) / (float)d;
+  const float rstd = 1.0f / sqrtf(var + kLnEps);
+  for (int c = lane; c < d; c += kWave) {
+    const float xh = (x[c] - mean) * rstd;
+    y[c] = xh * gamma[c] + beta[c];
+    if (xhat_out) xhat_out[c] = xh;
+  }
+  if (rstd_out && lane == 0) *rstd_out = rstd;
+}
+
+// K4: item tower for n rows. Optional saves for the backward pass:
+// z [n, d+32], xhat [n, d], rstd [n].
+__global__ __launch_bounds__(kBlock) void tt_item_forward_kernel(TTDev P, const int32_t* __restrict__ item,
+                                                                  const int32_t* __restrict__ man,
+                                                                  const int32_t* __restrict__ cat,
+                                                                  const float* __restrict__ numeric, int64_t n,
+                                                                  float* __restrict__ out, float* __restrict__ z_save,
+                                                                  float* __restrict__ xhat_save,
+                                                                  float* __restrict__ rstd_save) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int d = P.d, dz = P.d + 32;
+  float* zs = smem;              // [kTR][dz]
+  float* ps = smem + kTR * dz;   // [kTR][d]
+  const int64_t r0 = (int64_t)blockIdx.x * kTR;
+  const int rows = (int)((n - r0) < kTR ? (n - r0) : kTR);
+  // gather the concat input
+  for (int o = threadIdx.x; o < kTR * dz; o += blockDim.x) {
+    const int r = o / dz, c = o % dz;
+    float v = 0.f;
+    if (r < rows) {
+      const int64_t g = r0 + r;
+      if (c < d) {
+        v = P.ie[(int64_t)item[g] * d + c];
+      } else if (c < d + 8) {
+        v = P.me[(int64_t)man[g] * 8 + (c - d)];
+      } else if (c < d + 16) {
+        v = P.ce[(int64_t)cat[g] * 8 + (c - d - 8)];
+      } else {
+        const int j = c - d - 16;
+        const float x0 = numeric[g * 2], x1 = numeric[g * 2 + 1];
+        const float h = x0 * P.w1[j] + x1 * P.w1[16 + j] + P.b1[j];
+        v = h > 0.f ? h : 0.f;
+      }
+    }
+    zs[o] = v;
+  }
+  __syncthreads();
+  // Dense(d): p = z @ W2 + b2 (W2 [dz][d] row-major, column reads coalesced)
+  for (int o = threadIdx.x; o < kTR * d; o += blockDim.x) {
+    const int r = o / d, j = o % d;
+    const float* zr = zs + r * dz;
+    float acc = 0.f;
+    for (int k = 0; k < dz; ++k) acc = fmaf(zr[k], P.w2[(int64_t)k * d + j], acc);
+    ps[o] = acc + P.b2[j];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r = w; r < rows; r += kBlock / 64) {
+    const int64_t g = r0 + r;
+    ln_row(ps + r * d, d, P.gi, P.bi, out + g * d, xhat_save ? xhat_save + g * d : nullptr,
+           rstd_save ? rstd_save + g : nullptr, lane);
+  }
+  if (z_save) {
+    for (int o = threadIdx.x; o < rows * dz; o += blockDim.x) z_save[r0 * dz + o] = zs[o];
+  }
+}
+
+// K5: user tower.
+__global__ __launch_bounds__(kBlock) void tt_user_forward_kernel(TTDev P, const int32_t* __restrict__ user,
+                                                                  int64_t n, float* __restrict__ out,
+                                                                  float* __restrict__ xhat_save,
+                                                                  float* __restrict__ rstd_save) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (g >= n) return;
+  const int d = P.d;
+  ln_row(P.ue + (int64_t)user[g] * d, d, P.gu, P.bu, out + g * d, xhat_save ? xhat_save + g * d : nullptr,
+         rstd_save ? rstd_save + g : nullptr, lane);
+}
+
+// Dot(axes=1): out[b*N + j] = <U[b], V[j]>, one thread per (b, j).
+__global__ __launch_bounds__(kBlock) void tt_score_kernel(const float* __restrict__ U, int B,
+                                                          const float* __restrict__ V, int64_t N, int d,
+                                                          float* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (j >= N || b >= B) return;
+  const float* u = U + (int64_t)b * d;
+  const float* v = V + j * d;
+  float acc = 0.f;
+  for (int c = 0; c < d; ++c) acc = fmaf(u[c], v[c], acc);
+  out[(int64_t)b * N + j] = acc;
+}
+
+// Paired dot: out[r] = <U[r], V[r]> (model.predict on per-row inputs).
+__global__ __launch_bounds__(kBlock) void tt_pair_score_kernel(const float* __restrict__ U,
+                                                               const float* __restrict__ V, int64_t n, int d,
+                                                               float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < d; c += kWave) s = fmaf(U[r * d + c], V[r * d + c], s);
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s;
+}
+
+// Backward of one training batch, kTR samples per workgroup. Inputs are the
+// forward saves; outputs: per-sample embedding-row grads and per-block
+// partial sums of the dense-parameter grads (reduced in fixed block order by
+// tt_reduce_partials -> deterministic).
+//
+// partial layout per block (floats): dW2[dz*d] | db2[d] | dgi[d] | dbi[d] |
+//                                    dgu[d] | dbu[d] | dW1[32] | db1[16] | sq_err[1] | abs_err[1]
+__global__ __launch_bounds__(kBlock) void tt_backward_kernel(
+    TTDev P, const float* __restrict__ y, int64_t B, const float* __restrict__ uvec,
+    const float* __restrict__ uxhat, const float* __restrict__ urstd, const float* __restrict__ ivec,
+    const float* __restrict__ ixhat, const float* __restrict__ irstd, const float* __restrict__ zsave,
+    const float* __restrict__ numeric, float* __restrict__ g_user, float* __restrict__ g_item,
+    float* __restrict__ g_man, float* __restrict__ g_cat, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int d = P.d, dz = P.d + 32;
+  const int64_t r0 = (int64_t)blockIdx.x * kTR;
+  const int rows = (int)((B - r0) < kTR ? (B - r0) : kTR);
+  float* dp = smem;                  // [kTR][d]  grad of the Dense(d) output
+  float* dpre = dp + kTR * d;        // [kTR][16] grad of the Dense(16) pre-activation
+  float* dyh = dpre + kTR * 16;      // [kTR]     dL/dscore
+  float* red = dyh + kTR;            // [8]: sq err, abs err per wave
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const size_t plen = (size_t)dz * d + 5 * (size_t)d + 48 + 2;
+  float* part = partial + (size_t)blockIdx.x * plen;
+
+  // score, MSE grad, LN backward (item -> dp, user -> g_user)
+  float loss_acc = 0.f, abs_acc = 0.f;
+  for (int r = w; r < kTR; r += kBlock / 64) {
+    if (r >= rows) {
+      for (int c = lane; c < d; c += kWave) dp[r * d + c] = 0.f;
+      if (lane == 0) dyh[r] = 0.f;
+      continue;
+    }
+    const int64_t g = r0 + r;
+    float s = 0.f;
+    for (int c = lane; c < d; c += kWave) s = fmaf(uvec[g * d + c], ivec[g * d + c], s);
+    const float yhat = wave_sum(s);
+    const float e = yhat - y[g];
+    const float dy = 2.0f * e / (float)B;
+    if (lane == 0) {
+      dyh[r] = dy;
+      loss_acc += e * e;
+      abs_acc += fabsf(e);
+    }
+    // item LN backward: dxh = dy*u*gamma ; dx = rstd*(dxh - mean(dxh) - xh*mean(dxh*xh))
+    float m1 = 0.f, m2 = 0.f;
+    for (int c = lane; c < d; c += kWave) {
+      const float dxh = dy * uvec[g * d + c] * P.gi[c];
+      m1 += dxh;
+      m2 += dxh * ixhat[g * d + c];
+    }
+    m1 = wave_sum(m1) / (float)d;
+    m2 = wave_sum(m2) / (float)d;
+    for (int c = lane; c < d; c += kWave) {
+      const float xh = ixhat[g * d + c];
+      const float dxh = dy * uvec[g * d + c] * P.gi[c];
+      dp[r * d + c] = irstd[g] * (dxh - m1 - xh * m2);
+    }
+    float u1 = 0.f, u2 = 0.f;
+    for (int c = lane; c < d; c += kWave) {
+      const float dxh = dy * ivec[g * d + c] * P.gu[c];
+      u1 += dxh;
+      u2 += dxh * uxhat[g * d + c];
+    }
+    u1 = wave_sum(u1) / (float)d;
+    u2 = wave_sum(u2) / (float)d;
+    for (int c = lane; c < d; c += kWave) {
+      const float xh = uxhat[g * d + c];
+      const float dxh = dy * ivec[g * d + c] * P.gu[c];
+      g_user[g * d + c] = urstd[g] * (dxh - u1 - xh * u2);
+    }
+  }
+  if (lane == 0) {
+    red[w] = loss_acc;
+    red[4 + w] = abs_acc;
+  }
+  __syncthreads();
+  // dz = dp @ W2^T -> item / manufacturer / category rows, and dh -> dpre
+  for (int o = threadIdx.x; o < kTR * dz; o += blockDim.x) {
+    const int r = o / dz, k = o % dz;
+    if (r >= rows) {
+      if (k >= d + 16) dpre[r * 16 + (k - d - 16)] = 0.f;
+      continue;
+    }
+    const int64_t g = r0 + r;
+    const float* dpr = dp + r * d;
+    const float* w2r = P.w2 + (int64_t)k * d;
+    float acc = 0.f;
+    for (int j = 0; j < d; ++j) acc = fmaf(dpr[j], w2r[j], acc);
+    if (k < d) {
+      g_item[g * d + k] = acc;
+    } else if (k < d + 8) {
+      g_man[g * 8 + (k - d)] = acc;
+    } else if (k < d + 16) {
+      g_cat[g * 8 + (k - d - 8)] = acc;
+    } else {
+      const int j = k - d - 16;
+      const float h = zsave[g * dz + k];
+      dpre[r * 16 + j] = h > 0.f ? acc : 0.f;  // relu'
+    }
+  }
+  __syncthreads();
+  // dense partials over this block's rows (fixed row order)
+  for (int o = threadIdx.x; o < dz * d; o += blockDim.x) {
+    const int k = o / d, j = o % d;
+    float acc = 0.f;
+    for (int r = 0; r < rows; ++r) acc = fmaf(zsave[(r0 + r) * dz + k], dp[r * d + j], acc);
+    part[o] = acc;
+  }
+  for (int j = threadIdx.x; j < d; j += blockDim.x) {
+    float db2 = 0.f, dgi = 0.f, dbi = 0.f, dgu = 0.f, dbu = 0.f;
+    for (int r = 0; r < rows; ++r) {
+      const int64_t g = r0 + r;
+      const float dy = dyh[r];
+      const float dvi = dy * uvec[g * d + j];  // d item_vec
+      const float dvu = dy * ivec[g * d + j];  // d user_vec
+      db2 += dp[r * d + j];
+      dgi = fmaf(dvi, ixhat[g * d + j], dgi);
+      dbi += dvi;
+      dgu = fmaf(dvu, uxhat[g * d + j], dgu);
+      dbu += dvu;
+    }
+    float* q = part + (size_t)dz * d;
+    q[j] = db2;
+    q[d + j] = dgi;
+    q[2 * d + j] = dbi;
+    q[3 * d + j] = dgu;
+    q[4 * d + j] = dbu;
+  }
+  if (threadIdx.x < 48) {
+    float* q = part + (size_t)dz * d + 5 * (size_t)d;
+    float acc = 0.f;
+    if (threadIdx.x < 32) {  // dW1[i][j] = sum_r x_i * dpre_j
+      const int i = threadIdx.x / 16, j = threadIdx.x % 16;
+      for (int r = 0; r < rows; ++r) acc = fmaf(numeric[(r0 + r) * 2 + i], dpre[r * 16 + j], acc);
+    } else {
+      const int j = threadIdx.x - 32;
+      for (int r = 0; r < rows; ++r) acc += dpre[r * 16 + j];
+    }
+    q[threadIdx.x] = acc;
+  }
+  if (threadIdx.x == 0) {
+    part[plen - 2] = red[0] + red[1] + red[2] + red[3];
+    part[plen - 1] = red[4] + red[5] + red[6] + red[7];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void tt_reduce_partials_kernel(const float* __restrict__ partial, int nblk,
+                                                                     size_t plen, float* __restrict__ out) {
+  const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= plen) return;
+  float acc = 0.f;
+  for (int b = 0; b < nblk; ++b) acc += partial[(size_t)b * plen + o];
+  out[o] = acc;
+}
+
+// ---------------------------------------------------------------- Adam
+// TF ResourceApplyAdam (dense): m += (g-m)*(1-b1); v += (g^2-v)*(1-b2);
+// var -= (m*alpha)/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t) (host f32).
+__global__ __launch_bounds__(kBlock) void adam_dense_kernel(float* __restrict__ var, float* __restrict__ m,
+                                                             float* __restrict__ v, const float* __restrict__ g,
+                                                             int64_t n, float alpha, float b1, float b2, float eps) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n) return;
+  const float gr = g[o];
+  float mo = m[o], vo = v[o];
+  mo += (gr - mo) * (1.0f - b1);
+  vo += (gr * gr - vo) * (1.0f - b2);
+  m[o] = mo;
+  v[o] = vo;
+  var[o] -= (mo * alpha) / (sqrtf(vo) + eps);
+}
+
+// IndexedSlices dedup (tf.unique order = first occurrence, segment sums in
+// sample order). One block; gsum row q is the summed grad of sample q when q
+// is the first occurrence of its index; mark[idx] = q.
+__global__ __launch_bounds__(1024) void sparse_dedup_kernel(const int32_t* __restrict__ idx, int B, int dim,
+                                                            const float* __restrict__ g, float* __restrict__ gsum,
+                                                            int32_t* __restrict__ mark) {
+  for (int s = threadIdx.x; s < B; s += blockDim.x) {
+    const int32_t key = idx[s];
+    bool first = true;
+    for (int t = 0; t < s; ++t)
+      if (idx[t] == key) {
+        first = false;
+        break;
+      }
+    if (!first) continue;
+    for (int c = 0; c < dim; ++c) {
+      float acc = 0.f;
+      bool any = false;
+      for (int t = s; t < B; ++t)
+        if (idx[t] == key) {
+          acc = any ? acc + g[(int64_t)t * dim + c] : g[(int64_t)t * dim + c];
+          any = true;
+        }
+      gsum[(int64_t)s * dim + c] = acc;
+    }
+    mark[key] = s;
+  }
+}
+
+// Keras OptimizerV2 Adam._resource_apply_sparse: whole-table decay of m and
+// v, scatter-add of the (deduplicated) slices, whole-table var update.
+__global__ __launch_bounds__(kBlock) void adam_sparse_table_kernel(float* __restrict__ var, float* __restrict__ m,
+                                                                    float* __restrict__ v, int64_t n_rows, int dim,
+                                                                    const int32_t* __restrict__ mark,
+                                                                    const float* __restrict__ gsum, float lr,
+                                                                    float b1, float omb1, float b2, float omb2,
+                                                                    float eps) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n_rows * dim) return;
+  const int64_t r = o / dim;
+  const int c = (int)(o - r * dim);
+  const int32_t q = mark[r];
+  float mo = m[o] * b1;
+  float vo = v[o] * b2;
+  if (q >= 0) {
+    const float gr = gsum[(int64_t)q * dim + c];
+    mo = mo + gr * omb1;
+    vo = vo + (gr * gr) * omb2;
+  }
+  m[o] = mo;
+  v[o] = vo;
+  var[o] = var[o] - (lr * mo) / (sqrtf(vo) + eps);
+}
+
+__global__ void sparse_unmark_kernel(const int32_t* __restrict__ idx, int B, int32_t* __restrict__ mark) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < B) mark[idx[s]] = -1;
+}
+
+static TTDev to_dev(const hrec_tt_params* p) {
+  TTDev t;
+  t.d = p->d;
+  t.ue = p->user_emb;
+  t.ie = p->item_emb;
+  t.me = p->man_emb;
+  t.ce = p->cat_emb;
+  t.w1 = p->w1;
+  t.b1 = p->b1;
+  t.w2 = p->w2;
+  t.b2 = p->b2;
+  t.gu = p->ln_user_gamma;
+  t.bu = p->ln_user_beta;
+  t.gi = p->ln_item_gamma;
+  t.bi = p->ln_item_beta;
+  return t;
+}
+
+static bool params_ok(const hrec_tt_params* p) {
+  return p && p->d >= 1 && p->d <= 1024 && p->user_emb && p->item_emb && p->man_emb && p->cat_emb && p->w1 &&
+         p->b1 && p->w2 && p->b2 && p->ln_user_gamma && p->ln_user_beta && p->ln_item_gamma && p->ln_item_beta;
+}
+
+}  // namespace hrec
+
+using namespace hrec;
+
+static size_t item_fwd_smem(int d) { return (size_t)kTR * (2 * d + 32) * sizeof(float); }
+
+extern "C" int hrec_tt_item_forward(const hrec_tt_params* params, const int32_t* item, const int32_t* manufacturer,
+                                    const int32_t* category, const float* numeric, int64_t n, float* item_vec,
+                                    void* stream) {
+  HREC_REQUIRE(params_ok(params), "tt_item_forward: bad parameter block");
+  HREC_REQUIRE(n >= 0, "tt_item_forward: negative n");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(item && manufacturer && category && numeric && item_vec, "tt_item_forward: null pointer");
+  const size_t sm = item_fwd_smem(params->d);
+  HREC_REQUIRE(sm <= 160 * 1024, "tt_item_forward: embedding_size too large for one LDS tile");
+  hipLaunchKernelGGL(tt_item_forward_kernel, dim3((unsigned)((n + kTR - 1) / kTR)), dim3(kBlock), sm,
+                     as_stream(stream), to_dev(params), item, manufacturer, category, numeric, n, item_vec,
+                     nullptr, nullptr, nullptr);
+  return check_launch("tt_item_forward_kernel");
+}
+
+extern "C" int hrec_tt_user_forward(const hrec_tt_params* params, const int32_t* user, int64_t n, float* user_vec,
+                                    void* stream) {
+  HREC_REQUIRE(params_ok(params), "tt_user_forward: bad parameter block");
+  HREC_REQUIRE(n >= 0, "tt_user_forward: negative n");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(user && user_vec, "tt_user_forward: null pointer");
+  hipLaunchKernelGGL(tt_user_forward_kernel, dim3((unsigned)((n + 3) / 4)), dim3(kBlock), 0, as_stream(stream),
+                     to_dev(params), user, n, user_vec, nullptr, nullptr);
+  return check_launch("tt_user_forward_kernel");
+}
+
+extern "C" int hrec_tt_score(const float* user_vec, int n_users, const float* item_vec, int64_t n_items, int d,
+                             float* out, void* stream) {
+  HREC_REQUIRE(n_users >= 0 && n_items >= 0 && d >= 1, "tt_score: bad shape");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(n_users < 65536, "tt_score: at most 65535 users per call");
+  HREC_REQUIRE(user_vec && item_vec && out, "tt_score: null pointer");
+  hipLaunchKernelGGL(tt_score_kernel, dim3((unsigned)((n_items + kBlock - 1) / kBlock), (unsigned)n_users),
+                     dim3(kBlock), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
+  return check_launch("tt_score_kernel");
+}
+
+static size_t partial_len(int d) { return (size_t)(d + 32) * d + 5 * (size_t)d + 48 + 2; }
+
+extern "C" size_t hrec_tt_train_workspace_bytes(int d, int64_t batch) {
+  const int64_t nblk = (batch + kTR - 1) / kTR;
+  const size_t f = (size_t)batch * (4 * (size_t)d + (d + 32) + 2) + (size_t)nblk * partial_len(d);
+  return f * sizeof(float) + 256;
+}
+
+extern "C" size_t hrec_tt_grad_len(int d) { return partial_len(d); }
+
+extern "C" int hrec_tt_forward_backward(const hrec_tt_params* params, const int32_t* user, const int32_t* item,
+                                        const int32_t* manufacturer, const int32_t* category, const float* numeric,
+                                        const float* y, int64_t batch, float* grad_dense, float* g_user,
+                                        float* g_item, float* g_man, float* g_cat, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+  HREC_REQUIRE(params_ok(params), "tt_forward_backward: bad parameter block");
+  HREC_REQUIRE(batch >= 1 && batch < (1ll << 31), "tt_forward_backward: bad batch");
+  HREC_REQUIRE(user && item && manufacturer && category && numeric && y && grad_dense && g_user && g_item && g_man &&
+                   g_cat && workspace,
+               "tt_forward_backward: null pointer");
+  const int d = params->d;
+  const size_t need = hrec_tt_train_workspace_bytes(d, batch);
+  HREC_REQUIRE(workspace_bytes >= need, "tt_forward_backward: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t s = as_stream(stream);
+  const TTDev P = to_dev(params);
+  float* w = (float*)workspace;
+  float* uvec = w;
+  float* uxh = uvec + batch * d;
+  float* ivec = uxh + batch * d;
+  float* ixh = ivec + batch * d;
+  float* zs = ixh + batch * d;
+  float* urs = zs + batch * (d + 32);
+  float* irs = urs + batch;
+  float* part = irs + batch;
+  const int nblk = (int)((batch + kTR - 1) / kTR);
+  hipLaunchKernelGGL(tt_user_forward_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(kBlock), 0, s, P, user, batch,
+                     uvec, uxh, urs);
+  int rc = check_launch("tt_user_forward_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(tt_item_forward_kernel, dim3((unsigned)nblk), dim3(kBlock), item_fwd_smem(d), s, P, item,
+                     manufacturer, category, numeric, batch, ivec, zs, ixh, irs);
+  rc = check_launch("tt_item_forward_kernel");
+  if (rc) return rc;
+  const size_t bsm = ((size_t)kTR * d + kTR * 16 + kTR + 8) * sizeof(float);
+  hipLaunchKernelGGL(tt_backward_kernel, dim3((unsigned)nblk), dim3(kBlock), bsm, s, P, y, batch, uvec, uxh, urs,
+                     ivec, ixh, irs, zs, numeric, g_user, g_item, g_man, g_cat, part);
+  rc = check_launch("tt_backward_kernel");
+  if (rc) return rc;
+  const size_t plen = partial_len(d);
+  hipLaunchKernelGGL(tt_reduce_partials_kernel, dim3((unsigned)((plen + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     part, nblk, plen, grad_dense);
+  return check_launch("tt_reduce_partials_kernel");
+}
+
+extern "C" int hrec_adam_dense(float* var, float* m, float* v, const float* grad, int64_t n, float alpha,
+                               float beta1, float beta2, float epsilon, void* stream) {
+  HREC_REQUIRE(n >= 0, "adam_dense: negative n");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(var && m && v && grad, "adam_dense: null pointer");
+  hipLaunchKernelGGL(adam_dense_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     as_stream(stream), var, m, v, grad, n, alpha, beta1, beta2, epsilon);
+  return check_launch("adam_dense_kernel");
+}
+
+extern "C" int hrec_adam_sparse(float* var, float* m, float* v, int64_t n_rows, int dim, const int32_t* indices,
+                                const float* grad_rows, int batch, int32_t* mark, float* gsum, float lr, float beta1,
+                                float one_minus_beta1, float beta2, float one_minus_beta2, float epsilon,
+                                void* stream) {
+  HREC_REQUIRE(n_rows >= 0 && dim >= 1 && batch >= 0, "adam_sparse: bad shape");
+  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(var && m && v && mark, "adam_sparse: null pointer");
+  HREC_REQUIRE(batch == 0 || (indices && grad_rows && gsum), "adam_sparse: null slices");
+  hipStream_t s = as_stream(stream);
+  if (batch > 0) {
+    hipLaunchKernelGGL(sparse_dedup_kernel, dim3(1), dim3(1024), 0, s, indices, batch, dim, grad_rows, gsum, mark);
+    int rc = check_launch("sparse_dedup_kernel");
+    if (rc) return rc;
+  }
+  const int64_t total = n_rows * dim;
+  hipLaunchKernelGGL(adam_sparse_table_kernel, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     var, m, v, n_rows, dim, mark, gsum, lr, beta1, one_minus_beta1, beta2, one_minus_beta2,
+                     epsilon);
+  int rc = check_launch("adam_sparse_table_kernel");
+  if (rc || batch == 0) return rc;
+  hipLaunchKernelGGL(sparse_unmark_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, indices, batch,
+                     mark);
+  return check_launch("sparse_unmark_kernel");
+}
+
+extern "C" int hrec_tt_pair_score(const float* user_vec, const float* item_vec, int64_t n, int d, float* out,
+                                  void* stream) {
+  HREC_REQUIRE(n >= 0 && d >= 1, "tt_pair_score: bad shape");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(user_vec && item_vec && out, "tt_pair_score: null pointer");
+  hipLaunchKernelGGL(tt_pair_score_kernel, dim3((unsigned)((n + 3) / 4)), dim3(kBlock), 0, as_stream(stream),
+                     user_vec, item_vec, n, d, out);
+  return check_launch("tt_pair_score_kernel");
+}

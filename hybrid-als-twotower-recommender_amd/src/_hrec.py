@@ -44,6 +44,31 @@ _SIGNATURES = {
                                 _vp]),
 }
 
+
+
+class TTParams(ctypes.Structure):
+    """hrec_tt_params (include/hrec.h)."""
+    _fields_ = [("d", ctypes.c_int32), ("reserved", ctypes.c_int32)] + [
+        (name, _vp) for name in ("user_emb", "item_emb", "man_emb", "cat_emb", "w1", "b1", "w2", "b2",
+                                 "ln_user_gamma", "ln_user_beta", "ln_item_gamma", "ln_item_beta")]
+
+
+_PP = ctypes.POINTER(TTParams)
+_SIGNATURES.update({
+    "hrec_tt_item_forward": (_c_i32, [_PP, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp]),
+    "hrec_tt_user_forward": (_c_i32, [_PP, _vp, _c_i64, _vp, _vp]),
+    "hrec_tt_score": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _vp, _vp]),
+    "hrec_tt_pair_score": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _vp, _vp]),
+    "hrec_tt_train_workspace_bytes": (_c_sz, [_c_i32, _c_i64]),
+    "hrec_tt_grad_len": (_c_sz, [_c_i32]),
+    "hrec_tt_forward_backward": (_c_i32, [_PP, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _c_sz, _vp]),
+    "hrec_adam_dense": (_c_i32, [_vp, _vp, _vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                 ctypes.c_float, _vp]),
+    "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
+                         [ctypes.c_float] * 6 + [_vp]),
+})
+
 ABI_VERSION = 1
 _LIB = None
 
@@ -220,3 +245,95 @@ def cosine_sim(feats, query_rows):
         _dev(feats, torch.float64, "feats"), n_items, dim, _dev(query_rows, torch.int64, "query_rows"),
         query_rows.numel(), _dev(out, torch.float64, "out"), _stream()))
     return out
+
+
+# -------------------------------------------------------------- two-tower
+def tt_params(d, tensors):
+    """Build the hrec_tt_params block from a dict of device f32 tensors (the
+    caller keeps the tensors alive)."""
+    p = TTParams()
+    p.d = int(d)
+    for name, _ in TTParams._fields_[2:]:
+        setattr(p, name, _dev(tensors[name], torch.float32, name).value)
+    return p
+
+
+def tt_item_forward(params, item, man, cat, numeric):
+    n = item.numel()
+    out = torch.empty((n, params.d), dtype=torch.float32, device=item.device)
+    _check("hrec_tt_item_forward", lib().hrec_tt_item_forward(
+        ctypes.byref(params), _dev(item, torch.int32, "item"), _dev(man, torch.int32, "manufacturer"),
+        _dev(cat, torch.int32, "category"), _dev(numeric, torch.float32, "numeric"), n,
+        _dev(out, torch.float32, "item_vec"), _stream()))
+    return out
+
+
+def tt_user_forward(params, user):
+    n = user.numel()
+    out = torch.empty((n, params.d), dtype=torch.float32, device=user.device)
+    _check("hrec_tt_user_forward", lib().hrec_tt_user_forward(
+        ctypes.byref(params), _dev(user, torch.int32, "user"), n, _dev(out, torch.float32, "user_vec"),
+        _stream()))
+    return out
+
+
+def tt_score(user_vec, item_vec):
+    B, d = user_vec.shape
+    N = item_vec.shape[0]
+    out = torch.empty((B, N), dtype=torch.float32, device=user_vec.device)
+    _check("hrec_tt_score", lib().hrec_tt_score(
+        _dev(user_vec, torch.float32, "user_vec"), B, _dev(item_vec, torch.float32, "item_vec"), N, d,
+        _dev(out, torch.float32, "out"), _stream()))
+    return out
+
+
+def tt_pair_score(user_vec, item_vec):
+    n, d = user_vec.shape
+    out = torch.empty(n, dtype=torch.float32, device=user_vec.device)
+    _check("hrec_tt_pair_score", lib().hrec_tt_pair_score(
+        _dev(user_vec, torch.float32, "user_vec"), _dev(item_vec, torch.float32, "item_vec"), n, d,
+        _dev(out, torch.float32, "out"), _stream()))
+    return out
+
+
+def tt_grad_len(d):
+    return int(lib().hrec_tt_grad_len(int(d)))
+
+
+def tt_forward_backward(params, user, item, man, cat, numeric, y, ws=None):
+    """Returns (grad_dense [grad_len], g_user, g_item, g_man, g_cat)."""
+    B = user.numel()
+    d = params.d
+    dev = user.device
+    need = int(lib().hrec_tt_train_workspace_bytes(d, B))
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    gd = torch.empty(tt_grad_len(d), dtype=torch.float32, device=dev)
+    gu = torch.empty((B, d), dtype=torch.float32, device=dev)
+    gi = torch.empty((B, d), dtype=torch.float32, device=dev)
+    gm = torch.empty((B, 8), dtype=torch.float32, device=dev)
+    gc = torch.empty((B, 8), dtype=torch.float32, device=dev)
+    _check("hrec_tt_forward_backward", lib().hrec_tt_forward_backward(
+        ctypes.byref(params), _dev(user, torch.int32, "user"), _dev(item, torch.int32, "item"),
+        _dev(man, torch.int32, "manufacturer"), _dev(cat, torch.int32, "category"),
+        _dev(numeric, torch.float32, "numeric"), _dev(y, torch.float32, "y"), B,
+        _dev(gd, torch.float32, "grad_dense"), _dev(gu, torch.float32, "g_user"),
+        _dev(gi, torch.float32, "g_item"), _dev(gm, torch.float32, "g_man"), _dev(gc, torch.float32, "g_cat"),
+        _dev(ws, torch.uint8, "workspace"), ws.numel(), _stream()))
+    return gd, gu, gi, gm, gc
+
+
+def adam_dense(var, m, v, grad, alpha, beta1, beta2, eps):
+    _check("hrec_adam_dense", lib().hrec_adam_dense(
+        _dev(var, torch.float32, "var"), _dev(m, torch.float32, "m"), _dev(v, torch.float32, "v"),
+        _dev(grad, torch.float32, "grad"), var.numel(), float(alpha), float(beta1), float(beta2), float(eps),
+        _stream()))
+
+
+def adam_sparse(var, m, v, indices, grad_rows, mark, gsum, lr, beta1, omb1, beta2, omb2, eps):
+    n_rows, dim = var.shape
+    _check("hrec_adam_sparse", lib().hrec_adam_sparse(
+        _dev(var, torch.float32, "var"), _dev(m, torch.float32, "m"), _dev(v, torch.float32, "v"), n_rows, dim,
+        _dev(indices, torch.int32, "indices"), _dev(grad_rows, torch.float32, "grad_rows"), indices.numel(),
+        _dev(mark, torch.int32, "mark"), _dev(gsum, torch.float32, "gsum"), float(lr), float(beta1),
+        float(omb1), float(beta2), float(omb2), float(eps), _stream()))

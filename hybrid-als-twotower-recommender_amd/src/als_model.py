@@ -1,0 +1,321 @@
+"""ALS collaborative filtering — drop-in for the reference's src/als_model.py.
+
+Same class, method names, arguments, return values and error sentinels as
+src/als_model.py:21-177; the Spark engine underneath (ALS.fit at :62,
+ALSModel.transform at :75) is replaced by libhrec's HIP kernels:
+
+  train            -> host CSR/CSC ingest + hrec_als_init_factors +
+                      max_iter x (item half-sweep, user half-sweep)  [K1]
+  predict_for_user -> hrec_als_score (JVM-exact f32 dot, NaN for unknown
+                      ids = coldStartStrategy "drop")                [K2]
+                      + cold-start fallback via hrec_cosine_sim +
+                      hrec_topk_f64 (_find_similar_items)            [K3]
+
+`initialize_spark` / `stop_spark` keep their names: they bind / release the
+HIP device session that plays the SparkSession's role.
+"""
+import json
+import os
+import pickle
+import warnings
+
+import numpy as np
+import torch
+
+from . import _hrec
+from .als_engine import DeviceALS, padded_k
+from .data_preprocessing import get_item_features
+from .synthetic import DeviceCSR
+
+warnings.filterwarnings("ignore")
+
+
+class DeviceSession:
+    """What SparkSession is to the reference: the engine handle (one HIP
+    device, its default stream)."""
+
+    def __init__(self, device=None):
+        _hrec.require_device()
+        _hrec.lib()
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+
+    def stop(self):
+        torch.cuda.synchronize(self.device)
+
+
+class DeviceALSFactors:
+    """The fitted model (Spark's ALSModel): ids + factor matrices on the device."""
+
+    def __init__(self, user_ids, item_ids, U, V, k):
+        self.user_ids = np.asarray(user_ids)   # sorted unique raw ids
+        self.item_ids = np.asarray(item_ids)
+        self.U = U                               # [n_users, kp] f32 device
+        self.V = V                               # [n_items, kp] f32 device
+        self.k = int(k)
+        self.Vt = _hrec.transpose(V) if V.shape[0] else V.t().contiguous()
+
+    @staticmethod
+    def _lookup(ids, keys):
+        keys = np.asarray(keys)
+        if len(ids) == 0:
+            return np.full(keys.shape, -1, dtype=np.int64)
+        pos = np.searchsorted(ids, keys)
+        pos = np.clip(pos, 0, len(ids) - 1)
+        ok = ids[pos] == keys
+        return np.where(ok, pos, -1).astype(np.int64)
+
+    def score(self, user_ids, item_list):
+        """f32 [len(user_ids), len(item_list)]; NaN where either id is unknown."""
+        dev = self.U.device
+        urows = torch.as_tensor(self._lookup(self.user_ids, user_ids), device=dev)
+        irows = torch.as_tensor(self._lookup(self.item_ids, item_list), device=dev)
+        return _hrec.als_score(self.U, urows, self.Vt, irows, irows.numel(), self.k)
+
+    def save(self, path):
+        os.makedirs(path, exist_ok=True)
+        np.save(os.path.join(path, "userIds.npy"), self.user_ids)
+        np.save(os.path.join(path, "itemIds.npy"), self.item_ids)
+        np.save(os.path.join(path, "userFactors.npy"), self.U[:, : self.k].cpu().numpy())
+        np.save(os.path.join(path, "itemFactors.npy"), self.V[:, : self.k].cpu().numpy())
+        with open(os.path.join(path, "metadata.json"), "w") as f:
+            json.dump({"class": "hrec.DeviceALSFactors", "rank": self.k}, f)
+
+    @classmethod
+    def load(cls, path, device):
+        with open(os.path.join(path, "metadata.json")) as f:
+            k = int(json.load(f)["rank"])
+        kp = padded_k(k)
+
+        def fac(name):
+            a = np.load(os.path.join(path, name))
+            t = torch.zeros((a.shape[0], kp), dtype=torch.float32, device=device)
+            t[:, :k] = torch.as_tensor(a, device=device)
+            return t
+
+        return cls(np.load(os.path.join(path, "userIds.npy")), np.load(os.path.join(path, "itemIds.npy")),
+                   fac("userFactors.npy"), fac("itemFactors.npy"), k)
+
+
+def _int_ids(col, name):
+    a = np.asarray(col)
+    if a.dtype.kind == "f":
+        if not np.all(np.isfinite(a)) or not np.all(a == np.floor(a)):
+            raise ValueError(f"{name} must hold integer ids (Spark casts them to Int)")
+        a = a.astype(np.int64)
+    if a.dtype.kind not in "iu":
+        raise ValueError(f"{name} must hold integer ids, got dtype {a.dtype}")
+    a = a.astype(np.int64)
+    if a.size and (a.min() < -(2 ** 31) or a.max() >= 2 ** 31):
+        raise ValueError(f"{name} ids must fit a 32-bit Int (Spark ALS)")
+    return a
+
+
+def build_csr(rows, cols, vals, n_rows, device):
+    """Host ingest of COO ratings into a device CSR (stable by input order;
+    duplicate (u, i) rows stay separate terms, as in Spark)."""
+    order = np.argsort(rows, kind="stable")
+    counts = np.bincount(rows, minlength=n_rows)
+    indptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    return DeviceCSR(torch.as_tensor(indptr, device=device),
+                     torch.as_tensor(cols[order].astype(np.int32), device=device),
+                     torch.as_tensor(vals[order].astype(np.float32), device=device), 0, n_rows,
+                     int(cols.max()) + 1 if cols.size else 0)
+
+
+class ALSModel:
+    """src/als_model.py:21 — same constructor signature (+ optional seed)."""
+
+    def __init__(self, rank=10, max_iter=10, reg_param=0.1, cold_start_strategy="drop", seed=None):
+        self.rank = rank
+        self.max_iter = max_iter
+        self.reg_param = reg_param
+        self.cold_start_strategy = cold_start_strategy
+        self.model = None
+        self.spark = None
+        self.global_mean = 3.0
+        self.item_features = None
+        self.seed = seed
+        self._feat_cache = None
+
+    # -------------------------------------------------------- engine handle
+    def initialize_spark(self):
+        try:
+            if self.spark is None:
+                self.spark = DeviceSession()
+            return True
+        except Exception as e:
+            print(f"Spark init error: {str(e)}")
+            return False
+
+    def stop_spark(self):
+        if self.spark:
+            self.spark.stop()
+
+    # ---------------------------------------------------------------- train
+    def _fit(self, data, U0=None):
+        if self.cold_start_strategy not in ("drop", "nan"):
+            raise ValueError(f"coldStartStrategy {self.cold_start_strategy!r} is not supported")
+        dev = self.spark.device
+        users = _int_ids(data["userId"], "userId")
+        items = _int_ids(data["itemId"], "itemId")
+        ratings = np.asarray(data["average_review_rating"], dtype=np.float32)
+        user_ids, urow = np.unique(users, return_inverse=True)
+        item_ids, irow = np.unique(items, return_inverse=True)
+        k = int(self.rank)
+        csr = build_csr(urow, irow, ratings, len(user_ids), dev)
+        csc = build_csr(irow, urow, ratings, len(item_ids), dev)
+        eng = DeviceALS(len(user_ids), len(item_ids), k, float(self.reg_param), csr, csc)
+        if U0 is not None:
+            eng.set_user_factors(U0)
+        else:
+            seed = (hash(type(self).__name__) if self.seed is None else int(self.seed)) & ((1 << 63) - 1)
+            eng.init_user_factors(seed)
+        eng.fit(int(self.max_iter))
+        return DeviceALSFactors(user_ids, item_ids, eng.U[: len(user_ids)].contiguous(),
+                                eng.V[: len(item_ids)].contiguous(), k)
+
+    def train(self, data, initial_user_factors=None):
+        """src/als_model.py:43-66. `initial_user_factors` (optional, [n_users, rank]
+        in sorted-userId order) injects Spark's random init for parity runs."""
+        try:
+            if not self.initialize_spark():
+                return False
+            self.item_features = get_item_features(data)
+            self._feat_cache = None
+            self.global_mean = data["average_review_rating"].mean()
+            self.model = self._fit(data, initial_user_factors)
+            return True
+        except Exception as e:
+            print(f"Training error: {str(e)}")
+            return False
+
+    # --------------------------------------------------------------- predict
+    def predict_for_user(self, user_id, all_items):
+        try:
+            items = list(all_items)
+            # Spark's createDataFrame(pairs, IntegerType schema) at :71-75 rejects
+            # non-integer ids (e.g. the column names of a DataFrame).
+            for x in [user_id] + items:
+                if isinstance(x, (bool, np.bool_)) or not isinstance(x, (int, np.integer)):
+                    raise TypeError(f"field itemId: IntegerType() can not accept object {x!r} in type {type(x)}")
+            scores = self.model.score([user_id], items)[0].cpu().numpy() if items else np.zeros(0, np.float32)
+            missing = [n for n in range(len(items)) if np.isnan(scores[n])]
+            sims = self._similar_batch([items[n] for n in missing]) if missing else []
+            fallback = {}
+            for n, sim in zip(missing, sims):
+                fallback[n] = (np.mean([self.item_features[s]["rating"] for s in sim]) if sim
+                               else self.global_mean)
+            return [(item, float(scores[n])) if n not in fallback else (item, fallback[n])
+                    for n, item in enumerate(items)]
+        except Exception as e:
+            print(f"Prediction error: {str(e)}")
+            return []
+
+    def _feature_matrix(self):
+        if self._feat_cache is None:
+            feats = self.item_features or {}
+            ids = list(feats.keys())
+            if ids:
+                mat = np.stack([np.asarray(feats[i]["features"], dtype=np.float64).ravel() for i in ids])
+                dev_mat = torch.as_tensor(mat, device=self.spark.device if self.spark else "cuda")
+            else:
+                dev_mat = None
+            self._feat_cache = (ids, {i: n for n, i in enumerate(ids)}, dev_mat)
+        return self._feat_cache
+
+    def _similar_batch(self, query_items, k=3):
+        """_find_similar_items for many items at once on the device: cosine
+        similarities (hrec_cosine_sim) + stable top-k (dict order breaks
+        ties, like the reference's sorted()) + the sim > 0.5 filter."""
+        if self.item_features is None:
+            raise TypeError("'NoneType' object is not subscriptable")  # reference: None[item_id]
+        ids, pos, mat = self._feature_matrix()
+        res = [[] for _ in query_items]
+        q = [(n, pos[it]) for n, it in enumerate(query_items) if it in pos]
+        if not q or mat is None:
+            return res
+        dev = mat.device
+        for s in range(0, len(q), 4096):
+            chunk = q[s: s + 4096]
+            qrows = torch.as_tensor([r for _, r in chunk], dtype=torch.int64, device=dev)
+            sims = _hrec.cosine_sim(mat, qrows)
+            idx, val = _hrec.topk(sims, k)
+            idx, val = idx.cpu().numpy(), val.cpu().numpy()
+            for (n, _), ii, vv in zip(chunk, idx, val):
+                res[n] = [ids[j] for j, v in zip(ii, vv) if j >= 0 and v > 0.5]
+        return res
+
+    def _find_similar_items(self, item_id, k=3):
+        try:
+            self.item_features[item_id]
+            return self._similar_batch([item_id], k)[0]
+        except KeyError:
+            return []
+
+    # ----------------------------------------------------------- persistence
+    def save_model(self, model_path="models/als"):
+        try:
+            os.makedirs(os.path.dirname(model_path) or ".", exist_ok=True)
+            self.model.save(model_path)
+            metadata = {
+                "rank": self.rank,
+                "max_iter": self.max_iter,
+                "reg_param": self.reg_param,
+                "global_mean": self.global_mean,
+                "item_features": self.item_features,
+            }
+            with open(f"{model_path}_metadata.pkl", "wb") as f:
+                pickle.dump(metadata, f)
+            print(f"Model saved to {model_path}")
+        except Exception as e:
+            print(f"Saving error: {str(e)}")
+
+    def load_model(self, model_path="models/als"):
+        try:
+            if not self.initialize_spark():
+                raise RuntimeError("no device session")
+            self.model = DeviceALSFactors.load(model_path, self.spark.device)
+            with open(f"{model_path}_metadata.pkl", "rb") as f:
+                metadata = pickle.load(f)  # written by save_model above (own format)
+                self.rank = metadata["rank"]
+                self.max_iter = metadata["max_iter"]
+                self.reg_param = metadata["reg_param"]
+                self.global_mean = metadata["global_mean"]
+                self.item_features = metadata["item_features"]
+                self._feat_cache = None
+            return self
+        except Exception as e:
+            print(f"Loading error: {str(e)}")
+            return None
+
+
+def hyperparameter_tuning(train_data, val_data, param_grid):
+    """src/als_model.py:142-169 (driver loop over the device ALS)."""
+    best_params = None
+    best_f1 = 0.0
+    for params in param_grid:
+        model = ALSModel(**params)
+        if not model.train(train_data):
+            continue
+        f1_scores = []
+        for user_id in val_data["userId"].sample(50).unique():
+            sel = val_data[val_data["userId"] == user_id]
+            actual = dict(zip(sel["itemId"], sel["average_review_rating"]))
+            preds = model.predict_for_user(user_id, val_data["itemId"].unique())
+            f1_scores.append(compute_f1_score(actual, {item: score for item, score in preds}))
+        avg_f1 = np.mean(f1_scores)
+        if avg_f1 > best_f1:
+            best_f1 = avg_f1
+            best_params = params.copy()
+        model.stop_spark()
+    return best_params
+
+
+def compute_f1_score(actual, pred, k=10):
+    """src/als_model.py:171-177 (k = 0 raises ZeroDivisionError, as there)."""
+    actual_items = set(actual.keys())
+    pred_items = set(item for item, _ in sorted(pred.items(), key=lambda x: x[1], reverse=True)[:k])
+    tp = len(actual_items & pred_items)
+    precision = tp / k
+    recall = tp / len(actual_items) if actual_items else 0
+    return 2 * (precision * recall) / (precision + recall) if (precision + recall) > 0 else 0

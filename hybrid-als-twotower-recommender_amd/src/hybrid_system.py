@@ -1,0 +1,161 @@
+"""Hybrid ALS + two-tower fusion — drop-in for the reference's src/hybrid_system.py.
+
+Same class and methods as src/hybrid_system.py:20-120. adaptive_fusion and
+the top-k of get_hybrid_recommendations run on the device through
+hrec_fuse_topk (K9): sklearn MinMaxScaler arithmetic per model in its numpy
+dtype, the (0.8, 0.2) / (0.2, 0.8) weights chosen by the strict
+als_f1 > tt_f1 test, f64 fusion with numpy 1.21's scalar promotion (the
+pinned numpy, requirements.txt:5), and a stable descending top-k that keeps
+Python's sorted(..., reverse=True) tie order. The item order of the fused
+list is the iteration order of set(als).union(set(tt)) (:61), built on the
+host exactly as the reference builds it.
+"""
+import os
+import warnings
+
+import numpy as np
+import pandas as pd
+import torch
+from sklearn.preprocessing import MinMaxScaler
+
+from . import _hrec
+from .als_model import ALSModel
+from .evaluation import compute_f1_score
+from .two_tower_model import TwoTowerModel
+
+warnings.filterwarnings("ignore")
+
+_TOPK_MAX = 1024  # hrec_fuse_topk's top-k bound
+
+
+def _as_scores(values):
+    """np.array(list) as the reference builds it, then the dtype
+    MinMaxScaler computes in (ints/bools -> float64, float32 stays)."""
+    arr = np.array(values)
+    if arr.dtype == np.float32:
+        out = arr
+    else:
+        out = arr.astype(np.float64)
+    if out.size == 0:
+        raise ValueError("Found array with 0 sample(s) (shape=(0, 1)) while a minimum of 1 is required by "
+                         "MinMaxScaler.")
+    if np.isinf(out).any():
+        raise ValueError("Input X contains infinity or a value too large for dtype('float64').")
+    return out
+
+
+def fuse_device(als_scores, tt_scores, als_wins, top_k, device=None, want_fused=True):
+    """Fusion + stable top-k on the device. Returns (fused f64 [n] or None,
+    top indices, top scores) as numpy arrays."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    a = torch.as_tensor(als_scores, device=device)
+    t = torch.as_tensor(tt_scores, device=device)
+    n = a.numel()
+    kk = n if top_k is None else (max(n + top_k, 0) if top_k < 0 else min(top_k, n))
+    dev_k = kk if kk <= _TOPK_MAX else 0
+    idx, sc, fused = _hrec.fuse_topk(a, t, als_wins, dev_k, want_fused=want_fused or kk > _TOPK_MAX)
+    fused_np = fused.cpu().numpy() if fused is not None else None
+    if kk > _TOPK_MAX:  # beyond the device top-k bound: order the device-fused scores stably
+        order = np.argsort(-fused_np, kind="stable")[:kk]
+        return fused_np, order, fused_np[order]
+    return fused_np, idx.cpu().numpy(), sc.cpu().numpy()
+
+
+class HybridRecommendationSystem:
+    def __init__(self):
+        self.als_model = None
+        self.twotower_model = None
+        self.als_scaler = MinMaxScaler()
+        self.twotower_scaler = MinMaxScaler()
+        self.als_f1_score = 0.0
+        self.twotower_f1_score = 0.0
+        self.models_loaded = False
+
+    def load_models(self, als_model_path, twotower_model_path):
+        try:
+            print("=== Loading Pre-trained Models ===")
+            self.als_model = ALSModel().load_model(als_model_path)
+            self.twotower_model = TwoTowerModel.load_model(twotower_model_path)
+            self.models_loaded = True
+            print("\n=== Models loaded successfully ===")
+            return True
+        except Exception as e:
+            print(f"Error loading models: {str(e)}")
+            return False
+
+    def evaluate_individual_models(self, test_user_id, actual_ratings, all_items, k=10):
+        try:
+            als_preds = self.als_model.predict_for_user(test_user_id, all_items)
+            tt_preds = self.twotower_model.predict_for_user(test_user_id, all_items)
+            self.als_f1_score = compute_f1_score(actual_ratings, dict(als_preds))
+            self.twotower_f1_score = compute_f1_score(actual_ratings, dict(tt_preds))
+            print(f"Model F1 Scores - ALS: {self.als_f1_score:.4f}, "
+                  f"Two-Tower: {self.twotower_f1_score:.4f}")
+            return self.als_f1_score, self.twotower_f1_score
+        except Exception as e:
+            print(f"Error evaluating models: {str(e)}")
+            return 0.0, 0.0
+
+    def _union(self, als_predictions, twotower_predictions):
+        als_dict = dict(als_predictions)
+        tt_dict = dict(twotower_predictions)
+        items = list(set(als_dict.keys()).union(set(tt_dict.keys())))
+        als_scores = _as_scores([als_dict.get(item, 0) for item in items])
+        tt_scores = _as_scores([tt_dict.get(item, 0) for item in items])
+        return items, als_scores, tt_scores
+
+    def adaptive_fusion(self, als_predictions, twotower_predictions):
+        try:
+            items, als_scores, tt_scores = self._union(als_predictions, twotower_predictions)
+            fused, _, _ = fuse_device(als_scores, tt_scores, self.als_f1_score > self.twotower_f1_score, 0)
+            return [(item, fused[i]) for i, item in enumerate(items)]
+        except Exception as e:
+            print(f"Error in adaptive fusion: {str(e)}")
+            return []
+
+    def save_predictions(self, user_id, predictions, save_dir="results/predictions"):
+        os.makedirs(save_dir, exist_ok=True)
+        file_path = os.path.join(save_dir, f"user_{user_id}_predictions.csv")
+        df = pd.DataFrame(predictions, columns=["itemId", "hybrid_score"])
+        df["userId"] = user_id
+        df["prediction_rank"] = range(1, len(df) + 1)
+        df["timestamp"] = pd.Timestamp.now()
+        df.to_csv(file_path, index=False)
+        print(f"Predictions saved to {file_path}")
+        return file_path
+
+    def load_predictions(self, user_id, save_dir="results/predictions"):
+        file_path = os.path.join(save_dir, f"user_{user_id}_predictions.csv")
+        if not os.path.exists(file_path):
+            raise FileNotFoundError(f"No predictions found for user {user_id}")
+        df = pd.read_csv(file_path)
+        return list(zip(df["itemId"], df["hybrid_score"]))
+
+    def get_hybrid_recommendations(self, user_id, all_items, actual_ratings=None, top_k=5,
+                                   save_predictions=False):
+        if not self.models_loaded:
+            raise ValueError("Models not loaded. Call load_models() first.")
+        try:
+            als_preds = self.als_model.predict_for_user(user_id, all_items)
+            tt_preds = self.twotower_model.predict_for_user(user_id, all_items)
+            if actual_ratings:
+                self.evaluate_individual_models(user_id, actual_ratings, all_items)
+            try:
+                items, als_scores, tt_scores = self._union(als_preds, tt_preds)
+                fused, idx, sc = fuse_device(als_scores, tt_scores, self.als_f1_score > self.twotower_f1_score,
+                                             top_k, want_fused=save_predictions)
+            except Exception as e:  # adaptive_fusion's own guard (:73-75) -> []
+                print(f"Error in adaptive fusion: {str(e)}")
+                items, fused, idx, sc = [], None, [], []
+            top_recommendations = [(items[i], np.float64(s)) for i, s in zip(idx, sc)]
+            if save_predictions:
+                combined = [(item, fused[i]) for i, item in enumerate(items)] if fused is not None else []
+                self.save_predictions(user_id, combined)
+            return top_recommendations
+        except Exception as e:
+            print(f"Error generating recommendations: {str(e)}")
+            return []
+
+    def cleanup(self):
+        if self.als_model:
+            self.als_model.stop_spark()

@@ -144,6 +144,78 @@ int hrec_cosine_sim(const double* feats, int64_t n_items, int dim,
                     const int64_t* query_rows, int64_t n_query, double* out,
                     void* stream);
 
+/* ------------------------------------------------------------ two-tower --
+ * Keras graph of src/two_tower_model.py:38-89 (embedding_size d):
+ *   user_vec = LN_u(E_user[u]);  h = relu(numeric @ W1 + b1)  [Dense(16)]
+ *   z = [E_item[i] | E_man[m] (8) | E_cat[c] (8) | h (16)]    (d+32)
+ *   item_vec = LN_i(z @ W2 + b2) [Dense(d)];  score = <user_vec, item_vec>
+ * LayerNormalization: epsilon 1e-3, biased variance, y = xhat*gamma + beta.
+ * All tensors f32 row-major on the device; ids int32 (< 2^24, see D11). */
+typedef struct hrec_tt_params {
+  int32_t d;
+  int32_t reserved;
+  float* user_emb;      /* [n_users, d]    */
+  float* item_emb;      /* [n_items, d]    */
+  float* man_emb;       /* [n_man, 8]      */
+  float* cat_emb;       /* [n_cat, 8]      */
+  float* w1;            /* [2, 16]         */
+  float* b1;            /* [16]            */
+  float* w2;            /* [d + 32, d]     */
+  float* b2;            /* [d]             */
+  float* ln_user_gamma; /* [d] */
+  float* ln_user_beta;  /* [d] */
+  float* ln_item_gamma; /* [d] */
+  float* ln_item_beta;  /* [d] */
+} hrec_tt_params;
+
+/* Item tower over n candidate rows (the per-candidate graph evaluated by
+ * model.predict at src/two_tower_model.py:145). */
+int hrec_tt_item_forward(const hrec_tt_params* params, const int32_t* item,
+                         const int32_t* manufacturer, const int32_t* category,
+                         const float* numeric /* [n,2] */, int64_t n,
+                         float* item_vec /* [n,d] */, void* stream);
+/* User tower for n users. */
+int hrec_tt_user_forward(const hrec_tt_params* params, const int32_t* user, int64_t n,
+                         float* user_vec /* [n,d] */, void* stream);
+/* Dot(axes=1) of every user row with every item row: out[b*n_items + j]. */
+int hrec_tt_score(const float* user_vec, int n_users, const float* item_vec,
+                  int64_t n_items, int d, float* out, void* stream);
+
+/* Row-wise dot: out[r] = <user_vec[r], item_vec[r]> (n rows of d). */
+int hrec_tt_pair_score(const float* user_vec, const float* item_vec, int64_t n, int d,
+                       float* out, void* stream);
+
+/* One minibatch of model.fit (src/two_tower_model.py:111): forward, MSE
+ * loss, backward. grad_dense receives hrec_tt_grad_len(d) floats:
+ * dW2[(d+32)*d] | db2[d] | dgamma_i[d] | dbeta_i[d] | dgamma_u[d] | dbeta_u[d]
+ * | dW1[32] | db1[16] | sum_sq_err[1] | sum_abs_err[1]  (loss = sum_sq_err/batch).
+ * g_user/g_item [batch,d], g_man/g_cat [batch,8]: per-sample embedding-row
+ * gradients (IndexedSlices values, duplicates not yet summed). */
+size_t hrec_tt_train_workspace_bytes(int d, int64_t batch);
+size_t hrec_tt_grad_len(int d);
+int hrec_tt_forward_backward(const hrec_tt_params* params, const int32_t* user,
+                             const int32_t* item, const int32_t* manufacturer,
+                             const int32_t* category, const float* numeric,
+                             const float* y, int64_t batch, float* grad_dense,
+                             float* g_user, float* g_item, float* g_man, float* g_cat,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
+/* TF 2.8 ResourceApplyAdam (dense variables): m += (g-m)(1-b1);
+ * v += (g^2-v)(1-b2); var -= m*alpha/(sqrt(v)+eps). alpha (host, f32) =
+ * lr*sqrt(1-b2^t)/(1-b1^t). */
+int hrec_adam_dense(float* var, float* m, float* v, const float* grad, int64_t n,
+                    float alpha, float beta1, float beta2, float epsilon, void* stream);
+/* Keras OptimizerV2 Adam._resource_apply_sparse on an embedding table:
+ * duplicate indices summed in sample order (tf.unique + segment sum), then
+ * m = m*b1 (whole table), m[idx] += g*(1-b1); v likewise with g^2; var -=
+ * lr*m/(sqrt(v)+eps) over the WHOLE table. mark: int32[n_rows] all -1 on
+ * entry (restored on exit); gsum: [batch, dim] scratch. */
+int hrec_adam_sparse(float* var, float* m, float* v, int64_t n_rows, int dim,
+                     const int32_t* indices, const float* grad_rows, int batch,
+                     int32_t* mark, float* gsum, float lr, float beta1,
+                     float one_minus_beta1, float beta2, float one_minus_beta2,
+                     float epsilon, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

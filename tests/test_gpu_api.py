@@ -1,0 +1,358 @@
+"""GPU: the drop-in API (src.als_model / src.two_tower_model / src.hybrid_system)
+through the C-ABI, against the oracle and the reference's golden vectors.
+
+Tolerances: ALS factors rtol 1e-4 after max_iter epochs (f64 Gramian, other
+summation order); ALS scores and fusion bit-exact; two-tower forward rtol
+1e-5 and gradients / parameters after Adam steps rtol 1e-4 against a float64
+restatement of the Keras graph (GPU computes in f32, as Keras does).
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+from conftest import dec_pairs, load_golden
+
+from oracle import als as oals
+from oracle import build as obuild
+from oracle import fusion as ofus
+from oracle import two_tower as ott
+
+pytestmark = pytest.mark.gpu
+
+
+# --------------------------------------------------------------------- ALS
+def _ratings_frame(rng, n_users=60, n_items=45, n=900):
+    users = rng.integers(0, n_users, n) * 7 + 3      # sparse raw ids
+    items = rng.integers(0, n_items, n) * 5 + 11
+    return pd.DataFrame({
+        "userId": users, "itemId": items,
+        "average_review_rating": rng.integers(0, 19, n),
+        "price": np.round(rng.uniform(1, 300, n), 2),
+        "manufacturer_id": rng.integers(0, 9, n), "category_id": rng.integers(0, 5, n),
+    })
+
+
+def _frame_csr(df):
+    u_ids, urow = np.unique(df["userId"].to_numpy(), return_inverse=True)
+    i_ids, irow = np.unique(df["itemId"].to_numpy(), return_inverse=True)
+    r = df["average_review_rating"].to_numpy().astype(np.float32)
+
+    def csr(rows, cols, n):
+        order = np.argsort(rows, kind="stable")
+        ip = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=n))]).astype(np.int64)
+        return ip, cols[order].astype(np.int32), r[order]
+
+    return u_ids, i_ids, csr(urow, irow, len(u_ids)), csr(irow, urow, len(i_ids))
+
+
+def test_als_train_matches_oracle(device):
+    from src.als_model import ALSModel
+
+    rng = np.random.default_rng(0)
+    df = _ratings_frame(rng)
+    u_ids, i_ids, ucsr, icsc = _frame_csr(df)
+    k = 10
+    U0 = rng.normal(size=(len(u_ids), k)).astype(np.float32)
+    U0 /= np.linalg.norm(U0, axis=1, keepdims=True)
+    m = ALSModel(rank=k, max_iter=10, reg_param=0.1)
+    assert m.train(df, initial_user_factors=U0) is True
+    U, V = oals.fit(ucsr, icsc, U0, k, 0.1, 10, sweep=obuild.half_sweep)
+    np.testing.assert_allclose(m.model.U[:, :k].cpu().numpy(), U, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(m.model.V[:, :k].cpu().numpy(), V, rtol=1e-4, atol=1e-5)
+    assert m.global_mean == df["average_review_rating"].mean()
+
+    # predict_for_user: known items bit-exact (JVM f32 dot), unknown -> fallback
+    uid = int(u_ids[3])
+    query = list(i_ids[:20]) + [999999, int(i_ids[5])]
+    got = m.predict_for_user(uid, query)
+    Ug = m.model.U[:, :k].cpu().numpy()
+    Vg = m.model.V[:, :k].cpu().numpy()
+    row = oals.score_matrix(Ug[3:4], Vg)[0]
+    spark = {int(i): float(row[n]) for n, i in enumerate(i_ids)}
+    exp = ofus.als_predict_with_fallback(spark, m.item_features, m.global_mean, query)
+    assert [i for i, _ in got] == [i for i, _ in exp]
+    for (_, a), (_, b) in zip(got, exp):
+        assert float(a) == float(b)
+
+    # unknown user -> every item through the fallback
+    got = m.predict_for_user(-5, query[:6])
+    exp = ofus.als_predict_with_fallback({}, m.item_features, m.global_mean, query[:6])
+    assert [float(s) for _, s in got] == [float(s) for _, s in exp]
+
+
+def test_als_train_error_sentinel(device, capsys):
+    from src.als_model import ALSModel
+
+    m = ALSModel(rank=8)
+    assert m.train(pd.DataFrame({"userId": [0.5], "itemId": [1], "average_review_rating": [3]})) is False
+    assert "Training error" in capsys.readouterr().out
+    assert m.predict_for_user(1, [1, 2]) == []  # no model -> reference sentinel
+
+
+def _rank1_model(device, item_scores, item_features, global_mean):
+    """A fitted model whose JVM-order dot reproduces given predictions (k=1,
+    U = [1.0]: 0 + 1*v is exact)."""
+    from src.als_model import ALSModel, DeviceALSFactors
+
+    ids = np.array(sorted(item_scores), dtype=np.int64)
+    V = torch.zeros((len(ids), 16), dtype=torch.float32, device=device)
+    V[:, 0] = torch.as_tensor(np.array([item_scores[i] for i in ids], np.float32))
+    U = torch.zeros((1, 16), dtype=torch.float32, device=device)
+    U[0, 0] = 1.0
+    m = ALSModel(rank=1)
+    m.initialize_spark()
+    m.model = DeviceALSFactors(np.array([7]), ids, U, V, 1)
+    m.item_features = item_features
+    m.global_mean = global_mean
+    return m
+
+
+def test_als_fallback_golden(device):
+    for case in load_golden("als_fallback.json")["cases"]:
+        feats = {int(i): {"features": np.asarray(f, dtype=np.float64), "rating": r}
+                 for i, f, r in case["item_features"]}
+        known = {int(i): p for i, p in case["spark_predictions"] if p is not None}
+        m = _rank1_model(device, known, feats, case["global_mean"])
+        got = m.predict_for_user(7, case["query"])
+        exp = dec_pairs(case["result"])
+        assert [i for i, _ in got] == [i for i, _ in exp]
+        for (_, a), (_, b) in zip(got, exp):
+            assert float(a) == float(b) and type(a) is type(b)
+
+
+def test_similar_items_golden(device):
+    from src.als_model import ALSModel
+
+    for case in load_golden("similar_items.json")["cases"]:
+        m = ALSModel()
+        m.initialize_spark()
+        m.item_features = {int(i): {"features": np.asarray(f, dtype=np.float64), "rating": r}
+                           for i, f, r in case["item_features"]}
+        for q in case["queries"]:
+            assert m._find_similar_items(q) == case["similar"][str(q)]
+
+
+def test_als_save_load_roundtrip(device, tmp_path):
+    from src.als_model import ALSModel
+
+    rng = np.random.default_rng(1)
+    df = _ratings_frame(rng, 30, 20, 300)
+    m = ALSModel(rank=6, max_iter=3, seed=3)
+    assert m.train(df)
+    path = str(tmp_path / "models" / "als")
+    m.save_model(path)
+    m2 = ALSModel().load_model(path)
+    assert m2 is not None and m2.rank == 6 and m2.global_mean == m.global_mean
+    q = list(df["itemId"].unique()[:10])
+    assert m.predict_for_user(int(df["userId"].iloc[0]), q) == m2.predict_for_user(int(df["userId"].iloc[0]), q)
+    assert ALSModel().load_model(str(tmp_path / "missing")) is None
+
+
+# --------------------------------------------------------------- two-tower
+def _tt_params(rng, nu, ni, nm, nc, d):
+    p = ott_init = {
+        "user_emb": rng.uniform(-0.5, 0.5, (nu, d)), "item_emb": rng.uniform(-0.5, 0.5, (ni, d)),
+        "man_emb": rng.uniform(-0.5, 0.5, (nm, 8)), "cat_emb": rng.uniform(-0.5, 0.5, (nc, 8)),
+        "w1": rng.normal(size=(2, 16)), "b1": rng.normal(size=16) * 0.1,
+        "w2": rng.normal(size=(d + 32, d)) * 0.2, "b2": rng.normal(size=d) * 0.1,
+        "ln_user_gamma": 1 + 0.1 * rng.normal(size=d), "ln_user_beta": 0.1 * rng.normal(size=d),
+        "ln_item_gamma": 1 + 0.1 * rng.normal(size=d), "ln_item_beta": 0.1 * rng.normal(size=d),
+    }
+    return {k: np.asarray(v, np.float32) for k, v in ott_init.items()}
+
+
+def _tt_batch(rng, B, nu, ni, nm, nc):
+    return (rng.integers(0, nu, B).astype(np.int32), rng.integers(0, ni, B).astype(np.int32),
+            rng.integers(0, nm, B).astype(np.int32), rng.integers(0, nc, B).astype(np.int32),
+            rng.uniform(0, 1, (B, 2)).astype(np.float32), rng.integers(0, 19, B).astype(np.float32))
+
+
+@pytest.mark.parametrize("d", [50, 64, 128])
+def test_tt_forward_backward_matches_oracle(device, d):
+    from src import _hrec
+    from src.tt_engine import DeviceTwoTower
+
+    rng = np.random.default_rng(d)
+    nu, ni, nm, nc, B = 40, 30, 7, 5, 77
+    p = _tt_params(rng, nu, ni, nm, nc, d)
+    eng = DeviceTwoTower(nu, ni, nm, nc, d, init=p)
+    u, i, m, c, x, y = _tt_batch(rng, B, nu, ni, nm, nc)
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    cache = ott.forward(p, u, i, m, c, x)
+    np.testing.assert_allclose(eng.user_vectors(T(u)).cpu().numpy(), cache["uvec"], rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(eng.item_vectors(T(i), T(m), T(c), T(x)).cpu().numpy(), cache["ivec"],
+                               rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(eng.predict_rows(T(u), T(i), T(m), T(c), T(x)).cpu().numpy(), cache["yhat"],
+                               rtol=1e-5, atol=1e-4)
+    gd, gu, gi, gm, gc = _hrec.tt_forward_backward(eng.params, T(u), T(i), T(m), T(c), T(x), T(y))
+    grads, rows, sq, ab = ott.backward(p, cache, y)
+    gd = gd.cpu().numpy()
+    for name, (off, shape) in eng.layout.items():
+        got = gd[off: off + int(np.prod(shape))].reshape(shape)
+        scale = np.abs(grads[name]).max() + 1e-12
+        np.testing.assert_allclose(got, grads[name], rtol=1e-4, atol=1e-4 * scale, err_msg=name)
+    for name, g in (("user_emb", gu), ("item_emb", gi), ("man_emb", gm), ("cat_emb", gc)):
+        scale = np.abs(rows[name]).max() + 1e-12
+        np.testing.assert_allclose(g.cpu().numpy(), rows[name], rtol=1e-4, atol=1e-4 * scale, err_msg=name)
+    np.testing.assert_allclose(gd[eng.n_dense:], [sq, ab], rtol=1e-5)
+
+
+def test_tt_adam_steps_match_oracle(device):
+    from src.tt_engine import TABLES, DeviceTwoTower
+
+    rng = np.random.default_rng(9)
+    nu, ni, nm, nc, d, B = 25, 20, 4, 3, 32, 64
+    p = _tt_params(rng, nu, ni, nm, nc, d)
+    eng = DeviceTwoTower(nu, ni, nm, nc, d, learning_rate=0.01, init=p)
+    pref = {k: v.copy() for k, v in p.items()}
+    slots = {k: (np.zeros_like(v), np.zeros_like(v)) for k, v in pref.items()}
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    for it in range(6):
+        u, i, m, c, x, y = _tt_batch(rng, B, nu, ni, nm, nc)  # many duplicate ids per batch
+        eng.train_step(T(u), T(i), T(m), T(c), T(x), T(y))
+        ott.train_step(pref, slots, u, i, m, c, x, y, it, lr=0.01)
+    for name in list(ott.DENSE) + list(TABLES):
+        np.testing.assert_allclose(eng.tensors[name].cpu().numpy(), pref[name], rtol=1e-4, atol=2e-6,
+                                   err_msg=name)
+
+
+def _tt_frame(rng, n, nu, ni, nm, nc):
+    return pd.DataFrame({
+        "userId": rng.integers(0, nu, n), "itemId": rng.integers(0, ni, n),
+        "manufacturer_id": rng.integers(0, nm, n), "category_id": rng.integers(0, nc, n),
+        "price": np.round(rng.uniform(1, 300, n), 2), "average_review_rating": rng.integers(0, 19, n),
+    })
+
+
+def test_twotower_api_train_predict_save_load(device, tmp_path):
+    from src.two_tower_model import TwoTowerModel
+
+    rng = np.random.default_rng(4)
+    train = _tt_frame(rng, 600, 50, 40, 6, 4)
+    val = _tt_frame(rng, 120, 50, 40, 6, 4)
+    tt = TwoTowerModel(50, 40, 6, 4, embedding_size=24)
+    hist = tt.train(train, val, batch_size=64, epochs=4)
+    assert tt.is_trained and len(hist.history["loss"]) >= 1 and "val_loss" in hist.history
+    assert hist.history["loss"][-1] < hist.history["loss"][0]
+    cand = train[["itemId", "manufacturer_id", "category_id", "price", "average_review_rating"]].head(17)
+    preds = tt.predict_for_user(5, cand)
+    assert [i for i, _ in preds] == list(cand["itemId"])
+    assert all(isinstance(s, np.float32) for _, s in preds)
+    p = {k: v for k, v in tt.model.state_dict().items() if not k.startswith("__")}
+    num = tt.scaler.transform(cand[["price", "average_review_rating"]]).astype(np.float32)
+    c = ott.forward(p, np.full(len(cand), 5), cand["itemId"].to_numpy(), cand["manufacturer_id"].to_numpy(),
+                    cand["category_id"].to_numpy(), num)
+    np.testing.assert_allclose([s for _, s in preds], c["yhat"], rtol=1e-5, atol=1e-4)
+    path = str(tmp_path / "models" / "twotower.keras")
+    tt.save_model(path)
+    tt2 = TwoTowerModel.load_model(path)
+    assert tt2.predict_for_user(5, cand) == preds
+
+
+def test_twotower_golden_input_assembly(device):
+    """predict_for_user feeds the tower exactly the inputs the reference
+    builds (pinned by tests/golden/tt_inputs.json)."""
+    from src.two_tower_model import TwoTowerModel
+
+    for case in load_golden("tt_inputs.json")["cases"]:
+        train = pd.DataFrame(case["train"])
+        cand = pd.DataFrame(case["candidates"])
+        tt = TwoTowerModel(50, 80, 9, 4, embedding_size=16)
+        tt.build_model()
+        feats = tt._prepare_features(train)
+        assert feats["numeric_in"].tolist() == case["prepare_numeric_in"]
+        seen = {}
+        orig = tt._device_inputs
+
+        def spy(f):
+            seen.update(f)
+            return orig(f)
+
+        tt._device_inputs = spy
+        out = tt.predict_for_user(31, cand)
+        for k, v in case["inputs"].items():
+            assert np.asarray(seen[k]).tolist() == v, k
+        assert [i for i, _ in out] == [i for i, _ in dec_pairs(case["result"])]
+
+
+# ------------------------------------------------------------------ hybrid
+class _Fixed:
+    def __init__(self, preds):
+        self.preds = preds
+
+    def predict_for_user(self, user_id, all_items):
+        return list(self.preds)
+
+
+@pytest.mark.parametrize("case", load_golden("fusion.json")["cases"], ids=lambda c: c["name"])
+def test_hybrid_api_golden(device, case):
+    from src.hybrid_system import HybridRecommendationSystem
+
+    als = dec_pairs(case["als"])
+    tt = dec_pairs(case["tt"])
+    h = HybridRecommendationSystem()
+    h.als_f1_score, h.twotower_f1_score = case["als_f1"], case["tt_f1"]
+    combined = h.adaptive_fusion(als, tt)
+    exp_c = dec_pairs(case["combined"])
+    legacy = ofus.adaptive_fusion(als, tt, case["als_f1"], case["tt_f1"], legacy=True)
+    assert [i for i, _ in combined] == [i for i, _ in exp_c]
+    # pinned-numpy semantics bit-exact; the golden (numpy 2 promotion when the
+    # TT scores are float32) within 1e-6 relative
+    assert [float(s) for _, s in combined] == [float(s) for _, s in legacy]
+    np.testing.assert_allclose([float(s) for _, s in combined], [float(s) for _, s in exp_c], rtol=1e-6,
+                               atol=1e-7)
+    h.models_loaded = True
+    h.als_model, h.twotower_model = _Fixed(als), _Fixed(tt)
+    top = h.get_hybrid_recommendations(0, [], top_k=case["top_k"])
+    assert top == [(i, s) for i, s in ofus.top_k(legacy, case["top_k"])]
+    exp_top = dec_pairs(case["top"])
+    if all(isinstance(s, float) or not isinstance(s, np.float32) for _, s in tt):
+        assert [i for i, _ in top] == [i for i, _ in exp_top]
+
+
+def test_hybrid_not_loaded_raises(device):
+    from src.hybrid_system import HybridRecommendationSystem
+
+    with pytest.raises(ValueError, match="Models not loaded"):
+        HybridRecommendationSystem().get_hybrid_recommendations(1, [1, 2])
+
+
+def test_hybrid_end_to_end(device, tmp_path):
+    from src.als_model import ALSModel
+    from src.hybrid_system import HybridRecommendationSystem
+    from src.two_tower_model import TwoTowerModel
+
+    rng = np.random.default_rng(12)
+    df = _tt_frame(rng, 800, 60, 35, 5, 4)
+    als = ALSModel(rank=8, max_iter=4, seed=1)
+    assert als.train(df)
+    tt = TwoTowerModel(60, 35, 5, 4, embedding_size=16)
+    tt.train(df, batch_size=128, epochs=2)
+    als.save_model(str(tmp_path / "als"))
+    tt.save_model(str(tmp_path / "tt.keras"))
+    h = HybridRecommendationSystem()
+    assert h.load_models(str(tmp_path / "als"), str(tmp_path / "tt.keras"))
+    items = df[["itemId", "manufacturer_id", "category_id", "price", "average_review_rating"]].drop_duplicates(
+        "itemId")
+    uid = int(df["userId"].iloc[0])
+    actual = {int(i): 1.0 for i in df[df["userId"] == uid]["itemId"]}
+    # the reference hands the same all_items object to both models (D9)
+    top = h.get_hybrid_recommendations(uid, items, actual_ratings=actual, top_k=5, save_predictions=True)
+    assert len(top) == 5
+    saved = h.load_predictions(uid)
+    assert len(saved) == len(items)
+    # iterating a DataFrame yields column names: the ALS side fails -> [] (as Spark's
+    # IntegerType schema does) and the fusion sees ALS = 0 everywhere
+    assert h.als_model.predict_for_user(uid, items) == []
+    # same ranking as the oracle fusion over the two models' own outputs
+    a = h.als_model.predict_for_user(uid, items)
+    t = h.twotower_model.predict_for_user(uid, items)
+    exp = ofus.top_k(ofus.adaptive_fusion(a, t, h.als_f1_score, h.twotower_f1_score, legacy=True), 5)
+    assert top == exp
+    # with an id list for ALS and the frame for the two-tower side
+    item_ids = [int(i) for i in items["itemId"]]
+    a = h.als_model.predict_for_user(uid, item_ids)
+    assert len(a) == len(item_ids)
+    fused = h.adaptive_fusion(a, t)
+    assert [float(s) for _, s in fused] == [float(s) for _, s in
+                                            ofus.adaptive_fusion(a, t, h.als_f1_score, h.twotower_f1_score)]

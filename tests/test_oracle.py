@@ -172,3 +172,47 @@ def test_als_score_matrix_matches_scalar_predict():
     users = np.repeat(np.arange(4), 9)
     items = np.tile(np.arange(9), 4)
     np.testing.assert_array_equal(m.reshape(-1), oals.predict(U, V, users, items))
+
+
+# -------------------------------------------------------------- two-tower
+def test_tt_oracle_gradcheck():
+    """The two-tower backward restatement against central finite differences."""
+    rng = np.random.default_rng(2)
+    d, B = 6, 5
+    p = {
+        "user_emb": rng.normal(size=(4, d)), "item_emb": rng.normal(size=(5, d)),
+        "man_emb": rng.normal(size=(3, 8)), "cat_emb": rng.normal(size=(2, 8)),
+        "w1": rng.normal(size=(2, 16)), "b1": rng.normal(size=16),
+        "w2": rng.normal(size=(d + 32, d)) * 0.3, "b2": rng.normal(size=d),
+        "ln_user_gamma": 1 + 0.2 * rng.normal(size=d), "ln_user_beta": rng.normal(size=d),
+        "ln_item_gamma": 1 + 0.2 * rng.normal(size=d), "ln_item_beta": rng.normal(size=d),
+    }
+    user = np.array([0, 1, 1, 3, 2])
+    item = np.array([4, 0, 4, 2, 1])
+    man = np.array([0, 2, 1, 1, 0])
+    cat = np.array([1, 0, 1, 1, 0])
+    x = rng.uniform(0, 1, (B, 2))
+    y = rng.integers(0, 19, B).astype(np.float64)
+
+    def loss(q):
+        c = ott.forward(q, user, item, man, cat, x)
+        return float(((c["yhat"] - y) ** 2).mean())
+
+    c = ott.forward(p, user, item, man, cat, x)
+    grads, rows, _, _ = ott.backward(p, c, y)
+    # scatter the per-sample rows into dense table grads
+    for name, idx in (("user_emb", user), ("item_emb", item), ("man_emb", man), ("cat_emb", cat)):
+        g = np.zeros_like(p[name])
+        np.add.at(g, idx, rows[name])
+        grads[name] = g
+    h = 1e-6
+    for name in p:
+        it = np.nditer(p[name], flags=["multi_index"])
+        for _ in it:
+            ix = it.multi_index
+            q1 = {k: v.copy() for k, v in p.items()}
+            q2 = {k: v.copy() for k, v in p.items()}
+            q1[name][ix] += h
+            q2[name][ix] -= h
+            fd = (loss(q1) - loss(q2)) / (2 * h)
+            assert abs(fd - grads[name][ix]) <= 1e-5 * max(1.0, abs(fd)), (name, ix, fd, grads[name][ix])
