@@ -40,7 +40,7 @@ class DeviceALS:
     replicated factor matrices."""
 
     def __init__(self, n_users, n_items, rank_k, reg_param, user_csr: DeviceCSR,
-                 item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0):
+                 item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0, sweep=None):
         self.n_users, self.n_items = int(n_users), int(n_items)
         self.k = int(rank_k)
         self.kp = padded_k(self.k)
@@ -48,6 +48,9 @@ class DeviceALS:
         self.user_csr, self.item_csc = user_csr, item_csc
         self.world, self.rank, self.group = int(world), int(rank), group
         self.accum_mode = int(accum_mode)
+        # the half-sweep launcher (K1); tests inject the CPU oracle here to
+        # exercise the sharding/all-gather logic on gloo without a GPU
+        self.sweep = sweep or _hrec.als_half_sweep
         dev = user_csr.indptr.device
         self.u_per = user_csr.n_rows
         self.i_per = item_csc.n_rows
@@ -80,13 +83,13 @@ class DeviceALS:
             dist.all_gather_into_tensor(full, local, group=self.group)
 
     def item_half_sweep(self):
-        _hrec.als_half_sweep(self.item_csc.indptr, self.item_csc.indices, self.item_csc.values,
-                             self.U, self.k, self.reg, self.V_local, self.accum_mode)
+        self.sweep(self.item_csc.indptr, self.item_csc.indices, self.item_csc.values,
+                   self.U, self.k, self.reg, self.V_local, self.accum_mode)
         self._gather(self.V, self.V_local)
 
     def user_half_sweep(self):
-        _hrec.als_half_sweep(self.user_csr.indptr, self.user_csr.indices, self.user_csr.values,
-                             self.V, self.k, self.reg, self.U_local, self.accum_mode)
+        self.sweep(self.user_csr.indptr, self.user_csr.indices, self.user_csr.values,
+                   self.V, self.k, self.reg, self.U_local, self.accum_mode)
         self._gather(self.U, self.U_local)
 
     def epoch(self):
