@@ -92,9 +92,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--score-users", type=int, default=1024)
-    ap.add_argument("--cpu-user-rows", type=int, default=12000)
-    ap.add_argument("--cpu-item-rows", type=int, default=1200)
+    ap.add_argument("--cpu-user-rows", type=int, default=600000)
+    ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--accum-mode", type=int, default=0, choices=[0, 1],
+                    help="0: f64 matrix-core Gramian; 1: f32 matrix cores, f64 across 16-rating chunks")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -115,7 +117,8 @@ def main():
     i0, i_per = shard_range(n_items, world, rank)
     csr = synthetic.generate(n_users, n_items, cfg["density"], False, u0, u_per)
     csc = synthetic.generate(n_users, n_items, cfg["density"], True, i0, i_per)
-    eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group)
+    eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group,
+                    accum_mode=args.accum_mode)
     eng.init_user_factors(synthetic.SEED_INIT)
     torch.cuda.synchronize()
 
@@ -137,11 +140,13 @@ def main():
     for _ in range(args.steps):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         e[0].record(stream)
-        _hrec.als_half_sweep(csc.indptr, csc.indices, csc.values, eng.U, k, eng.reg, eng.V_local)
+        _hrec.als_half_sweep(csc.indptr, csc.indices, csc.values, eng.U, k, eng.reg, eng.V_local,
+                             args.accum_mode)
         e[1].record(stream)
         eng._gather(eng.V, eng.V_local)
         e[2].record(stream)
-        _hrec.als_half_sweep(csr.indptr, csr.indices, csr.values, eng.V, k, eng.reg, eng.U_local)
+        _hrec.als_half_sweep(csr.indptr, csr.indices, csr.values, eng.V, k, eng.reg, eng.U_local,
+                             args.accum_mode)
         e[3].record(stream)
         eng._gather(eng.U, eng.U_local)
         ev.append(e)

@@ -13,11 +13,44 @@
 // component T of the lane's vector is exactly the MFMA operand of tile T
 // (A[i=l&15][k=l>>4], B[k=l>>4][j=l&15]) — no shuffles, fully coalesced
 // 256-B row reads. Tile pair (I,J), I<=J, accumulates G[NT*m+I][NT*m'+J].
+#include <type_traits>
+
 #include "common.h"
+
+// Occupancy target of the half-sweep (waves per SIMD; caps VGPRs at 168 for
+// 3) and the pipeline chunk (steps of 4 ratings) per accumulation mode.
+#ifndef HREC_ALS_WAVES
+#define HREC_ALS_WAVES 2
+#endif
+#ifndef HREC_ALS_CH0
+#define HREC_ALS_CH0 8
+#endif
+#ifndef HREC_ALS_ABLATE
+#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip the solve, 2 = skip the MFMA Gramian
+#endif
+#ifndef HREC_ALS_BCAST_LDS
+#define HREC_ALS_BCAST_LDS 1  // Cholesky column broadcast: 1 = LDS ds_read_b128, 0 = v_readlane
+#endif
+#ifndef HREC_ALS_FAST_RSQ
+#define HREC_ALS_FAST_RSQ 1  // pivot 1/sqrt by v_rsq_f64 + one Newton step (else sqrt + divide)
+#endif
+#ifndef HREC_ALS_SOLVE
+#define HREC_ALS_SOLVE 1  // 1 = blocked tile-layout Cholesky (MFMA trailing updates); 0 = row-per-lane
+#endif
+#ifndef HREC_ALS_PANEL_ROLLED
+#define HREC_ALS_PANEL_ROLLED 0  // 1 = one rolled copy of the panel code (smaller, spills at 2 waves)
+#endif
+#ifndef HREC_ALS_SOLVE_UNROLL
+#define HREC_ALS_SOLVE_UNROLL 8  // unroll of the two 64-step triangular-solve loops
+#endif
+#ifndef HREC_ALS_CH1
+#define HREC_ALS_CH1 4
+#endif
 
 namespace hrec {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 template <int NT>
 struct Vec;
@@ -45,6 +78,25 @@ struct Vec<1> {
 
 __device__ __forceinline__ int tri(int i) { return (i * (i + 1)) >> 1; }
 
+#ifdef HREC_ALS_STAMPS
+// Diagnostic build only: per-phase cycle sums (s_memtime) over all waves.
+__device__ unsigned long long g_als_stamps[8];
+#define STAMP(i)                                                                      \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                       \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if (threadIdx.x == 0 && (i) > 0) atomicAdd(&g_als_stamps[(i) > 0 ? (i) - 1 : 0], _t - _stamp_prev); \
+    _stamp_prev = _t;                                                                 \
+  } while (0)
+#define STAMP_DECL unsigned long long _stamp_prev = 0
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#define STAMP_DECL
+#endif
+
 // Wave-uniform broadcast of lane `src`'s double (two v_readlane_b32).
 __device__ __forceinline__ double bcast(double v, int src) {
   const long long x = __double_as_longlong(v);
@@ -61,7 +113,10 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // diagonal are never read, so lanes update them unmasked. The packed LDS
 // array is reused once to transpose L for the back substitution.
 template <int KP>
-__device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, double bi, int lane) {
+__device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, double* __restrict__ col, double bi,
+                                                      int lane) {
+  STAMP_DECL;
+  STAMP(0);
   const int i = lane < KP ? lane : KP - 1;
   double a[KP];
 #pragma unroll
@@ -69,17 +124,48 @@ __device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, do
     const int hi = i > c ? i : c, lo = i > c ? c : i;
     a[c] = A[tri(hi) + lo];
   }
+  STAMP(4);  // phase 4: row load from LDS
   double myrd = 0.0;  // lane j keeps 1 / L[j][j]
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    const double d = sqrt(bcast(a[j], j));
-    const double rd = 1.0 / d;
-    const double l = (lane == j) ? d : a[j] * rd;
+    // pivot: lane j's diagonal is current (column j was updated first, via a
+    // readlane, at step j-1 — the short critical path of the factorisation)
+    const double piv = bcast(a[j], j);
+#if HREC_ALS_FAST_RSQ
+    double rs = __builtin_amdgcn_rsq(piv);
+    rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
+    const double d = piv * rs;
+#else
+    const double d = sqrt(piv);
+    const double rs = 1.0 / d;
+#endif
+    const double l = (lane == j) ? d : a[j] * rs;
     a[j] = l;
-    myrd = (lane == j) ? rd : myrd;
+    myrd = (lane == j) ? rs : myrd;
+    if (j + 1 < KP) a[j + 1] = fma(-l, bcast(l, j + 1), a[j + 1]);
+#if HREC_ALS_BCAST_LDS
+    // remaining columns: column j of L to LDS once, then wave-uniform
+    // ds_read_b128 broadcasts (two entries per read), off the critical path.
+    if (j + 2 < KP) {
+      if (lane < KP) col[lane] = l;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int c = j + 1; c < KP; ++c) a[c] = fma(-l, bcast(l, c), a[c]);
+      for (int c0 = (j + 2) & ~1; c0 < KP; c0 += 2) {
+        const double2 lc = *reinterpret_cast<const double2*>(col + c0);
+        if (c0 > j + 1) a[c0] = fma(-l, lc.x, a[c0]);
+        a[c0 + 1] = fma(-l, lc.y, a[c0 + 1]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+#else
+#pragma unroll
+    for (int c = j + 2; c < KP; ++c) a[c] = fma(-l, bcast(l, c), a[c]);
+#endif
   }
+  STAMP(5);  // phase 5: factorisation
   // forward: L y = b
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
@@ -87,6 +173,7 @@ __device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, do
     const double upd = fma(-a[j], yj, bi);
     bi = (lane == j) ? yj : ((lane > j) ? upd : bi);
   }
+  STAMP(6);  // phase 6: forward substitution
   // transpose L through LDS: lane i stores row i, then reads column i.
   __syncthreads();
   if (lane < KP) {
@@ -104,19 +191,36 @@ __device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, do
     const double upd = fma(-a[j], xj, bi);
     bi = (lane == j) ? xj : ((lane < j) ? upd : bi);
   }
+  STAMP(7);  // phase 7: transpose + back substitution
   return bi;
 }
 
 // NT floats per lane (kp = 16*NT), CH steps of 4 nnz per pipeline chunk.
-template <int NT, int CH>
-__global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
+// MODE 0: v_mfma_f64_16x16x4_f64 accumulates the Gramian in f64 (Spark's
+//         f64 NormalEquation, any row length).
+// MODE 1: v_mfma_f32_16x16x4_f32 (2x the f64 matrix rate) accumulates each
+//         chunk of 4*CH ratings in f32 (an exact f32 fma chain), and the chunk
+//         partials are flushed into f64 accumulators — f64 summation across
+//         chunks, f32 rounding only inside a chunk.
+template <int NT, int CH, int MODE>
+__global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int k,
     double reg, float* __restrict__ dst) {
   constexpr int KP = 16 * NT;
   constexpr int NPAIR = NT * (NT + 1) / 2;
   constexpr int CHN = 4 * CH;  // nnz per chunk (<= 64)
+#if HREC_ALS_SOLVE == 1
+  __shared__ double Up[KP * (KP + 1) / 2];  // U, column-packed: U[tri(c) + q], q <= c
+  __shared__ double stage[MODE == 1 ? 256 : 1];
+#if HREC_ALS_PANEL_ROLLED
+  __shared__ __attribute__((aligned(16))) double colbuf[64];
+#endif
+  double* A = nullptr;
+#else
   __shared__ double A[KP * (KP + 1) / 2];
+  __shared__ __attribute__((aligned(16))) double colbuf[KP];
+#endif
   __shared__ double bsh[KP];
 
   const int lane = threadIdx.x;
@@ -132,9 +236,12 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
     return;
   }
 
+  STAMP_DECL;
+  STAMP(0);
   d4 acc[NPAIR];
 #pragma unroll
   for (int p = 0; p < NPAIR; ++p) acc[p] = d4{0.0, 0.0, 0.0, 0.0};
+  f4 fa[NPAIR];
   double bp[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) bp[t] = 0.0;
@@ -173,6 +280,10 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
     int i2;
     float r2;
     load_iv(base + 2 * CHN, i2, r2);
+    if (MODE == 1) {
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p) fa[p] = f4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       const double rv = (double)__shfl(r0, 4 * s + sub, kWave);
@@ -184,12 +295,24 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
       for (int I = 0; I < NT; ++I) {
 #pragma unroll
         for (int J = I; J < NT; ++J) {
-          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
+          if (HREC_ALS_ABLATE == 2) {
+            acc[p][0] += a[I] * a[J];  // ablation: no matrix cores
+          } else if (MODE == 0)
+            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
+          else
+            fa[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(buf[s].x[I], buf[s].x[J], fa[p], 0, 0, 0);
           ++p;
         }
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) bp[t] = fma(rv, a[t], bp[t]);
+    }
+    if (MODE == 1) {
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[p][rr] += (double)fa[p][rr];
+      }
     }
     if (more) {
 #pragma unroll
@@ -201,18 +324,245 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
     r1 = r2;
   }
 
+  STAMP(1);  // phase 1: Gramian (gather + MFMA)
   // b: sum the four row-groups of lanes.
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     bp[t] += __shfl_xor(bp[t], 16, kWave);
     bp[t] += __shfl_xor(bp[t], 32, kWave);
   }
+#if HREC_ALS_SOLVE == 1
+  // ---- blocked Cholesky in the matrix-core tile layout -------------------
+  // Work in the permuted basis q = 16*T + m  <->  physical column NT*m + T:
+  // tile (I,J) of the accumulators is then block (I,J) of the permuted
+  // Gramian (rows of block I, columns of block J, I <= J: the upper block
+  // triangle). A symmetric permutation does not change the solution; b and
+  // x are permuted on the way in and out. Factor A = U^T U block row by
+  // block row: a 16-pivot panel step with one LANE PER COLUMN (compact,
+  // fully in registers), then the trailing update of every later block
+  // U_KM -= U_JK^T U_JM on the f64 matrix cores, straight from the
+  // accumulator registers (the C/D layout of tile (J,K) is exactly the A/B
+  // operand layout of the 4 k-steps). U accumulates, column-packed, in LDS
+  // (U[tri(c) + q], q <= c) for the two triangular solves.
+  (void)A;
+  if (sub == 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bsh[16 * t + col] = bp[t];  // permuted b
+  }
+  if (MODE == 1) {
+    // f32 C/D map (row = 4*(lane>>4) + reg) -> f64 map (row = (lane>>4) + 4*reg)
+#pragma unroll
+    for (int p = 0; p < NPAIR; ++p) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) stage[(4 * sub + rr) * 16 + col] = acc[p][rr];
+      __syncthreads();
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[p][rr] = stage[(sub + 4 * rr) * 16 + col];
+      __syncthreads();
+    }
+  }
+  STAMP(2);  // phase 2: b + layout
+  // lambda = numExplicits * regParam on the diagonal (1.0 on padding columns)
+  const double lambda = (double)n * reg;
+  {
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        if (sub + 4 * rr == col) acc[p][rr] += (NT * col + I < k) ? lambda : 1.0;
+      }
+      p += NT - I;
+    }
+  }
+  double myrd = 0.0;  // lane c keeps 1 / U[c][c]
+#if HREC_ALS_PANEL_ROLLED
+  auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
+  // Block rows J = 0..NT-1 in a ROLLED loop (one copy of the panel code);
+  // only the tile-register moves are specialised per J.
+#pragma unroll 1
+  for (int J = 0; J < NT; ++J) {
+    // (a) block row J -> LDS (only q <= c: the upper triangle)
+    auto write_row = [&](auto JC) {
+      constexpr int JJ = decltype(JC)::value;
+#pragma unroll
+      for (int K = JJ; K < NT; ++K) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int q = 16 * JJ + sub + 4 * rr, c = 16 * K + col;
+          if (q <= c) Up[tri(c) + q] = acc[pidx(JJ, K)][rr];
+        }
+      }
+    };
+    switch (J) {
+      case 0: write_row(std::integral_constant<int, 0>{}); break;
+      case 1: if constexpr (NT > 1) write_row(std::integral_constant<int, 1>{}); break;
+      case 2: if constexpr (NT > 2) write_row(std::integral_constant<int, 2>{}); break;
+      default: if constexpr (NT > 3) write_row(std::integral_constant<int, 3>{}); break;
+    }
+    __syncthreads();
+    // (b) lane c >= 16J owns column c of block row J
+    const int c = lane;
+    const int j0 = 16 * J;
+    const bool own = c >= j0 && c < KP;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int q = j0 + m;
+      a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
+    }
+    // (c) 16 pivots, right-looking, columns on lanes; the pivot row is
+    //     broadcast through LDS (wave-uniform ds_read_b128 pairs)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int pv = j0 + i;
+      const double piv = bcast(a[i], pv);
+      double rs = __builtin_amdgcn_rsq(piv);
+      rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
+      const double d = piv * rs;
+      a[i] = (c == pv) ? d : a[i] * rs;
+      myrd = (c == pv) ? rs : myrd;
+      if (i < 15) {
+        if (c < KP) colbuf[c] = a[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
+          const double2 u = *reinterpret_cast<const double2*>(colbuf + j0 + m0);
+          if (m0 > i) a[m0] = fma(-u.x, a[i], a[m0]);
+          a[m0 + 1] = fma(-u.y, a[i], a[m0 + 1]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    // (d) U row block J -> LDS
+    if (own) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int q = j0 + m;
+        if (q <= c) Up[tri(c) + q] = a[m];
+      }
+    }
+    __syncthreads();
+    // (e) U_JK (K > J) back into tile registers; (f) trailing MFMA update
+    auto trail = [&](auto JC) {
+      constexpr int JJ = decltype(JC)::value;
+#pragma unroll
+      for (int K = JJ + 1; K < NT; ++K) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[pidx(JJ, K)][rr] = Up[tri(16 * K + col) + 16 * JJ + sub + 4 * rr];
+      }
+#pragma unroll
+      for (int K = JJ + 1; K < NT; ++K) {
+#pragma unroll
+        for (int M = K; M < NT; ++M) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(JJ, K)][rr], acc[pidx(JJ, M)][rr],
+                                                                    acc[pidx(K, M)], 0, 0, 0);
+        }
+      }
+    };
+    switch (J) {
+      case 0: trail(std::integral_constant<int, 0>{}); break;
+      case 1: if constexpr (NT > 1) trail(std::integral_constant<int, 1>{}); break;
+      case 2: if constexpr (NT > 2) trail(std::integral_constant<int, 2>{}); break;
+      default: if constexpr (NT > 3) trail(std::integral_constant<int, 3>{}); break;
+    }
+  }
+#else
+  auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
+#pragma unroll
+  for (int J = 0; J < NT; ++J) {
+    // (a) block row J -> LDS (only q <= c: the upper triangle)
+#pragma unroll
+    for (int K = J; K < NT; ++K) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int q = 16 * J + sub + 4 * rr, c = 16 * K + col;
+        if (q <= c) Up[tri(c) + q] = acc[pidx(J, K)][rr];
+      }
+    }
+    __syncthreads();
+    // (b) lane c >= 16J owns column c of block row J
+    const int c = lane;
+    const bool own = c >= 16 * J && c < KP;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int q = 16 * J + m;
+      a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
+    }
+    // (c) 16 pivots, right-looking, columns on lanes, v_readlane broadcasts
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int pv = 16 * J + i;
+      const double piv = bcast(a[i], pv);
+      double rs = __builtin_amdgcn_rsq(piv);
+      rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
+      const double d = piv * rs;
+      a[i] = (c == pv) ? d : a[i] * rs;
+      myrd = (c == pv) ? rs : myrd;
+#pragma unroll
+      for (int m = i + 1; m < 16; ++m) a[m] = fma(-bcast(a[i], 16 * J + m), a[i], a[m]);
+    }
+    // (d) U row block J -> LDS
+    if (own) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int q = 16 * J + m;
+        if (q <= c) Up[tri(c) + q] = a[m];
+      }
+    }
+    __syncthreads();
+    // (e) U_JK (K > J) back into tile registers; (f) trailing MFMA update
+#pragma unroll
+    for (int K = J + 1; K < NT; ++K) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[pidx(J, K)][rr] = Up[tri(16 * K + col) + 16 * J + sub + 4 * rr];
+    }
+#pragma unroll
+    for (int K = J + 1; K < NT; ++K) {
+#pragma unroll
+      for (int M = K; M < NT; ++M) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(J, K)][rr], acc[pidx(J, M)][rr],
+                                                                  acc[pidx(K, M)], 0, 0, 0);
+      }
+    }
+  }
+#endif
+  STAMP(3);  // phase 3: factorisation
+  // forward  U^T y = b   (lane c: y_c = (b_c - sum_{q<c} U[q][c] y_q) / U[c][c])
+  double bi = lane < KP ? bsh[lane] : 0.0;
+#pragma unroll HREC_ALS_SOLVE_UNROLL
+  for (int q = 0; q < KP; ++q) {
+    const double uqc = (lane > q && lane < KP) ? Up[tri(lane) + q] : 0.0;
+    bi = (lane == q) ? bi * myrd : bi;
+    const double yq = bcast(bi, q);
+    bi = (lane > q) ? fma(-uqc, yq, bi) : bi;
+  }
+  // back     U x = y     (lane c: x_c = (y_c - sum_{q>c} U[c][q] x_q) / U[c][c])
+#pragma unroll HREC_ALS_SOLVE_UNROLL
+  for (int q = KP - 1; q >= 0; --q) {
+    const double ucq = (lane < q) ? Up[tri(q) + lane] : 0.0;
+    bi = (lane == q) ? bi * myrd : bi;
+    const double xq = bcast(bi, q);
+    bi = (lane < q) ? fma(-ucq, xq, bi) : bi;
+  }
+  STAMP(4);  // phase 4: triangular solves
+  if (lane < KP) out[NT * (lane & 15) + (lane >> 4)] = (float)bi;
+}
+#else
   if (sub == 0) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) bsh[NT * col + t] = bp[t];
   }
-  // Gramian -> packed lower triangle. f64 16x16x4 C/D map:
-  // col = lane&15, row = (lane>>4) + 4*reg.
+  // Gramian -> packed lower triangle. C/D maps: f64 16x16x4 col = lane&15,
+  // row = (lane>>4) + 4*reg; f32 16x16x4 col = lane&15, row = 4*(lane>>4) + reg.
   {
     int p = 0;
 #pragma unroll
@@ -221,7 +571,7 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
       for (int J = I; J < NT; ++J) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int pr = NT * (sub + 4 * rr) + I;  // physical row
+          const int pr = NT * (MODE == 0 ? sub + 4 * rr : 4 * sub + rr) + I;  // physical row
           const int qc = NT * col + J;             // physical column
           const double v = acc[p][rr];
           if (I != J || pr >= qc) {
@@ -236,14 +586,16 @@ __global__ __launch_bounds__(64) void als_half_sweep_f64_kernel(
   }
   __syncthreads();
 
+  STAMP(2);  // phase 2: b reduce + Gramian -> LDS
   // Spark CholeskySolver: ata[diag] += numExplicits * regParam.
   const double lambda = (double)n * reg;
   if (lane < KP) A[tri(lane) + lane] += (lane < k) ? lambda : 1.0;
   const double b_in = lane < KP ? bsh[lane] : 0.0;
   __syncthreads();
-  const double x = solve_spd_rows_impl<KP>(A, b_in, lane);
+  const double x = HREC_ALS_ABLATE == 1 ? b_in + A[tri(lane < KP ? lane : 0)] : solve_spd_rows_impl<KP>(A, colbuf, b_in, lane);
   if (lane < KP) out[lane] = (float)x;
 }
+#endif
 
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int64_t rows,
                                                         int64_t cols, float* __restrict__ out) {
@@ -274,7 +626,7 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
   HREC_REQUIRE(k >= 1 && k <= kp, "als_half_sweep: need 1 <= k <= kp (k=%d kp=%d)", k, kp);
   HREC_REQUIRE(n_rows >= 0 && n_src >= 0, "als_half_sweep: negative size");
   HREC_REQUIRE(n_rows < 0x7fffffffll, "als_half_sweep: too many rows for one launch");
-  HREC_REQUIRE(accum_mode == 0, "als_half_sweep: accum_mode %d unsupported", accum_mode);
+  HREC_REQUIRE(accum_mode == 0 || accum_mode == 1, "als_half_sweep: accum_mode %d unsupported", accum_mode);
   HREC_REQUIRE(reg_param >= 0.0, "als_half_sweep: reg_param must be >= 0");
   if (n_rows == 0) return HREC_OK;
   HREC_REQUIRE(indptr && dst_factors, "als_half_sweep: null pointer");
@@ -282,20 +634,19 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
                "als_half_sweep: null source factors / CSR arrays");
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)n_rows), block(64);
-  switch (kp) {
-    case 64:
-      hipLaunchKernelGGL((als_half_sweep_f64_kernel<4, 8>), grid, block, 0, s, indptr, indices, values,
-                         n_rows, src_factors, k, reg_param, dst_factors);
-      break;
-    case 32:
-      hipLaunchKernelGGL((als_half_sweep_f64_kernel<2, 8>), grid, block, 0, s, indptr, indices, values,
-                         n_rows, src_factors, k, reg_param, dst_factors);
-      break;
-    default:
-      hipLaunchKernelGGL((als_half_sweep_f64_kernel<1, 8>), grid, block, 0, s, indptr, indices, values,
-                         n_rows, src_factors, k, reg_param, dst_factors);
-      break;
+#define HREC_SWEEP(NT, CH, M)                                                                      \
+  hipLaunchKernelGGL((als_half_sweep_f64_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
+                     n_rows, src_factors, k, reg_param, dst_factors)
+  if (accum_mode == 0) {
+    if (kp == 64) HREC_SWEEP(4, HREC_ALS_CH0, 0);
+    else if (kp == 32) HREC_SWEEP(2, 8, 0);
+    else HREC_SWEEP(1, 8, 0);
+  } else {
+    if (kp == 64) HREC_SWEEP(4, HREC_ALS_CH1, 1);
+    else if (kp == 32) HREC_SWEEP(2, 4, 1);
+    else HREC_SWEEP(1, 4, 1);
   }
+#undef HREC_SWEEP
   return check_launch("als_half_sweep_f64_kernel");
 }
 
@@ -307,3 +658,14 @@ extern "C" int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, f
   hipLaunchKernelGGL(transpose_kernel, grid, block, 0, as_stream(stream), in, rows, cols, out);
   return check_launch("transpose_kernel");
 }
+
+#ifdef HREC_ALS_STAMPS
+extern "C" int hrec_debug_als_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_als_stamps), sizeof(g_als_stamps)) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_als_stamps), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

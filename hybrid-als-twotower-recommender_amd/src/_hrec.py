@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libhrec.so")
+LIB_PATH = os.environ.get("HREC_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libhrec.so")
 
 _c_i32 = ctypes.c_int
 _c_i64 = ctypes.c_int64

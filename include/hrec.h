@@ -84,7 +84,11 @@ int hrec_als_init_factors(uint64_t seed, int64_t row_begin, int64_t n_rows,
  * v_j = src_factors[indices[j]], accumulated in f64 (accum_mode 0), solved
  * by Cholesky in f64, stored as f32 in dst_factors[r*kp .. +kp).
  * Rows with n_r == 0 get a zero vector (Spark has no factor for them).
- * accum_mode: 0 = f64 Gramian (Spark-exact semantics). */
+ * accum_mode: 0 = Gramian accumulated in f64 on the f64 matrix cores
+ *             (Spark's f64 NormalEquation);
+ *             1 = f32 matrix-core products summed in f32 within chunks of 16
+ *             ratings, chunks summed in f64 (2x the matrix rate; parity
+ *             checked at rtol 1e-4 in tests/test_gpu_core.py). */
 int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices,
                         const float* values, int64_t n_rows,
                         const float* src_factors, int64_t n_src, int k, int kp,
