@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_prof_summary.json"),
+                    help="rocprofv3 PMC summary (scripts/gpu_profile.sh) for roofline.traffic")
     ap.add_argument("--accum-mode", type=int, default=0, choices=[0, 1],
                     help="0: f64 matrix-core Gramian; 1: f32 matrix cores, f64 across 16-rating chunks")
     args = ap.parse_args()
@@ -188,6 +190,11 @@ def main():
         scoring = {"pairs_per_s": B * n_items / sc_s, "ms_per_batch": sc_s * 1e3, "users": B,
                    "items": n_items, "top_k": 5, "dtype": "f32 (JVM-exact, no FMA)"}
 
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.accum_mode == 0:
+        with open(args.traffic_json) as f:
+            traffic = json.load(f)["als_half_sweep"].get("hbm_bytes_avg_per_launch")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(eng, cfg, min(args.cpu_user_rows, n_users), min(args.cpu_item_rows, n_items))
@@ -221,7 +228,11 @@ def main():
                 "peak": F64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / F64_MFMA_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_note": ("HBM-side bytes per launch from rocprofv3 FETCH_SIZE(x2, gfx950) + WRITE_SIZE, "
+                                 "separate PMC passes of this command (scripts/gpu_profile.sh -> profiles/)"),
+                "algorithmic_flops_per_launch": flops / 2,
+                "avg_launch_ms": (item_ms + user_ms) / 2,
                 "kernel_ms_per_epoch": {"item": item_ms, "user": user_ms},
                 "gather_view": {"algorithmic_GBps": bytes_ / kern_s / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
                                 "frac": bytes_ / kern_s / 1e9 / HBM_PEAK_GBS},
