@@ -598,7 +598,7 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
 #endif
 
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int64_t rows,
-                                                        int64_t cols, float* __restrict__ out) {
+                                                        int64_t cols, float* __restrict__ out, int64_t ld_out) {
   __shared__ float tile[64][65];
   const int64_t r0 = (int64_t)blockIdx.x * 64;
   const int64_t c0 = (int64_t)blockIdx.y * 64;
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
   __syncthreads();
   for (int i = ty; i < 64; i += 4) {
     const int64_t c = c0 + i, r = r0 + tx;
-    if (r < rows && c < cols) out[c * rows + r] = tile[tx][i];
+    if (r < rows && c < cols) out[c * ld_out + r] = tile[tx][i];
   }
 }
 
@@ -650,12 +650,14 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
   return check_launch("als_half_sweep_f64_kernel");
 }
 
-extern "C" int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, float* out, void* stream) {
+extern "C" int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, float* out, int64_t ld_out,
+                                  void* stream) {
   HREC_REQUIRE(rows >= 0 && cols >= 0, "transpose: negative size");
+  HREC_REQUIRE(ld_out >= rows, "transpose: ld_out < rows");
   if (rows == 0 || cols == 0) return HREC_OK;
   HREC_REQUIRE(in && out, "transpose: null pointer");
   const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((cols + 63) / 64)), block(256);
-  hipLaunchKernelGGL(transpose_kernel, grid, block, 0, as_stream(stream), in, rows, cols, out);
+  hipLaunchKernelGGL(transpose_kernel, grid, block, 0, as_stream(stream), in, rows, cols, out, ld_out);
   return check_launch("transpose_kernel");
 }
 

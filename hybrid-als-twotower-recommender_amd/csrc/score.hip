@@ -54,6 +54,109 @@ __global__ __launch_bounds__(256) void als_score_kernel(const float* __restrict_
   }
 }
 
+
+// Fast path of K2 for whole item ranges (no item_rows gather): 4 items per
+// thread (two float2 loads of the transposed item matrix per rank step),
+// UB users per block kept TRANSPOSED in LDS (one ds_read_b128 feeds 4 users),
+// packed f32 multiply + add (v_pk_mul_f32 / v_pk_add_f32; contraction off so
+// every product and sum is rounded exactly like the JVM loop).
+// FILTER: instead of writing the scores, append (score, item) pairs with
+// score >= thr[b] to a per-user candidate list (wave-aggregated atomics).
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+template <int UB, bool FILTER>
+__global__ __launch_bounds__(256) void als_score_fast_kernel(
+    const float* __restrict__ U, const int64_t* __restrict__ user_rows, int n_users,
+    const float* __restrict__ Vt, int64_t ld, int64_t n_items, int k, int kp, float* __restrict__ out,
+    const float* __restrict__ thr, int thr_stride, int cap, float* __restrict__ cand_v,
+    int64_t* __restrict__ cand_i, int* __restrict__ cand_n) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) float us[64][UB];
+  __shared__ int uok[UB];
+  // grid: x = user group (fastest-varying), y = 1024-item slice, so the
+  // blocks of one item slice are dispatched back to back and share it in L2
+  const int b0 = blockIdx.x * UB;
+  for (int t = threadIdx.x; t < UB * 64; t += blockDim.x) {
+    const int b = t / 64, c = t % 64;
+    const int64_t ur = (b0 + b < n_users) ? user_rows[b0 + b] : -1;
+    us[c][b] = (ur >= 0 && c < kp) ? U[ur * kp + c] : 0.f;
+    if (c == 0) uok[b] = ur >= 0;
+  }
+  __syncthreads();
+  const int64_t j0 = (int64_t)blockIdx.y * 1024 + 2 * threadIdx.x;
+  const int64_t j1 = j0 + 512;
+  f2v acc0[UB], acc1[UB];
+#pragma unroll
+  for (int b = 0; b < UB; ++b) {
+    acc0[b] = f2v{0.f, 0.f};
+    acc1[b] = f2v{0.f, 0.f};
+  }
+  const bool in0 = j0 < ld, in1 = j1 < ld;
+  for (int c = 0; c < k; ++c) {
+    const float* vr = Vt + (int64_t)c * ld;
+    const f2v v0 = in0 ? *reinterpret_cast<const f2v*>(vr + j0) : f2v{0.f, 0.f};
+    const f2v v1 = in1 ? *reinterpret_cast<const f2v*>(vr + j1) : f2v{0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < UB; b += 4) {
+      const float4 u4 = *reinterpret_cast<const float4*>(&us[c][b]);
+      const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f2v us2 = f2v{uu[q], uu[q]};
+        const f2v p0 = us2 * v0;
+        const f2v p1 = us2 * v1;
+        acc0[b + q] = acc0[b + q] + p0;
+        acc1[b + q] = acc1[b + q] + p1;
+      }
+    }
+  }
+  if (!FILTER) {
+    const float qnan = __builtin_nanf("");
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      if (b0 + b >= n_users) break;
+      float* o = out + (int64_t)(b0 + b) * n_items;
+      const bool ok = uok[b];
+      if (j0 < n_items) o[j0] = ok ? acc0[b].x : qnan;
+      if (j0 + 1 < n_items) o[j0 + 1] = ok ? acc0[b].y : qnan;
+      if (j1 < n_items) o[j1] = ok ? acc1[b].x : qnan;
+      if (j1 + 1 < n_items) o[j1 + 1] = ok ? acc1[b].y : qnan;
+    }
+  } else {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      if (b0 + b >= n_users || !uok[b]) continue;  // block-uniform
+      const float t = thr[(int64_t)(b0 + b) * thr_stride];
+      const float sv[4] = {acc0[b].x, acc0[b].y, acc1[b].x, acc1[b].y};
+      const int64_t sj[4] = {j0, j0 + 1, j1, j1 + 1};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool pass = sj[e] < n_items && sv[e] >= t;
+        const uint64_t m = __ballot(pass);
+        if (m == 0) continue;
+        int base = 0;
+        const int leader = __builtin_ctzll(m);
+        if (lane == leader) base = atomicAdd(&cand_n[b0 + b], __popcll(m));
+        base = __shfl(base, leader, kWave);
+        if (pass) {
+          const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (pos < cap) {
+            cand_v[(int64_t)(b0 + b) * cap + pos] = sv[e];
+            cand_i[(int64_t)(b0 + b) * cap + pos] = sj[e];
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void cand_overflow_kernel(const int* __restrict__ cand_n, int n_users, int cap, int* __restrict__ flag) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < n_users; b += gridDim.x * blockDim.x)
+    if (cand_n[b] > cap) atomicOr(flag, 1);
+}
+
 // ----------------------------------------------------------------- top-k
 // Order: larger value first; equal values -> smaller index first (a stable
 // descending sort of the input order). NaN sorts last.
@@ -273,7 +376,7 @@ __global__ __launch_bounds__(256) void cosine_kernel(const double* __restrict__ 
 
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
-              T* out_val, void* ws, size_t ws_bytes, hipStream_t s);
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr);
 
 }  // namespace hrec
 
@@ -296,10 +399,10 @@ static size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
 namespace hrec {
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
-              T* out_val, void* ws, size_t ws_bytes, hipStream_t s) {
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx) {
   // Multi-pass: segments -> candidates (kk per segment) -> ... -> one segment.
   const T* cur_v = vals;
-  const int64_t* cur_i = nullptr;
+  const int64_t* cur_i = src_idx;
   int64_t m = n, stride = row_stride;
   char* w = (char*)ws;
   size_t used = 0;
@@ -425,4 +528,87 @@ extern "C" int hrec_cosine_sim(const double* feats, int64_t n_items, int dim, co
   const dim3 grid((unsigned)((n_items + 255) / 256), (unsigned)n_query);
   hipLaunchKernelGGL(cosine_kernel, grid, dim3(256), 0, as_stream(stream), feats, n_items, dim, query_rows, out);
   return check_launch("cosine_kernel");
+}
+
+static constexpr int kScoreUB = 16;
+static constexpr int kSample = 2048;
+static constexpr int kCap = 4096;
+
+extern "C" size_t hrec_als_score_topk_workspace_bytes(int n_users, int64_t n_items, int top_k) {
+  const size_t B = (size_t)n_users;
+  const int64_t S = n_items < kSample ? n_items : kSample;
+  size_t b = B * (size_t)S * 4 + 256;                          // sample scores
+  b += topk_ws_bytes(B, S, top_k, 4) + 256;                     // sample top-k workspace
+  b += B * (size_t)top_k * 12 + 256;                            // sample top-k values / indices
+  b += B * (size_t)kCap * 12 + 256;                             // candidates
+  b += B * 4 + 256 + 16;                                        // counters + flag
+  b += topk_ws_bytes(B, kCap, top_k, 4) + 256;                  // final top-k workspace
+  return b;
+}
+
+static char* carve(char*& p, size_t bytes) {
+  char* r = p;
+  p += (bytes + 255) & ~(size_t)255;
+  return r;
+}
+
+extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* user_rows, int n_users,
+                                   const float* item_factors_t, int64_t ld_items, int64_t n_items, int k, int kp,
+                                   int top_k, int64_t* out_idx, float* out_val, int* overflow, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  HREC_REQUIRE(kp == 16 || kp == 32 || kp == 64, "als_score_topk: kp must be 16, 32 or 64");
+  HREC_REQUIRE(k >= 1 && k <= kp, "als_score_topk: need 1 <= k <= kp");
+  HREC_REQUIRE(n_users >= 0 && n_users < 65536 && n_items >= 0, "als_score_topk: bad shape");
+  HREC_REQUIRE(ld_items >= n_items && ld_items % 4 == 0, "als_score_topk: ld_items must be >= n_items and %% 4");
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "als_score_topk: top_k must be in [1, 1024]");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(user_factors && user_rows && item_factors_t && out_idx && out_val && overflow && workspace,
+               "als_score_topk: null pointer");
+  const size_t need = hrec_als_score_topk_workspace_bytes(n_users, n_items, top_k);
+  HREC_REQUIRE(workspace_bytes >= need, "als_score_topk: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t s = as_stream(stream);
+  const int kk = (int)(top_k < n_items ? top_k : n_items);
+  char* p = (char*)workspace;
+  const int64_t S = n_items < kSample ? n_items : kSample;
+  float* samp = (float*)carve(p, (size_t)n_users * S * 4);
+  char* tws = carve(p, topk_ws_bytes(n_users, S, kk, 4));
+  float* sv = (float*)carve(p, (size_t)n_users * kk * 4);
+  int64_t* si = (int64_t*)carve(p, (size_t)n_users * kk * 8);
+  float* cv = (float*)carve(p, (size_t)n_users * kCap * 4);
+  int64_t* ci = (int64_t*)carve(p, (size_t)n_users * kCap * 8);
+  int* cn = (int*)carve(p, (size_t)n_users * 4 + 16);
+  char* fws = carve(p, topk_ws_bytes(n_users, kCap, kk, 4));
+  const dim3 blk(256);
+  const unsigned gy = (unsigned)((n_users + kScoreUB - 1) / kScoreUB);
+  if (hipMemsetAsync(overflow, 0, sizeof(int), s) != hipSuccess) return check_launch("score_topk memset");
+  if (n_items <= kSample) {  // small: score everything, exact top-k
+    hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, false>), dim3(gy, (unsigned)((n_items + 1023) / 1024)), blk,
+                       0, s, user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, samp,
+                       nullptr, 0, 0, nullptr, nullptr, nullptr);
+    int rc = check_launch("als_score_fast_kernel");
+    if (rc) return rc;
+    return topk_rows<float>(samp, n_users, n_items, n_items, kk, out_idx, out_val, tws, (size_t)1 << 62, s);
+  }
+  // 1) thresholds: the kk-th best of the first S items bounds the final kk-th from below
+  hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, false>), dim3(gy, (unsigned)((S + 1023) / 1024)), blk, 0, s,
+                     user_factors, user_rows, n_users, item_factors_t, ld_items, S, k, kp, samp, nullptr, 0, 0,
+                     nullptr, nullptr, nullptr);
+  int rc = check_launch("als_score_fast_kernel(sample)");
+  if (rc) return rc;
+  rc = topk_rows<float>(samp, n_users, S, S, kk, si, sv, tws, (size_t)1 << 62, s);
+  if (rc) return rc;
+  // 2) fused score + filter over all items
+  if (hipMemsetAsync(ci, 0xff, (size_t)n_users * kCap * 8, s) != hipSuccess ||
+      hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
+    return check_launch("score_topk memset");
+  hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, true>), dim3(gy, (unsigned)((n_items + 1023) / 1024)), blk, 0,
+                     s, user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, nullptr,
+                     sv + (kk - 1), kk, kCap, cv, ci, cn);
+  rc = check_launch("als_score_fast_kernel(filter)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(cand_overflow_kernel, dim3(64), dim3(256), 0, s, cn, n_users, kCap, overflow);
+  rc = check_launch("cand_overflow_kernel");
+  if (rc) return rc;
+  // 3) exact stable top-k over the candidates (original item index breaks ties)
+  return topk_rows<float>(cv, n_users, kCap, kCap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
 }

@@ -32,9 +32,12 @@ _SIGNATURES = {
     "hrec_als_init_factors": (_c_i32, [_c_u64, _c_i64, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_als_half_sweep": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl,
                                      _c_i32, _vp, _vp]),
-    "hrec_transpose_f32": (_c_i32, [_vp, _c_i64, _c_i64, _vp, _vp]),
+    "hrec_transpose_f32": (_c_i32, [_vp, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "hrec_als_score": (_c_i32, [_vp, _vp, _c_i32, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp,
                                 _vp]),
+    "hrec_als_score_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
+    "hrec_als_score_topk": (_c_i32, [_vp, _vp, _c_i32, _vp, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
+                                     _vp, _c_sz, _vp]),
     "hrec_topk_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "hrec_topk_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_topk_f64": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
@@ -174,11 +177,14 @@ def als_half_sweep(indptr, indices, values, src_factors, k, reg_param, dst_facto
         _stream()))
 
 
-def transpose(x):
+def transpose(x, pad=4):
+    """[rows, cols] -> [cols, ld] with ld = rows rounded up to `pad` (the
+    padding columns are zero) so vector loads along rows stay aligned."""
     rows, cols = x.shape
-    out = torch.empty((cols, rows), dtype=torch.float32, device=x.device)
+    ld = -(-rows // pad) * pad
+    out = torch.zeros((cols, ld), dtype=torch.float32, device=x.device)
     _check("hrec_transpose_f32", lib().hrec_transpose_f32(
-        _dev(x, torch.float32, "in"), rows, cols, _dev(out, torch.float32, "out"), _stream()))
+        _dev(x, torch.float32, "in"), rows, cols, _dev(out, torch.float32, "out"), ld, _stream()))
     return out
 
 
@@ -193,6 +199,30 @@ def als_score(user_factors, user_rows, item_factors_t, item_rows, n_items, k, ou
         _dev(item_rows, torch.int64, "item_rows"), n_items, k, kp,
         _dev(out, torch.float32, "out"), _stream()))
     return out
+
+
+def als_score_topk(user_factors, user_rows, item_factors_t, n_items, k, top_k, check_overflow=True):
+    """Top-k of the JVM-exact ALS scores over items [0, n_items) for each
+    (known) user, without materialising the score matrix. Falls back to the
+    full score matrix + top-k when a user's survivor list overflowed."""
+    kp = user_factors.shape[1]
+    B = user_rows.numel()
+    kk = min(int(top_k), int(n_items))
+    dev = user_factors.device
+    out_i = torch.empty((B, kk), dtype=torch.int64, device=dev)
+    out_v = torch.empty((B, kk), dtype=torch.float32, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    need = int(lib().hrec_als_score_topk_workspace_bytes(B, n_items, kk))
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _check("hrec_als_score_topk", lib().hrec_als_score_topk(
+        _dev(user_factors, torch.float32, "user_factors"), _dev(user_rows, torch.int64, "user_rows"), B,
+        _dev(item_factors_t, torch.float32, "item_factors_t"), item_factors_t.shape[1], n_items, k, kp, kk,
+        _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float32, "out_val"),
+        _dev(flag, torch.int32, "overflow"), _dev(ws, torch.uint8, "ws"), need, _stream()))
+    if check_overflow and int(flag.item()) != 0:
+        scores = als_score(user_factors, user_rows, item_factors_t, None, n_items, k)
+        return topk(scores, kk)
+    return out_i, out_v
 
 
 # ------------------------------------------------------------------ top-k

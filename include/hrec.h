@@ -95,9 +95,9 @@ int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices,
                         double reg_param, int accum_mode, float* dst_factors,
                         void* stream);
 
-/* out[c*rows + r] = in[r*cols + c] (f32). */
+/* out[c*ld_out + r] = in[r*cols + c] (f32), ld_out >= rows. */
 int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, float* out,
-                       void* stream);
+                       int64_t ld_out, void* stream);
 
 /* ALS scoring (Spark ALSModel.transform predict UDF [ext], reached from
  * src/als_model.py:75): out[b*n_items + j] = sum_{c<k} U[u_b][c]*V[i_j][c]
@@ -109,6 +109,23 @@ int hrec_als_score(const float* user_factors, const int64_t* user_rows,
                    int n_users, const float* item_factors_t, int64_t ld_items,
                    const int64_t* item_rows, int64_t n_items, int k, int kp,
                    float* out, void* stream);
+
+/* Scoring consumed by a top-k, for whole item ranges (no id gather): the
+ * same JVM-exact f32 dot as hrec_als_score for every (user, item j < n_items)
+ * pair, but the B x n_items score matrix is never written: the top_k-th
+ * best score of the first 2048 items bounds each user's final top_k-th score
+ * from below, a fused pass keeps only pairs at or above that bound, and an
+ * exact stable top-k runs over the survivors. out_idx/out_val: [n_users,
+ * min(top_k, n_items)]. *overflow (device int) is set to 1 when some user had
+ * more than 4096 survivors (ties/adversarial scores): the result is then
+ * incomplete and the caller must fall back to hrec_als_score + hrec_topk_f32.
+ * Users must be known (user_rows >= 0). ld_items % 4 == 0. */
+size_t hrec_als_score_topk_workspace_bytes(int n_users, int64_t n_items, int top_k);
+int hrec_als_score_topk(const float* user_factors, const int64_t* user_rows,
+                        int n_users, const float* item_factors_t, int64_t ld_items,
+                        int64_t n_items, int k, int kp, int top_k, int64_t* out_idx,
+                        float* out_val, int* overflow, void* workspace,
+                        size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- top-k --
  * Stable descending top-k of each of n_rows rows (row i starts at

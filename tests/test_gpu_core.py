@@ -242,3 +242,36 @@ def test_engine_c2_shaped_fit_matches_oracle(device, mode):
     pred_g = (Ug[:200].astype(np.float64) @ Vg.T.astype(np.float64))
     pred_o = (U[:200].astype(np.float64) @ V.T.astype(np.float64))
     np.testing.assert_allclose(pred_g, pred_o, rtol=1e-4, atol=1e-6 * np.abs(pred_o).max())
+
+
+def _np_stable_topk(scores, k):
+    out = []
+    for row in scores:
+        order = np.lexsort((np.arange(len(row)), -row.astype(np.float64)))
+        out.append(order[:k])
+    return np.array(out)
+
+
+@pytest.mark.parametrize("n_items,quant", [(100_000, False), (1500, False), (30_000, True)])
+def test_als_score_topk_fused_matches_full(device, n_items, quant):
+    """Fused threshold-filtered top-k == stable top-k of the full JVM-exact
+    score matrix (bit-exact indices and values); quantised factors create
+    massive ties and exercise the overflow fallback."""
+    h = _hrec()
+    rng = np.random.default_rng(n_items)
+    k, kp, B = 64, 64, 40
+    U = np.zeros((B, kp), np.float32)
+    V = np.zeros((n_items, kp), np.float32)
+    U[:, :k] = rng.normal(size=(B, k))
+    V[:, :k] = rng.normal(size=(n_items, k))
+    if quant:
+        U[:, :k] = np.round(U[:, :k])
+        V[:, :k] = np.round(V[:, :k] * 0.5)
+    dU = torch.as_tensor(U, device=device)
+    Vt = h.transpose(torch.as_tensor(V, device=device))
+    users = torch.arange(B, dtype=torch.int64, device=device)
+    idx, val = h.als_score_topk(dU, users, Vt, n_items, k, 10)
+    full = oals.score_matrix(U[:, :k], V[:, :k])
+    exp_i = _np_stable_topk(full, 10)
+    np.testing.assert_array_equal(idx.cpu().numpy(), exp_i)
+    np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(full, exp_i, 1))
