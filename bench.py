@@ -31,6 +31,8 @@ sys.path.insert(0, ROOT)
 
 from src import _hrec, synthetic  # noqa: E402
 from src.als_engine import DeviceALS, shard_range  # noqa: E402
+from src.recommend import ShardedRecommender  # noqa: E402
+from src.tt_engine import DeviceTwoTower  # noqa: E402
 
 METRIC = "ALS epochs/sec + scored user-item pairs/sec at rank=64, 1/2/4/8 MI355X"
 F64_MFMA_PEAK_TFLOPS = 78.6  # AMD MI355X spec (FP64 matrix); not in MI355X_MICROARCH.md
@@ -92,6 +94,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--score-users", type=int, default=1024)
+    ap.add_argument("--hybrid-users", type=int, default=256,
+                    help="users per batch of the end-to-end hybrid top-5 measurement (0 = skip)")
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -189,6 +193,44 @@ def main():
                    "items": n_items, "top_k": 5, "dtype": "f32 (JVM-exact, no FMA)",
                    "kernel": "hrec_als_score_topk (sample bound + fused filter + exact top-k)"}
 
+    # End-to-end hybrid top-5 (HybridRecommendationSystem.get_hybrid_recommendations
+    # for a batch of users): JVM-exact ALS scores + two-tower Dot (d=64, Keras
+    # init) + per-model min-max fusion + stable top-5, items sharded across
+    # ranks with RCCL all-reduce (min/max) and all-gather (candidates).
+    hybrid = None
+    if args.hybrid_users > 0:
+        d = 64
+        n_loc = max(0, min(i_per, n_items - i0))
+        tt = DeviceTwoTower(n_users, n_items, 2651, 255, d, seed=1)
+        g = torch.Generator().manual_seed(5)
+        items = torch.arange(i0, i0 + n_loc, dtype=torch.int32)
+        man = torch.randint(0, 2651, (n_items,), generator=g, dtype=torch.int32)[i0: i0 + n_loc]
+        cat = torch.randint(0, 255, (n_items,), generator=g, dtype=torch.int32)[i0: i0 + n_loc]
+        num = torch.rand((n_items, 2), generator=g)[i0: i0 + n_loc].contiguous()
+        ivec = tt.item_vectors(items.cuda(), man.cuda(), cat.cuda(), num.cuda())
+        Vt_loc = _hrec.transpose(eng.V[i0: i0 + n_loc].contiguous())
+        rec = ShardedRecommender(eng.U, Vt_loc, ivec, i0, k, world=world, rank=rank, group=group)
+        Bh = args.hybrid_users
+        hu = (torch.arange(Bh, dtype=torch.int64) * (n_users // Bh)).cuda()
+        uvec = tt.user_vectors(hu.to(torch.int32))
+        for _ in range(2):
+            rec.recommend(hu, uvec, False, 5)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        reps = 5
+        h0 = time.perf_counter()
+        for _ in range(reps):
+            rec.recommend(hu, uvec, False, 5)
+        torch.cuda.synchronize()
+        ht = torch.tensor([(time.perf_counter() - h0) / reps], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
+        hs = float(ht.item())
+        hybrid = {"pairs_per_s": Bh * n_items / hs, "ms_per_batch": hs * 1e3, "users": Bh, "items": n_items,
+                  "top_k": 5, "d": d, "items_sharded_over": world,
+                  "steps": "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5"}
+
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.accum_mode == 0:
         with open(args.traffic_json) as f:
@@ -238,6 +280,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "scoring": scoring,
+            "hybrid_top5": hybrid,
         }
         print(json.dumps(line))
     if world > 1:

@@ -374,6 +374,70 @@ __global__ __launch_bounds__(256) void cosine_kernel(const double* __restrict__ 
   o[j] = dot;
 }
 
+
+// --------------------------------------------- batched fusion (K9, rows)
+// Per-row min / max of an f32 score matrix (NaN ignored, like np.nanmin):
+// out[r] = min, out[n_rows + r] = max (two contiguous halves, so the
+// cross-shard reduction is one MIN and one MAX all-reduce). One block per row.
+__global__ __launch_bounds__(256) void rows_minmax_kernel(const float* __restrict__ x, int64_t n, int64_t ld,
+                                                          float* __restrict__ out) {
+  __shared__ float smin[256], smax[256];
+  const float* r = x + (int64_t)blockIdx.x * ld;
+  float lo = __builtin_inff(), hi = -__builtin_inff();
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    lo = fminf(lo, r[j]);
+    hi = fmaxf(hi, r[j]);
+  }
+  smin[threadIdx.x] = lo;
+  smax[threadIdx.x] = hi;
+  __syncthreads();
+  for (int s2 = 128; s2 > 0; s2 >>= 1) {
+    if (threadIdx.x < s2) {
+      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s2]);
+      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s2]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = smin[0];              // mins  [n_rows]
+    out[gridDim.x + blockIdx.x] = smax[0];  // maxes [n_rows]
+  }
+}
+
+// fused[r][j] = w0 * minmax64(als[r][j]) + w1 * (double)minmax32(tt[r][j]),
+// with each row's min/max given (global over every shard of the row): the
+// ALS side is min-max scaled in f64 (the reference's als scores are Python
+// floats), the two-tower side in f32 (np.float32 scores), then f64 fusion
+// with numpy 1.21's scalar promotion — hrec_fuse_topk per row.
+__global__ __launch_bounds__(256) void fuse_rows_kernel(const float* __restrict__ als, const float* __restrict__ tt,
+                                                        int64_t n, int64_t ld, const float* __restrict__ als_mm,
+                                                        const float* __restrict__ tt_mm, double w0, double w1,
+                                                        double* __restrict__ fused) {
+#pragma clang fp contract(off)
+  const int64_t r = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int64_t R = gridDim.y;  // min/max layout: [2][n_rows]
+  const double amin = (double)als_mm[r], amax = (double)als_mm[R + r];
+  double arange = amax - amin;
+  if (arange < 10.0 * DBL_EPSILON) arange = 1.0;
+  const double ascale = 1.0 / arange;
+  const double amin_ = 0.0 - amin * ascale;
+  const float tmin = tt_mm[r], tmax = tt_mm[R + r];
+  float trange = tmax - tmin;
+  if (trange < 10.0f * FLT_EPSILON) trange = 1.0f;
+  const float tscale = 1.0f / trange;
+  const float tmin_ = 0.0f - tmin * tscale;
+  const double an = (double)als[r * ld + j] * ascale + amin_;
+  const float tn = tt[r * ld + j] * tscale + tmin_;
+  fused[r * n + j] = w0 * an + w1 * (double)tn;
+}
+
+__global__ void add_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t off) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && idx[i] >= 0) idx[i] += off;
+}
+
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
               T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr);
@@ -611,4 +675,58 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
   if (rc) return rc;
   // 3) exact stable top-k over the candidates (original item index breaks ties)
   return topk_rows<float>(cv, n_users, kCap, kCap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
+}
+
+extern "C" int hrec_rows_minmax_f32(const float* x, int64_t n_rows, int64_t n, int64_t ld, float* out, void* stream) {
+  HREC_REQUIRE(n_rows >= 0 && n >= 0 && ld >= n, "rows_minmax: bad shape");
+  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(n_rows < (1ll << 31), "rows_minmax: too many rows");
+  HREC_REQUIRE(x && out, "rows_minmax: null pointer");
+  hipLaunchKernelGGL(rows_minmax_kernel, dim3((unsigned)n_rows), dim3(256), 0, as_stream(stream), x, n, ld, out);
+  return check_launch("rows_minmax_kernel");
+}
+
+extern "C" size_t hrec_fuse_rows_workspace_bytes(int64_t n_rows, int64_t n, int top_k) {
+  return (size_t)n_rows * n * 8 + 256 + topk_ws_bytes(n_rows, n, top_k, 8);
+}
+
+extern "C" int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_rows, int64_t n, int64_t ld,
+                                   const float* als_minmax, const float* tt_minmax, int als_wins, int top_k,
+                                   int64_t idx_offset, int64_t* out_idx, double* out_val, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  HREC_REQUIRE(n_rows >= 0 && n >= 1 && ld >= n, "fuse_rows_topk: bad shape");
+  HREC_REQUIRE(n_rows < 65536, "fuse_rows_topk: at most 65535 rows per call");
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "fuse_rows_topk: top_k must be in [1, 1024]");
+  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(als && tt && als_minmax && tt_minmax && out_idx && out_val && workspace, "fuse_rows_topk: null pointer");
+  const size_t need = hrec_fuse_rows_workspace_bytes(n_rows, n, top_k);
+  HREC_REQUIRE(workspace_bytes >= need, "fuse_rows_topk: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t s = as_stream(stream);
+  double* fused = (double*)workspace;
+  char* tws = (char*)workspace + (((size_t)n_rows * n * 8 + 255) & ~(size_t)255);
+  const double w0 = als_wins ? 0.8 : 0.2, w1 = als_wins ? 0.2 : 0.8;
+  hipLaunchKernelGGL(fuse_rows_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n_rows), dim3(256), 0, s, als, tt,
+                     n, ld, als_minmax, tt_minmax, w0, w1, fused);
+  int rc = check_launch("fuse_rows_kernel");
+  if (rc) return rc;
+  const int kk = (int)(top_k < n ? top_k : n);
+  rc = topk_rows<double>(fused, n_rows, n, n, kk, out_idx, out_val, tws, (size_t)1 << 62, s);
+  if (rc || idx_offset == 0) return rc;
+  const int64_t tot = n_rows * kk;
+  hipLaunchKernelGGL(add_offset_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out_idx, tot, idx_offset);
+  return check_launch("add_offset_kernel");
+}
+
+extern "C" int hrec_topk_f64_keyed(const double* vals, const int64_t* keys, int64_t n_rows, int64_t n, int top_k,
+                                   int64_t* out_idx, double* out_val, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+  HREC_REQUIRE(n_rows >= 0 && n >= 0, "topk_f64_keyed: bad shape");
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "topk_f64_keyed: top_k must be in [1, 1024]");
+  if (n_rows == 0 || n == 0) return HREC_OK;
+  HREC_REQUIRE(n_rows < 65536, "topk_f64_keyed: at most 65535 rows per call");
+  HREC_REQUIRE(vals && keys && out_idx && out_val, "topk_f64_keyed: null pointer");
+  const int kk = (int)(top_k < n ? top_k : n);
+  HREC_REQUIRE(workspace_bytes >= topk_ws_bytes(n_rows, n, kk, 8), "topk_f64_keyed: workspace too small");
+  return topk_rows<double>(vals, n_rows, n, n, kk, out_idx, out_val, workspace, workspace_bytes, as_stream(stream),
+                           keys);
 }

@@ -135,6 +135,52 @@ __global__ __launch_bounds__(kBlock) void tt_score_kernel(const float* __restric
   out[(int64_t)b * N + j] = acc;
 }
 
+// K8: all-pairs Dot(axes=1) on the matrix cores, out[b*N + j] = <U[b], V[j]>.
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chain per k-step), 64 users x 64
+// items per 256-thread block, the d axis staged through LDS in chunks of 64
+// (rows padded to 65 floats: conflict-free column reads).
+typedef float f4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void tt_score_mfma_kernel(const float* __restrict__ U, int B,
+                                                            const float* __restrict__ V, int64_t N, int d,
+                                                            float* __restrict__ out) {
+  __shared__ float Us[64][65];
+  __shared__ float Vs[64][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * 64;
+  const int64_t j0 = (int64_t)blockIdx.x * 64;
+  f4v acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < d; k0 += 64) {
+    for (int o = threadIdx.x; o < 64 * 64; o += 256) {
+      const int r = o >> 6, c = o & 63;
+      const int kk = k0 + c;
+      Us[r][c] = (b0 + r < B && kk < d) ? U[(int64_t)(b0 + r) * d + kk] : 0.f;
+      Vs[r][c] = (j0 + r < N && kk < d) ? V[(j0 + r) * d + kk] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int ks = 0; ks < 16; ++ks) {
+      const float a = Us[16 * w + (lane & 15)][4 * ks + (lane >> 4)];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float b = Vs[16 * t + (lane & 15)][4 * ks + (lane >> 4)];
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int64_t j = j0 + 16 * t + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = b0 + 16 * w + 4 * (lane >> 4) + r;
+      if (b < B && j < N) out[(int64_t)b * N + j] = acc[t][r];
+    }
+  }
+}
+
 // Paired dot: out[r] = <U[r], V[r]> (model.predict on per-row inputs).
 __global__ __launch_bounds__(kBlock) void tt_pair_score_kernel(const float* __restrict__ U,
                                                                const float* __restrict__ V, int64_t n, int d,
@@ -441,9 +487,14 @@ extern "C" int hrec_tt_score(const float* user_vec, int n_users, const float* it
   if (n_users == 0 || n_items == 0) return HREC_OK;
   HREC_REQUIRE(n_users < 65536, "tt_score: at most 65535 users per call");
   HREC_REQUIRE(user_vec && item_vec && out, "tt_score: null pointer");
-  hipLaunchKernelGGL(tt_score_kernel, dim3((unsigned)((n_items + kBlock - 1) / kBlock), (unsigned)n_users),
-                     dim3(kBlock), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
-  return check_launch("tt_score_kernel");
+  if (n_users < 8) {  // GEMV-shaped: one thread per (user, item)
+    hipLaunchKernelGGL(tt_score_kernel, dim3((unsigned)((n_items + kBlock - 1) / kBlock), (unsigned)n_users),
+                       dim3(kBlock), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
+    return check_launch("tt_score_kernel");
+  }
+  hipLaunchKernelGGL(tt_score_mfma_kernel, dim3((unsigned)((n_items + 63) / 64), (unsigned)((n_users + 63) / 64)),
+                     dim3(256), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
+  return check_launch("tt_score_mfma_kernel");
 }
 
 static size_t partial_len(int d) { return (size_t)(d + 32) * d + 5 * (size_t)d + 48 + 2; }

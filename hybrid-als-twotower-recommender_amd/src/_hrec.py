@@ -42,6 +42,11 @@ _SIGNATURES = {
     "hrec_topk_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_topk_f64": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_cosine_sim": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp]),
+    "hrec_rows_minmax_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp]),
+    "hrec_fuse_rows_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),
+    "hrec_fuse_rows_topk": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp,
+                                     _vp, _c_sz, _vp]),
+    "hrec_topk_f64_keyed": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_fuse_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
     "hrec_fuse_topk": (_c_i32, [_vp, _vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_sz,
                                 _vp]),
@@ -367,3 +372,43 @@ def adam_sparse(var, m, v, indices, grad_rows, mark, gsum, lr, beta1, omb1, beta
         _dev(indices, torch.int32, "indices"), _dev(grad_rows, torch.float32, "grad_rows"), indices.numel(),
         _dev(mark, torch.int32, "mark"), _dev(gsum, torch.float32, "gsum"), float(lr), float(beta1),
         float(omb1), float(beta2), float(omb2), float(eps), _stream()))
+
+
+# --------------------------------------------------------- batched fusion
+def rows_minmax(x):
+    n_rows, n = x.shape
+    out = torch.empty((2, n_rows), dtype=torch.float32, device=x.device)  # [mins; maxes]
+    _check("hrec_rows_minmax_f32", lib().hrec_rows_minmax_f32(
+        _dev(x, torch.float32, "x"), n_rows, n, x.stride(0), _dev(out, torch.float32, "out"), _stream()))
+    return out
+
+
+def fuse_rows_topk(als, tt, als_mm, tt_mm, als_wins, top_k, idx_offset=0):
+    n_rows, n = als.shape
+    kk = min(int(top_k), n)
+    dev = als.device
+    out_i = torch.empty((n_rows, kk), dtype=torch.int64, device=dev)
+    out_v = torch.empty((n_rows, kk), dtype=torch.float64, device=dev)
+    need = int(lib().hrec_fuse_rows_workspace_bytes(n_rows, n, kk))
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _check("hrec_fuse_rows_topk", lib().hrec_fuse_rows_topk(
+        _dev(als, torch.float32, "als"), _dev(tt, torch.float32, "tt"), n_rows, n, als.stride(0),
+        _dev(als_mm, torch.float32, "als_minmax"), _dev(tt_mm, torch.float32, "tt_minmax"), int(bool(als_wins)),
+        kk, int(idx_offset), _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float64, "out_val"),
+        _dev(ws, torch.uint8, "ws"), need, _stream()))
+    return out_i, out_v
+
+
+def topk_keyed(vals, keys, top_k):
+    n_rows, n = vals.shape
+    kk = min(int(top_k), n)
+    dev = vals.device
+    out_i = torch.empty((n_rows, kk), dtype=torch.int64, device=dev)
+    out_v = torch.empty((n_rows, kk), dtype=torch.float64, device=dev)
+    need = int(lib().hrec_topk_workspace_bytes(n_rows, n, kk, 1))
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _check("hrec_topk_f64_keyed", lib().hrec_topk_f64_keyed(
+        _dev(vals, torch.float64, "vals"), _dev(keys, torch.int64, "keys"), n_rows, n, kk,
+        _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float64, "out_val"), _dev(ws, torch.uint8, "ws"),
+        need, _stream()))
+    return out_i, out_v

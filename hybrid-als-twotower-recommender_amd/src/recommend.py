@@ -1,0 +1,94 @@
+"""Batched hybrid top-k recommendations with the item set sharded across GPUs.
+
+What HybridRecommendationSystem.get_hybrid_recommendations does for one user
+(src/hybrid_system.py:95-116: ALS scores and two-tower scores for every
+candidate item, per-model MinMaxScaler over all candidates, weighted fusion,
+stable top-k) done for a BATCH of users on the device, with the candidate
+items split into contiguous shards, one per rank (SURVEY §8e, rows
+"Scoring" and "Hybrid fusion top-k"):
+
+  1. local scores: JVM-exact ALS dot (hrec_als_score) and two-tower Dot on
+     the matrix cores (hrec_tt_score) for the rank's item shard;
+  2. per-row min / max of both (hrec_rows_minmax_f32), made global by RCCL
+     all_reduce MIN / MAX (C2) — min and max are exact under any grouping;
+  3. fusion with the global scaler coefficients + local stable top-k with
+     global item ids (hrec_fuse_rows_topk);
+  4. RCCL all_gather of the [B, k] candidates (C3) and a keyed stable top-k
+     merge (hrec_topk_f64_keyed): ties break on the global item id, so every
+     world size returns the same items and scores as one GPU.
+
+The collectives and kernels are injectable (`ops`) so the orchestration can be
+exercised with gloo on CPU (tests/test_distributed.py).
+"""
+import torch
+import torch.distributed as dist
+
+from . import _hrec
+
+
+class DeviceOps:
+    """The libhrec implementations of the per-shard steps."""
+
+    @staticmethod
+    def als_scores(U, user_rows, Vt_local, n_local, k):
+        return _hrec.als_score(U, user_rows, Vt_local, None, n_local, k)
+
+    @staticmethod
+    def tt_scores(user_vecs, item_vecs_local):
+        return _hrec.tt_score(user_vecs, item_vecs_local)
+
+    rows_minmax = staticmethod(_hrec.rows_minmax)
+    fuse_rows_topk = staticmethod(_hrec.fuse_rows_topk)
+    topk_keyed = staticmethod(_hrec.topk_keyed)
+
+
+class ShardedRecommender:
+    def __init__(self, U, Vt_local, item_vecs_local, item_offset, k, world=1, rank=0, group=None, ops=None):
+        self.U = U                          # [n_users, kp] ALS user factors (replicated)
+        self.Vt = Vt_local                  # [kp, ld] transposed ALS item factors of this shard
+        self.iv = item_vecs_local           # [n_local, d] two-tower item vectors of this shard
+        self.n_local = item_vecs_local.shape[0]
+        self.offset = int(item_offset)
+        self.k = int(k)
+        self.world, self.rank, self.group = int(world), int(rank), group
+        self.ops = ops or DeviceOps
+
+    def recommend(self, user_rows, user_vecs, als_wins, top_k):
+        """user_rows: [B] int64 ALS rows; user_vecs: [B, d] two-tower user
+        vectors. Returns (global item ids [B, k], fused scores f64 [B, k])."""
+        o = self.ops
+        B = int(user_rows.shape[0])
+        dev = user_vecs.device
+        if self.n_local > 0:
+            als = o.als_scores(self.U, user_rows, self.Vt, self.n_local, self.k)
+            tt = o.tt_scores(user_vecs, self.iv)
+            a_mm = o.rows_minmax(als)
+            t_mm = o.rows_minmax(tt)
+        else:  # an empty shard contributes neutral min/max and no candidates
+            inf = float("inf")
+            a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
+            t_mm = a_mm.clone()
+        if self.world > 1:
+            for mm in (a_mm, t_mm):
+                dist.all_reduce(mm[0], op=dist.ReduceOp.MIN, group=self.group)
+                dist.all_reduce(mm[1], op=dist.ReduceOp.MAX, group=self.group)
+        if self.n_local > 0:
+            idx, val = o.fuse_rows_topk(als, tt, a_mm, t_mm, als_wins, top_k, self.offset)
+        else:
+            idx = torch.empty((B, 0), dtype=torch.int64, device=dev)
+            val = torch.empty((B, 0), dtype=torch.float64, device=dev)
+        if self.world == 1:
+            return idx, val
+        kk = int(top_k)
+        if idx.shape[1] < kk:  # every rank contributes k slots; -1 marks an empty one
+            pad = kk - idx.shape[1]
+            idx = torch.cat([idx, torch.full((B, pad), -1, dtype=torch.int64, device=dev)], 1)
+            val = torch.cat([val, torch.full((B, pad), float("-inf"), dtype=torch.float64, device=dev)], 1)
+        # rank-major concatenation [W*B, k] (the layout every backend accepts)
+        g_idx = torch.empty((self.world * B, kk), dtype=idx.dtype, device=idx.device)
+        g_val = torch.empty((self.world * B, kk), dtype=val.dtype, device=val.device)
+        dist.all_gather_into_tensor(g_idx, idx.contiguous(), group=self.group)
+        dist.all_gather_into_tensor(g_val, val.contiguous(), group=self.group)
+        cand_i = g_idx.view(self.world, B, kk).permute(1, 0, 2).reshape(B, self.world * kk).contiguous()
+        cand_v = g_val.view(self.world, B, kk).permute(1, 0, 2).reshape(B, self.world * kk).contiguous()
+        return o.topk_keyed(cand_v, cand_i, top_k)

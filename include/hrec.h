@@ -156,6 +156,30 @@ int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, int64_t n,
                    double* out_fused, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* Batched fusion for many users over one item range (a shard of the item
+ * set when the item rows are split across GPUs):
+ * hrec_rows_minmax_f32: out[r] = min, out[n_rows + r] = max of row r (NaN
+ * ignored) — reduced across shards by the caller (RCCL all-reduce MIN on the
+ * first half, MAX on the second);
+ * hrec_fuse_rows_topk: per row, MinMaxScaler of the ALS scores in f64 and of
+ * the two-tower scores in f32 with the GIVEN (global) row min/max, f64 fusion
+ * as hrec_fuse_topk, then the stable top-k of the row; indices are shifted by
+ * idx_offset (the shard's first global item). als/tt: [n_rows, ld] f32.
+ * hrec_topk_f64_keyed: stable top-k where keys[] (e.g. global item ids, -1 =
+ * empty slot) are both the tie-break and the returned ids — the merge of the
+ * per-shard candidates. */
+int hrec_rows_minmax_f32(const float* x, int64_t n_rows, int64_t n, int64_t ld,
+                         float* out, void* stream);
+size_t hrec_fuse_rows_workspace_bytes(int64_t n_rows, int64_t n, int top_k);
+int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_rows, int64_t n,
+                        int64_t ld, const float* als_minmax, const float* tt_minmax,
+                        int als_wins, int top_k, int64_t idx_offset, int64_t* out_idx,
+                        double* out_val, void* workspace, size_t workspace_bytes,
+                        void* stream);
+int hrec_topk_f64_keyed(const double* vals, const int64_t* keys, int64_t n_rows, int64_t n,
+                        int top_k, int64_t* out_idx, double* out_val, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------ cold-start sim --
  * ALSModel._find_similar_items (src/als_model.py:93-104): out[q*n_items+j] =
  * cosine(feats[query_rows[q]], feats[j]) with sklearn's normalise-then-dot
@@ -198,7 +222,8 @@ int hrec_tt_item_forward(const hrec_tt_params* params, const int32_t* item,
 /* User tower for n users. */
 int hrec_tt_user_forward(const hrec_tt_params* params, const int32_t* user, int64_t n,
                          float* user_vec /* [n,d] */, void* stream);
-/* Dot(axes=1) of every user row with every item row: out[b*n_items + j]. */
+/* Dot(axes=1) of every user row with every item row: out[b*n_items + j]
+ * (f32; on the matrix cores for n_users >= 8). */
 int hrec_tt_score(const float* user_vec, int n_users, const float* item_vec,
                   int64_t n_items, int d, float* out, void* stream);
 

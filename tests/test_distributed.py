@@ -65,7 +65,7 @@ def test_sharded_als_matches_unsharded(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, U0, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=60) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -87,3 +87,105 @@ def test_shard_ranges_cover_and_pad():
             assert all(s[1] == per for s in spans)
             assert per * w >= n and per == -(-n // w)  # covers [0, n); tail shards padded
             assert [s[0] for s in spans] == [r * per for r in range(w)]
+
+
+# ------------------------------------------------ sharded hybrid top-k (C2/C3)
+class _CpuOps:
+    """CPU stand-ins with the kernels' arithmetic (exact on integer-valued data)."""
+
+    @staticmethod
+    def als_scores(U, user_rows, Vt_local, n_local, k):
+        s = oals.score_matrix(U[user_rows.numpy(), :k].numpy(), Vt_local[:k, :n_local].numpy().T)
+        return torch.from_numpy(s)
+
+    @staticmethod
+    def tt_scores(user_vecs, item_vecs_local):
+        return torch.from_numpy((user_vecs.numpy().astype(np.float64) @ item_vecs_local.numpy().T.astype(np.float64))
+                                .astype(np.float32))
+
+    @staticmethod
+    def rows_minmax(x):
+        a = x.numpy()
+        return torch.from_numpy(np.stack([np.nanmin(a, axis=1), np.nanmax(a, axis=1)]).astype(np.float32))
+
+    @staticmethod
+    def fuse_rows_topk(als, tt, a_mm, t_mm, als_wins, top_k, offset):
+        w0, w1 = (0.8, 0.2) if als_wins else (0.2, 0.8)
+        out_i, out_v = [], []
+        for r in range(als.shape[0]):
+            amin, amax = float(a_mm[0, r]), float(a_mm[1, r])
+            rng = amax - amin
+            rng = 1.0 if rng < 10 * np.finfo(np.float64).eps else rng
+            sc = 1.0 / rng
+            an = als[r].numpy().astype(np.float64) * sc + (0.0 - amin * sc)
+            tmin, tmax = np.float32(t_mm[0, r]), np.float32(t_mm[1, r])
+            trng = np.float32(tmax - tmin)
+            trng = np.float32(1.0) if trng < np.float32(10) * np.finfo(np.float32).eps else trng
+            ts = np.float32(np.float32(1.0) / trng)
+            tn = tt[r].numpy() * ts + np.float32(np.float32(0.0) - tmin * ts)
+            f = w0 * an + w1 * tn.astype(np.float64)
+            order = np.lexsort((np.arange(len(f)), -f))[:top_k]
+            out_i.append(order + offset)
+            out_v.append(f[order])
+        return torch.from_numpy(np.array(out_i)), torch.from_numpy(np.array(out_v))
+
+    @staticmethod
+    def topk_keyed(vals, keys, top_k):
+        out_i, out_v = [], []
+        for v, kk in zip(vals.numpy(), keys.numpy()):
+            ok = kk >= 0
+            v, kk = v[ok], kk[ok]
+            order = np.lexsort((kk, -v))[:top_k]
+            out_i.append(kk[order])
+            out_v.append(v[order])
+        return torch.from_numpy(np.array(out_i)), torch.from_numpy(np.array(out_v))
+
+
+def _hybrid_data():
+    rng = np.random.default_rng(7)
+    n_users, n_items, k, d = 12, 101, 8, 6
+    U = rng.integers(-3, 4, (n_users, 16)).astype(np.float32)
+    V = rng.integers(-3, 4, (n_items, 16)).astype(np.float32)
+    uv = rng.integers(-2, 3, (5, d)).astype(np.float32)
+    iv = rng.integers(-2, 3, (n_items, d)).astype(np.float32)
+    return U, V, uv, iv, k
+
+
+def _hybrid_run(world, rank, U, V, uv, iv, k, group=None):
+    from src.als_engine import shard_range
+    from src.recommend import ShardedRecommender
+
+    i0, per = shard_range(V.shape[0], world, rank)
+    Vl = V[i0: i0 + per]
+    rec = ShardedRecommender(torch.from_numpy(U), torch.from_numpy(np.ascontiguousarray(Vl.T)),
+                             torch.from_numpy(iv[i0: i0 + per]), i0, k, world=world, rank=rank, group=group,
+                             ops=_CpuOps)
+    rows = torch.tensor([0, 3, 5, 7, 11], dtype=torch.int64)
+    return [t.numpy() for t in rec.recommend(rows, torch.from_numpy(uv), True, 7)]
+
+
+def _hybrid_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    U, V, uv, iv, k = _hybrid_data()
+    q.put((rank, _hybrid_run(world, rank, U, V, uv, iv, k, dist.group.WORLD)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 24])
+def test_sharded_hybrid_topk_matches_single(world):
+    U, V, uv, iv, k = _hybrid_data()
+    ref_i, ref_v = _hybrid_run(1, 0, U, V, uv, iv, k)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=60) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, (gi, gv) in res:
+        np.testing.assert_array_equal(gi, ref_i)
+        np.testing.assert_array_equal(gv, ref_v)

@@ -356,3 +356,37 @@ def test_hybrid_end_to_end(device, tmp_path):
     fused = h.adaptive_fusion(a, t)
     assert [float(s) for _, s in fused] == [float(s) for _, s in
                                             ofus.adaptive_fusion(a, t, h.als_f1_score, h.twotower_f1_score)]
+
+
+def test_batched_hybrid_matches_per_user_fusion(device):
+    """ShardedRecommender (1 GPU) == the reference's per-user fusion + top-k
+    over the same ALS (JVM-exact) and two-tower scores, bit for bit."""
+    from src import _hrec
+    from src.recommend import ShardedRecommender
+
+    rng = np.random.default_rng(21)
+    n_users, n_items, k, d, B = 300, 5000, 32, 24, 40
+    U = np.zeros((n_users, 32), np.float32)
+    U[:, :k] = rng.normal(size=(n_users, k))
+    V = np.zeros((n_items, 32), np.float32)
+    V[:, :k] = rng.normal(size=(n_items, k))
+    uvec = torch.as_tensor(rng.normal(size=(B, d)).astype(np.float32), device=device)
+    ivec = torch.as_tensor(rng.normal(size=(n_items, d)).astype(np.float32), device=device)
+    dU = torch.as_tensor(U, device=device)
+    Vt = _hrec.transpose(torch.as_tensor(V, device=device))
+    rows = torch.as_tensor(rng.choice(n_users, B, replace=False), device=device)
+    rec = ShardedRecommender(dU, Vt, ivec, 0, k)
+    for als_wins in (True, False):
+        idx, val = rec.recommend(rows, uvec, als_wins, 5)
+        tt = _hrec.tt_score(uvec, ivec).cpu().numpy()
+        als = oals.score_matrix(U[rows.cpu().numpy(), :k], V[:, :k])
+        for b in range(B):
+            a_pairs = [(j, float(als[b, j])) for j in range(n_items)]
+            t_pairs = [(j, tt[b, j]) for j in range(n_items)]
+            f1 = (0.5, 0.1) if als_wins else (0.1, 0.5)
+            exp = ofus.top_k(ofus.adaptive_fusion(a_pairs, t_pairs, *f1, legacy=True), 5)
+            assert idx[b].cpu().tolist() == [i for i, _ in exp]
+            assert val[b].cpu().tolist() == [float(s) for _, s in exp]
+    # the MFMA Dot agrees with a float64 reference
+    ref = uvec.double().cpu().numpy() @ ivec.double().cpu().numpy().T
+    np.testing.assert_allclose(_hrec.tt_score(uvec, ivec).cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
