@@ -37,14 +37,17 @@
 #ifndef HREC_ALS_SOLVE
 #define HREC_ALS_SOLVE 1  // 1 = blocked tile-layout Cholesky (MFMA trailing updates); 0 = row-per-lane
 #endif
-#ifndef HREC_ALS_PANEL_ROLLED
-#define HREC_ALS_PANEL_ROLLED 0  // 1 = one rolled copy of the panel code (smaller, spills at 2 waves)
-#endif
 #ifndef HREC_ALS_SOLVE_UNROLL
 #define HREC_ALS_SOLVE_UNROLL 8  // unroll of the two 64-step triangular-solve loops
 #endif
 #ifndef HREC_ALS_CH1
 #define HREC_ALS_CH1 4
+#endif
+#ifndef HREC_ALS_PIPE
+#define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
+#endif
+#ifndef HREC_ALS_PF
+#define HREC_ALS_PF 8  // PIPE: gather prefetch distance in steps of 4 ratings
 #endif
 
 namespace hrec {
@@ -77,6 +80,33 @@ struct Vec<1> {
 };
 
 __device__ __forceinline__ int tri(int i) { return (i * (i + 1)) >> 1; }
+
+// Structured buffer loads (buffer_load_dword* ... idxen offen): address =
+// base + vindex * stride + voffset, with the hardware range check
+// (vindex >= num_records reads as zero).
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ f4 sbuf_load_f4(i4v rsrc, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.buffer.load.v4f32");
+__device__ f2 sbuf_load_f2(i4v rsrc, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.buffer.load.v2f32");
+__device__ float sbuf_load_f1(i4v rsrc, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.buffer.load.f32");
+
+template <int NT>
+__device__ __forceinline__ Vec<NT> struct_load(i4v rsrc, int vindex, int voffset) {
+  Vec<NT> v;
+  if constexpr (NT == 4) {
+    const f4 t = sbuf_load_f4(rsrc, vindex, voffset, 0, 0);
+    v.x[0] = t.x, v.x[1] = t.y, v.x[2] = t.z, v.x[3] = t.w;
+  } else if constexpr (NT == 2) {
+    const f2 t = sbuf_load_f2(rsrc, vindex, voffset, 0, 0);
+    v.x[0] = t.x, v.x[1] = t.y;
+  } else {
+    v.x[0] = sbuf_load_f1(rsrc, vindex, voffset, 0, 0);
+  }
+  return v;
+}
 
 #ifdef HREC_ALS_STAMPS
 // Diagnostic build only: per-phase cycle sums (s_memtime) over all waves.
@@ -205,17 +235,16 @@ __device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, do
 template <int NT, int CH, int MODE>
 __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int k,
-    double reg, float* __restrict__ dst) {
+    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
+    int k, double reg, float* __restrict__ dst) {
   constexpr int KP = 16 * NT;
   constexpr int NPAIR = NT * (NT + 1) / 2;
   constexpr int CHN = 4 * CH;  // nnz per chunk (<= 64)
 #if HREC_ALS_SOLVE == 1
   __shared__ double Up[KP * (KP + 1) / 2];  // U, column-packed: U[tri(c) + q], q <= c
   __shared__ double stage[MODE == 1 ? 256 : 1];
-#if HREC_ALS_PANEL_ROLLED
   __shared__ __attribute__((aligned(16))) double colbuf[64];
-#endif
+  __shared__ double dsh[KP];  // pivots U[r][r]
   double* A = nullptr;
 #else
   __shared__ double A[KP * (KP + 1) / 2];
@@ -266,6 +295,97 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     }
   };
 
+  // PIPE for kp = 64 (at kp <= 32 the scheduler hoists the unrolled window
+  // into a spill; those sizes keep the chunked loop)
+  if constexpr (HREC_ALS_PIPE && NT == 4) {
+  // Ring pipeline over WINDOWS of 16 steps (64 nnz: one index and one rating
+  // per lane). Step s's gather is issued PF steps ahead into ring slot
+  // s % PF; the index reaches the lane group by ds_bpermute and feeds a
+  // structured buffer load (vindex = source row, stride = one factor row,
+  // voffset = this lane's 16-B column slice). Padding entries carry index -1:
+  // the buffer range check returns zeros for them, so the loop has no
+  // branches, masks or address arithmetic on the VALU.
+  constexpr int PF = HREC_ALS_PF;
+  static_assert(16 % PF == 0, "prefetch distance must divide the window");
+  const int voff = NT * 4 * col;
+  const int bp_addr = 4 * sub;  // ds_bpermute byte address of nnz (4s + sub) is 16 s + 4 sub
+  const uint64_t sbase = (uint64_t)src;
+  i4v rsrc;
+  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(sbase >> 32) | ((KP * 4) << 16));
+  rsrc.z = __builtin_amdgcn_readfirstlane((int)n_src);
+  rsrc.w = 0x00020000;
+  auto load_win = [&](int64_t w, int& ii, float& vv) {
+    const int64_t p = beg + 64 * w + lane;
+    const int64_t pc = p < end ? p : end - 1;
+    const int iraw = indices[pc];
+    const float vraw = values[pc];
+    ii = p < end ? iraw : -1;
+    vv = p < end ? vraw : 0.f;
+  };
+  auto bperm = [&](int win, int s) -> int { return __builtin_amdgcn_ds_bpermute(bp_addr + 16 * s, win); };
+  const int64_t nsteps = (n + 3) >> 2;
+  int iw0, iw1;
+  float rw0, rw1;
+  load_win(0, iw0, rw0);
+  load_win(1, iw1, rw1);
+  Vec<NT> ring[PF];
+#pragma unroll
+  for (int s = 0; s < PF; ++s) ring[s] = struct_load<NT>(rsrc, bperm(iw0, s), voff);
+  int nidx = bperm(iw0, PF);  // source row of the next gather (one step ahead)
+  for (int64_t w = 0;; ++w) {
+    int iw2;
+    float rw2;
+    load_win(w + 2, iw2, rw2);
+    bool stop = false;
+    const int rem = __builtin_amdgcn_readfirstlane((int)(nsteps - 16 * w < 16 ? nsteps - 16 * w : 16));
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s >= rem) {  // wave-uniform (scalar) tail exit
+        stop = true;
+        break;
+      }
+      const Vec<NT> cur = ring[s % PF];
+      double a[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) a[t] = (double)cur.x[t];
+      ring[s % PF] = struct_load<NT>(rsrc, nidx, voff);
+      nidx = (s + 1 + PF < 16) ? bperm(iw0, s + 1 + PF) : bperm(iw1, s + 1 + PF - 16);
+      const float rf = __int_as_float(__builtin_amdgcn_ds_bpermute(bp_addr + 16 * s, __float_as_int(rw0)));
+      const double rv = (double)rf;
+      if (MODE == 1 && (s % HREC_ALS_CH1) == 0) {
+#pragma unroll
+        for (int p = 0; p < NPAIR; ++p) fa[p] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      int p = 0;
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+#pragma unroll
+        for (int J = I; J < NT; ++J) {
+          if (MODE == 0)
+            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
+          else
+            fa[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x[I], cur.x[J], fa[p], 0, 0, 0);
+          ++p;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bp[t] = fma(rv, a[t], bp[t]);
+      if (MODE == 1 && ((s % HREC_ALS_CH1) == HREC_ALS_CH1 - 1 || s + 1 == rem)) {
+#pragma unroll
+        for (int p2 = 0; p2 < NPAIR; ++p2) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) acc[p2][rr] += (double)fa[p2][rr];
+        }
+      }
+    }
+    if (stop || 16 * (w + 1) >= nsteps) break;
+    iw0 = iw1;
+    rw0 = rw1;
+    iw1 = iw2;
+    rw1 = rw2;
+  }
+  } else {
   int i0, i1;
   float r0, r1;
   load_iv(beg, i0, r0);
@@ -323,6 +443,7 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     i1 = i2;
     r1 = r2;
   }
+  }
 
   STAMP(1);  // phase 1: Gramian (gather + MFMA)
   // b: sum the four row-groups of lanes.
@@ -375,104 +496,12 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
       p += NT - I;
     }
   }
+  // The factor is stored UNIT-DIAGONAL: Ut[r][c] = U[r][c] / U[r][r] (row
+  // scaled), column-packed in LDS (Ut[tri(c) + r], r <= c), with the pivots
+  // d_r = U[r][r] in dsh. Then U^T y = b, U x = y become
+  //   Ut^T w = b,  v = D^-2 w,  Ut x = v        (w = D y)
+  // and each of the 2 x KP substitution steps is one broadcast + one masked fma.
   double myrd = 0.0;  // lane c keeps 1 / U[c][c]
-#if HREC_ALS_PANEL_ROLLED
-  auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
-  // Block rows J = 0..NT-1 in a ROLLED loop (one copy of the panel code);
-  // only the tile-register moves are specialised per J.
-#pragma unroll 1
-  for (int J = 0; J < NT; ++J) {
-    // (a) block row J -> LDS (only q <= c: the upper triangle)
-    auto write_row = [&](auto JC) {
-      constexpr int JJ = decltype(JC)::value;
-#pragma unroll
-      for (int K = JJ; K < NT; ++K) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int q = 16 * JJ + sub + 4 * rr, c = 16 * K + col;
-          if (q <= c) Up[tri(c) + q] = acc[pidx(JJ, K)][rr];
-        }
-      }
-    };
-    switch (J) {
-      case 0: write_row(std::integral_constant<int, 0>{}); break;
-      case 1: if constexpr (NT > 1) write_row(std::integral_constant<int, 1>{}); break;
-      case 2: if constexpr (NT > 2) write_row(std::integral_constant<int, 2>{}); break;
-      default: if constexpr (NT > 3) write_row(std::integral_constant<int, 3>{}); break;
-    }
-    __syncthreads();
-    // (b) lane c >= 16J owns column c of block row J
-    const int c = lane;
-    const int j0 = 16 * J;
-    const bool own = c >= j0 && c < KP;
-    double a[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int q = j0 + m;
-      a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
-    }
-    // (c) 16 pivots, right-looking, columns on lanes; the pivot row is
-    //     broadcast through LDS (wave-uniform ds_read_b128 pairs)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int pv = j0 + i;
-      const double piv = bcast(a[i], pv);
-      double rs = __builtin_amdgcn_rsq(piv);
-      rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
-      const double d = piv * rs;
-      a[i] = (c == pv) ? d : a[i] * rs;
-      myrd = (c == pv) ? rs : myrd;
-      if (i < 15) {
-        if (c < KP) colbuf[c] = a[i];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(colbuf + j0 + m0);
-          if (m0 > i) a[m0] = fma(-u.x, a[i], a[m0]);
-          a[m0 + 1] = fma(-u.y, a[i], a[m0 + 1]);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    // (d) U row block J -> LDS
-    if (own) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const int q = j0 + m;
-        if (q <= c) Up[tri(c) + q] = a[m];
-      }
-    }
-    __syncthreads();
-    // (e) U_JK (K > J) back into tile registers; (f) trailing MFMA update
-    auto trail = [&](auto JC) {
-      constexpr int JJ = decltype(JC)::value;
-#pragma unroll
-      for (int K = JJ + 1; K < NT; ++K) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) acc[pidx(JJ, K)][rr] = Up[tri(16 * K + col) + 16 * JJ + sub + 4 * rr];
-      }
-#pragma unroll
-      for (int K = JJ + 1; K < NT; ++K) {
-#pragma unroll
-        for (int M = K; M < NT; ++M) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-            acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(JJ, K)][rr], acc[pidx(JJ, M)][rr],
-                                                                    acc[pidx(K, M)], 0, 0, 0);
-        }
-      }
-    };
-    switch (J) {
-      case 0: trail(std::integral_constant<int, 0>{}); break;
-      case 1: if constexpr (NT > 1) trail(std::integral_constant<int, 1>{}); break;
-      case 2: if constexpr (NT > 2) trail(std::integral_constant<int, 2>{}); break;
-      default: if constexpr (NT > 3) trail(std::integral_constant<int, 3>{}); break;
-    }
-  }
-#else
   auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
 #pragma unroll
   for (int J = 0; J < NT; ++J) {
@@ -495,7 +524,9 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
       const int q = 16 * J + m;
       a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
     }
-    // (c) 16 pivots, right-looking, columns on lanes, v_readlane broadcasts
+    // (c) 16 pivots, right-looking, columns on lanes. The pivot row of U goes
+    //     to LDS once per pivot and comes back as wave-uniform ds_read_b128
+    //     pairs; row pv of Ut is written beside it.
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int pv = 16 * J + i;
@@ -503,55 +534,66 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
       double rs = __builtin_amdgcn_rsq(piv);
       rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
       const double d = piv * rs;
-      a[i] = (c == pv) ? d : a[i] * rs;
+      a[i] = (c == pv) ? d : a[i] * rs;  // U[pv][c]
       myrd = (c == pv) ? rs : myrd;
+      if (own && c > pv) Up[tri(c) + pv] = a[i] * rs;  // Ut[pv][c]
+      if (c == pv) dsh[pv] = d;
+      if (i < 15) {
+        if (c < KP) colbuf[c] = a[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-      for (int m = i + 1; m < 16; ++m) a[m] = fma(-bcast(a[i], 16 * J + m), a[i], a[m]);
-    }
-    // (d) U row block J -> LDS
-    if (own) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const int q = 16 * J + m;
-        if (q <= c) Up[tri(c) + q] = a[m];
+        for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
+          const double2 u = *reinterpret_cast<const double2*>(colbuf + 16 * J + m0);
+          if (m0 > i) a[m0] = fma(-u.x, a[i], a[m0]);
+          a[m0 + 1] = fma(-u.y, a[i], a[m0 + 1]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
       }
     }
     __syncthreads();
-    // (e) U_JK (K > J) back into tile registers; (f) trailing MFMA update
+    // (e) U_JK = D_J Ut_JK (K > J) back into tile registers; (f) trailing
+    //     update U_KM -= U_JK^T U_JM on the f64 matrix cores
+    if (J + 1 < NT) {
+      double dq[4];
 #pragma unroll
-    for (int K = J + 1; K < NT; ++K) {
+      for (int rr = 0; rr < 4; ++rr) dq[rr] = dsh[16 * J + sub + 4 * rr];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[pidx(J, K)][rr] = Up[tri(16 * K + col) + 16 * J + sub + 4 * rr];
-    }
-#pragma unroll
-    for (int K = J + 1; K < NT; ++K) {
-#pragma unroll
-      for (int M = K; M < NT; ++M) {
+      for (int K = J + 1; K < NT; ++K) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(J, K)][rr], acc[pidx(J, M)][rr],
-                                                                  acc[pidx(K, M)], 0, 0, 0);
+          acc[pidx(J, K)][rr] = Up[tri(16 * K + col) + 16 * J + sub + 4 * rr] * dq[rr];
+      }
+#pragma unroll
+      for (int K = J + 1; K < NT; ++K) {
+#pragma unroll
+        for (int M = K; M < NT; ++M) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(J, K)][rr], acc[pidx(J, M)][rr],
+                                                                    acc[pidx(K, M)], 0, 0, 0);
+        }
       }
     }
   }
-#endif
   STAMP(3);  // phase 3: factorisation
-  // forward  U^T y = b   (lane c: y_c = (b_c - sum_{q<c} U[q][c] y_q) / U[c][c])
+  // forward  Ut^T w = b   (step q: lanes c > q subtract Ut[q][c] * w_q)
   double bi = lane < KP ? bsh[lane] : 0.0;
 #pragma unroll HREC_ALS_SOLVE_UNROLL
   for (int q = 0; q < KP; ++q) {
-    const double uqc = (lane > q && lane < KP) ? Up[tri(lane) + q] : 0.0;
-    bi = (lane == q) ? bi * myrd : bi;
-    const double yq = bcast(bi, q);
-    bi = (lane > q) ? fma(-uqc, yq, bi) : bi;
+    const double u = Up[tri(lane < KP ? lane : KP - 1) + q];  // in bounds; used by lanes > q only
+    const double wq = bcast(bi, q);
+    if (lane > q) bi = fma(-u, wq, bi);
   }
-  // back     U x = y     (lane c: x_c = (y_c - sum_{q>c} U[c][q] x_q) / U[c][c])
+  bi *= myrd * myrd;  // v = D^-2 w
+  // back     Ut x = v     (step q: lanes c < q subtract Ut[c][q] * x_q)
 #pragma unroll HREC_ALS_SOLVE_UNROLL
   for (int q = KP - 1; q >= 0; --q) {
-    const double ucq = (lane < q) ? Up[tri(q) + lane] : 0.0;
-    bi = (lane == q) ? bi * myrd : bi;
+    const double u = Up[tri(q) + (lane < KP ? lane : 0)];  // Ut[lane][q] for lane < q
     const double xq = bcast(bi, q);
-    bi = (lane < q) ? fma(-ucq, xq, bi) : bi;
+    if (lane < q) bi = fma(-u, xq, bi);
   }
   STAMP(4);  // phase 4: triangular solves
   if (lane < KP) out[NT * (lane & 15) + (lane >> 4)] = (float)bi;
@@ -632,11 +674,12 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
   HREC_REQUIRE(indptr && dst_factors, "als_half_sweep: null pointer");
   HREC_REQUIRE(n_src > 0 && src_factors && indices && values,
                "als_half_sweep: null source factors / CSR arrays");
+  HREC_REQUIRE(n_src < 0x7fffffffll, "als_half_sweep: too many source rows for one launch");
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)n_rows), block(64);
 #define HREC_SWEEP(NT, CH, M)                                                                      \
   hipLaunchKernelGGL((als_half_sweep_f64_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
-                     n_rows, src_factors, k, reg_param, dst_factors)
+                     n_rows, src_factors, n_src, k, reg_param, dst_factors)
   if (accum_mode == 0) {
     if (kp == 64) HREC_SWEEP(4, HREC_ALS_CH0, 0);
     else if (kp == 32) HREC_SWEEP(2, 8, 0);

@@ -101,6 +101,30 @@ def test_half_sweep_matches_oracle(device, k, kp, mode):
     assert (got[0] == 0).all(), "a row without ratings has no factor"
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_half_sweep_window_boundaries(device, mode):
+    """Row lengths around every pipeline boundary of the kp=64 kernel (steps of
+    4 ratings, windows of 64, prefetch distance) and gathers of the first and
+    last source rows (the structured-buffer range check must keep them)."""
+    h = _hrec()
+    k, kp, n_src = 64, 64, 301
+    deg = np.array([0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65, 66, 67, 95, 96, 97,
+                    127, 128, 129, 130, 191, 192, 193, 255, 256, 257, 1000, 1023, 1024, 1025])
+    rng = np.random.default_rng(11)
+    indptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    indices = rng.integers(0, n_src, indptr[-1]).astype(np.int32)
+    indices[::7] = n_src - 1
+    indices[3::11] = 0
+    values = rng.integers(0, 19, indptr[-1]).astype(np.float32)
+    src = rng.normal(size=(n_src, kp)).astype(np.float32)
+    d_ip, d_ix, d_v = _csr_to_dev(indptr, indices, values, device)
+    dst = torch.full((len(deg), kp), 3.0, device=device)
+    h.als_half_sweep(d_ip, d_ix, d_v, torch.as_tensor(src, device=device), k, 0.1, dst, accum_mode=mode)
+    exp = obuild.half_sweep(indptr, indices, values, src, k, 0.1)
+    rtol, atol = (1e-5, 1e-6) if mode == 0 else (1e-4, 1e-5)
+    np.testing.assert_allclose(dst.cpu().numpy(), exp, rtol=rtol, atol=atol)
+
+
 def test_half_sweep_spark_literal_small(device):
     h = _hrec()
     indptr, indices, values, src = _problem(7, 12, 20, 10, 20, 16)
