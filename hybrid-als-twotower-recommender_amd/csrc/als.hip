@@ -26,22 +26,22 @@
 #define HREC_ALS_CH0 8
 #endif
 #ifndef HREC_ALS_ABLATE
-#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip the solve, 2 = skip the MFMA Gramian
-#endif
-#ifndef HREC_ALS_BCAST_LDS
-#define HREC_ALS_BCAST_LDS 1  // Cholesky column broadcast: 1 = LDS ds_read_b128, 0 = v_readlane
-#endif
-#ifndef HREC_ALS_FAST_RSQ
-#define HREC_ALS_FAST_RSQ 1  // pivot 1/sqrt by v_rsq_f64 + one Newton step (else sqrt + divide)
-#endif
-#ifndef HREC_ALS_SOLVE
-#define HREC_ALS_SOLVE 1  // 1 = blocked tile-layout Cholesky (MFMA trailing updates); 0 = row-per-lane
+#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip factor+solve, 3 = skip the substitutions
 #endif
 #ifndef HREC_ALS_SOLVE_UNROLL
 #define HREC_ALS_SOLVE_UNROLL 8  // unroll of the two 64-step triangular-solve loops
 #endif
 #ifndef HREC_ALS_CH1
 #define HREC_ALS_CH1 4
+#endif
+#ifndef HREC_ALS_PERSIST
+#define HREC_ALS_PERSIST 0  // 1 = persistent 8-wave blocks (rows strided over waves) ...
+#endif
+#ifndef HREC_ALS_STAGGER
+#define HREC_ALS_STAGGER 1  // PERSIST: waves 4-7 start half an average row late (SIMD partners out of phase)
+#endif
+#ifndef HREC_ALS_PRIO
+#define HREC_ALS_PRIO 3  // wave priority (s_setprio) during the factor/solve phase; 0 = off
 #endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
@@ -135,127 +135,48 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
-// Solve (L L^T) x = b for the SPD matrix held as a packed lower triangle in
-// LDS (row i at tri(i)), b_i in lane i. Right-looking Cholesky with the
-// matrix in REGISTERS: lane i owns row i (a[c] = A[i][c]); every column
-// broadcast is a v_readlane, so the O(k^3/6) update is pure VALU with static
-// register indices (fully unrolled) and no LDS traffic. Entries right of the
-// diagonal are never read, so lanes update them unmasked. The packed LDS
-// array is reused once to transpose L for the back substitution.
-template <int KP>
-__device__ __forceinline__ double solve_spd_rows_impl(double* __restrict__ A, double* __restrict__ col, double bi,
-                                                      int lane) {
-  STAMP_DECL;
-  STAMP(0);
-  const int i = lane < KP ? lane : KP - 1;
-  double a[KP];
-#pragma unroll
-  for (int c = 0; c < KP; ++c) {
-    const int hi = i > c ? i : c, lo = i > c ? c : i;
-    a[c] = A[tri(hi) + lo];
-  }
-  STAMP(4);  // phase 4: row load from LDS
-  double myrd = 0.0;  // lane j keeps 1 / L[j][j]
-#pragma unroll
-  for (int j = 0; j < KP; ++j) {
-    // pivot: lane j's diagonal is current (column j was updated first, via a
-    // readlane, at step j-1 — the short critical path of the factorisation)
-    const double piv = bcast(a[j], j);
-#if HREC_ALS_FAST_RSQ
-    double rs = __builtin_amdgcn_rsq(piv);
-    rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
-    const double d = piv * rs;
-#else
-    const double d = sqrt(piv);
-    const double rs = 1.0 / d;
-#endif
-    const double l = (lane == j) ? d : a[j] * rs;
-    a[j] = l;
-    myrd = (lane == j) ? rs : myrd;
-    if (j + 1 < KP) a[j + 1] = fma(-l, bcast(l, j + 1), a[j + 1]);
-#if HREC_ALS_BCAST_LDS
-    // remaining columns: column j of L to LDS once, then wave-uniform
-    // ds_read_b128 broadcasts (two entries per read), off the critical path.
-    if (j + 2 < KP) {
-      if (lane < KP) col[lane] = l;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int c0 = (j + 2) & ~1; c0 < KP; c0 += 2) {
-        const double2 lc = *reinterpret_cast<const double2*>(col + c0);
-        if (c0 > j + 1) a[c0] = fma(-l, lc.x, a[c0]);
-        a[c0 + 1] = fma(-l, lc.y, a[c0 + 1]);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-#else
-#pragma unroll
-    for (int c = j + 2; c < KP; ++c) a[c] = fma(-l, bcast(l, c), a[c]);
-#endif
-  }
-  STAMP(5);  // phase 5: factorisation
-  // forward: L y = b
-#pragma unroll
-  for (int j = 0; j < KP; ++j) {
-    const double yj = bcast(bi, j) * bcast(myrd, j);
-    const double upd = fma(-a[j], yj, bi);
-    bi = (lane == j) ? yj : ((lane > j) ? upd : bi);
-  }
-  STAMP(6);  // phase 6: forward substitution
-  // transpose L through LDS: lane i stores row i, then reads column i.
-  __syncthreads();
-  if (lane < KP) {
-#pragma unroll
-    for (int c = 0; c < KP; ++c)
-      if (c <= lane) A[tri(lane) + c] = a[c];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < KP; ++c) a[c] = (c >= i) ? A[tri(c) + i] : 0.0;  // a[c] = L[c][i]
-  // backward: L^T x = y
-#pragma unroll
-  for (int j = KP - 1; j >= 0; --j) {
-    const double xj = bcast(bi, j) * bcast(myrd, j);
-    const double upd = fma(-a[j], xj, bi);
-    bi = (lane == j) ? xj : ((lane < j) ? upd : bi);
-  }
-  STAMP(7);  // phase 7: transpose + back substitution
-  return bi;
+// Orders this wave's LDS accesses around a point (one wave owns each LDS
+// slice; a wave's LDS operations complete in issue order).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Per-wave LDS slice of the half-sweep (doubles).
+template <int KP>
+struct RowLds {
+  static constexpr int kUp = KP * (KP + 1) / 2;  // Ut, column-packed
+  // Up doubles as the MODE 1 re-layout stage (256); keep colbuf 16-B aligned
+  static constexpr int kUpPad = ((kUp > 256 ? kUp : 256) + 1) & ~1;
+  static constexpr int kSize = kUpPad + 128 + 3 * KP;
+};
+
+// One destination row on one wave (lane = 0..63), all scratch in `lds`.
 // NT floats per lane (kp = 16*NT), CH steps of 4 nnz per pipeline chunk.
 // MODE 0: v_mfma_f64_16x16x4_f64 accumulates the Gramian in f64 (Spark's
 //         f64 NormalEquation, any row length).
 // MODE 1: v_mfma_f32_16x16x4_f32 (2x the f64 matrix rate) accumulates each
-//         chunk of 4*CH ratings in f32 (an exact f32 fma chain), and the chunk
+//         chunk of 16 ratings in f32 (an exact f32 fma chain), and the chunk
 //         partials are flushed into f64 accumulators — f64 summation across
 //         chunks, f32 rounding only inside a chunk.
 template <int NT, int CH, int MODE>
-__global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
-    int k, double reg, float* __restrict__ dst) {
+__device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __restrict__ indptr,
+                                        const int32_t* __restrict__ indices, const float* __restrict__ values,
+                                        const float* __restrict__ src, int64_t n_src, int k, double reg,
+                                        float* __restrict__ dst, double* __restrict__ lds) {
   constexpr int KP = 16 * NT;
   constexpr int NPAIR = NT * (NT + 1) / 2;
   constexpr int CHN = 4 * CH;  // nnz per chunk (<= 64)
-#if HREC_ALS_SOLVE == 1
-  __shared__ double Up[KP * (KP + 1) / 2];  // U, column-packed: U[tri(c) + q], q <= c
-  __shared__ double stage[MODE == 1 ? 256 : 1];
-  __shared__ __attribute__((aligned(16))) double colbuf[64];
-  __shared__ double dsh[KP];  // pivots U[r][r]
-  double* A = nullptr;
-#else
-  __shared__ double A[KP * (KP + 1) / 2];
-  __shared__ __attribute__((aligned(16))) double colbuf[KP];
-#endif
-  __shared__ double bsh[KP];
+  double* __restrict__ Up = lds;
+  double* __restrict__ stage = lds;
+  double* __restrict__ colbuf = lds + RowLds<KP>::kUpPad;
+  double* __restrict__ dsh = colbuf + 128;  // pivots d_r (two 64-entry row buffers before)
+  double* __restrict__ rdsh = dsh + KP;    // 1 / d_r
+  double* __restrict__ bsh = rdsh + KP;
 
-  const int lane = threadIdx.x;
   const int sub = lane >> 4;  // which nnz of the step this lane loads
   const int col = lane & 15;  // which NT-column group
-  const int64_t row = blockIdx.x;
   const int64_t beg = indptr[row];
   const int64_t end = indptr[row + 1];
   const int64_t n = end - beg;
@@ -415,9 +336,7 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
       for (int I = 0; I < NT; ++I) {
 #pragma unroll
         for (int J = I; J < NT; ++J) {
-          if (HREC_ALS_ABLATE == 2) {
-            acc[p][0] += a[I] * a[J];  // ablation: no matrix cores
-          } else if (MODE == 0)
+          if (MODE == 0)
             acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
           else
             fa[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(buf[s].x[I], buf[s].x[J], fa[p], 0, 0, 0);
@@ -446,13 +365,17 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
   }
 
   STAMP(1);  // phase 1: Gramian (gather + MFMA)
+  // The factor/solve phase is a latency-bound chain of f64 VALU ops, which
+  // cannot issue while the SIMD partner's f64 MFMAs hold the pipe; without a
+  // priority boost it starves behind the partner's Gramian and the two waves'
+  // solves end up serialised with an idle matrix core.
+  if (HREC_ALS_PRIO) __builtin_amdgcn_s_setprio(HREC_ALS_PRIO);
   // b: sum the four row-groups of lanes.
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     bp[t] += __shfl_xor(bp[t], 16, kWave);
     bp[t] += __shfl_xor(bp[t], 32, kWave);
   }
-#if HREC_ALS_SOLVE == 1
   // ---- blocked Cholesky in the matrix-core tile layout -------------------
   // Work in the permuted basis q = 16*T + m  <->  physical column NT*m + T:
   // tile (I,J) of the accumulators is then block (I,J) of the permuted
@@ -463,9 +386,7 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
   // fully in registers), then the trailing update of every later block
   // U_KM -= U_JK^T U_JM on the f64 matrix cores, straight from the
   // accumulator registers (the C/D layout of tile (J,K) is exactly the A/B
-  // operand layout of the 4 k-steps). U accumulates, column-packed, in LDS
-  // (U[tri(c) + q], q <= c) for the two triangular solves.
-  (void)A;
+  // operand layout of the 4 k-steps).
   if (sub == 0) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) bsh[16 * t + col] = bp[t];  // permuted b
@@ -476,10 +397,10 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     for (int p = 0; p < NPAIR; ++p) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) stage[(4 * sub + rr) * 16 + col] = acc[p][rr];
-      __syncthreads();
+      wave_lds_sync();
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) acc[p][rr] = stage[(sub + 4 * rr) * 16 + col];
-      __syncthreads();
+      wave_lds_sync();
     }
   }
   STAMP(2);  // phase 2: b + layout
@@ -496,12 +417,19 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
       p += NT - I;
     }
   }
-  // The factor is stored UNIT-DIAGONAL: Ut[r][c] = U[r][c] / U[r][r] (row
-  // scaled), column-packed in LDS (Ut[tri(c) + r], r <= c), with the pivots
-  // d_r = U[r][r] in dsh. Then U^T y = b, U x = y become
-  //   Ut^T w = b,  v = D^-2 w,  Ut x = v        (w = D y)
+  if constexpr (HREC_ALS_ABLATE == 1) {  // timing-only: Gramian without factor/solve
+    double sum = 0.0;
+#pragma unroll
+    for (int p = 0; p < NPAIR; ++p) sum += acc[p][0] + acc[p][1] + acc[p][2] + acc[p][3];
+    wave_lds_sync();
+    if (lane < KP) out[lane] = (float)(sum + bsh[lane]);
+    return;
+  }
+  // A = Ut^T D Ut with Ut unit upper triangular, stored column-packed in LDS
+  // (Ut[tri(c) + r], r <= c), pivots d_r in dsh and 1/d_r in rdsh. A x = b is
+  //   Ut^T w = b,  v = D^-1 w,  Ut x = v
   // and each of the 2 x KP substitution steps is one broadcast + one masked fma.
-  double myrd = 0.0;  // lane c keeps 1 / U[c][c]
+  // (Spark's dppsv factors A = U^T U with U = D^1/2 Ut: the same solution.)
   auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
 #pragma unroll
   for (int J = 0; J < NT; ++J) {
@@ -514,7 +442,7 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
         if (q <= c) Up[tri(c) + q] = acc[pidx(J, K)][rr];
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     // (b) lane c >= 16J owns column c of block row J
     const int c = lane;
     const bool own = c >= 16 * J && c < KP;
@@ -524,47 +452,54 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
       const int q = 16 * J + m;
       a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
     }
-    // (c) 16 pivots, right-looking, columns on lanes. The pivot row of U goes
-    //     to LDS once per pivot and comes back as wave-uniform ds_read_b128
-    //     pairs; row pv of Ut is written beside it.
+    // (c) 16 pivots of A = Ut^T D Ut (LDL^T: no square roots), right-looking,
+    //     columns on lanes. The unscaled pivot row goes to LDS (alternating
+    //     buffers) and comes back as wave-uniform ds_read_b128 pairs; the next
+    //     pivot is formed on its own lane ahead of that round trip (its update
+    //     needs only the lane's own entries), so the per-pivot critical path is
+    //     rcp -> Newton -> scale -> fma -> readlane.
+    double piv = bcast(a[0], 16 * J);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int pv = 16 * J + i;
-      const double piv = bcast(a[i], pv);
-      double rs = __builtin_amdgcn_rsq(piv);
-      rs = rs * fma(-0.5 * piv * rs, rs, 1.5);  // one Newton step: full f64 precision
-      const double d = piv * rs;
-      a[i] = (c == pv) ? d : a[i] * rs;  // U[pv][c]
-      myrd = (c == pv) ? rs : myrd;
-      if (own && c > pv) Up[tri(c) + pv] = a[i] * rs;  // Ut[pv][c]
-      if (c == pv) dsh[pv] = d;
+      double* cb = colbuf + 64 * (i & 1);
+      if (c < KP) cb[c] = a[i];  // A[pv][c] (lane pv: the pivot)
+      // 1 / piv: v_rcp_f64 (~2^-24 relative) + one Newton step
+      const double r0 = __builtin_amdgcn_rcp(piv);
+      const double r = fma(r0, fma(-piv, r0, 1.0), r0);
+      const double ut = a[i] * r;  // Ut[pv][c]
+      if (own && c > pv) Up[tri(c) + pv] = ut;
+      if (c == pv) {
+        dsh[pv] = piv;
+        rdsh[pv] = r;
+      }
       if (i < 15) {
-        if (c < KP) colbuf[c] = a[i];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        piv = bcast(fma(-a[i], ut, a[i + 1]), pv + 1);
+        wave_lds_sync();
 #pragma unroll
         for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(colbuf + 16 * J + m0);
-          if (m0 > i) a[m0] = fma(-u.x, a[i], a[m0]);
-          a[m0 + 1] = fma(-u.y, a[i], a[m0 + 1]);
+          const double2 u = *reinterpret_cast<const double2*>(cb + 16 * J + m0);
+          if (m0 > i) a[m0] = fma(-u.x, ut, a[m0]);
+          a[m0 + 1] = fma(-u.y, ut, a[m0 + 1]);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
       }
     }
-    __syncthreads();
-    // (e) U_JK = D_J Ut_JK (K > J) back into tile registers; (f) trailing
-    //     update U_KM -= U_JK^T U_JM on the f64 matrix cores
+    wave_lds_sync();
+    // (e) Ut_JK (K > J) back into tile registers, with a D_J-scaled copy;
+    // (f) trailing update A_KM -= Ut_JK^T D_J Ut_JM on the f64 matrix cores
     if (J + 1 < NT) {
       double dq[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) dq[rr] = dsh[16 * J + sub + 4 * rr];
+      d4 yv[NT];
 #pragma unroll
       for (int K = J + 1; K < NT; ++K) {
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          acc[pidx(J, K)][rr] = Up[tri(16 * K + col) + 16 * J + sub + 4 * rr] * dq[rr];
+        for (int rr = 0; rr < 4; ++rr) {
+          const double x = Up[tri(16 * K + col) + 16 * J + sub + 4 * rr];
+          acc[pidx(J, K)][rr] = x;
+          yv[K][rr] = x * dq[rr];
+        }
       }
 #pragma unroll
       for (int K = J + 1; K < NT; ++K) {
@@ -572,22 +507,28 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
         for (int M = K; M < NT; ++M) {
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr)
-            acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(J, K)][rr], acc[pidx(J, M)][rr],
+            acc[pidx(K, M)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[pidx(J, K)][rr], yv[M][rr],
                                                                     acc[pidx(K, M)], 0, 0, 0);
         }
       }
     }
   }
   STAMP(3);  // phase 3: factorisation
+  const int lc = lane < KP ? lane : KP - 1;
+  const double myrd = rdsh[lc];
+  if constexpr (HREC_ALS_ABLATE == 3) {  // timing-only: factor without the substitutions
+    if (lane < KP) out[lane] = (float)(myrd + Up[tri(lane)]);
+    return;
+  }
   // forward  Ut^T w = b   (step q: lanes c > q subtract Ut[q][c] * w_q)
   double bi = lane < KP ? bsh[lane] : 0.0;
 #pragma unroll HREC_ALS_SOLVE_UNROLL
   for (int q = 0; q < KP; ++q) {
-    const double u = Up[tri(lane < KP ? lane : KP - 1) + q];  // in bounds; used by lanes > q only
+    const double u = Up[tri(lc) + q];  // in bounds; used by lanes > q only
     const double wq = bcast(bi, q);
     if (lane > q) bi = fma(-u, wq, bi);
   }
-  bi *= myrd * myrd;  // v = D^-2 w
+  bi *= myrd;  // v = D^-1 w
   // back     Ut x = v     (step q: lanes c < q subtract Ut[c][q] * x_q)
 #pragma unroll HREC_ALS_SOLVE_UNROLL
   for (int q = KP - 1; q >= 0; --q) {
@@ -597,47 +538,41 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
   }
   STAMP(4);  // phase 4: triangular solves
   if (lane < KP) out[NT * (lane & 15) + (lane >> 4)] = (float)bi;
+  if (HREC_ALS_PRIO) __builtin_amdgcn_s_setprio(0);
+  wave_lds_sync();  // the next row on this wave reuses the LDS slice
 }
-#else
-  if (sub == 0) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) bsh[NT * col + t] = bp[t];
-  }
-  // Gramian -> packed lower triangle. C/D maps: f64 16x16x4 col = lane&15,
-  // row = (lane>>4) + 4*reg; f32 16x16x4 col = lane&15, row = 4*(lane>>4) + reg.
-  {
-    int p = 0;
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-#pragma unroll
-      for (int J = I; J < NT; ++J) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int pr = NT * (MODE == 0 ? sub + 4 * rr : 4 * sub + rr) + I;  // physical row
-          const int qc = NT * col + J;             // physical column
-          const double v = acc[p][rr];
-          if (I != J || pr >= qc) {
-            const int hi = pr > qc ? pr : qc;
-            const int lo = pr > qc ? qc : pr;
-            A[tri(hi) + lo] = v;
-          }
-        }
-        ++p;
-      }
-    }
-  }
-  __syncthreads();
 
-  STAMP(2);  // phase 2: b reduce + Gramian -> LDS
-  // Spark CholeskySolver: ata[diag] += numExplicits * regParam.
-  const double lambda = (double)n * reg;
-  if (lane < KP) A[tri(lane) + lane] += (lane < k) ? lambda : 1.0;
-  const double b_in = lane < KP ? bsh[lane] : 0.0;
-  __syncthreads();
-  const double x = HREC_ALS_ABLATE == 1 ? b_in + A[tri(lane < KP ? lane : 0)] : solve_spd_rows_impl<KP>(A, colbuf, b_in, lane);
-  if (lane < KP) out[lane] = (float)x;
+// One wave per destination row.
+template <int NT, int CH, int MODE>
+__global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
+    int k, double reg, float* __restrict__ dst) {
+  __shared__ __attribute__((aligned(16))) double lds[RowLds<16 * NT>::kSize];
+  als_row<NT, CH, MODE>(blockIdx.x, threadIdx.x, indptr, indices, values, src, n_src, k, reg, dst, lds);
 }
-#endif
+
+// Persistent variant: 8 waves per block (two per SIMD), rows strided over
+// all waves of the grid. With STAGGER, waves 4-7 — the SIMD partners of
+// waves 0-3 — start half an average row late, so the partners' latency-bound
+// factor/solve phases fall inside the other's matrix-core-bound Gramian.
+template <int NT, int CH, int MODE>
+__global__ __launch_bounds__(512) void als_half_sweep_persist_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
+    int k, double reg, float* __restrict__ dst) {
+  constexpr int L = RowLds<16 * NT>::kSize;
+  __shared__ __attribute__((aligned(16))) double lds[8 * L];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (HREC_ALS_STAGGER && w >= 4) {
+    // half the Gramian time of an average row: ~680 cycles per step of 4
+    const int64_t avg_steps = ((indptr[n_rows] - indptr[0]) / (n_rows > 0 ? n_rows : 1) + 3) / 4;
+    const int64_t cyc = avg_steps * 340;
+    for (int64_t t = 0; t < cyc; t += 64 * 120) __builtin_amdgcn_s_sleep(120);
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 8 + w; row < n_rows; row += (int64_t)gridDim.x * 8)
+    als_row<NT, CH, MODE>(row, lane, indptr, indices, values, src, n_src, k, reg, dst, lds + w * L);
+}
 
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int64_t rows,
                                                         int64_t cols, float* __restrict__ out, int64_t ld_out) {
@@ -676,10 +611,20 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
                "als_half_sweep: null source factors / CSR arrays");
   HREC_REQUIRE(n_src < 0x7fffffffll, "als_half_sweep: too many source rows for one launch");
   hipStream_t s = as_stream(stream);
+#if HREC_ALS_PERSIST
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t nb = (n_rows + 7) / 8;
+  const dim3 grid((unsigned)(nb < cus ? nb : cus)), block(512);
+#define HREC_SWEEP(NT, CH, M)                                                                          \
+  hipLaunchKernelGGL((als_half_sweep_persist_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
+                     n_rows, src_factors, n_src, k, reg_param, dst_factors)
+#else
   const dim3 grid((unsigned)n_rows), block(64);
 #define HREC_SWEEP(NT, CH, M)                                                                      \
   hipLaunchKernelGGL((als_half_sweep_f64_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
                      n_rows, src_factors, n_src, k, reg_param, dst_factors)
+#endif
   if (accum_mode == 0) {
     if (kp == 64) HREC_SWEEP(4, HREC_ALS_CH0, 0);
     else if (kp == 32) HREC_SWEEP(2, 8, 0);
