@@ -34,14 +34,8 @@
 #ifndef HREC_ALS_CH1
 #define HREC_ALS_CH1 4
 #endif
-#ifndef HREC_ALS_PERSIST
-#define HREC_ALS_PERSIST 0  // 1 = persistent 8-wave blocks (rows strided over waves) ...
-#endif
-#ifndef HREC_ALS_STAGGER
-#define HREC_ALS_STAGGER 1  // PERSIST: waves 4-7 start half an average row late (SIMD partners out of phase)
-#endif
-#ifndef HREC_ALS_PRIO
-#define HREC_ALS_PRIO 3  // wave priority (s_setprio) during the factor/solve phase; 0 = off
+#ifndef HREC_ALS_SPLIT
+#define HREC_ALS_SPLIT 0  // 1 = producer/consumer kernel (Gramian waves hand rows to factor/solve waves)
 #endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
@@ -152,7 +146,8 @@ struct RowLds {
   static constexpr int kSize = kUpPad + 128 + 3 * KP;
 };
 
-// One destination row on one wave (lane = 0..63), all scratch in `lds`.
+// Gramian + rhs of one destination row on one wave (lane = 0..63):
+// acc = sum_j v_j v_j^T (tile layout, + n*reg on the diagonal), b -> bsh.
 // NT floats per lane (kp = 16*NT), CH steps of 4 nnz per pipeline chunk.
 // MODE 0: v_mfma_f64_16x16x4_f64 accumulates the Gramian in f64 (Spark's
 //         f64 NormalEquation, any row length).
@@ -161,34 +156,19 @@ struct RowLds {
 //         partials are flushed into f64 accumulators — f64 summation across
 //         chunks, f32 rounding only inside a chunk.
 template <int NT, int CH, int MODE>
-__device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __restrict__ indptr,
-                                        const int32_t* __restrict__ indices, const float* __restrict__ values,
-                                        const float* __restrict__ src, int64_t n_src, int k, double reg,
-                                        float* __restrict__ dst, double* __restrict__ lds) {
+__device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, const int32_t* __restrict__ indices,
+                                         const float* __restrict__ values, const float* __restrict__ src,
+                                         int64_t n_src, int k, double reg, d4 (&acc)[NT * (NT + 1) / 2],
+                                         double* __restrict__ bsh, double* __restrict__ stage) {
   constexpr int KP = 16 * NT;
   constexpr int NPAIR = NT * (NT + 1) / 2;
   constexpr int CHN = 4 * CH;  // nnz per chunk (<= 64)
-  double* __restrict__ Up = lds;
-  double* __restrict__ stage = lds;
-  double* __restrict__ colbuf = lds + RowLds<KP>::kUpPad;
-  double* __restrict__ dsh = colbuf + 128;  // pivots d_r (two 64-entry row buffers before)
-  double* __restrict__ rdsh = dsh + KP;    // 1 / d_r
-  double* __restrict__ bsh = rdsh + KP;
-
   const int sub = lane >> 4;  // which nnz of the step this lane loads
   const int col = lane & 15;  // which NT-column group
-  const int64_t beg = indptr[row];
-  const int64_t end = indptr[row + 1];
   const int64_t n = end - beg;
-  float* __restrict__ out = dst + row * KP;
-  if (n == 0) {
-    if (lane < KP) out[lane] = 0.f;
-    return;
-  }
 
   STAMP_DECL;
   STAMP(0);
-  d4 acc[NPAIR];
 #pragma unroll
   for (int p = 0; p < NPAIR; ++p) acc[p] = d4{0.0, 0.0, 0.0, 0.0};
   f4 fa[NPAIR];
@@ -365,11 +345,6 @@ __device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __
   }
 
   STAMP(1);  // phase 1: Gramian (gather + MFMA)
-  // The factor/solve phase is a latency-bound chain of f64 VALU ops, which
-  // cannot issue while the SIMD partner's f64 MFMAs hold the pipe; without a
-  // priority boost it starves behind the partner's Gramian and the two waves'
-  // solves end up serialised with an idle matrix core.
-  if (HREC_ALS_PRIO) __builtin_amdgcn_s_setprio(HREC_ALS_PRIO);
   // b: sum the four row-groups of lanes.
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -417,6 +392,23 @@ __device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __
       p += NT - I;
     }
   }
+}
+
+// Factor + solve of one row's normal equations on one wave: acc (tile layout,
+// consumed), b in bsh; Ut in Up (KP(KP+1)/2), row buffers and pivots in
+// scratch (128 + 2 KP); x -> out[0..KP).
+template <int NT>
+__device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2], double* __restrict__ Up,
+                                           double* __restrict__ scratch, const double* __restrict__ bsh,
+                                           float* __restrict__ out) {
+  constexpr int KP = 16 * NT;
+  constexpr int NPAIR = NT * (NT + 1) / 2;
+  double* __restrict__ colbuf = scratch;    // two 64-entry row buffers (16-B aligned)
+  double* __restrict__ dsh = colbuf + 128;  // pivots d_r
+  double* __restrict__ rdsh = dsh + KP;     // 1 / d_r
+  const int sub = lane >> 4, col = lane & 15;
+  STAMP_DECL;
+  STAMP(0);
   if constexpr (HREC_ALS_ABLATE == 1) {  // timing-only: Gramian without factor/solve
     double sum = 0.0;
 #pragma unroll
@@ -538,8 +530,29 @@ __device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __
   }
   STAMP(4);  // phase 4: triangular solves
   if (lane < KP) out[NT * (lane & 15) + (lane >> 4)] = (float)bi;
-  if (HREC_ALS_PRIO) __builtin_amdgcn_s_setprio(0);
   wave_lds_sync();  // the next row on this wave reuses the LDS slice
+}
+
+
+// One destination row on one wave (lane = 0..63), all scratch in `lds`.
+template <int NT, int CH, int MODE>
+__device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __restrict__ indptr,
+                                        const int32_t* __restrict__ indices, const float* __restrict__ values,
+                                        const float* __restrict__ src, int64_t n_src, int k, double reg,
+                                        float* __restrict__ dst, double* __restrict__ lds) {
+  constexpr int KP = 16 * NT;
+  const int64_t beg = indptr[row];
+  const int64_t end = indptr[row + 1];
+  float* __restrict__ out = dst + row * KP;
+  if (end == beg) {
+    if (lane < KP) out[lane] = 0.f;
+    return;
+  }
+  d4 acc[NT * (NT + 1) / 2];
+  double* scratch = lds + RowLds<KP>::kUpPad;
+  double* bsh = scratch + 128 + 2 * KP;
+  gram_row<NT, CH, MODE>(beg, end, lane, indices, values, src, n_src, k, reg, acc, bsh, lds);
+  factor_row<NT>(lane, acc, lds, scratch, bsh, out);
 }
 
 // One wave per destination row.
@@ -552,26 +565,113 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
   als_row<NT, CH, MODE>(blockIdx.x, threadIdx.x, indptr, indices, values, src, n_src, k, reg, dst, lds);
 }
 
-// Persistent variant: 8 waves per block (two per SIMD), rows strided over
-// all waves of the grid. With STAGGER, waves 4-7 — the SIMD partners of
-// waves 0-3 — start half an average row late, so the partners' latency-bound
-// factor/solve phases fall inside the other's matrix-core-bound Gramian.
+// Producer/consumer variant: one block of 8 waves per CU. Wave p (0..3)
+// computes Gramians (matrix-core bound) and hands each row's normal equations
+// to its SIMD partner, wave p + 4, through a double-buffered LDS slot; the
+// partner factors and solves (latency-bound f64 VALU chain) while the
+// producer already accumulates the next row. Rows are claimed dynamically
+// from a device counter (zeroed by the launcher), one row ahead.
+template <int KP>
+struct SplitLds {
+  static constexpr int kUp = RowLds<KP>::kUpPad;
+  static constexpr int kSlot = kUp + KP;               // Gramian/Ut + b
+  static constexpr int kPair = 2 * kSlot + 128 + 2 * KP;  // two slots + consumer scratch
+  static constexpr int kSize = 4 * kPair;
+};
+
 template <int NT, int CH, int MODE>
-__global__ __launch_bounds__(512) void als_half_sweep_persist_kernel(
+__global__ __launch_bounds__(512) void als_half_sweep_split_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
-    int k, double reg, float* __restrict__ dst) {
-  constexpr int L = RowLds<16 * NT>::kSize;
-  __shared__ __attribute__((aligned(16))) double lds[8 * L];
+    int k, double reg, float* __restrict__ dst, unsigned long long* __restrict__ counter) {
+  constexpr int KP = 16 * NT;
+  constexpr int NPAIR = NT * (NT + 1) / 2;
+  using L = SplitLds<KP>;
+  __shared__ __attribute__((aligned(16))) double lds[L::kSize];
+  __shared__ int state[8];      // per slot: 0 empty, 1 full
+  __shared__ int64_t slot_row[8];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (HREC_ALS_STAGGER && w >= 4) {
-    // half the Gramian time of an average row: ~680 cycles per step of 4
-    const int64_t avg_steps = ((indptr[n_rows] - indptr[0]) / (n_rows > 0 ? n_rows : 1) + 3) / 4;
-    const int64_t cyc = avg_steps * 340;
-    for (int64_t t = 0; t < cyc; t += 64 * 120) __builtin_amdgcn_s_sleep(120);
+  const int pair = w & 3;
+  if (threadIdx.x < 8) state[threadIdx.x] = 0;
+  __syncthreads();
+  double* base = lds + pair * L::kPair;
+  auto slot_up = [&](int sl) { return base + sl * L::kSlot; };
+  auto slot_b = [&](int sl) { return base + sl * L::kSlot + L::kUp; };
+  int* st = state + 2 * pair;
+  int64_t* srow = slot_row + 2 * pair;
+  const int sub = lane >> 4, col = lane & 15;
+  auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
+
+  if (w < 4) {  // ---------------- producer: Gramians
+    auto fetch = [&]() -> int64_t {
+      unsigned long long v = 0;
+      if (lane == 0) v = atomicAdd(counter, 1ull);
+      return (int64_t)__builtin_amdgcn_readfirstlane((int)v) |
+             ((int64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
+    };
+    int sl = 0;
+    int64_t row = fetch();
+    while (true) {
+      const int64_t next = fetch();
+      while (__hip_atomic_load(&st[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+        __builtin_amdgcn_s_sleep(1);
+      if (row >= n_rows) {
+        srow[sl] = -1;
+        __hip_atomic_store(&st[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      const int64_t beg = indptr[row], end = indptr[row + 1];
+      if (end == beg) {
+        if (lane < KP) dst[row * KP + lane] = 0.f;
+        row = next;
+        continue;
+      }
+      d4 acc[NPAIR];
+      double* up = slot_up(sl);
+      gram_row<NT, CH, MODE>(beg, end, lane, indices, values, src, n_src, k, reg, acc, slot_b(sl), up);
+      // all tiles -> the slot (upper triangle, column-packed)
+#pragma unroll
+      for (int J = 0; J < NT; ++J) {
+#pragma unroll
+        for (int K = J; K < NT; ++K) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int q = 16 * J + sub + 4 * rr, c = 16 * K + col;
+            if (q <= c) up[tri(c) + q] = acc[pidx(J, K)][rr];
+          }
+        }
+      }
+      if (lane == 0) srow[sl] = row;
+      __hip_atomic_store(&st[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      sl ^= 1;
+      row = next;
+    }
+  } else {  // ---------------- consumer: factor + solve
+    double* scratch = base + 2 * L::kSlot;
+    int sl = 0;
+    while (true) {
+      while (__hip_atomic_load(&st[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 1)
+        __builtin_amdgcn_s_sleep(1);
+      const int64_t row = srow[sl];
+      if (row < 0) break;
+      double* up = slot_up(sl);
+      d4 acc[NPAIR];
+#pragma unroll
+      for (int J = 0; J < NT; ++J) {
+#pragma unroll
+        for (int K = J; K < NT; ++K) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int q = 16 * J + sub + 4 * rr, c = 16 * K + col;
+            acc[pidx(J, K)][rr] = q <= c ? up[tri(c) + q] : 0.0;
+          }
+        }
+      }
+      factor_row<NT>(lane, acc, up, scratch, slot_b(sl), dst + row * KP);
+      __hip_atomic_store(&st[sl], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      sl ^= 1;
+    }
   }
-  for (int64_t row = (int64_t)blockIdx.x * 8 + w; row < n_rows; row += (int64_t)gridDim.x * 8)
-    als_row<NT, CH, MODE>(row, lane, indptr, indices, values, src, n_src, k, reg, dst, lds + w * L);
 }
 
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int64_t rows,
@@ -595,6 +695,24 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
 
 using namespace hrec;
 
+#if HREC_ALS_SPLIT
+#include <mutex>
+#include <vector>
+// One 8-byte row counter per (device, stream), allocated on first use and
+// kept for the life of the process; zeroed on the stream before each launch.
+static unsigned long long* row_counter(int dev, hipStream_t s) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<int, hipStream_t>, unsigned long long*>> pool;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& e : pool)
+    if (e.first.first == dev && e.first.second == s) return e.second;
+  unsigned long long* p = nullptr;
+  if (hipMalloc(&p, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  pool.push_back({{dev, s}, p});
+  return p;
+}
+#endif
+
 extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices, const float* values,
                                    int64_t n_rows, const float* src_factors, int64_t n_src, int k,
                                    int kp, double reg_param, int accum_mode, float* dst_factors,
@@ -611,14 +729,16 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
                "als_half_sweep: null source factors / CSR arrays");
   HREC_REQUIRE(n_src < 0x7fffffffll, "als_half_sweep: too many source rows for one launch");
   hipStream_t s = as_stream(stream);
-#if HREC_ALS_PERSIST
+#if HREC_ALS_SPLIT
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t nb = (n_rows + 7) / 8;
-  const dim3 grid((unsigned)(nb < cus ? nb : cus)), block(512);
-#define HREC_SWEEP(NT, CH, M)                                                                          \
-  hipLaunchKernelGGL((als_half_sweep_persist_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
-                     n_rows, src_factors, n_src, k, reg_param, dst_factors)
+  unsigned long long* counter = row_counter(dev, s);
+  HREC_REQUIRE(counter != nullptr, "als_half_sweep: cannot allocate the row counter");
+  if (hipMemsetAsync(counter, 0, sizeof(unsigned long long), s) != hipSuccess) return check_launch("als_half_sweep: counter reset");
+  const dim3 grid((unsigned)cus), block(512);
+#define HREC_SWEEP(NT, CH, M)                                                                        \
+  hipLaunchKernelGGL((als_half_sweep_split_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
+                     n_rows, src_factors, n_src, k, reg_param, dst_factors, counter)
 #else
   const dim3 grid((unsigned)n_rows), block(64);
 #define HREC_SWEEP(NT, CH, M)                                                                      \
