@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ingest", dest="ingest", action="store_false",
+                    help="skip the COO -> CSR/CSC ingest measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_prof_summary.json"),
                     help="rocprofv3 PMC summary (scripts/gpu_profile.sh) for roofline.traffic")
     ap.add_argument("--accum-mode", type=int, default=0, choices=[0, 1],
@@ -231,6 +233,37 @@ def main():
                   "top_k": 5, "d": d, "items_sharded_over": world,
                   "steps": "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5"}
 
+    # Ingest (§8(f) row 1, ALSModel.train's DataFrame -> CSR/CSC step): the
+    # rank's user shard as COO columns (int64 ids, ratings) -> id codes +
+    # CSR + CSC on the device (hrec_encode_ids x2, hrec_coo_to_csr x2).
+    ingest = None
+    if rank == 0 and args.ingest:
+        counts = csr.indptr[1:] - csr.indptr[:-1]
+        uid = torch.repeat_interleave(torch.arange(u0, u0 + u_per, dtype=torch.int64, device="cuda"), counts)
+        iid = csr.indices.to(torch.int64)
+        vals = csr.values
+
+        def run_ingest():
+            _, urow = _hrec.encode_ids(uid, (u0, u0 + u_per - 1))
+            iu, irow = _hrec.encode_ids(iid, (0, n_items - 1))
+            a = _hrec.coo_to_csr(urow, irow, vals, u_per)
+            b = _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()))
+            return a, b
+
+        run_ingest()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        out = run_ingest()
+        torch.cuda.synchronize()
+        gs = time.perf_counter() - g0
+        ok = bool(torch.equal(out[0][0], csr.indptr) and torch.equal(out[0][1], csr.indices))
+        ingest = {"ratings_per_s": csr.nnz / gs, "ms": gs * 1e3, "ratings": csr.nnz,
+                  "steps": ("encode user ids + encode item ids (radix sort on the id range + scan) + CSR + CSC "
+                            "(stable radix sort)"),
+                  "csr_matches_generator": ok}
+        del uid, iid, out
+        torch.cuda.empty_cache()
+
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.accum_mode == 0:
         with open(args.traffic_json) as f:
@@ -281,6 +314,7 @@ def main():
             "cpu_baseline": cpu,
             "scoring": scoring,
             "hybrid_top5": hybrid,
+            "ingest": ingest,
         }
         print(json.dumps(line))
     if world > 1:

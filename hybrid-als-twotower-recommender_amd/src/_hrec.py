@@ -29,6 +29,12 @@ _SIGNATURES = {
                                  _vp, _vp, _vp, _vp]),
     "hrec_scan_workspace_bytes": (_c_sz, [_c_i64]),
     "hrec_exclusive_scan_i64": (_c_i32, [_vp, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "hrec_encode_ids_workspace_bytes": (_c_sz, [_c_i64]),
+    "hrec_encode_ids": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_minmax_i64_workspace_bytes": (_c_sz, [_c_i64]),
+    "hrec_minmax_i64": (_c_i32, [_vp, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "hrec_coo_to_csr_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hrec_coo_to_csr": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_als_init_factors": (_c_i32, [_c_u64, _c_i64, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_als_half_sweep": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl,
                                      _c_i32, _vp, _vp]),
@@ -161,6 +167,58 @@ def exclusive_scan(counts):
         _dev(counts, torch.int64, "counts"), n, _dev(out, torch.int64, "out"),
         _dev(ws, torch.uint8, "ws"), ws.numel(), _stream()))
     return out
+
+
+# ----------------------------------------------------------------- ingest
+def minmax_i64(x):
+    """(min, max) of a non-empty int64 device tensor (host ints)."""
+    n = x.numel()
+    out = torch.empty(2, dtype=torch.int64, device=x.device)
+    ws = torch.empty(max(int(lib().hrec_minmax_i64_workspace_bytes(n)), 16), dtype=torch.uint8, device=x.device)
+    _check("hrec_minmax_i64", lib().hrec_minmax_i64(
+        _dev(x, torch.int64, "x"), n, _dev(out, torch.int64, "out"), _dev(ws, torch.uint8, "ws"), ws.numel(),
+        _stream()))
+    lo, hi = out.tolist()
+    return lo, hi
+
+
+def encode_ids(ids, id_range=None):
+    """numpy.unique(ids, return_inverse=True) on the device: ids int64[n] ->
+    (sorted distinct ids int64[m], codes int32[n]). id_range = (lo, hi) with
+    lo <= ids <= hi if known; else it is measured on the device first."""
+    n = ids.numel()
+    dev = ids.device
+    uniq = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    codes = torch.empty(n, dtype=torch.int32, device=dev)
+    n_uniq = torch.zeros(1, dtype=torch.int64, device=dev)
+    if n == 0:
+        return uniq[:0], codes
+    lo, hi = minmax_i64(ids) if id_range is None else (int(id_range[0]), int(id_range[1]))
+    ws = torch.empty(max(int(lib().hrec_encode_ids_workspace_bytes(n)), 16), dtype=torch.uint8, device=dev)
+    _check("hrec_encode_ids", lib().hrec_encode_ids(
+        _dev(ids, torch.int64, "ids"), n, lo, hi, _dev(uniq, torch.int64, "uniq"),
+        _dev(n_uniq, torch.int64, "n_uniq"), _dev(codes, torch.int32, "codes"), _dev(ws, torch.uint8, "ws"),
+        ws.numel(), _stream()))
+    return uniq[: int(n_uniq.item())], codes
+
+
+def coo_to_csr(rows, cols, vals, n_rows):
+    """(indptr int64[n_rows+1], indices int32[nnz], values f32[nnz]) of the COO
+    (rows, cols, vals), rows ascending, a row's entries in input order."""
+    nnz = rows.numel()
+    dev = rows.device
+    if cols.numel() != nnz or vals.numel() != nnz:
+        raise HrecError("coo_to_csr: rows, cols and vals must have the same length")
+    indptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
+    indices = torch.empty(nnz, dtype=torch.int32, device=dev)
+    values = torch.empty(nnz, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(int(lib().hrec_coo_to_csr_workspace_bytes(nnz, n_rows)), 16), dtype=torch.uint8,
+                     device=dev)
+    _check("hrec_coo_to_csr", lib().hrec_coo_to_csr(
+        _dev(rows, torch.int32, "rows"), _dev(cols, torch.int32, "cols"), _dev(vals, torch.float32, "vals"),
+        nnz, n_rows, _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
+        _dev(values, torch.float32, "values"), _dev(ws, torch.uint8, "ws"), ws.numel(), _stream()))
+    return indptr, indices, values
 
 
 # -------------------------------------------------------------------- ALS

@@ -110,16 +110,12 @@ def _int_ids(col, name):
     return a
 
 
-def build_csr(rows, cols, vals, n_rows, device):
-    """Host ingest of COO ratings into a device CSR (stable by input order;
-    duplicate (u, i) rows stay separate terms, as in Spark)."""
-    order = np.argsort(rows, kind="stable")
-    counts = np.bincount(rows, minlength=n_rows)
-    indptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-    return DeviceCSR(torch.as_tensor(indptr, device=device),
-                     torch.as_tensor(cols[order].astype(np.int32), device=device),
-                     torch.as_tensor(vals[order].astype(np.float32), device=device), 0, n_rows,
-                     int(cols.max()) + 1 if cols.size else 0)
+def build_csr(rows, cols, vals, n_rows, n_cols):
+    """Device CSR of COO ratings (hrec_coo_to_csr): rows ascending, a row's
+    entries in input order; duplicate (u, i) ratings stay separate terms, as
+    in Spark. rows/cols int32, vals f32, all device tensors."""
+    indptr, indices, values = _hrec.coo_to_csr(rows, cols, vals, int(n_rows))
+    return DeviceCSR(indptr, indices, values, 0, int(n_rows), int(n_cols))
 
 
 class ALSModel:
@@ -156,14 +152,18 @@ class ALSModel:
         if self.cold_start_strategy not in ("drop", "nan"):
             raise ValueError(f"coldStartStrategy {self.cold_start_strategy!r} is not supported")
         dev = self.spark.device
-        users = _int_ids(data["userId"], "userId")
-        items = _int_ids(data["itemId"], "itemId")
-        ratings = np.asarray(data["average_review_rating"], dtype=np.float32)
-        user_ids, urow = np.unique(users, return_inverse=True)
-        item_ids, irow = np.unique(items, return_inverse=True)
+        users_h = _int_ids(data["userId"], "userId")
+        items_h = _int_ids(data["itemId"], "itemId")
+        users, items = torch.as_tensor(users_h).to(dev), torch.as_tensor(items_h).to(dev)
+        ratings = torch.as_tensor(np.asarray(data["average_review_rating"], dtype=np.float32)).to(dev)
+        # ingest on the device (§8(f) row 1): dense codes + CSR (users) / CSC (items)
+        rng = (lambda a: (int(a.min()), int(a.max())) if a.size else None)
+        user_ids_t, urow = _hrec.encode_ids(users, rng(users_h))
+        item_ids_t, irow = _hrec.encode_ids(items, rng(items_h))
+        user_ids, item_ids = user_ids_t.cpu().numpy(), item_ids_t.cpu().numpy()
         k = int(self.rank)
-        csr = build_csr(urow, irow, ratings, len(user_ids), dev)
-        csc = build_csr(irow, urow, ratings, len(item_ids), dev)
+        csr = build_csr(urow, irow, ratings, len(user_ids), len(item_ids))
+        csc = build_csr(irow, urow, ratings, len(item_ids), len(user_ids))
         eng = DeviceALS(len(user_ids), len(item_ids), k, float(self.reg_param), csr, csc)
         if U0 is not None:
             eng.set_user_factors(U0)

@@ -70,6 +70,39 @@ int hrec_exclusive_scan_i64(const int64_t* counts, int64_t n, int64_t* out,
                             void* workspace, size_t workspace_bytes,
                             void* stream);
 
+/* --------------------------------------------------------------- ingest --
+ * The DataFrame -> CSR/CSC step of ALSModel.train (src/als_model.py:51-62:
+ * Spark keys factors by the integer ids and keeps duplicate (user, item)
+ * ratings as separate terms).
+ *
+ * hrec_minmax_i64: out[0] = min(x), out[1] = max(x) (device), n >= 1.
+ * Workspace: hrec_minmax_i64_workspace_bytes(n). */
+size_t hrec_minmax_i64_workspace_bytes(int64_t n);
+int hrec_minmax_i64(const int64_t* x, int64_t n, int64_t* out, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
+/* hrec_encode_ids: ids[n] (int64, id_lo <= ids <= id_hi) -> uniq[*n_uniq]
+ * ascending distinct ids and codes[n] (int32 index into uniq), i.e.
+ * numpy.unique(ids, return_inverse=True). *n_uniq is written on the device.
+ * A range id_hi - id_lo < 2^31 sorts 32-bit keys on only the bits it spans;
+ * pass INT64_MIN, INT64_MAX when the range is unknown. n < 2^31.
+ * Workspace: hrec_encode_ids_workspace_bytes(n). */
+size_t hrec_encode_ids_workspace_bytes(int64_t n);
+int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi,
+                    int64_t* uniq, int64_t* n_uniq, int32_t* codes,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* hrec_coo_to_csr: (rows[nnz], cols[nnz], vals[nnz]) with 0 <= rows < n_rows
+ * -> indptr[n_rows+1], indices[nnz], values[nnz]; rows ascending, the entries
+ * of a row in input order (numpy.argsort(rows, kind="stable")). The CSC is
+ * the same call with rows and cols swapped. nnz, n_rows < 2^31.
+ * Workspace: hrec_coo_to_csr_workspace_bytes(nnz, n_rows). */
+size_t hrec_coo_to_csr_workspace_bytes(int64_t nnz, int64_t n_rows);
+int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const float* vals,
+                    int64_t nnz, int64_t n_rows, int64_t* indptr, int32_t* indices,
+                    float* values, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
 /* ------------------------------------------------------------------ ALS --
  * Initial factors (Spark ALS.initialize [ext: pyspark 3.5.1 ALS.scala]:
  * per row a Gaussian-like vector, L2-normalised, f32). Counter-based on

@@ -5,7 +5,7 @@ set -e
 python -c "import __graft_entry__ as g; g.build()"
 mkdir -p gpurun_out/sq
 export TMPDIR=/tmp
-A="--no-cpu-baseline --score-users 0 --hybrid-users 0 --steps 1 --warmup 0 $*"
+A="--no-cpu-baseline --no-ingest --score-users 0 --hybrid-users 0 --steps 1 --warmup 0 $*"
 timeout -k 10 120 rocprofv3 -L > gpurun_out/sq/counters.txt 2>&1 || true
 i=0
 for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" \

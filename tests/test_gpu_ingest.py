@@ -1,0 +1,100 @@
+"""Device ingest: DataFrame columns -> id codes -> CSR/CSC.
+
+Oracle: numpy's own definitions of the two steps the reference delegates to
+Spark (src/als_model.py:51-62) — numpy.unique(return_inverse=True) for the id
+encoding and a stable argsort by row for the CSR (Spark keeps duplicate
+(user, item) ratings as separate terms). Bit-exact: integer/index work.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _hrec():
+    from src import _hrec
+
+    return _hrec
+
+
+def _np_csr(rows, cols, vals, n_rows):
+    order = np.argsort(rows, kind="stable")
+    indptr = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=n_rows))]).astype(np.int64)
+    return indptr, cols[order], vals[order]
+
+
+@pytest.mark.parametrize("n,lo,hi", [(1, 5, 6), (17, -3, 4), (1000, 0, 50), (100000, -(2 ** 31), 2 ** 31),
+                                     (65537, 10 ** 12, 10 ** 12 + 7)])
+def test_encode_ids_matches_numpy_unique(device, n, lo, hi):
+    h = _hrec()
+    rng = np.random.default_rng(n)
+    ids = rng.integers(lo, hi, n, dtype=np.int64)
+    d_ids = torch.as_tensor(ids, device=device)
+    exp_u, exp_c = np.unique(ids, return_inverse=True)
+    assert h.minmax_i64(d_ids) == (int(ids.min()), int(ids.max()))
+    # measured range (narrow 32-bit path when it fits), a loose hint, and the
+    # unknown-range 64-bit path
+    for rng in (None, (int(ids.min()) - 3, int(ids.max()) + 5), (-(2 ** 63), 2 ** 63 - 1)):
+        uniq, codes = h.encode_ids(d_ids, rng)
+        np.testing.assert_array_equal(uniq.cpu().numpy(), exp_u)
+        np.testing.assert_array_equal(codes.cpu().numpy(), exp_c.astype(np.int32))
+
+
+def test_encode_ids_empty(device):
+    h = _hrec()
+    uniq, codes = h.encode_ids(torch.zeros(0, dtype=torch.int64, device=device))
+    assert uniq.numel() == 0 and codes.numel() == 0
+
+
+@pytest.mark.parametrize("nnz,n_rows,n_cols", [(1, 1, 1), (50, 7, 9), (10000, 3, 500), (200000, 4097, 1000),
+                                               (300000, 70000, 50)])
+def test_coo_to_csr_matches_stable_argsort(device, nnz, n_rows, n_cols):
+    h = _hrec()
+    rng = np.random.default_rng(nnz + n_rows)
+    rows = rng.integers(0, n_rows, nnz).astype(np.int32)
+    rows[: min(nnz, 5)] = n_rows - 1          # the last row is populated
+    cols = rng.integers(0, n_cols, nnz).astype(np.int32)
+    vals = rng.integers(0, 19, nnz).astype(np.float32)
+    vals[::3] += 0.25
+    ip, ix, v = h.coo_to_csr(torch.as_tensor(rows, device=device), torch.as_tensor(cols, device=device),
+                             torch.as_tensor(vals, device=device), n_rows)
+    e_ip, e_ix, e_v = _np_csr(rows, cols, vals, n_rows)
+    np.testing.assert_array_equal(ip.cpu().numpy(), e_ip)
+    np.testing.assert_array_equal(ix.cpu().numpy(), e_ix)
+    np.testing.assert_array_equal(v.cpu().numpy(), e_v)
+
+
+def test_coo_to_csr_empty_rows_and_duplicates(device):
+    """Leading, interior and trailing empty rows; repeated (row, col) pairs
+    stay separate entries in input order."""
+    h = _hrec()
+    rows = np.array([2, 2, 5, 2, 5, 2], np.int32)
+    cols = np.array([1, 1, 0, 3, 0, 1], np.int32)
+    vals = np.array([1, 2, 3, 4, 5, 6], np.float32)
+    ip, ix, v = h.coo_to_csr(*(torch.as_tensor(a, device=device) for a in (rows, cols, vals)), 8)
+    np.testing.assert_array_equal(ip.cpu().numpy(), [0, 0, 0, 4, 4, 4, 6, 6, 6])
+    np.testing.assert_array_equal(ix.cpu().numpy(), [1, 1, 3, 1, 0, 0])
+    np.testing.assert_array_equal(v.cpu().numpy(), [1, 2, 4, 6, 3, 5])
+
+
+def test_coo_to_csr_no_entries(device):
+    h = _hrec()
+    z = torch.zeros(0, dtype=torch.int32, device=device)
+    ip, ix, v = h.coo_to_csr(z, z, torch.zeros(0, dtype=torch.float32, device=device), 4)
+    np.testing.assert_array_equal(ip.cpu().numpy(), [0, 0, 0, 0, 0])
+
+
+def test_synthetic_csc_from_csr_via_ingest(device):
+    """The CSC built from the synthetic CSR's COO equals the generator's own
+    CSC (independent construction of the same matrix)."""
+    from src import synthetic
+
+    h = _hrec()
+    n_u, n_i, dens = 3000, 700, 0.02
+    csr = synthetic.generate(n_u, n_i, dens, False)
+    csc = synthetic.generate(n_u, n_i, dens, True)
+    counts = (csr.indptr[1:] - csr.indptr[:-1]).cpu()
+    urow = torch.repeat_interleave(torch.arange(n_u, dtype=torch.int32), counts).to(device)
+    ip, ix, v = h.coo_to_csr(csr.indices, urow, csr.values, n_i)
+    assert torch.equal(ip, csc.indptr) and torch.equal(ix, csc.indices) and torch.equal(v, csc.values)
