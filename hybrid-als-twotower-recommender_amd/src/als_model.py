@@ -17,6 +17,7 @@ HIP device session that plays the SparkSession's role.
 import json
 import os
 import pickle
+import time
 import warnings
 
 import numpy as np
@@ -71,29 +72,59 @@ class DeviceALSFactors:
         irows = torch.as_tensor(self._lookup(self.item_ids, item_list), device=dev)
         return _hrec.als_score(self.U, urows, self.Vt, irows, irows.numel(), self.k)
 
-    def save(self, path):
-        os.makedirs(path, exist_ok=True)
-        np.save(os.path.join(path, "userIds.npy"), self.user_ids)
-        np.save(os.path.join(path, "itemIds.npy"), self.item_ids)
-        np.save(os.path.join(path, "userFactors.npy"), self.U[:, : self.k].cpu().numpy())
-        np.save(os.path.join(path, "itemFactors.npy"), self.V[:, : self.k].cpu().numpy())
-        with open(os.path.join(path, "metadata.json"), "w") as f:
-            json.dump({"class": "hrec.DeviceALSFactors", "rank": self.k}, f)
+    # Spark 3.5 ALSModel directory layout (MLWriter): metadata/part-00000 is
+    # one JSON line with the model params and "rank"; userFactors/ and
+    # itemFactors/ are parquet datasets of (id: int, features: array<float>).
+    # A model saved here loads in Spark and vice versa.
+    def save(self, path, params=None):
+        import uuid
+
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        meta = {"class": "org.apache.spark.ml.recommendation.ALSModel", "timestamp": int(time.time() * 1000),
+                "sparkVersion": "3.5.1", "uid": f"ALS_{uuid.uuid4().hex[:12]}",
+                "paramMap": dict(params or {}),
+                "defaultParamMap": {"blockSize": 4096, "predictionCol": "prediction", "itemCol": "item",
+                                    "userCol": "user", "coldStartStrategy": "nan"},
+                "rank": self.k}
+        os.makedirs(os.path.join(path, "metadata"), exist_ok=True)
+        with open(os.path.join(path, "metadata", "part-00000"), "w") as f:
+            f.write(json.dumps(meta, separators=(",", ":")) + "\n")
+        open(os.path.join(path, "metadata", "_SUCCESS"), "w").close()
+        feat_t = pa.list_(pa.field("element", pa.float32(), nullable=False))
+        for name, ids, fac in (("userFactors", self.user_ids, self.U), ("itemFactors", self.item_ids, self.V)):
+            d = os.path.join(path, name)
+            os.makedirs(d, exist_ok=True)
+            mat = fac[:, : self.k].cpu().numpy()
+            feats = pa.FixedSizeListArray.from_arrays(pa.array(mat.reshape(-1), pa.float32()), self.k)
+            table = pa.table({"id": pa.array(np.asarray(ids, np.int32), pa.int32()),
+                              "features": feats.cast(feat_t)})
+            pq.write_table(table, os.path.join(d, f"part-00000-{uuid.uuid4()}-c000.snappy.parquet"),
+                           compression="snappy")
+            open(os.path.join(d, "_SUCCESS"), "w").close()
 
     @classmethod
     def load(cls, path, device):
-        with open(os.path.join(path, "metadata.json")) as f:
-            k = int(json.load(f)["rank"])
+        import pyarrow.parquet as pq
+
+        with open(os.path.join(path, "metadata", "part-00000")) as f:
+            k = int(json.loads(f.readline())["rank"])
         kp = padded_k(k)
 
         def fac(name):
-            a = np.load(os.path.join(path, name))
-            t = torch.zeros((a.shape[0], kp), dtype=torch.float32, device=device)
-            t[:, :k] = torch.as_tensor(a, device=device)
-            return t
+            t = pq.read_table(os.path.join(path, name))
+            ids = np.asarray(t.column("id").to_numpy(), np.int64)
+            flat = t.column("features").combine_chunks().flatten().to_numpy(zero_copy_only=False)
+            mat = np.asarray(flat, np.float32).reshape(len(ids), k)
+            order = np.argsort(ids, kind="stable")  # Spark writes partitions in any order
+            out = torch.zeros((len(ids), kp), dtype=torch.float32, device=device)
+            out[:, :k] = torch.as_tensor(mat[order], device=device)
+            return ids[order], out
 
-        return cls(np.load(os.path.join(path, "userIds.npy")), np.load(os.path.join(path, "itemIds.npy")),
-                   fac("userFactors.npy"), fac("itemFactors.npy"), k)
+        user_ids, U = fac("userFactors")
+        item_ids, V = fac("itemFactors")
+        return cls(user_ids, item_ids, U, V, k)
 
 
 def _int_ids(col, name):
@@ -256,7 +287,8 @@ class ALSModel:
     def save_model(self, model_path="models/als"):
         try:
             os.makedirs(os.path.dirname(model_path) or ".", exist_ok=True)
-            self.model.save(model_path)
+            self.model.save(model_path, {"userCol": "userId", "itemCol": "itemId", "predictionCol": "prediction",
+                                         "coldStartStrategy": self.cold_start_strategy, "blockSize": 4096})
             metadata = {
                 "rank": self.rank,
                 "max_iter": self.max_iter,

@@ -22,7 +22,9 @@ placeholders. Every number written below comes from the reference's code:
     returns fixed predictions;
   * TwoTowerModel.predict_for_user input assembly (src/two_tower_model.py:136-146)
     and _prepare_features (:123-134) with a recording fake Keras model;
-  * utils.scale_ratings_to_5 / normalize_predictions (src/utils.py:16-79).
+  * utils.scale_ratings_to_5 / normalize_predictions (src/utils.py:16-79);
+  * RecommenderEvaluator precision/recall/NDCG/MAE-RMSE/_binarize and the
+    comprehensive_evaluation entry point (src/evaluation.py:19-149).
 
 Output: tests/golden/*.json (data only: inputs and expected outputs).
 """
@@ -306,6 +308,51 @@ def utils_cases(ref):
     }
 
 
+def _exc(fn):
+    """Value of fn(), or the name of the exception it raises."""
+    try:
+        return {"ok": fn()}
+    except Exception as e:  # noqa: BLE001 - the exception type is the expected output
+        return {"raises": type(e).__name__}
+
+
+def evaluation_cases(ref):
+    """RecommenderEvaluator (src/evaluation.py:19-149) on per-user dicts.
+    Dicts are stored as [key, value] lists in insertion order."""
+    rng = np.random.default_rng(7)
+    ev = ref.ev.RecommenderEvaluator()
+    cases = []
+    for c in range(40):
+        n_act = int(rng.integers(1, 40))
+        items = rng.choice(200, size=n_act + 30, replace=False).tolist()
+        if c % 3 == 0:
+            actual = {int(i): int(rng.integers(0, 19)) for i in items[:n_act]}
+        else:
+            actual = {int(i): float(np.round(rng.uniform(1, 5), 1)) for i in items[:n_act]}
+        pred_items = items[n_act // 2: n_act // 2 + int(rng.integers(1, 45))]
+        if c % 4 == 1:
+            pred = {int(i): float(np.round(rng.uniform(0, 5), 0)) for i in pred_items}  # many ties
+        elif c % 4 == 2:
+            pred = {int(i): float(rng.normal()) for i in pred_items}
+        else:
+            pred = {int(i): float(np.float32(rng.uniform(1, 5))) for i in pred_items}
+        if c == 5:
+            pred = {i: 3.0 for i in pred}  # all tied
+        if c == 6:
+            actual = {i: 4 for i in actual}  # constant truth
+        k_vals = [0, 1, 3, 5, 10, 15, 20] if c % 5 == 0 else [5, 10]
+        case = {"actual": [[i, v] for i, v in actual.items()], "pred": [[i, v] for i, v in pred.items()],
+                "precision": [[k, _exc(lambda k=k: ev.precision_at_k(actual, pred, k))] for k in k_vals if k > 0],
+                "recall": [[k, _exc(lambda k=k: ev.recall_at_k(actual, pred, k))] for k in k_vals],
+                "ndcg": [[k, _exc(lambda k=k: float(ev.ndcg_at_k(actual, pred, k)))] for k in (5, 10)],
+                "mae_rmse": _exc(lambda: [float(x) for x in ev.mae_rmse(actual, pred)]),
+                "binarize": [[i, v] for i, v in ev._binarize(actual).items()],
+                "comprehensive": _exc(lambda: {kk: float(vv) for kk, vv in
+                                               ev.comprehensive_evaluation(actual, pred).items()})}
+        cases.append(case)
+    return cases
+
+
 def main():
     ref = load_reference()
     rng = np.random.default_rng(20250620)
@@ -318,6 +365,7 @@ def main():
         "als_fallback.json": als_fallback_cases(ref, rng),
         "tt_inputs.json": tt_input_cases(ref, rng),
         "utils.json": utils_cases(ref),
+        "evaluation.json": evaluation_cases(ref),
     }
     for name, data in files.items():
         with open(os.path.join(OUT, name), "w") as f:

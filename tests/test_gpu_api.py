@@ -148,6 +148,47 @@ def test_als_save_load_roundtrip(device, tmp_path):
     assert ALSModel().load_model(str(tmp_path / "missing")) is None
 
 
+def test_als_model_dir_is_spark_layout(device, tmp_path):
+    """save_model writes Spark 3.5's ALSModel directory (metadata JSON line +
+    userFactors/itemFactors parquet of (id int, features array<float>)); a
+    directory laid out like Spark's (several part files, rows in arbitrary
+    order) loads back to the same model."""
+    import json
+
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from src.als_model import ALSModel
+
+    rng = np.random.default_rng(2)
+    df = _ratings_frame(rng, 25, 15, 200)
+    m = ALSModel(rank=5, max_iter=2, seed=4)
+    assert m.train(df)
+    path = tmp_path / "als"
+    m.save_model(str(path))
+    meta = json.loads((path / "metadata" / "part-00000").read_text().splitlines()[0])
+    assert meta["class"] == "org.apache.spark.ml.recommendation.ALSModel" and meta["rank"] == 5
+    assert meta["paramMap"]["userCol"] == "userId" and meta["paramMap"]["itemCol"] == "itemId"
+    t = pq.read_table(str(path / "userFactors"))
+    assert t.schema.field("id").type == pa.int32()
+    assert t.schema.field("features").type.value_type == pa.float32()
+    ids = t.column("id").to_numpy()
+    feats = np.stack([np.asarray(x, np.float32) for x in t.column("features").to_pylist()])
+    np.testing.assert_array_equal(feats, m.model.U[:, :5].cpu().numpy())
+    # re-write userFactors as two shuffled part files, as Spark's partitions would be
+    perm = rng.permutation(len(ids))
+    for f in (path / "userFactors").glob("*.parquet"):
+        f.unlink()
+    for n, part in enumerate(np.array_split(perm, 2)):
+        pq.write_table(pa.table({"id": pa.array(ids[part], pa.int32()),
+                                 "features": pa.array([feats[i].tolist() for i in part], pa.list_(pa.float32()))}),
+                       str(path / "userFactors" / f"part-0000{n}-x.snappy.parquet"))
+    m2 = ALSModel().load_model(str(path))
+    assert m2 is not None
+    q = list(df["itemId"].unique()[:8])
+    for u in df["userId"].unique()[:5]:
+        assert m.predict_for_user(int(u), q) == m2.predict_for_user(int(u), q)
+
+
 # --------------------------------------------------------------- two-tower
 def _tt_params(rng, nu, ni, nm, nc, d):
     p = ott_init = {
