@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "hybrid-als-twotower-recommender_amd"))
 sys.path.insert(0, ROOT)
 
 from src import _hrec, synthetic  # noqa: E402
-from src.als_engine import DeviceALS, shard_range  # noqa: E402
+from src.als_engine import DeviceALS, shard_chunks, shard_range  # noqa: E402
 from src.recommend import ShardedRecommender  # noqa: E402
 from src.tt_engine import DeviceTwoTower  # noqa: E402
 
@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="W > 1: ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")
     ap.add_argument("--no-ingest", dest="ingest", action="store_false",
                     help="skip the COO -> CSR/CSC ingest measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_prof_summary.json"),
@@ -123,10 +125,15 @@ def main():
     n_users, n_items = cfg["users"], cfg["items"]
     u0, u_per = shard_range(n_users, world, rank)
     i0, i_per = shard_range(n_items, world, rank)
-    csr = synthetic.generate(n_users, n_items, cfg["density"], False, u0, u_per)
-    csc = synthetic.generate(n_users, n_items, cfg["density"], True, i0, i_per)
+    # ALS shards: chunk-interleaved when W > 1 so each chunk's all-gather
+    # overlaps the next chunk's half-sweep (src/als_engine.py)
+    chunks = args.chunks if world > 1 else 1
+    u_ranges, _ = shard_chunks(n_users, world, rank, chunks)
+    i_ranges, _ = shard_chunks(n_items, world, rank, chunks)
+    csr = synthetic.generate_ranges(n_users, n_items, cfg["density"], False, u_ranges)
+    csc = synthetic.generate_ranges(n_users, n_items, cfg["density"], True, i_ranges)
     eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group,
-                    accum_mode=args.accum_mode)
+                    accum_mode=args.accum_mode, chunks=chunks)
     eng.init_user_factors(synthetic.SEED_INIT)
     torch.cuda.synchronize()
 
@@ -146,17 +153,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        # events on the launch stream; at W = 1 they bracket exactly the two
+        # half-sweep kernels, at W > 1 also the all-gathers not hidden
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         e[0].record(stream)
-        _hrec.als_half_sweep(csc.indptr, csc.indices, csc.values, eng.U, k, eng.reg, eng.V_local,
-                             args.accum_mode)
+        eng.item_half_sweep()
         e[1].record(stream)
-        eng._gather(eng.V, eng.V_local)
+        eng.user_half_sweep()
         e[2].record(stream)
-        _hrec.als_half_sweep(csr.indptr, csr.indices, csr.values, eng.V, k, eng.reg, eng.U_local,
-                             args.accum_mode)
-        e[3].record(stream)
-        eng._gather(eng.U, eng.U_local)
         ev.append(e)
     torch.cuda.synchronize()
     if world > 1:
@@ -168,7 +172,7 @@ def main():
     elapsed = float(t.item())
 
     item_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
-    user_ms = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev)
+    user_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
     # per-rank algorithmic work of one epoch (both launches of the kernel)
     flops = algo_flops(csc.nnz, i_per, k) + algo_flops(csr.nnz, u_per, k)
     bytes_ = algo_bytes(csc.nnz, i_per, k) + algo_bytes(csr.nnz, u_per, k)
@@ -237,7 +241,7 @@ def main():
     # rank's user shard as COO columns (int64 ids, ratings) -> id codes +
     # CSR + CSC on the device (hrec_encode_ids x2, hrec_coo_to_csr x2).
     ingest = None
-    if rank == 0 and args.ingest:
+    if world == 1 and args.ingest:
         counts = csr.indptr[1:] - csr.indptr[:-1]
         uid = torch.repeat_interleave(torch.arange(u0, u0 + u_per, dtype=torch.int64, device="cuda"), counts)
         iid = csr.indices.to(torch.int64)
@@ -293,7 +297,9 @@ def main():
                              f"rank {k}, reg 0.1; step = one ALS epoch (item + user half-sweep)"),
                 "users": n_users, "items": n_items, "density": cfg["density"], "rank": k,
                 "nnz": nnz_user, "nnz_check_csc": nnz_item,
-                "parallelism": f"dp{world} (row-sharded users/items, RCCL all-gather of factors)",
+                "parallelism": (f"dp{world} (row-sharded users/items; {chunks} chunks per rank, each chunk's "
+                                f"RCCL all-gather of factors overlapping the next chunk's half-sweep)"
+                                if world > 1 else "dp1 (single GPU, no collectives)"),
             },
             "roofline": {
                 "kernel": "als_half_sweep_f64_kernel (item + user launches)",

@@ -4,10 +4,17 @@ reference calls at src/als_model.py:52-62, on MI355X.
 Per iteration (Spark ALS.train [ext]): item factors are solved from the
 user factors, then user factors from the new item factors — each a
 half-sweep (K1, hrec_als_half_sweep) over a CSR shard. With W ranks the
-dst rows of each side are split into W equal contiguous shards (the last
-padded with empty rows); after each half-sweep the shards are replicated
-with one RCCL all-gather (torch.distributed, backend "nccl" = RCCL over
-xGMI) so every rank holds the full source matrix for the next half-sweep.
+dst rows of each side are split into W equal shards (padded with empty
+rows); after each half-sweep the shards are replicated with RCCL
+all-gathers (torch.distributed, backend "nccl" = RCCL over xGMI) so every
+rank holds the full source matrix for the next half-sweep.
+
+With C > 1 chunks a rank's shard is C chunks of cs rows, interleaved with
+the other ranks' (rank r owns global rows [c·W·cs + r·cs, +cs) for
+c < C): the half-sweep runs chunk by chunk and each chunk's all-gather —
+contiguous in the replicated matrix — is issued on a side stream as soon as
+its kernel finishes, so C−1 of the C all-gathers overlap the next chunk's
+compute.
 """
 import math
 
@@ -35,12 +42,20 @@ def shard_range(n, world, rank):
     return rank * per, per
 
 
+def shard_chunks(n, world, rank, chunks):
+    """Chunk-interleaved shard: ([(global_begin, cs)] for c < chunks, cs).
+    chunks == 1 is shard_range's contiguous shard."""
+    per = math.ceil(n / world) if n else 0
+    cs = math.ceil(per / chunks) if per else 0
+    return [(c * world * cs + rank * cs, cs) for c in range(chunks)], cs
+
+
 class DeviceALS:
     """Holds one rank's CSR shard (user rows), CSC shard (item rows) and the
     replicated factor matrices."""
 
     def __init__(self, n_users, n_items, rank_k, reg_param, user_csr: DeviceCSR,
-                 item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0, sweep=None):
+                 item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0, sweep=None, chunks=1):
         self.n_users, self.n_items = int(n_users), int(n_items)
         self.k = int(rank_k)
         self.kp = padded_k(self.k)
@@ -54,9 +69,13 @@ class DeviceALS:
         dev = user_csr.indptr.device
         self.u_per = user_csr.n_rows
         self.i_per = item_csc.n_rows
+        self.chunks = int(chunks) if self.world > 1 else 1
         if self.world > 1:
-            assert user_csr.row_begin == self.rank * self.u_per
-            assert item_csc.row_begin == self.rank * self.i_per
+            ur, self.u_cs = shard_chunks(self.n_users, self.world, self.rank, self.chunks)
+            ir, self.i_cs = shard_chunks(self.n_items, self.world, self.rank, self.chunks)
+            assert self.u_per == self.chunks * self.u_cs and self.i_per == self.chunks * self.i_cs
+            assert user_csr.row_begin == ur[0][0] and item_csc.row_begin == ir[0][0]
+        self.comm = (torch.cuda.Stream(device=dev) if self.chunks > 1 and dev.type == "cuda" else None)
         # Replicated factors, padded to world * per rows for the all-gather.
         self.U = torch.zeros((self.u_per * self.world, self.kp), dtype=torch.float32, device=dev)
         self.V = torch.zeros((self.i_per * self.world, self.kp), dtype=torch.float32, device=dev)
@@ -82,15 +101,35 @@ class DeviceALS:
         if self.world > 1:
             dist.all_gather_into_tensor(full, local, group=self.group)
 
+    def _sweep(self, csr, src, local, full, cs):
+        """One half-sweep of this rank's rows + replication of the result."""
+        if self.chunks == 1:
+            self.sweep(csr.indptr, csr.indices, csr.values, src, self.k, self.reg, local, self.accum_mode)
+            self._gather(full, local)
+            return
+        W = self.world
+        compute = torch.cuda.current_stream() if self.comm is not None else None
+        for c in range(self.chunks):
+            rows = slice(c * cs, (c + 1) * cs)
+            self.sweep(csr.indptr[c * cs: (c + 1) * cs + 1], csr.indices, csr.values, src, self.k, self.reg,
+                       local[rows], self.accum_mode)
+            out = full[c * W * cs: (c + 1) * W * cs]
+            if self.comm is None:
+                dist.all_gather_into_tensor(out, local[rows], group=self.group)
+                continue
+            done = torch.cuda.Event()
+            done.record(compute)
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(done)
+                dist.all_gather_into_tensor(out, local[rows], group=self.group)
+        if self.comm is not None:
+            compute.wait_stream(self.comm)
+
     def item_half_sweep(self):
-        self.sweep(self.item_csc.indptr, self.item_csc.indices, self.item_csc.values,
-                   self.U, self.k, self.reg, self.V_local, self.accum_mode)
-        self._gather(self.V, self.V_local)
+        self._sweep(self.item_csc, self.U, self.V_local, self.V, getattr(self, "i_cs", self.i_per))
 
     def user_half_sweep(self):
-        self.sweep(self.user_csr.indptr, self.user_csr.indices, self.user_csr.values,
-                   self.V, self.k, self.reg, self.U_local, self.accum_mode)
-        self._gather(self.U, self.U_local)
+        self._sweep(self.user_csr, self.V, self.U_local, self.U, getattr(self, "u_cs", self.u_per))
 
     def epoch(self):
         """One Spark iteration: items from users, then users from items."""

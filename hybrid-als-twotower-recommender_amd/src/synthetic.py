@@ -74,3 +74,20 @@ def generate(n_users, n_items, density, transposed, row_begin=0, n_rows=None, se
                          indices, values)
     del counts
     return DeviceCSR(indptr, indices, values, row_begin, n_rows, n_cols)
+
+
+def generate_ranges(n_users, n_items, density, transposed, ranges, **kw):
+    """One CSR over several row ranges [(row_begin, n_rows), ...] of R or R^T,
+    concatenated in order (a chunk-interleaved shard, als_engine.shard_chunks)."""
+    parts = [generate(n_users, n_items, density, transposed, b, n, **kw) for b, n in ranges]
+    if len(parts) == 1:
+        return parts[0]
+    offs, ips = 0, [parts[0].indptr[:1]]
+    for p in parts:
+        ips.append(p.indptr[1:] + offs)
+        offs += p.nnz
+    indptr = torch.cat(ips)
+    indices = torch.cat([p.indices for p in parts])
+    values = torch.cat([p.values for p in parts])
+    return DeviceCSR(indptr, indices, values, ranges[0][0], sum(n for _, n in ranges), parts[0].n_cols)
+

@@ -24,25 +24,34 @@ def _oracle_sweep(indptr, indices, values, src, k, reg, dst, accum_mode=0):
     dst[: out.shape[0], :k] = torch.from_numpy(out)
 
 
-def _shard(n_users, n_items, transposed, world, rank):
-    from src.als_engine import shard_range
+def _shard(n_users, n_items, transposed, world, rank, chunks=1):
+    """This rank's (chunk-interleaved) shard, built by the C oracle generator
+    range by range and concatenated like synthetic.generate_ranges."""
+    from src.als_engine import shard_chunks
     from src.synthetic import DeviceCSR
 
     total = n_items if transposed else n_users
-    r0, per = shard_range(total, world, rank)
-    ip, ix, v = obuild.synth_csr(n_users, n_items, DENS, int(transposed), r0, per, SEED, SEED2)
-    return DeviceCSR(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(v), r0, per,
+    ranges, _ = shard_chunks(total, world, rank, chunks)
+    ips, ixs, vs, off = [np.zeros(1, np.int64)], [], [], 0
+    for r0, cnt in ranges:
+        ip, ix, v = obuild.synth_csr(n_users, n_items, DENS, int(transposed), r0, cnt, SEED, SEED2)
+        ips.append(ip[1:] + off)
+        ixs.append(ix)
+        vs.append(v)
+        off += len(ix)
+    return DeviceCSR(torch.from_numpy(np.concatenate(ips)), torch.from_numpy(np.concatenate(ixs)),
+                     torch.from_numpy(np.concatenate(vs)), ranges[0][0], sum(c for _, c in ranges),
                      n_users if transposed else n_items)
 
 
-def _worker(rank, world, port, U0, q):
+def _worker(rank, world, port, U0, q, chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from src.als_engine import DeviceALS
 
-    eng = DeviceALS(N_USERS, N_ITEMS, K, REG, _shard(N_USERS, N_ITEMS, False, world, rank),
-                    _shard(N_USERS, N_ITEMS, True, world, rank), world=world, rank=rank,
-                    group=dist.group.WORLD, sweep=_oracle_sweep)
+    eng = DeviceALS(N_USERS, N_ITEMS, K, REG, _shard(N_USERS, N_ITEMS, False, world, rank, chunks),
+                    _shard(N_USERS, N_ITEMS, True, world, rank, chunks), world=world, rank=rank,
+                    group=dist.group.WORLD, sweep=_oracle_sweep, chunks=chunks)
     eng.set_user_factors(U0)
     eng.fit(ITERS)
     q.put((rank, eng.user_factors.numpy().copy(), eng.item_factors.numpy().copy()))
@@ -55,14 +64,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_als_matches_unsharded(world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 1), (2, 3), (3, 4)])
+def test_sharded_als_matches_unsharded(world, chunks):
+    """Contiguous shards (chunks=1) and chunk-interleaved shards whose
+    per-chunk all-gathers overlap the next chunk's sweep (chunks>1)."""
     rng = np.random.default_rng(0)
     U0 = rng.normal(size=(N_USERS, K)).astype(np.float32)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, U0, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, U0, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=60) for _ in range(world)]
@@ -87,6 +98,23 @@ def test_shard_ranges_cover_and_pad():
             assert all(s[1] == per for s in spans)
             assert per * w >= n and per == -(-n // w)  # covers [0, n); tail shards padded
             assert [s[0] for s in spans] == [r * per for r in range(w)]
+
+
+def test_shard_chunks_tile_the_padded_matrix():
+    from src.als_engine import shard_chunks, shard_range
+
+    for n in (1, 7, 57, 103, 1000):
+        for w in (1, 2, 3, 8):
+            for c in (1, 2, 3, 4):
+                owned = []
+                for r in range(w):
+                    ranges, cs = shard_chunks(n, w, r, c)
+                    assert len(ranges) == c and all(cnt == cs for _, cnt in ranges)
+                    owned += [b + i for b, cnt in ranges for i in range(cnt)]
+                # every row of the padded [c*w*cs] matrix owned exactly once
+                assert sorted(owned) == list(range(c * w * cs)) and c * w * cs >= n
+                if c == 1:
+                    assert shard_chunks(n, w, 0, 1)[0][0] == shard_range(n, w, 0)
 
 
 # ------------------------------------------------ sharded hybrid top-k (C2/C3)
