@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=4,
-                    help="W > 1: ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")
+                    help="W > 1: user-side ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")
     ap.add_argument("--no-ingest", dest="ingest", action="store_false",
                     help="skip the COO -> CSR/CSC ingest measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_prof_summary.json"),
@@ -129,7 +129,7 @@ def main():
     # overlaps the next chunk's half-sweep (src/als_engine.py)
     chunks = args.chunks if world > 1 else 1
     u_ranges, _ = shard_chunks(n_users, world, rank, chunks)
-    i_ranges, _ = shard_chunks(n_items, world, rank, chunks)
+    i_ranges, _ = shard_chunks(n_items, world, rank, 1)
     csr = synthetic.generate_ranges(n_users, n_items, cfg["density"], False, u_ranges)
     csc = synthetic.generate_ranges(n_users, n_items, cfg["density"], True, i_ranges)
     eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group,
@@ -297,8 +297,8 @@ def main():
                              f"rank {k}, reg 0.1; step = one ALS epoch (item + user half-sweep)"),
                 "users": n_users, "items": n_items, "density": cfg["density"], "rank": k,
                 "nnz": nnz_user, "nnz_check_csc": nnz_item,
-                "parallelism": (f"dp{world} (row-sharded users/items; {chunks} chunks per rank, each chunk's "
-                                f"RCCL all-gather of factors overlapping the next chunk's half-sweep)"
+                "parallelism": (f"dp{world} (row-sharded users/items; user side in {chunks} chunks per rank, "
+                                f"each chunk's RCCL all-gather overlapping the next chunk's half-sweep)"
                                 if world > 1 else "dp1 (single GPU, no collectives)"),
             },
             "roofline": {

@@ -9,12 +9,14 @@ rows); after each half-sweep the shards are replicated with RCCL
 all-gathers (torch.distributed, backend "nccl" = RCCL over xGMI) so every
 rank holds the full source matrix for the next half-sweep.
 
-With C > 1 chunks a rank's shard is C chunks of cs rows, interleaved with
+With C > 1 chunks a side's shard is C chunks of cs rows, interleaved with
 the other ranks' (rank r owns global rows [c·W·cs + r·cs, +cs) for
 c < C): the half-sweep runs chunk by chunk and each chunk's all-gather —
 contiguous in the replicated matrix — is issued on a side stream as soon as
 its kernel finishes, so C−1 of the C all-gathers overlap the next chunk's
-compute.
+compute. Chunking pays on the user side (many short rows, the large factor
+matrix); the item side's few long rows would lose more to per-launch tails
+than its small all-gather costs, so the two sides take separate counts.
 """
 import math
 
@@ -55,7 +57,8 @@ class DeviceALS:
     replicated factor matrices."""
 
     def __init__(self, n_users, n_items, rank_k, reg_param, user_csr: DeviceCSR,
-                 item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0, sweep=None, chunks=1):
+                 item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0, sweep=None, chunks=1,
+                 item_chunks=1):
         self.n_users, self.n_items = int(n_users), int(n_items)
         self.k = int(rank_k)
         self.kp = padded_k(self.k)
@@ -69,13 +72,17 @@ class DeviceALS:
         dev = user_csr.indptr.device
         self.u_per = user_csr.n_rows
         self.i_per = item_csc.n_rows
-        self.chunks = int(chunks) if self.world > 1 else 1
+        # row chunks per side (user side: `chunks`, item side: `item_chunks`)
+        self.u_chunks = int(chunks) if self.world > 1 else 1
+        self.i_chunks = int(item_chunks) if self.world > 1 else 1
+        self.u_cs, self.i_cs = self.u_per, self.i_per
         if self.world > 1:
-            ur, self.u_cs = shard_chunks(self.n_users, self.world, self.rank, self.chunks)
-            ir, self.i_cs = shard_chunks(self.n_items, self.world, self.rank, self.chunks)
-            assert self.u_per == self.chunks * self.u_cs and self.i_per == self.chunks * self.i_cs
+            ur, self.u_cs = shard_chunks(self.n_users, self.world, self.rank, self.u_chunks)
+            ir, self.i_cs = shard_chunks(self.n_items, self.world, self.rank, self.i_chunks)
+            assert self.u_per == self.u_chunks * self.u_cs and self.i_per == self.i_chunks * self.i_cs
             assert user_csr.row_begin == ur[0][0] and item_csc.row_begin == ir[0][0]
-        self.comm = (torch.cuda.Stream(device=dev) if self.chunks > 1 and dev.type == "cuda" else None)
+        chunked = max(self.u_chunks, self.i_chunks) > 1
+        self.comm = torch.cuda.Stream(device=dev) if chunked and dev.type == "cuda" else None
         # Replicated factors, padded to world * per rows for the all-gather.
         self.U = torch.zeros((self.u_per * self.world, self.kp), dtype=torch.float32, device=dev)
         self.V = torch.zeros((self.i_per * self.world, self.kp), dtype=torch.float32, device=dev)
@@ -101,15 +108,15 @@ class DeviceALS:
         if self.world > 1:
             dist.all_gather_into_tensor(full, local, group=self.group)
 
-    def _sweep(self, csr, src, local, full, cs):
+    def _sweep(self, csr, src, local, full, cs, chunks):
         """One half-sweep of this rank's rows + replication of the result."""
-        if self.chunks == 1:
+        if chunks == 1:
             self.sweep(csr.indptr, csr.indices, csr.values, src, self.k, self.reg, local, self.accum_mode)
             self._gather(full, local)
             return
         W = self.world
         compute = torch.cuda.current_stream() if self.comm is not None else None
-        for c in range(self.chunks):
+        for c in range(chunks):
             rows = slice(c * cs, (c + 1) * cs)
             self.sweep(csr.indptr[c * cs: (c + 1) * cs + 1], csr.indices, csr.values, src, self.k, self.reg,
                        local[rows], self.accum_mode)
@@ -126,10 +133,10 @@ class DeviceALS:
             compute.wait_stream(self.comm)
 
     def item_half_sweep(self):
-        self._sweep(self.item_csc, self.U, self.V_local, self.V, getattr(self, "i_cs", self.i_per))
+        self._sweep(self.item_csc, self.U, self.V_local, self.V, self.i_cs, self.i_chunks)
 
     def user_half_sweep(self):
-        self._sweep(self.user_csr, self.V, self.U_local, self.U, getattr(self, "u_cs", self.u_per))
+        self._sweep(self.user_csr, self.V, self.U_local, self.U, self.u_cs, self.u_chunks)
 
     def epoch(self):
         """One Spark iteration: items from users, then users from items."""

@@ -49,9 +49,11 @@ def _worker(rank, world, port, U0, q, chunks=1):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from src.als_engine import DeviceALS
 
+    # user side in `chunks` chunks, item side in chunks - 1 (both layouts mixed)
+    ichunks = max(1, chunks - 1)
     eng = DeviceALS(N_USERS, N_ITEMS, K, REG, _shard(N_USERS, N_ITEMS, False, world, rank, chunks),
-                    _shard(N_USERS, N_ITEMS, True, world, rank, chunks), world=world, rank=rank,
-                    group=dist.group.WORLD, sweep=_oracle_sweep, chunks=chunks)
+                    _shard(N_USERS, N_ITEMS, True, world, rank, ichunks), world=world, rank=rank,
+                    group=dist.group.WORLD, sweep=_oracle_sweep, chunks=chunks, item_chunks=ichunks)
     eng.set_user_factors(U0)
     eng.fit(ITERS)
     q.put((rank, eng.user_factors.numpy().copy(), eng.item_factors.numpy().copy()))

@@ -315,10 +315,10 @@ def _chunked_worker(rank, world, port, chunks, q):
 
     n_u, n_i, dens, k = 700, 300, 0.05, 32
     ur, _ = shard_chunks(n_u, world, rank, chunks)
-    ir, _ = shard_chunks(n_i, world, rank, chunks)
+    ir, _ = shard_chunks(n_i, world, rank, 2)
     eng = DeviceALS(n_u, n_i, k, 0.1, synthetic.generate_ranges(n_u, n_i, dens, False, ur),
                     synthetic.generate_ranges(n_u, n_i, dens, True, ir), world=world, rank=rank,
-                    group=dist.group.WORLD, chunks=chunks)
+                    group=dist.group.WORLD, chunks=chunks, item_chunks=2)
     eng.init_user_factors(synthetic.SEED_INIT)
     eng.fit(3)
     torch.cuda.synchronize()
