@@ -379,28 +379,46 @@ __global__ __launch_bounds__(256) void cosine_kernel(const double* __restrict__ 
 // Per-row min / max of an f32 score matrix (NaN ignored, like np.nanmin):
 // out[r] = min, out[n_rows + r] = max (two contiguous halves, so the
 // cross-shard reduction is one MIN and one MAX all-reduce). One block per row.
-__global__ __launch_bounds__(256) void rows_minmax_kernel(const float* __restrict__ x, int64_t n, int64_t ld,
-                                                          float* __restrict__ out) {
-  __shared__ float smin[256], smax[256];
+// Per-row min / max (NaN ignored, like fminf). One 1024-thread block per
+// row streams it with 16-B loads (rows 16-B aligned) — HBM-bound.
+__global__ __launch_bounds__(1024) void rows_minmax_kernel(const float* __restrict__ x, int64_t n, int64_t ld,
+                                                           int vec4, float* __restrict__ out) {
+  __shared__ float smin[16], smax[16];
   const float* r = x + (int64_t)blockIdx.x * ld;
   float lo = __builtin_inff(), hi = -__builtin_inff();
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
+  int64_t j0 = 0;
+  if (vec4) {
+    const int64_t n4 = n >> 2;
+    const float4* r4 = reinterpret_cast<const float4*>(r);
+    for (int64_t j = threadIdx.x; j < n4; j += 1024) {
+      const float4 v = r4[j];
+      lo = fminf(fminf(lo, v.x), fminf(v.y, fminf(v.z, v.w)));
+      hi = fmaxf(fmaxf(hi, v.x), fmaxf(v.y, fmaxf(v.z, v.w)));
+    }
+    j0 = n4 << 2;
+  }
+  for (int64_t j = j0 + threadIdx.x; j < n; j += 1024) {
     lo = fminf(lo, r[j]);
     hi = fmaxf(hi, r[j]);
   }
-  smin[threadIdx.x] = lo;
-  smax[threadIdx.x] = hi;
-  __syncthreads();
-  for (int s2 = 128; s2 > 0; s2 >>= 1) {
-    if (threadIdx.x < s2) {
-      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s2]);
-      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s2]);
-    }
-    __syncthreads();
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, off, kWave));
+    hi = fmaxf(hi, __shfl_xor(hi, off, kWave));
   }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smin[w] = lo;
+    smax[w] = hi;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    out[blockIdx.x] = smin[0];              // mins  [n_rows]
-    out[gridDim.x + blockIdx.x] = smax[0];  // maxes [n_rows]
+    for (int q = 1; q < 16; ++q) {
+      lo = fminf(lo, smin[q]);
+      hi = fmaxf(hi, smax[q]);
+    }
+    out[blockIdx.x] = lo;              // mins  [n_rows]
+    out[gridDim.x + blockIdx.x] = hi;  // maxes [n_rows]
   }
 }
 
@@ -431,6 +449,183 @@ __global__ __launch_bounds__(256) void fuse_rows_kernel(const float* __restrict_
   const double an = (double)als[r * ld + j] * ascale + amin_;
   const float tn = tt[r * ld + j] * tscale + tmin_;
   fused[r * n + j] = w0 * an + w1 * (double)tn;
+}
+
+// fuse_rows_kernel's arithmetic + a stable top-kk (kk <= kFuseK) of each
+// segment of kFuseSeg items, without materialising the fused row. One WAVE
+// per segment (no block barriers). Each fused f64 becomes an order-preserving
+// u64 key (NaN lowest, as `better` ranks it), so every comparison is one
+// integer compare; lane l holds items seg0 + 64 e + l (ascending e =
+// ascending index, so a strict '>' keeps the earlier item on ties).
+//   1. t = the kk-th best of the 64 lane maxima (kk rounds of a wave
+//      arg-best; the winning LANE drops out) — a lower bound of the
+//      segment's kk-th best, since those kk maxima are kk distinct items;
+//   2. items not worse than t are the candidates (ballot-compacted into LDS;
+//      typically ~kk of them; more than 64 — heavy ties — falls back to
+//      exact rescans);
+//   3. kk rounds of a wave arg-best over the candidates (key desc, index asc)
+//      -> [row][seg*kk] (value, index).
+constexpr int kFuseK = 8;
+constexpr int kFusePer = 16;
+constexpr int kFuseSeg = 64 * kFusePer;
+
+__device__ __forceinline__ uint64_t order_key(double v) {
+  if (v != v) return 0;  // NaN ranks below every number
+  const uint64_t b = (uint64_t)__double_as_longlong(v + 0.0);  // -0 -> +0 (they compare equal)
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key_value(uint64_t k) {
+  if (k == 0) return __builtin_nan("");
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+struct KI {
+  uint64_t k;
+  int64_t i;  // INT64_MAX: no item
+};
+__device__ __forceinline__ bool ki_better(const KI& a, const KI& b) {  // a ranks before b
+  return a.i != INT64_MAX && (b.i == INT64_MAX || a.k > b.k || (a.k == b.k && a.i < b.i));
+}
+__device__ __forceinline__ KI wave_best_ki(KI x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    KI y;
+    y.k = ((uint64_t)(uint32_t)__shfl_xor((int)(x.k >> 32), off, kWave) << 32) |
+          (uint32_t)__shfl_xor((int)x.k, off, kWave);
+    y.i = __shfl_xor(x.i, off, kWave);
+    if (ki_better(y, x)) x = y;
+  }
+  return x;
+}
+
+template <int KK>
+__global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
+    const float* __restrict__ als, const float* __restrict__ tt, int64_t n, int64_t ld, int64_t segs,
+    const float* __restrict__ als_mm, const float* __restrict__ tt_mm, double w0, double w1,
+    double* __restrict__ cand_v, int64_t* __restrict__ cand_i) {
+#pragma clang fp contract(off)
+  __shared__ uint64_t ck_sh[4][128];  // [64, 128): scratch slots of non-candidates
+  __shared__ int ce_sh[4][128];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wv;
+  if (seg >= segs) return;
+  const int64_t r = blockIdx.y;
+  const int64_t R = gridDim.y;
+  const double amin = (double)als_mm[r], amax = (double)als_mm[R + r];
+  double arange = amax - amin;
+  if (arange < 10.0 * DBL_EPSILON) arange = 1.0;
+  const double ascale = 1.0 / arange;
+  const double amin_ = 0.0 - amin * ascale;
+  const float tmin = tt_mm[r], tmax = tt_mm[R + r];
+  float trange = tmax - tmin;
+  if (trange < 10.0f * FLT_EPSILON) trange = 1.0f;
+  const float tscale = 1.0f / trange;
+  const float tmin_ = 0.0f - tmin * tscale;
+  const int64_t seg0 = seg * kFuseSeg;
+  const float* __restrict__ ar = als + r * ld + seg0 + lane;
+  const float* __restrict__ tr = tt + r * ld + seg0 + lane;
+  const int nvalid = (int)((n - seg0) < kFuseSeg ? (n - seg0) : kFuseSeg);  // items of this segment
+  uint64_t key[kFusePer];
+  float av[kFusePer], tv[kFusePer];
+  if (nvalid == kFuseSeg) {  // full segment: unconditional loads
+#pragma unroll
+    for (int e = 0; e < kFusePer; ++e) {
+      av[e] = ar[e * 64];
+      tv[e] = tr[e * 64];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < kFusePer; ++e) {
+      const int off = e * 64 + lane < nvalid ? e * 64 : 0;  // the lane's first item is in range
+      av[e] = ar[off];
+      tv[e] = tr[off];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < kFusePer; ++e) {
+    const double an = (double)av[e] * ascale + amin_;
+    const float tn = tv[e] * tscale + tmin_;
+    const uint64_t kv = order_key(w0 * an + w1 * (double)tn);
+    key[e] = e * 64 + lane < nvalid ? kv : 0;
+  }
+  const int nmine = nvalid > lane ? (nvalid - lane + 63) >> 6 : 0;  // live items of this lane
+  // 1. lane arg-best (strict '>' in ascending e keeps the earliest of equals)
+  uint64_t bk = key[0];
+  int be = 0;
+#pragma unroll
+  for (int e = 1; e < kFusePer; ++e) {
+    const bool gt = key[e] > bk;
+    bk = gt ? key[e] : bk;
+    be = gt ? e : be;
+  }
+  KI mine{bk, nmine > 0 ? seg0 + (int64_t)be * 64 + lane : INT64_MAX};
+  KI t{0, INT64_MAX};
+  for (int q = 0; q < KK; ++q) {
+    const KI w = wave_best_ki(mine);
+    if (w.i == INT64_MAX) break;
+    t = w;
+    if (w.i == mine.i) mine.i = INT64_MAX;
+  }
+  // 2. candidates: items not worse than t (no t: fewer than kk items, take all)
+  int nc = 0;
+  bool overflow = false;
+#pragma unroll
+  for (int e = 0; e < kFusePer; ++e) {
+    const int64_t j = seg0 + (int64_t)e * 64 + lane;
+    const bool live = e < nmine;
+    const bool c = live && (t.i == INT64_MAX || key[e] > t.k || (key[e] == t.k && j <= t.i));
+    const uint64_t m = __ballot(c);
+    const int cnt = __popcll(m);
+    if (nc + cnt > 64) {
+      overflow = true;
+      break;
+    }
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const int slot = c ? nc + below : 64 + lane;  // branch-free append
+    ck_sh[wv][slot] = key[e];
+    ce_sh[wv][slot] = e * 64 + lane;
+    nc += cnt;
+  }
+  const int64_t obase = r * segs * KK + seg * KK;
+  if (!overflow) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    KI c{0, INT64_MAX};
+    if (lane < nc) c = KI{ck_sh[wv][lane], seg0 + ce_sh[wv][lane]};
+    for (int q = 0; q < KK; ++q) {
+      const KI w = wave_best_ki(c);
+      if (lane == 0) {
+        cand_v[obase + q] = key_value(w.k);
+        cand_i[obase + q] = w.i == INT64_MAX ? -1 : w.i;
+      }
+      if (w.i == c.i) c.i = INT64_MAX;
+    }
+    return;
+  }
+  // heavy ties: exact selection by rescans (the winning lane drops its item)
+  uint32_t live_mask = nmine >= 32 ? 0xffffffffu : ((1u << nmine) - 1u);  // kFusePer <= 32
+  auto rescan = [&](KI& m2) {
+    m2 = KI{0, INT64_MAX};
+#pragma unroll
+    for (int e = 0; e < kFusePer; ++e) {
+      const KI x{key[e], seg0 + (int64_t)e * 64 + lane};
+      if (((live_mask >> e) & 1u) && ki_better(x, m2)) m2 = x;
+    }
+  };
+  KI m2;
+  rescan(m2);
+  for (int q = 0; q < KK; ++q) {
+    const KI w = wave_best_ki(m2);
+    if (lane == 0) {
+      cand_v[obase + q] = key_value(w.k);
+      cand_i[obase + q] = w.i == INT64_MAX ? -1 : w.i;
+    }
+    if (w.i != INT64_MAX && w.i == m2.i) {
+      live_mask &= ~(1u << (int)((w.i - seg0) >> 6));
+      rescan(m2);
+    }
+  }
 }
 
 __global__ void add_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t off) {
@@ -508,6 +703,14 @@ extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_row
   HREC_REQUIRE(user_factors && user_rows && item_factors_t && out, "als_score: null pointer");
   HREC_REQUIRE(item_rows != nullptr || n_items <= ld_items, "als_score: n_items > ld_items");
   constexpr int UB = 16;
+  if (item_rows == nullptr && ld_items % 2 == 0 && (reinterpret_cast<uintptr_t>(item_factors_t) & 7) == 0) {
+    // every item in order: the packed-f32 kernel (same JVM-exact chain)
+    const dim3 grid((unsigned)((n_users + UB - 1) / UB), (unsigned)((n_items + 1023) / 1024));
+    hipLaunchKernelGGL((als_score_fast_kernel<UB, false>), grid, dim3(256), 0, as_stream(stream), user_factors,
+                       user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, out, nullptr, 0, 0, nullptr,
+                       nullptr, nullptr);
+    return check_launch("als_score_fast_kernel");
+  }
   const dim3 grid((unsigned)((n_items + 255) / 256), (unsigned)((n_users + UB - 1) / UB));
   hipLaunchKernelGGL((als_score_kernel<UB>), grid, dim3(256), 0, as_stream(stream), user_factors, user_rows,
                      n_users, item_factors_t, ld_items, item_rows, n_items, k, kp, out);
@@ -682,7 +885,9 @@ extern "C" int hrec_rows_minmax_f32(const float* x, int64_t n_rows, int64_t n, i
   if (n_rows == 0) return HREC_OK;
   HREC_REQUIRE(n_rows < (1ll << 31), "rows_minmax: too many rows");
   HREC_REQUIRE(x && out, "rows_minmax: null pointer");
-  hipLaunchKernelGGL(rows_minmax_kernel, dim3((unsigned)n_rows), dim3(256), 0, as_stream(stream), x, n, ld, out);
+  const int vec4 = (ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  hipLaunchKernelGGL(rows_minmax_kernel, dim3((unsigned)n_rows), dim3(1024), 0, as_stream(stream), x, n, ld, vec4,
+                     out);
   return check_launch("rows_minmax_kernel");
 }
 
@@ -702,15 +907,38 @@ extern "C" int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_
   const size_t need = hrec_fuse_rows_workspace_bytes(n_rows, n, top_k);
   HREC_REQUIRE(workspace_bytes >= need, "fuse_rows_topk: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t s = as_stream(stream);
-  double* fused = (double*)workspace;
-  char* tws = (char*)workspace + (((size_t)n_rows * n * 8 + 255) & ~(size_t)255);
   const double w0 = als_wins ? 0.8 : 0.2, w1 = als_wins ? 0.2 : 0.8;
-  hipLaunchKernelGGL(fuse_rows_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n_rows), dim3(256), 0, s, als, tt,
-                     n, ld, als_minmax, tt_minmax, w0, w1, fused);
-  int rc = check_launch("fuse_rows_kernel");
-  if (rc) return rc;
   const int kk = (int)(top_k < n ? top_k : n);
-  rc = topk_rows<double>(fused, n_rows, n, n, kk, out_idx, out_val, tws, (size_t)1 << 62, s);
+  int rc;
+  if (kk <= kFuseK) {
+    // fused values never hit HBM: segment candidates, then the merge
+    const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg;
+    double* cv = (double*)workspace;
+    int64_t* ci = (int64_t*)((char*)workspace + (((size_t)n_rows * segs * kk * 8 + 255) & ~(size_t)255));
+    char* tws = (char*)ci + (((size_t)n_rows * segs * kk * 8 + 255) & ~(size_t)255);
+    const dim3 g((unsigned)((segs + 3) / 4), (unsigned)n_rows);
+#define HREC_FUSE_K(K)                                                                                        \
+  case K:                                                                                                     \
+    hipLaunchKernelGGL(fuse_segment_topk_kernel<K>, g, dim3(256), 0, s, als, tt, n, ld, segs, als_minmax, tt_minmax, \
+                       w0, w1, cv, ci);                                                                      \
+    break;
+    switch (kk) {
+      HREC_FUSE_K(1) HREC_FUSE_K(2) HREC_FUSE_K(3) HREC_FUSE_K(4) HREC_FUSE_K(5) HREC_FUSE_K(6) HREC_FUSE_K(7)
+      default: HREC_FUSE_K(8)
+    }
+#undef HREC_FUSE_K
+    rc = check_launch("fuse_segment_topk_kernel");
+    if (rc) return rc;
+    rc = topk_rows<double>(cv, n_rows, segs * kk, segs * kk, kk, out_idx, out_val, tws, (size_t)1 << 62, s, ci);
+  } else {
+    double* fused = (double*)workspace;
+    char* tws = (char*)workspace + (((size_t)n_rows * n * 8 + 255) & ~(size_t)255);
+    hipLaunchKernelGGL(fuse_rows_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n_rows), dim3(256), 0, s, als,
+                       tt, n, ld, als_minmax, tt_minmax, w0, w1, fused);
+    rc = check_launch("fuse_rows_kernel");
+    if (rc) return rc;
+    rc = topk_rows<double>(fused, n_rows, n, n, kk, out_idx, out_val, tws, (size_t)1 << 62, s);
+  }
   if (rc || idx_offset == 0) return rc;
   const int64_t tot = n_rows * kk;
   hipLaunchKernelGGL(add_offset_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out_idx, tot, idx_offset);

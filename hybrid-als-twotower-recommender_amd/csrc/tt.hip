@@ -143,40 +143,60 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void tt_score_mfma_kernel(const float* __restrict__ U, int B,
                                                             const float* __restrict__ V, int64_t N, int d,
                                                             float* __restrict__ out) {
+  // One 64-item tile per block; the block walks every 64-user tile, so each
+  // item vector is read from HBM once (the user vectors stay in L2).
   __shared__ float Us[64][65];
   __shared__ float Vs[64][65];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b0 = blockIdx.y * 64;
   const int64_t j0 = (int64_t)blockIdx.x * 64;
-  f4v acc[4];
+  const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    f4v acc[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < d; k0 += 64) {
-    for (int o = threadIdx.x; o < 64 * 64; o += 256) {
-      const int r = o >> 6, c = o & 63;
-      const int kk = k0 + c;
-      Us[r][c] = (b0 + r < B && kk < d) ? U[(int64_t)(b0 + r) * d + kk] : 0.f;
-      Vs[r][c] = (j0 + r < N && kk < d) ? V[(j0 + r) * d + kk] : 0.f;
-    }
-    __syncthreads();
+    for (int t = 0; t < 4; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < d; k0 += 64) {
+      __syncthreads();  // the previous tile's readers are done with Us/Vs
+      for (int o = threadIdx.x; o < 64 * 64; o += 256) {
+        const int r = o >> 6, c = o & 63;
+        const int kk = k0 + c;
+        Us[r][c] = (b0 + r < B && kk < d) ? U[(int64_t)(b0 + r) * d + kk] : 0.f;
+        if (b0 == 0 || d > 64) Vs[r][c] = (j0 + r < N && kk < d) ? V[(j0 + r) * d + kk] : 0.f;
+      }
+      __syncthreads();
 #pragma unroll 4
-    for (int ks = 0; ks < 16; ++ks) {
-      const float a = Us[16 * w + (lane & 15)][4 * ks + (lane >> 4)];
+      for (int ks = 0; ks < 16; ++ks) {
+        const float a = Us[16 * w + (lane & 15)][4 * ks + (lane >> 4)];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float b = Vs[16 * t + (lane & 15)][4 * ks + (lane >> 4)];
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) {
+          const float b = Vs[16 * t + (lane & 15)][4 * ks + (lane >> 4)];
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+        }
       }
     }
+    // stage the 64 x 64 tile in LDS (over Us), then write each user's 64
+    // items as 256 contiguous bytes (16 lanes x float4)
     __syncthreads();
-  }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int64_t j = j0 + 16 * t + (lane & 15);
+    for (int t = 0; t < 4; ++t) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = b0 + 16 * w + 4 * (lane >> 4) + r;
-      if (b < B && j < N) out[(int64_t)b * N + j] = acc[t][r];
+      for (int r = 0; r < 4; ++r) Us[16 * w + 4 * (lane >> 4) + r][16 * t + (lane & 15)] = acc[t][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = q * 256 + threadIdx.x;
+      const int row = o >> 4, c4 = (o & 15) * 4;
+      const int b = b0 + row;
+      const int64_t j = j0 + c4;
+      if (b >= B) continue;
+      float* dst = out + (int64_t)b * N + j;
+      if (vec && j + 3 < N) {
+        *reinterpret_cast<float4*>(dst) =
+            make_float4(Us[row][c4], Us[row][c4 + 1], Us[row][c4 + 2], Us[row][c4 + 3]);
+      } else {
+        for (int e = 0; e < 4; ++e)
+          if (j + e < N) dst[e] = Us[row][c4 + e];
+      }
     }
   }
 }
@@ -492,7 +512,8 @@ extern "C" int hrec_tt_score(const float* user_vec, int n_users, const float* it
                        dim3(kBlock), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
     return check_launch("tt_score_kernel");
   }
-  hipLaunchKernelGGL(tt_score_mfma_kernel, dim3((unsigned)((n_items + 63) / 64), (unsigned)((n_users + 63) / 64)),
+  HREC_REQUIRE((n_items + 63) / 64 < (1ll << 32), "tt_score: grid too large");
+  hipLaunchKernelGGL(tt_score_mfma_kernel, dim3((unsigned)((n_items + 63) / 64)),
                      dim3(256), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
   return check_launch("tt_score_mfma_kernel");
 }
