@@ -195,9 +195,14 @@ def main():
             _hrec.als_score_topk(eng.U, users, Vt, n_items, k, 5)
         torch.cuda.synchronize()
         sc_s = (time.perf_counter() - s0) / reps
-        scoring = {"pairs_per_s": B * n_items / sc_s, "ms_per_batch": sc_s * 1e3, "users": B,
+        pps = B * n_items / sc_s
+        scoring = {"pairs_per_s": pps, "ms_per_batch": sc_s * 1e3, "users": B,
                    "items": n_items, "top_k": 5, "dtype": "f32 (JVM-exact, no FMA)",
-                   "kernel": "hrec_als_score_topk (sample bound + fused filter + exact top-k)"}
+                   "kernel": "hrec_als_score_topk (sample bound + fused filter + exact top-k)",
+                   # JVM-exact: k rounded products + k rounded sums per pair, no FMA/MFMA
+                   # -> bound by the f32 VALU (packed mul/add: half the 157.3 TF FMA peak)
+                   "roofline": {"bound": "valu-f32 (mul+add, no FMA)", "achieved": pps * 2 * k / 1e12,
+                                "peak": 78.6, "unit": "TFLOP/s", "frac": pps * 2 * k / 1e12 / 78.6}}
 
     # End-to-end hybrid top-5 (HybridRecommendationSystem.get_hybrid_recommendations
     # for a batch of users): JVM-exact ALS scores + two-tower Dot (d=64, Keras
