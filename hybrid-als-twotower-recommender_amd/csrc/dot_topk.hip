@@ -1,0 +1,458 @@
+// K8: user x item dot-product scoring on the matrix cores, with a fused top-k
+// survivor filter — the "scored user-item pairs" half of the metric at
+// BASELINE configs c4 (two-tower d = 128, 50M candidates) and c5 (bf16
+// factors, d = 256).
+//
+// Replaces the two-tower scoring of the reference — Keras Dot(axes=1) over
+// every candidate in model.predict (src/two_tower_model.py:80, :136-146) —
+// and the ranking that follows it (sorted(..., reverse=True)[:k],
+// src/hybrid_system.py:108; src/evaluation.py ranks the same way). The item
+// tower output is computed once (hrec_tt_item_forward), so scoring is a GEMM
+// [users, d] x [d, items] whose result is never written to HBM: every tile
+// is compared in registers with a per-user lower bound of the k-th best
+// score, and only survivors are appended to a per-user candidate list, which
+// an exact stable top-k then ranks (ties -> smaller item index = the order
+// of the reference's candidate list, which Python's stable sort keeps).
+//
+// Tiling (gfx950): a 512-thread block owns 128 users x 256 items; wave w
+// computes 64 users (w & 1) x 64 items (w >> 1) as 4 x 4 tiles of 16 x 16.
+// Every lane fetches 16 B per operand fragment: for bf16 that is one
+// v_mfma_f32_16x16x32_bf16 operand (8 consecutive k), for f32 the operands of
+// four v_mfma_f32_16x16x4_f32 steps (k = 16s + 4g + e, g = lane >> 4). The
+// block's user rows sit in LDS (rows padded by 16 B: conflict-free b128
+// reads); item fragments are loaded straight from HBM (each item is read by
+// the 2 user-waves of its column; the user tiles of one item group run on the
+// same XCD, so the other user tiles hit that XCD's L2).
+#include <float.h>
+#include <stdlib.h>
+
+#include "common.h"
+
+namespace hrec {
+
+typedef float dot_f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 dot_bf8 __attribute__((ext_vector_type(8)));
+
+constexpr int kDotThreads = 512;
+
+template <bool BF16, int DK>
+struct DotShape {
+  static constexpr int kElem = BF16 ? 2 : 4;
+  static constexpr int kStep = BF16 ? 32 : 16;     // k per 16-B lane fragment (over the 4 lane groups)
+  static constexpr int kSteps = DK / kStep;
+  static constexpr int kChunks = DK * kElem / 16;   // 16-B chunks per row
+  static constexpr int kRow = DK * kElem + 16;      // LDS bytes per user row
+};
+
+typedef int dot_rsrc __attribute__((ext_vector_type(4)));
+// buffer_load_dwordx4 ... idxen offen (structured: vindex * stride + voffset)
+__device__ dot_f4 dot_sbuf_load(dot_rsrc rsrc, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.buffer.load.v4f32");
+
+union DotFrag {
+  int4 i;
+  dot_f4 f;
+};
+
+template <bool BF16>
+__device__ __forceinline__ void dot_mma(const DotFrag& a, const DotFrag& b, dot_f4& acc) {
+  if constexpr (BF16) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dot_bf8, a.i), __builtin_bit_cast(dot_bf8, b.i),
+                                                  acc, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.f[e], b.f[e], acc, 0, 0, 0);
+  }
+}
+
+// FILTER = false: out[b * ldo + j] = score of item row j * item_step (j < n_items).
+// FILTER = true:  append (score, j + idx_offset) to user b's candidate list when
+//                 score >= thr[b * thr_stride] (a NaN threshold admits every score).
+// Wave grid WU (users) x 8/WU (items); each wave owns NU x NI tiles of 16 x 16:
+// a block covers 16 NU WU users x 16 NI (8/WU) items.
+template <int NU_, int NI_, int WU_>
+struct DotTiling {
+  static constexpr int NU = NU_, NI = NI_, WU = WU_, WI = 8 / WU_;
+  static constexpr int kUsers = 16 * NU * WU;
+  static constexpr int kItems = 16 * NI * WI;
+};
+
+template <bool BF16, int DK, bool FILTER, class TL>
+__global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
+    const char* __restrict__ U, int B, const char* __restrict__ V, int64_t n_rows, int64_t n_items,
+    int64_t item_step, int n_ut, float* __restrict__ out, int64_t ldo, const float* __restrict__ thr, int thr_stride,
+    int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n, int64_t idx_offset) {
+  using S = DotShape<BF16, DK>;
+  constexpr int NU = TL::NU, NI = TL::NI;
+  __shared__ __attribute__((aligned(16))) char us[TL::kUsers * S::kRow];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int wu = w % TL::WU, wi = w / TL::WU;
+  // XCD-aware map (blocks go round-robin over the 8 XCDs): XCD x takes the
+  // consecutive logical blocks [x * nblk/8, (x+1) * nblk/8), user tile fastest.
+  const int per_xcd = gridDim.x >> 3;
+  const int lin = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int ut = lin % n_ut;
+  const int64_t ig = lin / n_ut, n_ig = gridDim.x / n_ut;
+  const int64_t n_it = (n_items + TL::kItems - 1) / TL::kItems;
+  if (ig >= n_it) return;  // block-uniform
+  const int b0 = ut * TL::kUsers;
+  for (int o = threadIdx.x; o < TL::kUsers * S::kChunks; o += kDotThreads) {
+    const int r = o / S::kChunks, q = o % S::kChunks;
+    int4 v = {0, 0, 0, 0};
+    if (b0 + r < B) v = *reinterpret_cast<const int4*>(U + (int64_t)(b0 + r) * (DK * S::kElem) + 16 * q);
+    *reinterpret_cast<int4*>(us + r * S::kRow + 16 * q) = v;
+  }
+  const int ub = b0 + 16 * NU * wu + 4 * g;  // user of (tile u, reg r): ub + 16 u + r
+  float th[FILTER ? NU : 1][4];  // NaN = absent user (never passes), -inf = admit every score
+  if constexpr (FILTER) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = ub + 16 * u + r;
+        float t = __builtin_nanf("");
+        if (b < B) {
+          t = thr[(int64_t)b * thr_stride];
+          t = t == t ? t : -INFINITY;
+        }
+        th[u][r] = t;
+      }
+  }
+  __syncthreads();
+  const char* ubase = us + (16 * NU * wu + c) * S::kRow + 16 * g;
+  // Item fragments: structured buffer loads (address = V + vindex * row
+  // bytes + 16 g; the hardware range check returns zeros for vindex >=
+  // n_rows, so tails need no clamping), flowing through a ring of P steps
+  // issued P steps ahead across tile boundaries (the next tile's first steps
+  // load during the current tile's last MFMAs).
+  constexpr int PB = FILTER ? 4 : 2;
+  constexpr int P = BF16 ? (S::kSteps < PB ? S::kSteps : PB) : (S::kSteps < 2 ? S::kSteps : 2);
+  static_assert(S::kSteps % P == 0, "ring depth must divide the k steps");
+  const uint64_t vb = (uint64_t)V;
+  dot_rsrc rsrc;
+  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
+  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * S::kElem) << 16));
+  rsrc.z = __builtin_amdgcn_readfirstlane((int)n_rows);
+  rsrc.w = 0x00020000;
+  const int voff = 16 * g;
+  auto rows_of = [&](int64_t tile, int (&vi)[NI]) {
+    const int64_t jb = tile * TL::kItems + 16 * NI * wi;
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int64_t j = jb + 16 * t + c;
+      vi[t] = j < n_items ? (int)(j * item_step) : 0x7fffffff;
+    }
+  };
+  int vcur[NI], vnext[NI];
+  rows_of(ig, vcur);
+  DotFrag ring[P][NI];
+#pragma unroll
+  for (int q = 0; q < P; ++q)
+#pragma unroll
+    for (int t = 0; t < NI; ++t) ring[q][t].f = dot_sbuf_load(rsrc, vcur[t], voff + 64 * q, 0, 0);
+  for (int64_t it = ig; it < n_it; it += n_ig) {
+    const int64_t j0 = it * TL::kItems + 16 * NI * wi;
+    rows_of(it + n_ig, vnext);
+    dot_f4 acc[NU][NI];
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int t = 0; t < NI; ++t) acc[u][t] = dot_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k0 = 0; k0 < S::kSteps; k0 += P) {  // P steps per trip: ring slots stay compile-time
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const int ks = k0 + q;
+        DotFrag b[NI];
+        const bool same = ks + P < S::kSteps;
+        const int off = voff + 64 * (same ? ks + P : ks + P - S::kSteps);
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+          b[t] = ring[q][t];
+          ring[q][t].f = dot_sbuf_load(rsrc, same ? vcur[t] : vnext[t], off, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          DotFrag a;
+          a.i = *reinterpret_cast<const int4*>(ubase + 16 * u * S::kRow + 64 * ks);
+#pragma unroll
+          for (int t = 0; t < NI; ++t) dot_mma<BF16>(a, b[t], acc[u][t]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep each step's LDS reads in its step (VGPR budget)
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NI; ++t) vcur[t] = vnext[t];
+    // C/D layout of a 16 x 16 f32 tile: column = lane & 15 (item), row = 4g + r (user)
+    if constexpr (!FILTER) {
+#pragma unroll
+      for (int t = 0; t < NI; ++t) {
+        const int64_t j = j0 + 16 * t + c;
+        if (j >= n_items) continue;
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int b = ub + 16 * u + r;
+            if (b < B) out[(int64_t)b * ldo + j] = acc[u][t][r];
+          }
+      }
+    } else {
+      // Fast path: one v_cmp per score into a wave mask; survivors are rare,
+      // so the append path below runs for few tiles. Items past n_items
+      // (zero fragments) are rejected there.
+      uint64_t any = 0;
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int t = 0; t < NI; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) any |= __ballot(acc[u][t][r] >= th[u][r]);
+      if (any) {
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+          const int64_t j = j0 + 16 * t + c;
+#pragma unroll
+          for (int u = 0; u < NU; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float sc = acc[u][t][r];
+              if (j < n_items && sc >= th[u][r]) {
+                const int b = ub + 16 * u + r;
+                const int pos = atomicAdd(&cand_n[b], 1);
+                if (pos < cap) {
+                  cand_v[(int64_t)b * cap + pos] = sc;
+                  cand_i[(int64_t)b * cap + pos] = j + idx_offset;
+                }
+              }
+            }
+        }
+      }
+    }
+  }
+}
+
+__global__ void dot_overflow_kernel(const int* __restrict__ cand_n, int n_users, int cap, int* __restrict__ flag) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < n_users; b += gridDim.x * blockDim.x)
+    if (cand_n[b] > cap) atomicOr(flag, 1);
+}
+
+__global__ void dot_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t off) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && idx[i] >= 0) idx[i] += off;
+}
+
+// f32 -> bf16 bit patterns, round to nearest even (NaN stays NaN).
+__global__ void f32_to_bf16_kernel(const float* __restrict__ in, int64_t n, uint16_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t x = __float_as_uint(in[i]);
+    uint16_t h;
+    if ((x & 0x7fffffffu) > 0x7f800000u) h = (uint16_t)((x >> 16) | 0x40);
+    else h = (uint16_t)((x + 0x7fffu + ((x >> 16) & 1u)) >> 16);
+    out[i] = h;
+  }
+}
+
+// Tilings: FILTER passes keep each item fragment for 128 users (item bytes
+// through the vector cache halve vs 64 x 64 wave tiles; the user fragments
+// come from LDS, which has twice the bandwidth); HREC_DOT_TILING (0/1)
+// selects the variant for measurements.
+typedef DotTiling<4, 4, 2> DotTileA;   // 128 users x 256 items, wave 64 x 64
+typedef DotTiling<8, 2, 1> DotTileB;   // 128 users x 256 items, wave 128 x 32
+
+// Grid of the tile kernel: 8 * n_ut * m blocks (a multiple of 8 so the XCD map
+// is a bijection), about two 512-thread blocks per CU, no more item groups
+// than item tiles.
+static unsigned dot_grid(int n_ut, int64_t n_items, int tile_items) {
+  const int64_t n_it = (n_items + tile_items - 1) / tile_items;
+  int64_t m = (512 + 8 * n_ut - 1) / (8 * n_ut);
+  const int64_t m_max = (n_it + 7) / 8;
+  if (m > m_max) m = m_max;
+  if (m < 1) m = 1;
+  return (unsigned)(8 * n_ut * m);
+}
+
+static int dot_tiling_choice() {
+  static int v = [] {
+    const char* e = getenv("HREC_DOT_TILING");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <bool FILTER, class TL>
+static int dot_launch_t(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
+                        int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
+                        int64_t* ci, int* cn, int64_t off, hipStream_t s) {
+  const int n_ut = (B + TL::kUsers - 1) / TL::kUsers;
+  const dim3 grid(dot_grid(n_ut, n_items, TL::kItems)), block(kDotThreads);
+  const char* u = (const char*)U;
+  const char* v = (const char*)V;
+#define HREC_DOT(BF, DK)                                                                                         \
+  hipLaunchKernelGGL((dot_tile_kernel<BF, DK, FILTER, TL>), grid, block, 0, s, u, B, v, n_rows, n_items, step, n_ut, \
+                     out, ldo, thr, thr_stride, cap, cv, ci, cn, off)
+  if (bf16) {
+    switch (dk) {
+      case 32: HREC_DOT(true, 32); break;
+      case 64: HREC_DOT(true, 64); break;
+      case 128: HREC_DOT(true, 128); break;
+      default: HREC_DOT(true, 256); break;
+    }
+  } else {
+    switch (dk) {
+      case 32: HREC_DOT(false, 32); break;
+      case 64: HREC_DOT(false, 64); break;
+      case 128: HREC_DOT(false, 128); break;
+      default: HREC_DOT(false, 256); break;
+    }
+  }
+#undef HREC_DOT
+  return check_launch("dot_tile_kernel");
+}
+
+template <bool FILTER>
+static int dot_launch(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
+                      int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
+                      int64_t* ci, int* cn, int64_t off, hipStream_t s) {
+  if constexpr (!FILTER) {
+    return dot_launch_t<false, DotTileA>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
+                                         cv, ci, cn, off, s);
+  }
+  switch (dot_tiling_choice()) {
+    case 0:
+      return dot_launch_t<FILTER, DotTileA>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
+                                            cv, ci, cn, off, s);
+    default:
+      return dot_launch_t<FILTER, DotTileB>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
+                                            cv, ci, cn, off, s);
+  }
+}
+
+// Sample size and candidate capacity of the threshold filter: the k-th best
+// of S strided items is a lower bound of the k-th best of all n items, and
+// about k * n / S items beat it, so S = 4 k n / cap leaves ~4x headroom.
+static int64_t dot_cap(int kk) { return kk <= 64 ? 8192 : 128 * (int64_t)kk; }
+static int64_t dot_sample(int64_t n, int kk) {
+  if (n <= 16384) return n;
+  int64_t s = (4 * (int64_t)kk * n + dot_cap(kk) - 1) / dot_cap(kk);
+  if (s < 8192) s = 8192;
+  return s < n ? s : n;
+}
+
+static char* dot_carve(char*& p, size_t bytes) {
+  char* r = p;
+  p += (bytes + 255) & ~(size_t)255;
+  return r;
+}
+
+}  // namespace hrec
+
+using namespace hrec;
+
+static int dot_check(const void* U, int B, const void* V, int64_t n_items, int dk, int dtype, const char* who) {
+  HREC_REQUIRE(dk == 32 || dk == 64 || dk == 128 || dk == 256, "%s: dk must be 32, 64, 128 or 256 (got %d)", who, dk);
+  HREC_REQUIRE(dtype == 0 || dtype == 1, "%s: dtype must be 0 (f32) or 1 (bf16)", who);
+  HREC_REQUIRE(B >= 0 && n_items >= 0, "%s: negative size", who);
+  HREC_REQUIRE(B <= (1 << 24), "%s: at most 2^24 users per call", who);
+  HREC_REQUIRE(n_items < 0x7fffffffll, "%s: n_items must be < 2^31 - 1", who);
+  HREC_REQUIRE(B == 0 || n_items == 0 || (U && V), "%s: null pointer", who);
+  HREC_REQUIRE(((uintptr_t)U & 15) == 0 && ((uintptr_t)V & 15) == 0, "%s: vectors must be 16-B aligned", who);
+  return HREC_OK;
+}
+
+extern "C" int hrec_f32_to_bf16(const float* in, int64_t n, uint16_t* out, void* stream) {
+  HREC_REQUIRE(n >= 0, "f32_to_bf16: negative size");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(in && out, "f32_to_bf16: null pointer");
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), in, n, out);
+  return check_launch("f32_to_bf16_kernel");
+}
+
+extern "C" int hrec_dot_scores(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
+                               int dtype, float* out, int64_t ld_out, void* stream) {
+  int rc = dot_check(user_vec, n_users, item_vec, n_items, dk, dtype, "dot_scores");
+  if (rc) return rc;
+  HREC_REQUIRE(ld_out >= n_items, "dot_scores: ld_out < n_items");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(out, "dot_scores: null output");
+  return dot_launch<false>(user_vec, n_users, item_vec, n_items, n_items, 1, dk, dtype, out, ld_out, nullptr, 0, 0, nullptr,
+                           nullptr, nullptr, 0, as_stream(stream));
+}
+
+extern "C" size_t hrec_dot_topk_workspace_bytes(int n_users, int64_t n_items, int top_k) {
+  const size_t B = (size_t)(n_users > 0 ? n_users : 0);
+  const int kk = (int)(top_k < n_items ? top_k : n_items);
+  if (kk <= 0) return 256;
+  const int64_t S = dot_sample(n_items, kk), cap = dot_cap(kk);
+  size_t b = B * (size_t)S * 4 + 256;                 // sample scores
+  b += topk_ws_bytes(B, S, kk, 4) + 256;               // sample top-k workspace
+  b += B * (size_t)kk * 12 + 512;                      // sample top-k values / indices
+  b += B * (size_t)cap * 12 + 512;                     // candidates
+  b += B * 4 + 256;                                    // counters
+  b += topk_ws_bytes(B, cap, kk, 4) + 256;             // final top-k workspace
+  return b;
+}
+
+extern "C" int hrec_dot_topk(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
+                             int dtype, int top_k, const float* thr_in, int64_t idx_offset, int64_t* out_idx,
+                             float* out_val, int* overflow, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = dot_check(user_vec, n_users, item_vec, n_items, dk, dtype, "dot_topk");
+  if (rc) return rc;
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "dot_topk: top_k must be in [1, 1024]");
+  HREC_REQUIRE(n_users < 65536, "dot_topk: at most 65535 users per call");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(out_idx && out_val && overflow && workspace, "dot_topk: null pointer");
+  const size_t need = hrec_dot_topk_workspace_bytes(n_users, n_items, top_k);
+  HREC_REQUIRE(workspace_bytes >= need, "dot_topk: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t s = as_stream(stream);
+  const int kk = (int)(top_k < n_items ? top_k : n_items);
+  const int64_t S = dot_sample(n_items, kk), cap = dot_cap(kk);
+  char* p = (char*)workspace;
+  float* samp = (float*)dot_carve(p, (size_t)n_users * S * 4);
+  char* tws = dot_carve(p, topk_ws_bytes(n_users, S, kk, 4));
+  float* sv = (float*)dot_carve(p, (size_t)n_users * kk * 4);
+  int64_t* si = (int64_t*)dot_carve(p, (size_t)n_users * kk * 8);
+  float* cv = (float*)dot_carve(p, (size_t)n_users * cap * 4);
+  int64_t* ci = (int64_t*)dot_carve(p, (size_t)n_users * cap * 8);
+  int* cn = (int*)dot_carve(p, (size_t)n_users * 4);
+  char* fws = dot_carve(p, topk_ws_bytes(n_users, cap, kk, 4));
+  if (hipMemsetAsync(overflow, 0, sizeof(int), s) != hipSuccess) return check_launch("dot_topk: memset");
+  if (S == n_items && thr_in == nullptr) {  // small: every score, exact top-k
+    rc = dot_launch<false>(user_vec, n_users, item_vec, n_items, n_items, 1, dk, dtype, samp, n_items, nullptr, 0, 0, nullptr,
+                           nullptr, nullptr, 0, s);
+    if (rc) return rc;
+    rc = topk_rows<float>(samp, n_users, n_items, n_items, kk, out_idx, out_val, tws, (size_t)1 << 62, s);
+  } else {
+    const float* thr = thr_in;
+    int thr_stride = 1;
+    if (thr == nullptr) {  // 1) thresholds: the kk-th best of S strided items
+      const int64_t step = n_items / S;
+      rc = dot_launch<false>(user_vec, n_users, item_vec, n_items, S, step, dk, dtype, samp, S, nullptr, 0, 0, nullptr,
+                             nullptr, nullptr, 0, s);
+      if (rc) return rc;
+      rc = topk_rows<float>(samp, n_users, S, S, kk, si, sv, tws, (size_t)1 << 62, s);
+      if (rc) return rc;
+      thr = sv + (kk - 1);
+      thr_stride = kk;
+    }
+    // 2) fused score + survivor filter over every item
+    if (hipMemsetAsync(ci, 0xff, (size_t)n_users * cap * 8, s) != hipSuccess ||
+        hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
+      return check_launch("dot_topk: memset");
+    rc = dot_launch<true>(user_vec, n_users, item_vec, n_items, n_items, 1, dk, dtype, nullptr, 0, thr, thr_stride, (int)cap,
+                          cv, ci, cn, 0, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(dot_overflow_kernel, dim3(64), dim3(256), 0, s, cn, n_users, (int)cap, overflow);
+    rc = check_launch("dot_overflow_kernel");
+    if (rc) return rc;
+    // 3) exact stable top-k of the survivors (item index breaks ties)
+    rc = topk_rows<float>(cv, n_users, cap, cap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
+  }
+  if (rc || idx_offset == 0) return rc;
+  const int64_t tot = (int64_t)n_users * kk;
+  hipLaunchKernelGGL(dot_offset_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out_idx, tot, idx_offset);
+  return check_launch("dot_offset_kernel");
+}

@@ -633,16 +633,13 @@ __global__ void add_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t 
   if (i < n && idx[i] >= 0) idx[i] += off;
 }
 
-template <typename T>
-int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
-              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr);
-
 }  // namespace hrec
 
 using namespace hrec;
 
 // Workspace for a stable top-k of n_rows rows of n elements (bytes).
-static size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
+namespace hrec {
+size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
   size_t total = 0;
   int64_t m = n;
   while (true) {
@@ -654,6 +651,7 @@ static size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
   }
   return total + 256;
 }
+}  // namespace hrec
 
 namespace hrec {
 template <typename T>
@@ -691,6 +689,10 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
     stride = cand;
   }
 }
+template int topk_rows<float>(const float*, int64_t, int64_t, int64_t, int, int64_t*, float*, void*, size_t,
+                              hipStream_t, const int64_t*);
+template int topk_rows<double>(const double*, int64_t, int64_t, int64_t, int, int64_t*, double*, void*, size_t,
+                               hipStream_t, const int64_t*);
 }  // namespace hrec
 
 extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_rows, int n_users,

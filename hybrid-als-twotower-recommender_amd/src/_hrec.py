@@ -79,6 +79,11 @@ _SIGNATURES.update({
                                           _vp, _c_sz, _vp]),
     "hrec_adam_dense": (_c_i32, [_vp, _vp, _vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                  ctypes.c_float, _vp]),
+    "hrec_f32_to_bf16": (_c_i32, [_vp, _c_i64, _vp, _vp]),
+    "hrec_dot_scores": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i64, _vp]),
+    "hrec_dot_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
+    "hrec_dot_topk": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp,
+                               _c_sz, _vp]),
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
                          [ctypes.c_float] * 6 + [_vp]),
 })
@@ -378,6 +383,123 @@ def tt_score(user_vec, item_vec):
         _dev(user_vec, torch.float32, "user_vec"), B, _dev(item_vec, torch.float32, "item_vec"), N, d,
         _dev(out, torch.float32, "out"), _stream()))
     return out
+
+
+# ------------------------------------------------- matrix-core dot + top-k
+DOT_DK = (32, 64, 128, 256)
+
+
+def dot_dk(d):
+    """Row width the dot kernels read (d zero-padded up to 32/64/128/256)."""
+    for dk in DOT_DK:
+        if d <= dk:
+            return dk
+    raise HrecError(f"dot: vector width {d} > 256 is not supported")
+
+
+def to_bf16(x):
+    """f32 device tensor -> bfloat16 tensor (round to nearest even, on the device)."""
+    x = x.contiguous()
+    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    _check("hrec_f32_to_bf16", lib().hrec_f32_to_bf16(
+        _dev(x, torch.float32, "in"), x.numel(), _vp(out.data_ptr()), _stream()))
+    return out
+
+
+def dot_operand(x, dtype=torch.float32):
+    """[n, d] f32 vectors -> the kernels' operand: rows of dot_dk(d) elements,
+    zero-padded, in f32 or bf16 (16-B aligned, contiguous)."""
+    n, d = x.shape
+    dk = dot_dk(d)
+    if d != dk or not x.is_contiguous():
+        padded = torch.zeros((n, dk), dtype=x.dtype, device=x.device)
+        padded[:, :d] = x
+        x = padded
+    if dtype == torch.bfloat16:
+        return x if x.dtype == torch.bfloat16 else to_bf16(x)
+    if x.dtype != torch.float32:
+        raise HrecError(f"dot_operand: expected float32, got {x.dtype}")
+    return x
+
+
+def _dot_args(U, V):
+    if U.dtype != V.dtype or U.dtype not in (torch.float32, torch.bfloat16):
+        raise HrecError("dot: operands must both be float32 or both bfloat16 (see dot_operand)")
+    if U.shape[1] != V.shape[1] or U.shape[1] not in DOT_DK:
+        raise HrecError(f"dot: operand widths {U.shape[1]} / {V.shape[1]} must match and be one of {DOT_DK}")
+    for t, name in ((U, "user_vec"), (V, "item_vec")):
+        if not t.is_cuda or not t.is_contiguous():
+            raise HrecError(f"dot: {name} must be a contiguous device tensor")
+    return U.shape[1], int(U.dtype == torch.bfloat16)
+
+
+def dot_scores(U, V):
+    """out[b, j] = <U[b], V[j]> on the matrix cores (f32 accumulation).
+    U, V: operands from dot_operand (same dtype and width)."""
+    dk, bf = _dot_args(U, V)
+    B, N = U.shape[0], V.shape[0]
+    out = torch.empty((B, N), dtype=torch.float32, device=U.device)
+    _check("hrec_dot_scores", lib().hrec_dot_scores(
+        _vp(U.data_ptr()), B, _vp(V.data_ptr()), N, dk, bf, _dev(out, torch.float32, "out"), N, _stream()))
+    return out
+
+
+DOT_USER_CHUNK = 4096
+
+
+def dot_topk(U, V, top_k, idx_offset=0, max_rounds=2):
+    """Stable top-k of <U[b], V[j]> over all j, never materialising the score
+    matrix (hrec_dot_topk). Ties -> smaller j. Returns (idx int64 [B, kk]
+    (+ idx_offset), val f32 [B, kk]), kk = min(top_k, N). When a user's
+    survivor list overflows, the k-th best of the survivors (a valid, higher
+    lower bound) seeds another round; after max_rounds the exact chunked path
+    (scores + top-k per chunk + keyed merge) answers."""
+    dk, bf = _dot_args(U, V)
+    B, N = U.shape[0], V.shape[0]
+    kk = min(int(top_k), int(N))
+    dev = U.device
+    out_i = torch.empty((B, kk), dtype=torch.int64, device=dev)
+    out_v = torch.empty((B, kk), dtype=torch.float32, device=dev)
+    if B == 0 or kk == 0:
+        return out_i, out_v
+    for b0 in range(0, B, DOT_USER_CHUNK):
+        b1 = min(B, b0 + DOT_USER_CHUNK)
+        Ub = U[b0:b1]
+        nb = b1 - b0
+        need = int(lib().hrec_dot_topk_workspace_bytes(nb, N, kk))
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        oi, ov = out_i[b0:b1], out_v[b0:b1]
+        thr = None
+        for _ in range(max_rounds):
+            _check("hrec_dot_topk", lib().hrec_dot_topk(
+                _vp(Ub.data_ptr()), nb, _vp(V.data_ptr()), N, dk, bf, kk,
+                None if thr is None else _dev(thr, torch.float32, "thr"), int(idx_offset),
+                _dev(oi, torch.int64, "out_idx"), _dev(ov, torch.float32, "out_val"),
+                _dev(flag, torch.int32, "overflow"), _dev(ws, torch.uint8, "ws"), need, _stream()))
+            if int(flag.item()) == 0:
+                break
+            thr = ov[:, kk - 1].contiguous()
+        else:
+            ci, cv = _dot_topk_chunked(Ub, V, kk, idx_offset)
+            oi.copy_(ci)
+            ov.copy_(cv)
+    return out_i, out_v
+
+
+def _dot_topk_chunked(U, V, kk, idx_offset, chunk=1 << 20):
+    """Exact fallback: dot_scores per item chunk, per-chunk stable top-k with
+    global ids, keyed merge (ties -> smaller id)."""
+    cand_i, cand_v = [], []
+    for j0 in range(0, V.shape[0], chunk):
+        s = dot_scores(U, V[j0:j0 + chunk])
+        i, v = topk(s, kk)
+        cand_i.append(i + (j0 + idx_offset))
+        cand_v.append(v.double())
+    ci = torch.cat(cand_i, 1).contiguous()
+    cv = torch.cat(cand_v, 1).contiguous()
+    i, v = topk_keyed(cv, ci, kk)
+    return i, v.float()
 
 
 def tt_pair_score(user_vec, item_vec):

@@ -295,6 +295,34 @@ int hrec_adam_sparse(float* var, float* m, float* v, int64_t n_rows, int dim,
                      float one_minus_beta1, float beta2, float one_minus_beta2,
                      float epsilon, void* stream);
 
+/* ---------------------------------------------------------------------
+ * Matrix-core dot-product scoring + fused top-k (csrc/dot_topk.hip).
+ * Replaces Keras Dot(axes=1) over every candidate in model.predict
+ * (src/two_tower_model.py:80, :136-146) and the ranking after it
+ * (sorted(..., reverse=True)[:k], src/hybrid_system.py:108), at BASELINE
+ * configs c4 (d = 128, 50M candidates) and c5 (bf16, d = 256).
+ * Operands: row-major [n, dk] with dk in {32, 64, 128, 256} (the model's d
+ * zero-padded), 16-B aligned; dtype 0 = f32 (exact f32 fma chains on
+ * v_mfma_f32_16x16x4_f32, k order permuted), 1 = bf16 bit patterns
+ * (v_mfma_f32_16x16x32_bf16, f32 accumulation). n_items < 2^31. */
+int hrec_f32_to_bf16(const float* in, int64_t n, uint16_t* out, void* stream);
+/* out[b*ld_out + j] = <U[b], V[j]> for b < n_users, j < n_items. */
+int hrec_dot_scores(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
+                    int dtype, float* out, int64_t ld_out, void* stream);
+size_t hrec_dot_topk_workspace_bytes(int n_users, int64_t n_items, int top_k);
+/* Stable top-k (larger first, ties -> smaller item index) of every user's
+ * scores over items [0, n_items), without writing the score matrix: the
+ * k-th best of a strided item sample (or thr_in[b] when thr_in != NULL) is a
+ * lower bound of the k-th best; a fused score + filter pass appends the
+ * survivors to a per-user list, ranked by an exact stable top-k. out_idx
+ * gets idx_offset added (item shards). *overflow != 0 when a user had more
+ * survivors than the list holds — then rerun with thr_in = out_val[:, k-1]
+ * (the k-th best survivor is a higher valid bound). n_users < 65536. */
+int hrec_dot_topk(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
+                  int dtype, int top_k, const float* thr_in, int64_t idx_offset, int64_t* out_idx,
+                  float* out_val, int* overflow, void* workspace, size_t workspace_bytes,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,152 @@
+"""GPU parity of the matrix-core dot-product scoring + fused top-k
+(csrc/dot_topk.hip, hrec_dot_scores / hrec_dot_topk) — the two-tower
+candidate scoring of src/two_tower_model.py:80,136-146 ranked like
+src/hybrid_system.py:108 (stable sort, ties keep candidate order).
+
+Tolerances (written here, per north_star "float scores within 1e-4 rtol"):
+* f32 operands: every score is an exact f32 fma chain (the MFMA's k order),
+  so |score - f64 dot| <= 1e-6 * sum_k |u_k v_k| (the guide's measured
+  0.75-1.5e-7 per unit of sum|ab| at K <= 1024, with margin);
+* bf16 operands: products are exact in f32, accumulation f32 -> the same
+  bound against the f64 dot of the bf16-ROUNDED vectors;
+* top-k: BIT-EXACT (indices and values) against a stable sort of the same
+  kernel's full score matrix (the filter pass computes identical values), and
+  against the f64 oracle ranking wherever the k-th and (k+1)-th oracle scores
+  are separated by more than the score tolerance (SURVEY App. A.3 rule).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _h():
+    from src import _hrec
+
+    return _hrec
+
+
+def _vecs(n, d, seed, scale=1.0):
+    g = np.random.default_rng(seed)
+    return (g.standard_normal((n, d)) * scale).astype(np.float32)
+
+
+def _bf16_round(x):
+    """f32 -> nearest-even bf16 -> f32 (numpy, the oracle of the device cast)."""
+    b = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    r = ((b + 0x7FFF + ((b >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def _stable_topk(scores, k):
+    """Python's sorted(..., reverse=True)[:k] order on each row: larger first,
+    ties -> smaller index."""
+    idx = np.argsort(-scores.astype(np.float64), axis=1, kind="stable")[:, :k]
+    return idx, np.take_along_axis(scores, idx, 1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,N,d", [(1, 1, 8), (5, 300, 50), (130, 1000, 64), (257, 777, 128), (64, 513, 256),
+                                   (3, 40, 32)])
+def test_dot_scores_vs_f64(device, dtype, B, N, d):
+    h = _h()
+    U = _vecs(B, d, 1)
+    V = _vecs(N, d, 2)
+    Ud = h.dot_operand(torch.from_numpy(U).to(device), dtype)
+    Vd = h.dot_operand(torch.from_numpy(V).to(device), dtype)
+    got = h.dot_scores(Ud, Vd).cpu().numpy()
+    if dtype == torch.bfloat16:
+        U, V = _bf16_round(U), _bf16_round(V)
+        np.testing.assert_array_equal(Ud.float().cpu().numpy()[:, :d], U)  # device RNE cast is bit-exact
+    ref = U.astype(np.float64) @ V.astype(np.float64).T
+    bound = 1e-6 * (np.abs(U).astype(np.float64) @ np.abs(V).astype(np.float64).T) + 1e-30
+    assert np.all(np.abs(got - ref) <= bound), np.max(np.abs(got - ref) / bound)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,N,d,k", [(7, 5000, 64, 5), (130, 40000, 128, 5), (3, 100003, 64, 10),
+                                     (1, 20000, 256, 1), (200, 17000, 32, 64), (2, 3, 64, 5)])
+def test_dot_topk_bit_exact_vs_full_scores(device, dtype, B, N, d, k):
+    """Sample-threshold + fused filter (N > 16384) and the small exact path
+    return exactly the stable top-k of the full score matrix."""
+    h = _h()
+    Ud = h.dot_operand(torch.from_numpy(_vecs(B, d, 3)).to(device), dtype)
+    Vd = h.dot_operand(torch.from_numpy(_vecs(N, d, 4)).to(device), dtype)
+    full = h.dot_scores(Ud, Vd).cpu().numpy()
+    ei, ev = _stable_topk(full, min(k, N))
+    gi, gv = h.dot_topk(Ud, Vd, k)
+    np.testing.assert_array_equal(gi.cpu().numpy(), ei)
+    np.testing.assert_array_equal(gv.cpu().numpy(), ev)
+
+
+def test_dot_topk_ties_keep_candidate_order(device):
+    """Duplicated item vectors score identically: the reference's stable sort
+    keeps candidate (index) order among them."""
+    h = _h()
+    base = _vecs(50, 64, 5)
+    V = np.concatenate([base] * 600)  # 30000 items, every score repeated 600 times
+    Ud = h.dot_operand(torch.from_numpy(_vecs(9, 64, 6)).to(device))
+    Vd = h.dot_operand(torch.from_numpy(V).to(device))
+    gi, gv = h.dot_topk(Ud, Vd, 5)
+    full = h.dot_scores(Ud, Vd).cpu().numpy()
+    ei, ev = _stable_topk(full, 5)
+    np.testing.assert_array_equal(gi.cpu().numpy(), ei)
+    np.testing.assert_array_equal(gv.cpu().numpy(), ev)
+    best = np.argmax(full[:, :50], axis=1)
+    np.testing.assert_array_equal(gi.cpu().numpy()[:, :5], best[:, None] + 50 * np.arange(5)[None, :])
+
+
+def test_dot_topk_overflow_falls_back_exactly(device):
+    """Every item scores the same -> every item survives every threshold: the
+    overflow flag triggers the refinement round and then the exact chunked
+    path, which returns the first k items (stable order)."""
+    h = _h()
+    V = np.tile(_vecs(1, 32, 7), (70000, 1))
+    Ud = h.dot_operand(torch.from_numpy(_vecs(4, 32, 8)).to(device))
+    Vd = h.dot_operand(torch.from_numpy(V).to(device))
+    gi, gv = h.dot_topk(Ud, Vd, 6)
+    np.testing.assert_array_equal(gi.cpu().numpy(), np.tile(np.arange(6), (4, 1)))
+    full = h.dot_scores(Ud, Vd[:1]).cpu().numpy()
+    np.testing.assert_array_equal(gv.cpu().numpy(), np.repeat(full, 6, axis=1))
+
+
+def test_dot_topk_offset_and_shards_merge(device):
+    """Item shards with idx_offset + a keyed merge == the unsharded top-k
+    (the per-rank step of the sharded c4 scoring)."""
+    h = _h()
+    U = _vecs(33, 128, 9)
+    V = _vecs(50000, 128, 10)
+    Ud = h.dot_operand(torch.from_numpy(U).to(device))
+    Vd = h.dot_operand(torch.from_numpy(V).to(device))
+    ei, ev = h.dot_topk(Ud, Vd, 5)
+    parts_i, parts_v = [], []
+    for lo, hi in ((0, 17000), (17000, 17001), (17001, 50000)):
+        i, v = h.dot_topk(Ud, Vd[lo:hi].contiguous(), 5, idx_offset=lo)
+        parts_i.append(i)
+        parts_v.append(v.double())
+    mi, mv = h.topk_keyed(torch.cat(parts_v, 1).contiguous(), torch.cat(parts_i, 1).contiguous(), 5)
+    np.testing.assert_array_equal(mi.cpu().numpy(), ei.cpu().numpy())
+    np.testing.assert_array_equal(mv.float().cpu().numpy(), ev.cpu().numpy())
+
+
+def test_dot_topk_matches_f64_ranking_outside_ties(device):
+    """Against the f64 oracle ranking: indices equal wherever the oracle's
+    k-th and (k+1)-th scores differ by more than the score tolerance."""
+    h = _h()
+    B, N, d, k = 64, 60000, 128, 5
+    U, V = _vecs(B, d, 11), _vecs(N, d, 12)
+    gi, gv = h.dot_topk(h.dot_operand(torch.from_numpy(U).to(device)),
+                        h.dot_operand(torch.from_numpy(V).to(device)), k)
+    ref = U.astype(np.float64) @ V.astype(np.float64).T
+    order = np.argsort(-ref, axis=1, kind="stable")
+    tol = 1e-6 * (np.abs(U).astype(np.float64) @ np.abs(V).astype(np.float64).T).max()
+    gi = gi.cpu().numpy()
+    checked = 0
+    for b in range(B):
+        r = ref[b, order[b]]
+        if r[k - 1] - r[k] > 2 * tol and np.all(r[:k - 1] - r[1:k] > 2 * tol):
+            np.testing.assert_array_equal(gi[b], order[b, :k])
+            checked += 1
+        np.testing.assert_allclose(gv.cpu().numpy()[b], r[:k], rtol=1e-4, atol=tol)
+    assert checked >= B // 2
