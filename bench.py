@@ -14,7 +14,10 @@ Also measured in the same run (not the headline value):
   * roofline of the dominant kernel (als_half_sweep_f64_kernel), timed with
     HIP events on the stream it is launched on;
   * cpu_baseline: the C oracle (Spark ALS restated, OpenMP) on rank 0 over a
-    bounded row sample of the same matrix, extrapolated to one epoch.
+    bounded row sample of the same matrix, extrapolated to one epoch;
+  * tt_scoring_c4 (BASELINE configs[3]): two-tower d = 128, 50M candidate
+    items split across the ranks, a batch of users ranked top-5 by the fused
+    matrix-core dot + top-k (f32 = Keras numerics, and bf16), C3 merge.
 """
 import argparse
 import json
@@ -31,12 +34,14 @@ sys.path.insert(0, ROOT)
 
 from src import _hrec, synthetic  # noqa: E402
 from src.als_engine import DeviceALS, shard_chunks, shard_range  # noqa: E402
-from src.recommend import ShardedRecommender  # noqa: E402
+from src.recommend import ShardedRecommender, ShardedScorer  # noqa: E402
 from src.tt_engine import DeviceTwoTower  # noqa: E402
 
 METRIC = "ALS epochs/sec + scored user-item pairs/sec at rank=64, 1/2/4/8 MI355X"
 F64_MFMA_PEAK_TFLOPS = 78.6  # AMD MI355X spec (FP64 matrix); not in MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA = f32 VALU peak (64 flop/clk/SIMD)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 
 CONFIGS = {
     "c2": dict(users=1_000_000, items=100_000, density=0.005, rank=64),
@@ -96,6 +101,9 @@ def main():
     ap.add_argument("--score-users", type=int, default=1024)
     ap.add_argument("--hybrid-users", type=int, default=256,
                     help="users per batch of the end-to-end hybrid top-5 measurement (0 = skip)")
+    ap.add_argument("--c4-items", type=int, default=50_000_000,
+                    help="two-tower scoring (c4): candidate items in total over all ranks (0 = skip)")
+    ap.add_argument("--c4-users", type=int, default=1024)
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -273,6 +281,52 @@ def main():
         del uid, iid, out
         torch.cuda.empty_cache()
 
+    # Two-tower scoring at BASELINE c4: d = 128 item vectors (N(0, 1/d),
+    # generated on the device), items sharded over the ranks; one batch of
+    # users ranked top-5 against every item (fused dot + filter + top-k;
+    # the [B, N] score matrix is never written), C3 merge across ranks.
+    tt_c4 = None
+    if args.c4_items > 0:
+        tt_c4 = {}
+        d4 = 128
+        c0, c_per = shard_range(args.c4_items, world, rank)
+        c_loc = max(0, min(c_per, args.c4_items - c0))
+        g4 = torch.Generator(device="cuda").manual_seed(1000 + rank)
+        V4 = torch.randn((c_loc, d4), device="cuda", generator=g4).mul_(d4 ** -0.5)
+        U4 = torch.randn((args.c4_users, d4), device="cuda", generator=torch.Generator(device="cuda").manual_seed(7))
+        for name, dt, peak in (("f32", torch.float32, F32_MFMA_PEAK_TFLOPS),
+                               ("bf16", torch.bfloat16, BF16_MFMA_PEAK_TFLOPS)):
+            Vd = _hrec.dot_operand(V4, dt)
+            Ud = _hrec.dot_operand(U4, dt)
+            sc = ShardedScorer(Vd, c0, world=world, rank=rank, group=group)
+            sc.topk(Ud, 5)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            reps = 3
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            q0 = time.perf_counter()
+            e0.record(stream)
+            for _ in range(reps):
+                sc.topk(Ud, 5)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            qt = torch.tensor([(time.perf_counter() - q0) / reps], dtype=torch.float64, device="cuda")
+            if world > 1:
+                dist.all_reduce(qt, op=dist.ReduceOp.MAX)
+            qs = float(qt.item())
+            local_s = e0.elapsed_time(e1) / reps / 1e3  # this rank's launches, HIP events on the launch stream
+            tf = 2.0 * args.c4_users * c_loc * d4 / local_s / 1e12
+            tt_c4[name] = {"pairs_per_s": args.c4_users * args.c4_items / qs, "ms_per_batch": qs * 1e3,
+                           "roofline": {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
+                                        "frac": tf / peak}}
+            del Vd, Ud
+        tt_c4.update({"users": args.c4_users, "items": args.c4_items, "d": d4, "top_k": 5,
+                      "items_sharded_over": world,
+                      "kernel": "hrec_dot_topk (sample bound + fused matrix-core dot + survivor filter + exact top-k)"})
+        del V4, U4
+        torch.cuda.empty_cache()
+
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.accum_mode == 0:
         with open(args.traffic_json) as f:
@@ -326,6 +380,7 @@ def main():
             "scoring": scoring,
             "hybrid_top5": hybrid,
             "ingest": ingest,
+            "tt_scoring_c4": tt_c4,
         }
         print(json.dumps(line))
     if world > 1:

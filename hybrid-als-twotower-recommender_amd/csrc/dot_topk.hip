@@ -26,6 +26,8 @@
 #include <float.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace hrec {
@@ -84,7 +86,12 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
     int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n, int64_t idx_offset) {
   using S = DotShape<BF16, DK>;
   constexpr int NU = TL::NU, NI = TL::NI;
-  __shared__ __attribute__((aligned(16))) char us[TL::kUsers * S::kRow];
+  // User rows in LDS. Rows of >= 16 chunks of 16 B are XOR-swizzled (chunk q
+  // of row r at q ^ (r & 15)): the 16 lanes of every ds_read_b128 lane group
+  // then hit 16 distinct bank quads; shorter rows are padded by 16 B.
+  constexpr bool kSwz = S::kChunks >= 16;
+  constexpr int kRowB = kSwz ? S::kChunks * 16 : S::kRow;
+  __shared__ __attribute__((aligned(16))) char us[TL::kUsers * kRowB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int wu = w % TL::WU, wi = w / TL::WU;
@@ -101,31 +108,41 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
     const int r = o / S::kChunks, q = o % S::kChunks;
     int4 v = {0, 0, 0, 0};
     if (b0 + r < B) v = *reinterpret_cast<const int4*>(U + (int64_t)(b0 + r) * (DK * S::kElem) + 16 * q);
-    *reinterpret_cast<int4*>(us + r * S::kRow + 16 * q) = v;
+    *reinterpret_cast<int4*>(us + r * kRowB + 16 * (kSwz ? q ^ (r & 15) : q)) = v;
   }
-  const int ub = b0 + 16 * NU * wu + 4 * g;  // user of (tile u, reg r): ub + 16 u + r
-  float th[FILTER ? NU : 1][4];  // NaN = absent user (never passes), -inf = admit every score
+  // MFMA roles: A = items (output rows), B = users (output columns), so the
+  // C/D layout puts ONE user on each lane per user tile: user ub + 16 u,
+  // items j0 + 16 t + 4 g + r.
+  const int ub = b0 + 16 * NU * wu + c;
+  float th[FILTER ? NU : 1];  // NaN = absent user (never passes), -inf = admit every score
   if constexpr (FILTER) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = ub + 16 * u + r;
-        float t = __builtin_nanf("");
-        if (b < B) {
-          t = thr[(int64_t)b * thr_stride];
-          t = t == t ? t : -INFINITY;
-        }
-        th[u][r] = t;
+    for (int u = 0; u < NU; ++u) {
+      const int b = ub + 16 * u;
+      float t = __builtin_nanf("");
+      if (b < B) {
+        t = thr[(int64_t)b * thr_stride];
+        t = t == t ? t : -INFINITY;
       }
+      th[u] = t;
+    }
   }
   __syncthreads();
-  const char* ubase = us + (16 * NU * wu + c) * S::kRow + 16 * g;
+  const char* ubase = us + (16 * NU * wu + c) * kRowB;
+  const int xq = c ^ g;  // swizzled chunk of step ks: (4 ks + g) ^ c = 4 ks ^ (c ^ g)
+  auto user_frag = [&](int u, int ks) {
+    DotFrag a;
+    const int off = kSwz ? 16 * ((4 * ks) ^ xq) : 64 * ks + 16 * g;
+    a.i = *reinterpret_cast<const int4*>(ubase + 16 * u * kRowB + off);
+    return a;
+  };
   // Item fragments: structured buffer loads (address = V + vindex * row
   // bytes + 16 g; the hardware range check returns zeros for vindex >=
   // n_rows, so tails need no clamping), flowing through a ring of P steps
   // issued P steps ahead across tile boundaries (the next tile's first steps
-  // load during the current tile's last MFMAs).
+  // load during the current tile's last MFMAs). User fragments are read one
+  // step ahead from LDS (the last step of a tile reads step 0 again: users
+  // do not change between tiles).
   constexpr int PB = FILTER ? 4 : 2;
   constexpr int P = BF16 ? (S::kSteps < PB ? S::kSteps : PB) : (S::kSteps < 2 ? S::kSteps : 2);
   static_assert(S::kSteps % P == 0, "ring depth must divide the k steps");
@@ -151,6 +168,9 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
   for (int q = 0; q < P; ++q)
 #pragma unroll
     for (int t = 0; t < NI; ++t) ring[q][t].f = dot_sbuf_load(rsrc, vcur[t], voff + 64 * q, 0, 0);
+  DotFrag ua[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) ua[u] = user_frag(u, 0);
   for (int64_t it = ig; it < n_it; it += n_ig) {
     const int64_t j0 = it * TL::kItems + 16 * NI * wi;
     rows_of(it + n_ig, vnext);
@@ -164,7 +184,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
 #pragma unroll
       for (int q = 0; q < P; ++q) {
         const int ks = k0 + q;
-        DotFrag b[NI];
+        DotFrag b[NI], a[NU];
         const bool same = ks + P < S::kSteps;
         const int off = voff + 64 * (same ? ks + P : ks + P - S::kSteps);
 #pragma unroll
@@ -172,30 +192,33 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
           b[t] = ring[q][t];
           ring[q][t].f = dot_sbuf_load(rsrc, same ? vcur[t] : vnext[t], off, 0, 0);
         }
+        const int kn = ks + 1 < S::kSteps ? ks + 1 : 0;
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-          DotFrag a;
-          a.i = *reinterpret_cast<const int4*>(ubase + 16 * u * S::kRow + 64 * ks);
-#pragma unroll
-          for (int t = 0; t < NI; ++t) dot_mma<BF16>(a, b[t], acc[u][t]);
+          a[u] = ua[u];
+          ua[u] = user_frag(u, kn);
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep each step's LDS reads in its step (VGPR budget)
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int t = 0; t < NI; ++t) dot_mma<BF16>(b[t], a[u], acc[u][t]);
+        __builtin_amdgcn_sched_barrier(0);  // keep each step's prefetches in its step (VGPR budget)
       }
     }
 #pragma unroll
     for (int t = 0; t < NI; ++t) vcur[t] = vnext[t];
-    // C/D layout of a 16 x 16 f32 tile: column = lane & 15 (item), row = 4g + r (user)
     if constexpr (!FILTER) {
 #pragma unroll
-      for (int t = 0; t < NI; ++t) {
-        const int64_t j = j0 + 16 * t + c;
-        if (j >= n_items) continue;
+      for (int u = 0; u < NU; ++u) {
+        const int b = ub + 16 * u;
+        if (b >= B) continue;
+        float* o = out + (int64_t)b * ldo;
 #pragma unroll
-        for (int u = 0; u < NU; ++u)
+        for (int t = 0; t < NI; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int b = ub + 16 * u + r;
-            if (b < B) out[(int64_t)b * ldo + j] = acc[u][t][r];
+            const int64_t j = j0 + 16 * t + 4 * g + r;
+            if (j < n_items) o[j] = acc[u][t][r];
           }
       }
     } else {
@@ -208,18 +231,18 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
 #pragma unroll
         for (int t = 0; t < NI; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) any |= __ballot(acc[u][t][r] >= th[u][r]);
+          for (int r = 0; r < 4; ++r) any |= __ballot(acc[u][t][r] >= th[u]);
       if (any) {
 #pragma unroll
-        for (int t = 0; t < NI; ++t) {
-          const int64_t j = j0 + 16 * t + c;
+        for (int u = 0; u < NU; ++u) {
+          const int b = ub + 16 * u;
 #pragma unroll
-          for (int u = 0; u < NU; ++u)
+          for (int t = 0; t < NI; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+              const int64_t j = j0 + 16 * t + 4 * g + r;
               const float sc = acc[u][t][r];
-              if (j < n_items && sc >= th[u][r]) {
-                const int b = ub + 16 * u + r;
+              if (j < n_items && sc >= th[u]) {
                 const int pos = atomicAdd(&cand_n[b], 1);
                 if (pos < cap) {
                   cand_v[(int64_t)b * cap + pos] = sc;
@@ -254,6 +277,189 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ in, int64_t n, uint
   }
 }
 
+// Resident-users variant: the block keeps UB users (up to 128 KB of LDS) and
+// every wave keeps its 32 items' fragments for the whole d in registers while
+// it sweeps all UB users in chunks of 128 — an item fragment is fetched from
+// L2 once per UB users instead of once per 128 (the L2 re-reads and misses
+// of the 128-user tiling were the stall). During the last chunk each item
+// fragment is refilled with the next tile's as soon as its step has used it
+// the last time, so the loads have a whole chunk plus a step to land.
+constexpr int kResUserBytes = 128 * 1024;
+constexpr int kResNU = 4;  // user tiles per chunk (64 users): leaves VGPRs for the prefetches
+
+template <bool BF16, int DK, bool FILTER>
+__global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
+    const char* __restrict__ U, int B, int UB, const char* __restrict__ V, int64_t n_rows, int64_t n_items,
+    int64_t item_step, int n_ut, float* __restrict__ out, int64_t ldo, const float* __restrict__ thr, int thr_stride,
+    int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n, int64_t idx_offset) {
+  using S = DotShape<BF16, DK>;
+  constexpr int NU = kResNU, NI = 2, KS = S::kSteps;
+  constexpr int CU = 16 * NU;  // users per chunk
+  constexpr int kItems = 8 * 16 * NI;  // per block tile
+  constexpr bool kSwz = S::kChunks >= 16;
+  constexpr int kRowB = kSwz ? S::kChunks * 16 : S::kRow;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  char* us = dsm;                                      // UB user rows
+  float* ths = reinterpret_cast<float*>(dsm + (size_t)UB * kRowB);  // UB thresholds
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int per_xcd = gridDim.x >> 3;
+  const int lin = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int ut = lin % n_ut;
+  const int64_t ig = lin / n_ut, n_ig = gridDim.x / n_ut;
+  const int64_t n_it = (n_items + kItems - 1) / kItems;
+  if (ig >= n_it) return;  // block-uniform
+  const int b0 = ut * UB;
+  for (int o = threadIdx.x; o < UB * S::kChunks; o += kDotThreads) {
+    const int r = o / S::kChunks, q = o % S::kChunks;
+    int4 v = {0, 0, 0, 0};
+    if (b0 + r < B) v = *reinterpret_cast<const int4*>(U + (int64_t)(b0 + r) * (DK * S::kElem) + 16 * q);
+    *reinterpret_cast<int4*>(us + r * kRowB + 16 * (kSwz ? q ^ (r & 15) : q)) = v;
+  }
+  if (FILTER) {
+    for (int o = threadIdx.x; o < UB; o += kDotThreads) {
+      float t = __builtin_nanf("");  // absent user: never passes
+      if (b0 + o < B) {
+        t = thr[(int64_t)(b0 + o) * thr_stride];
+        t = t == t ? t : -INFINITY;  // NaN bound admits every score
+      }
+      ths[o] = t;
+    }
+  }
+  __syncthreads();
+  const int xq = c ^ g;
+  const uint64_t vb = (uint64_t)V;
+  dot_rsrc rsrc;
+  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
+  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * S::kElem) << 16));
+  rsrc.z = __builtin_amdgcn_readfirstlane((int)n_rows);
+  rsrc.w = 0x00020000;
+  const int voff = 16 * g;
+  auto rows_of = [&](int64_t tile, int (&vi)[NI]) {
+    const int64_t jb = tile * kItems + 16 * NI * w;
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int64_t j = jb + 16 * t + c;
+      vi[t] = (tile < n_it && j < n_items) ? (int)(j * item_step) : 0x7fffffff;
+    }
+  };
+  int vnext[NI];
+  rows_of(ig, vnext);
+  DotFrag it_f[KS][NI];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int t = 0; t < NI; ++t) it_f[ks][t].f = dot_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+  const int n_ch = (UB + 16 * NU - 1) / (16 * NU);
+  DotFrag ua[NU];  // user fragments of the next step (chunk 0, step 0 first)
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int off = kSwz ? 16 * xq : 16 * g;
+    ua[u].i = *reinterpret_cast<const int4*>(us + (16 * u + c) * kRowB + off);
+  }
+  for (int64_t it = ig; it < n_it; it += n_ig) {
+    const int64_t j0 = it * kItems + 16 * NI * w;
+    rows_of(it + n_ig, vnext);
+    auto user_frag = [&](int ch, int u, int ks) {
+      DotFrag a;
+      const int off = kSwz ? 16 * ((4 * ks) ^ xq) : 64 * ks + 16 * g;
+      a.i = *reinterpret_cast<const int4*>(us + (CU * ch + 16 * u + c) * kRowB + off);
+      return a;
+    };
+    // The last chunk is peeled (compile-time LAST): its item refills are then
+    // unconditional, so the waitcnt pass can count them instead of draining.
+    auto chunk = [&](int ch, auto last_t) {
+      constexpr bool last = decltype(last_t)::value;
+      // the next chunk's first user fragments load during this chunk's last
+      // step (after the last chunk: chunk 0 again, for the next tile)
+      const int ch_next = ch + 1 < n_ch ? ch + 1 : 0;
+      dot_f4 acc[NU][NI];
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int t = 0; t < NI; ++t) acc[u][t] = dot_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        DotFrag a[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          a[u] = ua[u];
+          ua[u] = ks + 1 < KS ? user_frag(ch, u, ks + 1) : user_frag(ch_next, u, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int t = 0; t < NI; ++t) dot_mma<BF16>(it_f[ks][t], a[u], acc[u][t]);
+        if constexpr (last) {  // step ks of this tile is done: refill it with the next tile's
+#pragma unroll
+          for (int t = 0; t < NI; ++t) it_f[ks][t].f = dot_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+        }
+        // Order the step: each next-step user read sits between MFMA pairs, so
+        // the LDS reads overlap the whole step instead of trailing it.
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, NI, 0);  // MFMA
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // C/D: lane holds user (CU ch + 16 u + c), items j0 + 16 t + 4 g + r
+      if constexpr (!FILTER) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int b = b0 + CU * ch + 16 * u + c;
+          if (b >= B || CU * ch + 16 * u + c >= UB) continue;
+          float* o = out + (int64_t)b * ldo;
+#pragma unroll
+          for (int t = 0; t < NI; ++t) {
+            const int64_t j = j0 + 16 * t + 4 * g;
+            if (j + 3 < n_items && (ldo & 3) == 0) {
+              *reinterpret_cast<float4*>(o + j) = make_float4(acc[u][t][0], acc[u][t][1], acc[u][t][2], acc[u][t][3]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (j + r < n_items) o[j + r] = acc[u][t][r];
+            }
+          }
+        }
+      } else {
+        float th[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) th[u] = CU * ch + 16 * u + c < UB ? ths[CU * ch + 16 * u + c] : __builtin_nanf("");
+        uint64_t any = 0;
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int t = 0; t < NI; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) any |= __ballot(acc[u][t][r] >= th[u]);
+        if (any) {
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            const int b = b0 + CU * ch + 16 * u + c;
+#pragma unroll
+            for (int t = 0; t < NI; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int64_t j = j0 + 16 * t + 4 * g + r;
+                const float sc = acc[u][t][r];
+                if (j < n_items && sc >= th[u]) {
+                  const int pos = atomicAdd(&cand_n[b], 1);
+                  if (pos < cap) {
+                    cand_v[(int64_t)b * cap + pos] = sc;
+                    cand_i[(int64_t)b * cap + pos] = j + idx_offset;
+                  }
+                }
+              }
+          }
+        }
+      }
+    };
+    for (int ch = 0; ch + 1 < n_ch; ++ch) chunk(ch, std::false_type{});
+    chunk(n_ch - 1, std::true_type{});
+  }
+}
+
 // Tilings: FILTER passes keep each item fragment for 128 users (item bytes
 // through the vector cache halve vs 64 x 64 wave tiles; the user fragments
 // come from LDS, which has twice the bandwidth); HREC_DOT_TILING (0/1)
@@ -276,7 +482,7 @@ static unsigned dot_grid(int n_ut, int64_t n_items, int tile_items) {
 static int dot_tiling_choice() {
   static int v = [] {
     const char* e = getenv("HREC_DOT_TILING");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -312,14 +518,59 @@ static int dot_launch_t(const void* U, int B, const void* V, int64_t n_rows, int
 }
 
 template <bool FILTER>
+static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
+                          int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
+                          int64_t* ci, int* cn, int64_t off, hipStream_t s) {
+  const int row_b = dk * (bf16 ? 2 : 4);
+  const int row_lds = row_b >= 256 ? row_b : row_b + 16;
+  int ub_max = kResUserBytes / row_lds;
+  ub_max = ub_max / (16 * kResNU) * (16 * kResNU);
+  const int n_ut = (B + ub_max - 1) / ub_max;
+  int UB = (B + n_ut - 1) / n_ut;
+  UB = (UB + 16 * kResNU - 1) / (16 * kResNU) * (16 * kResNU);
+  const size_t lds = (size_t)UB * row_lds + (size_t)UB * 4;
+  const dim3 grid(dot_grid(n_ut, n_items, 256)), block(kDotThreads);
+  const char* u = (const char*)U;
+  const char* v = (const char*)V;
+#define HREC_DOTR(BF, DK)                                                                                      \
+  do {                                                                                                         \
+    auto kfn = dot_res_kernel<BF, DK, FILTER>;                                                                 \
+    if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+      return check_launch("dot_res_kernel: LDS attribute");                                                   \
+    hipLaunchKernelGGL(kfn, grid, block, lds, s, u, B, UB, v, n_rows, n_items, step, n_ut, out, ldo, thr,         \
+                       thr_stride, cap, cv, ci, cn, off);                                                      \
+  } while (0)
+  if (bf16) {
+    switch (dk) {
+      case 32: HREC_DOTR(true, 32); break;
+      case 64: HREC_DOTR(true, 64); break;
+      case 128: HREC_DOTR(true, 128); break;
+      default: HREC_DOTR(true, 256); break;
+    }
+  } else {
+    switch (dk) {
+      case 32: HREC_DOTR(false, 32); break;
+      case 64: HREC_DOTR(false, 64); break;
+      default: HREC_DOTR(false, 128); break;
+    }
+  }
+#undef HREC_DOTR
+  return check_launch("dot_res_kernel");
+}
+
+template <bool FILTER>
 static int dot_launch(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
                       int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
                       int64_t* ci, int* cn, int64_t off, hipStream_t s) {
+  const int choice = dot_tiling_choice();
+  if (choice == 2 && (bf16 || dk <= 128))
+    return dot_launch_res<FILTER>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap, cv, ci,
+                                  cn, off, s);
   if constexpr (!FILTER) {
     return dot_launch_t<false, DotTileA>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
                                          cv, ci, cn, off, s);
   }
-  switch (dot_tiling_choice()) {
+  switch (choice) {
     case 0:
       return dot_launch_t<FILTER, DotTileA>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
                                             cv, ci, cn, off, s);

@@ -17,6 +17,12 @@ items split into contiguous shards, one per rank (SURVEY §8e, rows
      merge (hrec_topk_f64_keyed): ties break on the global item id, so every
      world size returns the same items and scores as one GPU.
 
+ShardedScorer does the same for the two-tower scoring alone (BASELINE c4:
+d = 128 embeddings, 50M candidates over 8 GPUs): each rank ranks its item
+shard with the fused matrix-core dot + top-k (hrec_dot_topk, global ids via
+the shard offset), then C3 + keyed merge as above — the score matrix never
+exists on any rank.
+
 The collectives and kernels are injectable (`ops`) so the orchestration can be
 exercised with gloo on CPU (tests/test_distributed.py).
 """
@@ -36,6 +42,10 @@ class DeviceOps:
     @staticmethod
     def tt_scores(user_vecs, item_vecs_local):
         return _hrec.tt_score(user_vecs, item_vecs_local)
+
+    @staticmethod
+    def dot_topk(user_vecs, item_vecs_local, top_k, offset):
+        return _hrec.dot_topk(user_vecs, item_vecs_local, top_k, idx_offset=offset)
 
     rows_minmax = staticmethod(_hrec.rows_minmax)
     fuse_rows_topk = staticmethod(_hrec.fuse_rows_topk)
@@ -79,16 +89,51 @@ class ShardedRecommender:
             val = torch.empty((B, 0), dtype=torch.float64, device=dev)
         if self.world == 1:
             return idx, val
-        kk = int(top_k)
-        if idx.shape[1] < kk:  # every rank contributes k slots; -1 marks an empty one
-            pad = kk - idx.shape[1]
-            idx = torch.cat([idx, torch.full((B, pad), -1, dtype=torch.int64, device=dev)], 1)
-            val = torch.cat([val, torch.full((B, pad), float("-inf"), dtype=torch.float64, device=dev)], 1)
-        # rank-major concatenation [W*B, k] (the layout every backend accepts)
-        g_idx = torch.empty((self.world * B, kk), dtype=idx.dtype, device=idx.device)
-        g_val = torch.empty((self.world * B, kk), dtype=val.dtype, device=val.device)
-        dist.all_gather_into_tensor(g_idx, idx.contiguous(), group=self.group)
-        dist.all_gather_into_tensor(g_val, val.contiguous(), group=self.group)
-        cand_i = g_idx.view(self.world, B, kk).permute(1, 0, 2).reshape(B, self.world * kk).contiguous()
-        cand_v = g_val.view(self.world, B, kk).permute(1, 0, 2).reshape(B, self.world * kk).contiguous()
-        return o.topk_keyed(cand_v, cand_i, top_k)
+        return merge_candidates(idx, val, top_k, self.world, self.group, o)
+
+
+def merge_candidates(idx, val, top_k, world, group, ops):
+    """C3: all_gather every rank's [B, <=k] candidates (global ids, -1 = empty
+    slot) and merge them by a keyed stable top-k (ties -> smaller id)."""
+    B = idx.shape[0]
+    dev = idx.device
+    kk = int(top_k)
+    if idx.shape[1] < kk:  # every rank contributes k slots; -1 marks an empty one
+        pad = kk - idx.shape[1]
+        idx = torch.cat([idx, torch.full((B, pad), -1, dtype=torch.int64, device=dev)], 1)
+        val = torch.cat([val, torch.full((B, pad), float("-inf"), dtype=val.dtype, device=dev)], 1)
+    # rank-major concatenation [W*B, k] (the layout every backend accepts)
+    g_idx = torch.empty((world * B, kk), dtype=idx.dtype, device=dev)
+    g_val = torch.empty((world * B, kk), dtype=val.dtype, device=dev)
+    dist.all_gather_into_tensor(g_idx, idx.contiguous(), group=group)
+    dist.all_gather_into_tensor(g_val, val.contiguous(), group=group)
+    cand_i = g_idx.view(world, B, kk).permute(1, 0, 2).reshape(B, world * kk).contiguous()
+    cand_v = g_val.view(world, B, kk).permute(1, 0, 2).reshape(B, world * kk).contiguous()
+    return ops.topk_keyed(cand_v, cand_i, top_k)
+
+
+class ShardedScorer:
+    """Two-tower (or any dot-product) top-k over an item axis sharded across
+    ranks: rank r holds item rows [offset, offset + n_local) of the candidate
+    matrix as a dot operand (hrec dot_operand: f32 or bf16, width 32..256)."""
+
+    def __init__(self, item_vecs_local, item_offset, world=1, rank=0, group=None, ops=None):
+        self.iv = item_vecs_local
+        self.n_local = item_vecs_local.shape[0]
+        self.offset = int(item_offset)
+        self.world, self.rank, self.group = int(world), int(rank), group
+        self.ops = ops or DeviceOps
+
+    def topk(self, user_vecs, top_k):
+        """user_vecs: [B, width] dot operand. Returns (global item ids [B, k],
+        scores [B, k]) — f32 on one rank, f64 after the merge."""
+        B = user_vecs.shape[0]
+        dev = user_vecs.device
+        if self.n_local > 0:
+            idx, val = self.ops.dot_topk(user_vecs, self.iv, top_k, self.offset)
+        else:
+            idx = torch.empty((B, 0), dtype=torch.int64, device=dev)
+            val = torch.empty((B, 0), dtype=torch.float32, device=dev)
+        if self.world == 1:
+            return idx, val
+        return merge_candidates(idx, val.double(), top_k, self.world, self.group, self.ops)

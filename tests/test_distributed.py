@@ -219,3 +219,62 @@ def test_sharded_hybrid_topk_matches_single(world):
     for _, (gi, gv) in res:
         np.testing.assert_array_equal(gi, ref_i)
         np.testing.assert_array_equal(gv, ref_v)
+
+
+# ------------------------------------------- sharded two-tower top-k (c4, C3)
+class _CpuDotOps(_CpuOps):
+    @staticmethod
+    def dot_topk(user_vecs, item_vecs_local, top_k, offset):
+        s = (user_vecs.numpy().astype(np.float64) @ item_vecs_local.numpy().T.astype(np.float64)).astype(np.float32)
+        kk = min(top_k, s.shape[1])
+        order = np.argsort(-s.astype(np.float64), axis=1, kind="stable")[:, :kk]
+        return torch.from_numpy(order + offset), torch.from_numpy(np.take_along_axis(s, order, 1))
+
+
+def _scorer_data():
+    rng = np.random.default_rng(11)
+    uv = rng.integers(-3, 4, (6, 8)).astype(np.float32)
+    iv = rng.integers(-3, 4, (53, 8)).astype(np.float32)  # integer data: many exact ties
+    return uv, iv
+
+
+def _scorer_run(world, rank, uv, iv, group=None):
+    from src.als_engine import shard_range
+    from src.recommend import ShardedScorer
+
+    i0, per = shard_range(iv.shape[0], world, rank)
+    sc = ShardedScorer(torch.from_numpy(iv[i0: i0 + per]), i0, world=world, rank=rank, group=group, ops=_CpuDotOps)
+    i, v = sc.topk(torch.from_numpy(uv), 7)
+    return i.numpy(), v.numpy().astype(np.float64)
+
+
+def _scorer_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    uv, iv = _scorer_data()
+    q.put((rank, _scorer_run(world, rank, uv, iv, dist.group.WORLD)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 24])
+def test_sharded_dot_topk_matches_single(world):
+    """Item-sharded two-tower top-k (local top-k with global ids, all_gather,
+    keyed merge) == one rank, ties included (ties -> smaller item id); world 24
+    leaves some ranks without items."""
+    uv, iv = _scorer_data()
+    ref_i, ref_v = _scorer_run(1, 0, uv, iv)
+    s = uv.astype(np.float64) @ iv.T.astype(np.float64)
+    np.testing.assert_array_equal(ref_i, np.argsort(-s, axis=1, kind="stable")[:, :7])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scorer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, (gi, gv) in res:
+        np.testing.assert_array_equal(gi, ref_i)
+        np.testing.assert_array_equal(gv, ref_v)
