@@ -717,7 +717,7 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
                                    int64_t n_rows, const float* src_factors, int64_t n_src, int k,
                                    int kp, double reg_param, int accum_mode, float* dst_factors,
                                    void* stream) {
-  HREC_REQUIRE(kp == 16 || kp == 32 || kp == 64, "als_half_sweep: kp must be 16, 32 or 64 (got %d)", kp);
+  HREC_REQUIRE(hrec_factor_ld_ok(kp), "als_half_sweep: kp must be 16, 32, 64, 96, 128, 192 or 256 (got %d)", kp);
   HREC_REQUIRE(k >= 1 && k <= kp, "als_half_sweep: need 1 <= k <= kp (k=%d kp=%d)", k, kp);
   HREC_REQUIRE(n_rows >= 0 && n_src >= 0, "als_half_sweep: negative size");
   HREC_REQUIRE(n_rows < 0x7fffffffll, "als_half_sweep: too many rows for one launch");
@@ -728,6 +728,11 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
   HREC_REQUIRE(n_src > 0 && src_factors && indices && values,
                "als_half_sweep: null source factors / CSR arrays");
   HREC_REQUIRE(n_src < 0x7fffffffll, "als_half_sweep: too many source rows for one launch");
+  if (kp > 64) {
+    HREC_REQUIRE(accum_mode == 0, "als_half_sweep: kp > 64 supports accum_mode 0 (f64) only");
+    return hrec_als_half_sweep_wide(indptr, indices, values, n_rows, src_factors, n_src, k, kp, reg_param,
+                                    dst_factors, stream);
+  }
   hipStream_t s = as_stream(stream);
 #if HREC_ALS_SPLIT
   int dev = 0, cus = 256;

@@ -1,0 +1,431 @@
+// K1 for ranks 65..256: ALS half-sweep with ONE WORKGROUP (8 waves) PER
+// DESTINATION ROW — same arithmetic as the one-wave kernel in als.hip
+// (Spark 3.5.1 ALS.computeFactors / NormalEquation.add / CholeskySolver
+// [ext], reached from src/als_model.py:62), for factor widths kp in
+// {96, 128, 192, 256} (BASELINE config c5 runs rank 256).
+//
+// Per row r:  A = sum_j v_j v_j^T (f64),  b = sum_j r_j v_j (f64),
+//             A[d][d] += reg * n  (1.0 on padding columns),  A x = b,  x -> f32.
+//
+// Layout. The Gramian is NT x NT tiles of 16 x 16 (NT = kp / 16); the
+// NT (NT + 1) / 2 upper tile pairs are dealt round-robin to the 8 waves
+// (pair p -> wave p % 8, slot p / 8) and stay in registers for the whole row
+// (v_mfma_f64_16x16x4_f64 C/D layout: row (lane >> 4) + 4 reg, column
+// lane & 15). A kp = 256 Gramian is 263 KB — more than the LDS — so the
+// factorisation and both substitutions also run on the register tiles.
+//
+// Phase 1 (Gramian): the row's ratings stream through LDS in windows of WR
+// ratings: the block gathers the WR source rows (coalesced float4 loads,
+// issued one window ahead), converts them once to f64 and stores them
+// [WR][kp + 16] (the 16-double pad makes the two rows of a ds_read_b64 lane
+// group hit disjoint banks). Every wave then feeds its tile pairs: operand of
+// tile T for rating step s is v[4 s + (lane >> 4)][16 T + (lane & 15)].
+// Threads t < kp accumulate b_t in f64.
+//
+// Phase 2 (factor): blocked right-looking LDL^T (A = U^T D U, U unit upper),
+// block row J at a time: the owners write block row J to an LDS panel; each
+// of up to 5 waves factors the 16 x 16 diagonal block redundantly (lanes
+// 0..15) beside 48 panel columns of its own (lane per column, pivot row by a
+// wave-private broadcast, 1/pivot by v_rcp_f64 + one Newton step — no square
+// roots, no cross-wave barrier per pivot); U_J goes back to the panel and
+// every owner of a trailing tile (K, M) applies A_KM -= U_JK^T D_J U_JM on
+// the f64 matrix cores; owners of row J keep U_JK in their registers.
+// Two barriers per block row (double-buffered panel).
+//
+// Phase 3 (solve): U^T w = b block by block (the owner of (J, J) solves its
+// 16 x 16 triangle; owners of (J, K) subtract U_JK^T w_J from b_K), v = w / D,
+// then U x = v from the last block up (owners of (J, M) subtract U_JM x_M
+// from v_J). Spark's dppsv factors A = R^T R with R = D^(1/2) U: the same x.
+#include "common.h"
+
+#ifndef HREC_WIDE_WAVES
+#define HREC_WIDE_WAVES(NT) 8
+#endif
+#ifndef HREC_WIDE_CUT
+#define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
+#endif
+
+namespace hrec {
+
+typedef double wd4 __attribute__((ext_vector_type(4)));
+
+// Waves per row: 8 for kp <= 128; 16 for kp >= 192, so that each wave's
+// share of the register-resident Gramian tiles (<= 9 x 8 VGPRs) fits the
+// 128 VGPRs of a 1024-thread block.
+template <int NT>
+struct WideShape {
+  static constexpr int WAVES = HREC_WIDE_WAVES(NT);
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int KP = 16 * NT;
+  static constexpr int NPAIR = NT * (NT + 1) / 2;
+  static constexpr int SLOTS = (NPAIR + WAVES - 1) / WAVES;
+  static constexpr int LD = KP + 16;                     // f64 row stride of windows and panels
+  static constexpr int WR = KP >= 192 ? 16 : 32;         // ratings per window
+  static constexpr int WIN = WR * LD;                    // doubles per window buffer
+  static constexpr int PANEL = 16 * LD;                  // doubles per panel buffer
+  static constexpr int BUF = WIN > PANEL ? WIN : PANEL;  // windows and panels share two buffers
+  static constexpr int F4 = WR * KP / 4;                 // float4 loads per window
+  static constexpr int F4_PER_T = (F4 + THREADS - 1) / THREADS;
+};
+
+// Pair p (row-major over the upper tile triangle) -> (I, J).
+template <int NT>
+__device__ __forceinline__ void pair_ij(int p, int& I, int& J) {
+  int i = 0;
+#pragma unroll
+  for (int r = 0; r < NT; ++r) {
+    const int len = NT - r;
+    if (p >= len && i == r) {
+      p -= len;
+      i = r + 1;
+    }
+  }
+  I = i;
+  J = i + p;
+}
+
+__device__ __forceinline__ double wbcast(double v, int src) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, src);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NT>
+__global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, const float* __restrict__ values,
+    int64_t n_rows, const float* __restrict__ src, int64_t n_src, int k, double reg, float* __restrict__ dst) {
+  using S = WideShape<NT>;
+  constexpr int KP = S::KP, LD = S::LD, WR = S::WR, kWideWaves = S::WAVES, kWideThreads = S::THREADS;
+  __shared__ __attribute__((aligned(16))) double buf[2][S::BUF];
+  __shared__ double bsh[KP];      // b, then w (forward), then v / x
+  __shared__ double dsh[KP];      // pivots D
+  __shared__ double rdsh[KP];     // 1 / D
+  __shared__ double xsh[KP];      // x blocks (backward)
+  __shared__ float rsh[2][WR];    // ratings of the two windows
+  __shared__ double tri[kWideWaves][16 * 17];  // per-wave scratch: pivot row / diagonal tile
+  __shared__ double udg[16 * 17];              // U_JJ of the current block row
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sub = lane >> 4, col = lane & 15;
+  const int64_t row = blockIdx.x;
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  float* __restrict__ out = dst + row * KP;
+  if (end == beg) {
+    if (tid < KP) out[tid] = 0.f;
+    return;
+  }
+  const int64_t n = end - beg;
+
+  // ---------------------------------------------------------------- phase 1
+  wd4 acc[S::SLOTS];
+  int pij[S::SLOTS];  // (I | J << 8) of each slot's tile pair, -1 = none (wave-uniform)
+#pragma unroll
+  for (int s = 0; s < S::SLOTS; ++s) {
+    acc[s] = wd4{0.0, 0.0, 0.0, 0.0};
+    const int p = s * kWideWaves + w;
+    int I = 0, J = 0;
+    pair_ij<NT>(p, I, J);
+    pij[s] = __builtin_amdgcn_readfirstlane(p < S::NPAIR ? (I | (J << 8)) : -1);
+  }
+  double bacc = 0.0;  // b[tid] for tid < KP
+  float4 ld[S::F4_PER_T];
+  float lr = 0.f;     // this thread's rating slot (tid < WR)
+  const int64_t nwin = (n + WR - 1) / WR;
+  auto load_window = [&](int64_t win) {
+#pragma unroll
+    for (int q = 0; q < S::F4_PER_T; ++q) {
+      const int e = tid + q * kWideThreads;
+      ld[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < S::F4) {
+        const int r = e / (KP / 4), c4 = e % (KP / 4);
+        const int64_t p = beg + win * WR + r;
+        if (p < end) {
+          const int64_t sr = indices[p];
+          if (sr >= 0 && sr < n_src) ld[q] = *reinterpret_cast<const float4*>(src + sr * KP + 4 * c4);
+        }
+      }
+    }
+    if (tid < WR) {
+      const int64_t p = beg + win * WR + tid;
+      lr = p < end ? values[p] : 0.f;
+    }
+  };
+  auto store_window = [&](int b) {
+#pragma unroll
+    for (int q = 0; q < S::F4_PER_T; ++q) {
+      const int e = tid + q * kWideThreads;
+      if (e < S::F4) {
+        const int r = e / (KP / 4), c4 = e % (KP / 4);
+        double* d = &buf[b][r * LD + 4 * c4];
+        *reinterpret_cast<double2*>(d) = make_double2((double)ld[q].x, (double)ld[q].y);
+        *reinterpret_cast<double2*>(d + 2) = make_double2((double)ld[q].z, (double)ld[q].w);
+      }
+    }
+    if (tid < WR) rsh[b][tid] = lr;
+  };
+  load_window(0);
+  store_window(0);
+  __syncthreads();
+  for (int64_t win = 0; win < nwin; ++win) {
+    const int cb = (int)(win & 1);
+    if (win + 1 < nwin) load_window(win + 1);
+    const double* wb = buf[cb];
+#pragma unroll 1
+    for (int st = 0; st < WR / 4; ++st) {
+      const double* vrow = wb + (4 * st + sub) * LD + col;
+#pragma unroll
+      for (int s = 0; s < S::SLOTS; ++s) {
+        if (pij[s] >= 0) {
+          const int I = pij[s] & 255, J = pij[s] >> 8;
+          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(vrow[16 * I], vrow[16 * J], acc[s], 0, 0, 0);
+        }
+      }
+    }
+    if (tid < KP) {
+#pragma unroll 4
+      for (int r = 0; r < WR; ++r) bacc = fma((double)rsh[cb][r], wb[r * LD + tid], bacc);
+    }
+    if (win + 1 < nwin) store_window(cb ^ 1);
+    __syncthreads();
+  }
+  // lambda = numExplicits * regParam on the diagonal (1.0 on padding columns)
+  const double lambda = (double)n * reg;
+#pragma unroll
+  for (int s = 0; s < S::SLOTS; ++s) {
+    if (pij[s] >= 0) {
+      const int I = pij[s] & 255, J = pij[s] >> 8;
+      if (I == J) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (sub + 4 * r == col) acc[s][r] += (16 * I + col < k) ? lambda : 1.0;
+      }
+    }
+  }
+  if (tid < KP) bsh[tid] = bacc;
+#if HREC_WIDE_CUT == 1
+  {
+    double t = bacc;
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) t += acc[s][0] + acc[s][1] + acc[s][2] + acc[s][3];
+    if (tid < KP) out[tid] = (float)t;
+    return;
+  }
+#endif
+
+  // ---------------------------------------------------------------- phase 2
+#pragma unroll 1
+  for (int J = 0; J < NT; ++J) {
+    double* P = buf[J & 1];
+    // (a) owners of block row J -> panel rows 0..15
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0) {
+        const int I = pij[s] & 255, K = pij[s] >> 8;
+        if (I == J) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) P[(sub + 4 * r) * LD + 16 * K + col] = acc[s][r];
+        }
+      }
+    }
+    __syncthreads();
+    // (b) panel: wave w < n_act takes the diagonal block (lanes 0..15,
+    //     redundantly) and 48 columns beyond it (lanes 16..63)
+    const int rest = KP - 16 * (J + 1);
+    const int n_act = rest > 0 ? (rest + 47) / 48 : 1;
+    if (HREC_WIDE_CUT != 3 && w < n_act) {
+      // lane per column, updated in place in LDS (registers stay free for the
+      // Gramian tiles): rows 16 J + m of panel column c live at P[m][c]; the
+      // diagonal block is copied into the wave's scratch first, so each
+      // active wave factors it privately (no cross-wave race, no barrier)
+      const int c = lane < 16 ? 16 * J + lane : 16 * (J + 1) + 48 * w + (lane - 16);
+      const bool own = c < KP;
+      double* pc = P + (own ? c : KP + (lane & 15));  // idle lanes touch only pad columns
+      double* cbw = tri[w];                           // pivot row inside the diagonal block
+      double* dg = tri[w] + 16 + 16 * (lane & 15);    // lanes 0..15: private diagonal column
+      if (lane < 16) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) dg[m] = P[m * LD + 16 * J + lane];
+      }
+      wave_sync_lds();
+#pragma unroll 1
+      for (int i = 0; i < 16; ++i) {
+        const double ai = lane < 16 ? dg[i] : pc[i * LD];
+        const double piv = wbcast(ai, i);  // lane i: column 16 J + i, row 16 J + i
+        const double r0 = __builtin_amdgcn_rcp(piv);
+        const double rp = fma(r0, fma(-piv, r0, 1.0), r0);
+        const double ut = ai * rp;  // U[16 J + i][c]
+        if (lane < 16) cbw[lane] = ai;
+        if (w == 0 && lane < 16) udg[i * 17 + lane] = lane > i ? ut : (lane == i ? 1.0 : 0.0);
+        if (w == 0 && lane == i) {
+          dsh[16 * J + i] = piv;
+          rdsh[16 * J + i] = rp;
+        }
+        wave_sync_lds();
+        if (lane < 16) {
+          for (int m = i + 1; m < 16; ++m) dg[m] = fma(-cbw[m], ut, dg[m]);
+        } else if (own) {
+          pc[i * LD] = ut;  // row i of the panel column becomes U
+          for (int m = i + 1; m < 16; ++m) pc[m * LD] = fma(-cbw[m], ut, pc[m * LD]);
+        }
+        wave_sync_lds();
+      }
+    }
+    __syncthreads();
+    // (c) trailing update A_KM -= U_JK^T D_J U_JM; owners of row J take U_JK
+    if (HREC_WIDE_CUT != 4)
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0) {
+        const int K = pij[s] & 255, M = pij[s] >> 8;
+        if (K == J && M == J) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s][r] = udg[(sub + 4 * r) * 17 + col];
+        } else if (K == J) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s][r] = P[(sub + 4 * r) * LD + 16 * M + col];
+        } else if (K > J) {
+          asm volatile("" ::: "memory");  // keep these LDS reads inside the branch (VGPR budget)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int q = 4 * kk + sub;
+            const double ua = -P[q * LD + 16 * K + col] * dsh[16 * J + q];
+            const double ub = P[q * LD + 16 * M + col];
+            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, ub, acc[s], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+#if HREC_WIDE_CUT == 2 || HREC_WIDE_CUT == 3 || HREC_WIDE_CUT == 4
+  {
+    double t = 0.0;
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) t += acc[s][0] + acc[s][1] + acc[s][2] + acc[s][3];
+    if (tid < KP) out[tid] = (float)t;
+    return;
+  }
+#endif
+  // ---------------------------------------------------------------- phase 3
+  // The owner of diagonal tile (J, J) stages it in its scratch: T[q][c].
+  auto stage_diag = [&](int s) {
+    double* T = tri[w];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[(sub + 4 * r) * 17 + col] = acc[s][r];
+    wave_sync_lds();
+  };
+  // forward: U^T w = b, then v = w / D (in bsh)
+#pragma unroll 1
+  for (int J = 0; J < NT; ++J) {
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0) {
+        const int I = pij[s] & 255, K = pij[s] >> 8;
+        if (I == J && K == J) {
+          stage_diag(s);
+          const double* T = tri[w];
+          double bi = lane < 16 ? bsh[16 * J + lane] : 0.0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const double wq = wbcast(bi, q);
+            if (lane > q && lane < 16) bi = fma(-T[q * 17 + lane], wq, bi);
+          }
+          if (lane < 16) {
+            xsh[16 * J + lane] = bi;                          // w_J
+            bsh[16 * J + lane] = bi * rdsh[16 * J + lane];    // v_J = w_J / D
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0) {
+        const int I = pij[s] & 255, K = pij[s] >> 8;
+        if (I == J && K > J) {  // b_K -= U_JK^T w_J
+          double part = 0.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part = fma(acc[s][r], xsh[16 * J + sub + 4 * r], part);
+          part += __shfl_xor(part, 16, kWave);
+          part += __shfl_xor(part, 32, kWave);
+          if (lane < 16) bsh[16 * K + lane] -= part;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // backward: U x = v (v in bsh, x -> xsh)
+#pragma unroll 1
+  for (int M = NT - 1; M >= 0; --M) {
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0) {
+        const int I = pij[s] & 255, K = pij[s] >> 8;
+        if (I == M && K == M) {
+          stage_diag(s);
+          const double* T = tri[w];
+          double bi = lane < 16 ? bsh[16 * M + lane] : 0.0;
+#pragma unroll
+          for (int q = 15; q >= 0; --q) {
+            const double xq = wbcast(bi, q);
+            if (lane < q) bi = fma(-T[lane * 17 + q], xq, bi);
+          }
+          if (lane < 16) xsh[16 * M + lane] = bi;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0) {
+        const int I = pij[s] & 255, K = pij[s] >> 8;
+        if (K == M && I < M) {  // v_I -= U_IM x_M
+          const double xm = xsh[16 * M + col];
+          double part[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            part[r] = acc[s][r] * xm;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) part[r] += __shfl_xor(part[r], off, kWave);
+          }
+          if (col == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bsh[16 * I + sub + 4 * r] -= part[r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < KP) out[tid] = (float)xsh[tid];
+}
+
+}  // namespace hrec
+
+using namespace hrec;
+
+int hrec_als_half_sweep_wide(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
+                             const float* src_factors, int64_t n_src, int k, int kp, double reg_param,
+                             float* dst_factors, void* stream) {
+  const dim3 grid((unsigned)n_rows);
+  hipStream_t s = as_stream(stream);
+#define HREC_WIDE(NT)                                                                                        \
+  hipLaunchKernelGGL((als_half_sweep_wide_kernel<NT>), grid, dim3(WideShape<NT>::THREADS), 0, s, indptr, indices, values, n_rows, \
+                     src_factors, n_src, k, reg_param, dst_factors)
+  switch (kp) {
+    case 96: HREC_WIDE(6); break;
+    case 128: HREC_WIDE(8); break;
+    case 192: HREC_WIDE(12); break;
+    default: HREC_WIDE(16); break;
+  }
+#undef HREC_WIDE
+  return check_launch("als_half_sweep_wide_kernel");
+}

@@ -19,6 +19,12 @@ int check_launch(const char* what);
 
 constexpr int kWave = 64;
 
+// Leading dimensions of factor matrices: 16/32/64 (one wave per row in the
+// half-sweep) and 96/128/192/256 (one workgroup per row, csrc/als_wide.hip).
+inline bool hrec_factor_ld_ok(int kp) {
+  return kp == 16 || kp == 32 || kp == 64 || kp == 96 || kp == 128 || kp == 192 || kp == 256;
+}
+
 // Stable descending top-k of n_rows rows (score.hip): larger first, equal
 // values -> smaller original index first (src_idx maps positions to original
 // indices; entries with index -1 are skipped). Workspace: topk_ws_bytes.
@@ -40,6 +46,12 @@ __host__ __device__ inline uint64_t pair_hash(uint64_t seed, uint64_t u, uint64_
 }
 
 }  // namespace hrec
+
+// csrc/als_wide.hip: the half-sweep for kp in {96, 128, 192, 256} (arguments
+// already validated by hrec_als_half_sweep).
+int hrec_als_half_sweep_wide(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
+                             const float* src_factors, int64_t n_src, int k, int kp, double reg_param,
+                             float* dst_factors, void* stream);
 
 #define HREC_REQUIRE(cond, ...)          \
   do {                                   \

@@ -7,6 +7,8 @@
 
 namespace hrec {
 
+constexpr int kScoreKMax = 256;  // widest factor row (rank 256)
+
 // --------------------------------------------------------------- ALS score
 // One thread per item; UB users per block row held in LDS (broadcast reads).
 // The item matrix is stored transposed [kp][ld] so every c-step is one
@@ -20,13 +22,13 @@ __global__ __launch_bounds__(256) void als_score_kernel(const float* __restrict_
                                                         int64_t n_items, int k, int kp,
                                                         float* __restrict__ out) {
 #pragma clang fp contract(off)
-  __shared__ float ush[UB][64];
+  __shared__ float ush[UB][kScoreKMax];
   __shared__ int uok[UB];
   const int b0 = blockIdx.y * UB;
-  for (int t = threadIdx.x; t < UB * 64; t += blockDim.x) {
-    const int b = t >> 6, c = t & 63;
+  for (int t = threadIdx.x; t < UB * kp; t += blockDim.x) {
+    const int b = t / kp, c = t % kp;
     const int64_t ur = (b0 + b < n_users) ? user_rows[b0 + b] : -1;
-    ush[b][c] = (ur >= 0 && c < kp) ? U[ur * kp + c] : 0.f;
+    ush[b][c] = ur >= 0 ? U[ur * kp + c] : 0.f;
     if (c == 0) uok[b] = ur >= 0;
   }
   __syncthreads();
@@ -71,15 +73,15 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
     const float* __restrict__ thr, int thr_stride, int cap, float* __restrict__ cand_v,
     int64_t* __restrict__ cand_i, int* __restrict__ cand_n) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) float us[64][UB];
+  __shared__ __attribute__((aligned(16))) float us[kScoreKMax][UB];
   __shared__ int uok[UB];
   // grid: x = user group (fastest-varying), y = 1024-item slice, so the
   // blocks of one item slice are dispatched back to back and share it in L2
   const int b0 = blockIdx.x * UB;
-  for (int t = threadIdx.x; t < UB * 64; t += blockDim.x) {
-    const int b = t / 64, c = t % 64;
+  for (int t = threadIdx.x; t < UB * kp; t += blockDim.x) {
+    const int b = t / kp, c = t % kp;
     const int64_t ur = (b0 + b < n_users) ? user_rows[b0 + b] : -1;
-    us[c][b] = (ur >= 0 && c < kp) ? U[ur * kp + c] : 0.f;
+    us[c][b] = ur >= 0 ? U[ur * kp + c] : 0.f;
     if (c == 0) uok[b] = ur >= 0;
   }
   __syncthreads();
@@ -698,7 +700,7 @@ template int topk_rows<double>(const double*, int64_t, int64_t, int64_t, int, in
 extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_rows, int n_users,
                               const float* item_factors_t, int64_t ld_items, const int64_t* item_rows,
                               int64_t n_items, int k, int kp, float* out, void* stream) {
-  HREC_REQUIRE(kp == 16 || kp == 32 || kp == 64, "als_score: kp must be 16, 32 or 64");
+  HREC_REQUIRE(hrec_factor_ld_ok(kp), "als_score: kp must be 16, 32, 64, 96, 128, 192 or 256");
   HREC_REQUIRE(k >= 1 && k <= kp, "als_score: need 1 <= k <= kp");
   HREC_REQUIRE(n_users >= 0 && n_items >= 0 && ld_items >= 0, "als_score: negative size");
   if (n_users == 0 || n_items == 0) return HREC_OK;
@@ -825,7 +827,7 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
                                    const float* item_factors_t, int64_t ld_items, int64_t n_items, int k, int kp,
                                    int top_k, int64_t* out_idx, float* out_val, int* overflow, void* workspace,
                                    size_t workspace_bytes, void* stream) {
-  HREC_REQUIRE(kp == 16 || kp == 32 || kp == 64, "als_score_topk: kp must be 16, 32 or 64");
+  HREC_REQUIRE(hrec_factor_ld_ok(kp), "als_score_topk: kp must be 16, 32, 64, 96, 128, 192 or 256");
   HREC_REQUIRE(k >= 1 && k <= kp, "als_score_topk: need 1 <= k <= kp");
   HREC_REQUIRE(n_users >= 0 && n_users < 65536 && n_items >= 0, "als_score_topk: bad shape");
   HREC_REQUIRE(ld_items >= n_items && ld_items % 4 == 0, "als_score_topk: ld_items must be >= n_items and %% 4");

@@ -63,20 +63,25 @@ __global__ __launch_bounds__(256) void synth_fill_kernel(uint64_t seed, uint64_t
 __global__ __launch_bounds__(256) void init_factors_kernel(uint64_t seed, int64_t row_begin,
                                                            int64_t n_rows, int k, int kp,
                                                            float* __restrict__ out) {
-  __shared__ float z_sh[4][64];
+  __shared__ float z_sh[4][256];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * 4 + w;
   if (r >= n_rows) return;
   const uint64_t g = (uint64_t)(row_begin + r);
-  float z = 0.f;
-  if (lane < k) {
-    uint32_t acc = 0;
+  float z[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc += (uint32_t)(pair_hash(seed, g, (uint64_t)(lane * 4 + t)) >> 42);
-    z = (float)acc * (1.0f / 4194304.0f) - 2.0f;
+  for (int q = 0; q < 4; ++q) {  // columns lane, lane + 64, lane + 128, lane + 192
+    const int c = lane + 64 * q;
+    z[q] = 0.f;
+    if (c < k) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc += (uint32_t)(pair_hash(seed, g, (uint64_t)(c * 4 + t)) >> 42);
+      z[q] = (float)acc * (1.0f / 4194304.0f) - 2.0f;
+    }
+    z_sh[w][c] = z[q];
   }
-  z_sh[w][lane] = z;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   double s = 0.0;
@@ -84,9 +89,13 @@ __global__ __launch_bounds__(256) void init_factors_kernel(uint64_t seed, int64_
     const double zc = (double)z_sh[w][c];
     s += zc * zc;
   }
-  float x = 0.f;
-  if (lane < k && s > 0.0) x = (float)((double)z * (1.0 / sqrt(s)));
-  if (lane < kp) out[r * kp + lane] = x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = lane + 64 * q;
+    float x = 0.f;
+    if (c < k && s > 0.0) x = (float)((double)z[q] * (1.0 / sqrt(s)));
+    if (c < kp) out[r * kp + c] = x;
+  }
 }
 
 }  // namespace hrec
@@ -153,7 +162,7 @@ extern "C" int hrec_exclusive_scan_i64(const int64_t* counts, int64_t n, int64_t
 
 extern "C" int hrec_als_init_factors(uint64_t seed, int64_t row_begin, int64_t n_rows, int k, int kp,
                                      float* out, void* stream) {
-  HREC_REQUIRE(k >= 1 && k <= kp && (kp == 16 || kp == 32 || kp == 64), "als_init_factors: bad k=%d kp=%d",
+  HREC_REQUIRE(k >= 1 && k <= kp && hrec_factor_ld_ok(kp), "als_init_factors: bad k=%d kp=%d",
                k, kp);
   HREC_REQUIRE(n_rows >= 0 && row_begin >= 0, "als_init_factors: negative size");
   if (n_rows == 0) return HREC_OK;

@@ -33,9 +33,10 @@ def padded_k(k):
         return 16
     if k <= 32:
         return 32
-    if k <= 64:
-        return 64
-    raise ValueError(f"rank {k} > 64 is not supported by the f64 half-sweep kernel")
+    for kp in (64, 96, 128, 192, 256):  # > 64: one workgroup per row (csrc/als_wide.hip)
+        if k <= kp:
+            return kp
+    raise ValueError(f"rank {k} > 256 is not supported by the half-sweep kernels")
 
 
 def shard_range(n, world, rank):

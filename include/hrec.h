@@ -18,7 +18,8 @@
  *   - every pointer is a DEVICE pointer owned by the caller, except where a
  *     parameter is documented as host memory;
  *   - row-major storage; factor matrices have a leading dimension `kp`
- *     (16, 32 or 64) >= k whose padding columns are kept at zero;
+ *     (16, 32, 64, 96, 128, 192 or 256) >= k whose padding columns are kept
+ *     at zero (kp > 64: one workgroup per row, csrc/als_wide.hip);
  *   - CSR: int64 indptr[n_rows+1] (local, starts at 0), int32 indices,
  *     f32 values;
  *   - `stream` is a hipStream_t passed as void* (NULL = default stream);

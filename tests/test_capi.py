@@ -44,7 +44,7 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     rc = lib.hrec_als_half_sweep(None, None, None, ctypes.c_int64(1), None, ctypes.c_int64(1), 8, 48,
                                  ctypes.c_double(0.1), 0, None, None)
     assert rc == -1
-    assert b"kp must be 16, 32 or 64" in lib.hrec_last_error()
+    assert b"kp must be 16, 32, 64, 96, 128, 192 or 256" in lib.hrec_last_error()
 
 
 def test_product_has_no_oracle_imports():
