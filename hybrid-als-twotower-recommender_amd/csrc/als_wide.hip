@@ -109,7 +109,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   __shared__ double rdsh[KP];     // 1 / D
   __shared__ double xsh[KP];      // x blocks (backward)
   __shared__ float rsh[2][WR];    // ratings of the two windows
-  __shared__ double tri[kWideWaves][16 * 17];  // per-wave scratch: pivot row / diagonal tile
+  __shared__ __attribute__((aligned(16))) double tri[kWideWaves][16 * 17];  // per-wave scratch: pivot rows / diagonal tile
   __shared__ double udg[16 * 17];              // U_JJ of the current block row
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -180,12 +180,33 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 #pragma unroll 1
     for (int st = 0; st < WR / 4; ++st) {
       const double* vrow = wb + (4 * st + sub) * LD + col;
+      // No per-slot branch (a slot without a pair accumulates tile (0, 0)
+      // into a register nobody reads). Slots go in groups of G: the operand
+      // reads of group g + 1 are issued before the MFMAs of group g, so the
+      // LDS latency hides behind G MFMAs (64 cycles each).
+      constexpr int G = 6, NG = (S::SLOTS + G - 1) / G;
+      double ra[2][G], rb[2][G];
+      auto rd = [&](int g, int bsel) {
 #pragma unroll
-      for (int s = 0; s < S::SLOTS; ++s) {
-        if (pij[s] >= 0) {
-          const int I = pij[s] & 255, J = pij[s] >> 8;
-          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(vrow[16 * I], vrow[16 * J], acc[s], 0, 0, 0);
+        for (int j = 0; j < G; ++j) {
+          const int s = g * G + j;
+          if (s < S::SLOTS) {
+            const int q = pij[s] < 0 ? 0 : pij[s];
+            ra[bsel][j] = vrow[16 * (q & 255)];
+            rb[bsel][j] = vrow[16 * (q >> 8)];
+          }
         }
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (g + 1 < NG) rd(g + 1, (g + 1) & 1);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const int s = g * G + j;
+          if (s < S::SLOTS) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[g & 1][j], rb[g & 1][j], acc[s], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (tid < KP) {
@@ -240,64 +261,89 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     const int rest = KP - 16 * (J + 1);
     const int n_act = rest > 0 ? (rest + 47) / 48 : 1;
     if (HREC_WIDE_CUT != 3 && w < n_act) {
-      // lane per column, updated in place in LDS (registers stay free for the
-      // Gramian tiles): rows 16 J + m of panel column c live at P[m][c]; the
-      // diagonal block is copied into the wave's scratch first, so each
-      // active wave factors it privately (no cross-wave race, no barrier)
+      // lane per column, column in registers, pivot loop rolled (a[] is only
+      // ever indexed by compile-time m; a[i] comes out through a select
+      // chain): lanes 0..15 of every active wave hold the diagonal block
+      // (read-only in P: each wave factors it privately, no cross-wave
+      // barrier per pivot), lanes 16..63 one panel column each.
       const int c = lane < 16 ? 16 * J + lane : 16 * (J + 1) + 48 * w + (lane - 16);
       const bool own = c < KP;
-      double* pc = P + (own ? c : KP + (lane & 15));  // idle lanes touch only pad columns
-      double* cbw = tri[w];                           // pivot row inside the diagonal block
-      double* dg = tri[w] + 16 + 16 * (lane & 15);    // lanes 0..15: private diagonal column
-      if (lane < 16) {
+      const double* pc = P + (own ? c : KP + (lane & 15));  // idle lanes read pad columns
+      double a[16];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) dg[m] = P[m * LD + 16 * J + lane];
-      }
-      wave_sync_lds();
+      for (int m = 0; m < 16; ++m) a[m] = pc[m * LD];
 #pragma unroll 1
       for (int i = 0; i < 16; ++i) {
-        const double ai = lane < 16 ? dg[i] : pc[i * LD];
+        double ai = a[0];
+#pragma unroll
+        for (int m = 1; m < 16; ++m) ai = i == m ? a[m] : ai;
         const double piv = wbcast(ai, i);  // lane i: column 16 J + i, row 16 J + i
         const double r0 = __builtin_amdgcn_rcp(piv);
         const double rp = fma(r0, fma(-piv, r0, 1.0), r0);
         const double ut = ai * rp;  // U[16 J + i][c]
+        double* cbw = tri[w] + 16 * (i & 1);  // pivot row inside the diagonal block (alternating)
         if (lane < 16) cbw[lane] = ai;
+        if (own && lane >= 16) P[i * LD + c] = ut;  // the panel column's row i becomes U
         if (w == 0 && lane < 16) udg[i * 17 + lane] = lane > i ? ut : (lane == i ? 1.0 : 0.0);
         if (w == 0 && lane == i) {
           dsh[16 * J + i] = piv;
           rdsh[16 * J + i] = rp;
         }
         wave_sync_lds();
-        if (lane < 16) {
-          for (int m = i + 1; m < 16; ++m) dg[m] = fma(-cbw[m], ut, dg[m]);
-        } else if (own) {
-          pc[i * LD] = ut;  // row i of the panel column becomes U
-          for (int m = i + 1; m < 16; ++m) pc[m * LD] = fma(-cbw[m], ut, pc[m * LD]);
+#pragma unroll
+        for (int m = 0; m < 16; m += 2) {
+          const double2 u = *reinterpret_cast<const double2*>(cbw + m);
+          if (m > i) a[m] = fma(-u.x, ut, a[m]);
+          if (m + 1 > i) a[m + 1] = fma(-u.y, ut, a[m + 1]);
         }
-        wave_sync_lds();
       }
     }
     __syncthreads();
-    // (c) trailing update A_KM -= U_JK^T D_J U_JM; owners of row J take U_JK
-    if (HREC_WIDE_CUT != 4)
+    // (c) trailing update A_KM -= U_JK^T D_J U_JM; owners of row J take U_JK.
+    // Slot rows K grow with the slot index, so the tiles still to update
+    // (K > J) are a suffix of the slots: walk it from the end, reading the
+    // next slot's panel operands before this slot's four MFMAs.
+    if (HREC_WIDE_CUT != 4) {
+      const double* dj = dsh + 16 * J;
+      auto opnd = [&](int s, double (&ua)[4], double (&ub)[4]) {
+        const int q0 = pij[s] < 0 ? 0 : pij[s];
+        const int K = q0 & 255, M = q0 >> 8;
 #pragma unroll
-    for (int s = 0; s < S::SLOTS; ++s) {
-      if (pij[s] >= 0) {
-        const int K = pij[s] & 255, M = pij[s] >> 8;
-        if (K == J && M == J) {
+        for (int kk = 0; kk < 4; ++kk) {
+          const int q = 4 * kk + sub;
+          ua[kk] = -P[q * LD + 16 * K + col] * dj[q];
+          ub[kk] = P[q * LD + 16 * M + col];
+        }
+      };
+      double ua[4], ub[4];
+      opnd(S::SLOTS - 1, ua, ub);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[s][r] = udg[(sub + 4 * r) * 17 + col];
-        } else if (K == J) {
+      for (int s = S::SLOTS - 1; s >= 0; --s) {
+        const int K = pij[s] & 255;
+        if (pij[s] >= 0 && K <= J) break;  // wave-uniform
+        double ca[4], cbv[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[s][r] = P[(sub + 4 * r) * LD + 16 * M + col];
-        } else if (K > J) {
-          asm volatile("" ::: "memory");  // keep these LDS reads inside the branch (VGPR budget)
+        for (int kk = 0; kk < 4; ++kk) {
+          ca[kk] = ua[kk];
+          cbv[kk] = ub[kk];
+        }
+        if (s > 0) opnd(s - 1, ua, ub);
+        if (pij[s] >= 0) {
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) {
-            const int q = 4 * kk + sub;
-            const double ua = -P[q * LD + 16 * K + col] * dsh[16 * J + q];
-            const double ub = P[q * LD + 16 * M + col];
-            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, ub, acc[s], 0, 0, 0);
+          for (int kk = 0; kk < 4; ++kk)
+            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[kk], cbv[kk], acc[s], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < S::SLOTS; ++s) {
+        if (pij[s] >= 0 && (pij[s] & 255) == J) {
+          const int M = pij[s] >> 8;
+          if (M == J) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[s][r] = udg[(sub + 4 * r) * 17 + col];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[s][r] = P[(sub + 4 * r) * LD + 16 * M + col];
           }
         }
       }
@@ -332,11 +378,14 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         if (I == J && K == J) {
           stage_diag(s);
           const double* T = tri[w];
+          double tc[16];  // column `lane` of U_JJ
+#pragma unroll
+          for (int q = 0; q < 16; ++q) tc[q] = T[q * 17 + col];
           double bi = lane < 16 ? bsh[16 * J + lane] : 0.0;
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const double wq = wbcast(bi, q);
-            if (lane > q && lane < 16) bi = fma(-T[q * 17 + lane], wq, bi);
+            if (lane > q && lane < 16) bi = fma(-tc[q], wq, bi);
           }
           if (lane < 16) {
             xsh[16 * J + lane] = bi;                          // w_J
@@ -372,11 +421,14 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         if (I == M && K == M) {
           stage_diag(s);
           const double* T = tri[w];
+          double tr[16];  // row `lane` of U_MM
+#pragma unroll
+          for (int q = 0; q < 16; ++q) tr[q] = T[col * 17 + q];
           double bi = lane < 16 ? bsh[16 * M + lane] : 0.0;
 #pragma unroll
           for (int q = 15; q >= 0; --q) {
             const double xq = wbcast(bi, q);
-            if (lane < q) bi = fma(-T[lane * 17 + q], xq, bi);
+            if (lane < q) bi = fma(-tr[q], xq, bi);
           }
           if (lane < 16) xsh[16 * M + lane] = bi;
         }
