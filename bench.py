@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--c4-items", type=int, default=50_000_000,
                     help="two-tower scoring (c4): candidate items in total over all ranks (0 = skip)")
     ap.add_argument("--c4-users", type=int, default=1024)
+    ap.add_argument("--c5-users", type=int, default=256,
+                    help="users per batch of the c5 hybrid top-5 (rank 256 + d 256, bf16; 0 = skip)")
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -250,6 +252,53 @@ def main():
                   "top_k": 5, "d": d, "items_sharded_over": world,
                   "steps": "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5"}
 
+    # BASELINE c5: rank-256 ALS factors + d = 256 two-tower vectors in bf16,
+    # end-to-end hybrid top-5 over c2's items (sharded): both score matrices
+    # on the bf16 matrix cores, per-model min-max fusion, stable top-5, C2/C3.
+    # Factors are Spark-style random init (hrec_als_init_factors) — throughput
+    # does not depend on their values; the rank-256 half-sweep is measured
+    # separately (scripts/wide_quick.py).
+    hybrid_c5 = None
+    if args.c5_users > 0:
+        k5, d5 = 256, 256
+        n_loc = max(0, min(i_per, n_items - i0))
+        U5 = torch.zeros((n_users, k5), dtype=torch.float32, device="cuda")
+        _hrec.als_init_factors(synthetic.SEED_INIT, 0, n_users, k5, k5, U5)
+        V5 = torch.zeros((n_loc, k5), dtype=torch.float32, device="cuda")
+        _hrec.als_init_factors(synthetic.SEED_INIT + 1, i0, n_loc, k5, k5, V5)
+        tt5 = DeviceTwoTower(n_users, n_items, 2651, 255, d5, seed=2)
+        g5 = torch.Generator().manual_seed(6)
+        items5 = torch.arange(i0, i0 + n_loc, dtype=torch.int32)
+        man5 = torch.randint(0, 2651, (n_items,), generator=g5, dtype=torch.int32)[i0: i0 + n_loc]
+        cat5 = torch.randint(0, 255, (n_items,), generator=g5, dtype=torch.int32)[i0: i0 + n_loc]
+        num5 = torch.rand((n_items, 2), generator=g5)[i0: i0 + n_loc].contiguous()
+        iv5 = tt5.item_vectors(items5.cuda(), man5.cuda(), cat5.cuda(), num5.cuda())
+        rec5 = ShardedRecommender(U5, None, iv5, i0, k5, world=world, rank=rank, group=group,
+                                  precision="bf16", V_local=V5)
+        B5 = args.c5_users
+        hu5 = (torch.arange(B5, dtype=torch.int64) * (n_users // B5)).cuda()
+        uv5 = tt5.user_vectors(hu5.to(torch.int32))
+        for _ in range(2):
+            rec5.recommend(hu5, uv5, False, 5)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        reps = 5
+        h0 = time.perf_counter()
+        for _ in range(reps):
+            rec5.recommend(hu5, uv5, False, 5)
+        torch.cuda.synchronize()
+        ht = torch.tensor([(time.perf_counter() - h0) / reps], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
+        hs = float(ht.item())
+        hybrid_c5 = {"pairs_per_s": B5 * n_items / hs, "ms_per_batch": hs * 1e3, "users": B5, "items": n_items,
+                     "top_k": 5, "rank": k5, "d": d5, "dtype": "bf16 operands, f32 accumulation",
+                     "items_sharded_over": world,
+                     "steps": "ALS + two-tower scores on bf16 MFMA (hrec_dot_scores) + min-max fusion + stable top-5"}
+        del U5, V5, tt5, rec5, iv5
+        torch.cuda.empty_cache()
+
     # Ingest (§8(f) row 1, ALSModel.train's DataFrame -> CSR/CSC step): the
     # rank's user shard as COO columns (int64 ids, ratings) -> id codes +
     # CSR + CSC on the device (hrec_encode_ids x2, hrec_coo_to_csr x2).
@@ -381,6 +430,7 @@ def main():
             "hybrid_top5": hybrid,
             "ingest": ingest,
             "tt_scoring_c4": tt_c4,
+            "hybrid_top5_c5": hybrid_c5,
         }
         print(json.dumps(line))
     if world > 1:

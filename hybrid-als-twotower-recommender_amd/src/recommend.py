@@ -47,13 +47,26 @@ class DeviceOps:
     def dot_topk(user_vecs, item_vecs_local, top_k, offset):
         return _hrec.dot_topk(user_vecs, item_vecs_local, top_k, idx_offset=offset)
 
+    @staticmethod
+    def operand(x, dtype):
+        return _hrec.dot_operand(x, dtype)
+
+    dot_scores = staticmethod(_hrec.dot_scores)
     rows_minmax = staticmethod(_hrec.rows_minmax)
     fuse_rows_topk = staticmethod(_hrec.fuse_rows_topk)
     topk_keyed = staticmethod(_hrec.topk_keyed)
 
 
 class ShardedRecommender:
-    def __init__(self, U, Vt_local, item_vecs_local, item_offset, k, world=1, rank=0, group=None, ops=None):
+    """precision "exact": JVM-exact ALS scores (Spark's f32 mul/add chain) and
+    f32 two-tower Dot — the reference's numerics. precision "bf16" (BASELINE
+    config c5: rank-256 factors and d = 256 towers stored in bf16): both
+    score matrices on the bf16 matrix cores (hrec_dot_scores, f32
+    accumulation) from bf16 copies of the factors / item vectors made once
+    here; pass V_local (the shard's ALS item factor rows) instead of Vt_local."""
+
+    def __init__(self, U, Vt_local, item_vecs_local, item_offset, k, world=1, rank=0, group=None, ops=None,
+                 precision="exact", V_local=None):
         self.U = U                          # [n_users, kp] ALS user factors (replicated)
         self.Vt = Vt_local                  # [kp, ld] transposed ALS item factors of this shard
         self.iv = item_vecs_local           # [n_local, d] two-tower item vectors of this shard
@@ -62,6 +75,23 @@ class ShardedRecommender:
         self.k = int(k)
         self.world, self.rank, self.group = int(world), int(rank), group
         self.ops = ops or DeviceOps
+        if precision not in ("exact", "bf16"):
+            raise ValueError(f"precision must be 'exact' or 'bf16', got {precision!r}")
+        self.precision = precision
+        if precision == "bf16":
+            if V_local is None:
+                raise ValueError("precision='bf16' needs V_local (ALS item factor rows of the shard)")
+            self.V_op = self.ops.operand(V_local, torch.bfloat16)
+            self.iv_op = self.ops.operand(item_vecs_local, torch.bfloat16)
+
+    def _scores(self, user_rows, user_vecs):
+        o = self.ops
+        if self.precision == "exact":
+            return (o.als_scores(self.U, user_rows, self.Vt, self.n_local, self.k),
+                    o.tt_scores(user_vecs, self.iv))
+        u_als = o.operand(self.U.index_select(0, user_rows), torch.bfloat16)
+        u_tt = o.operand(user_vecs, torch.bfloat16)
+        return o.dot_scores(u_als, self.V_op), o.dot_scores(u_tt, self.iv_op)
 
     def recommend(self, user_rows, user_vecs, als_wins, top_k):
         """user_rows: [B] int64 ALS rows; user_vecs: [B, d] two-tower user
@@ -70,8 +100,7 @@ class ShardedRecommender:
         B = int(user_rows.shape[0])
         dev = user_vecs.device
         if self.n_local > 0:
-            als = o.als_scores(self.U, user_rows, self.Vt, self.n_local, self.k)
-            tt = o.tt_scores(user_vecs, self.iv)
+            als, tt = self._scores(user_rows, user_vecs)
             a_mm = o.rows_minmax(als)
             t_mm = o.rows_minmax(tt)
         else:  # an empty shard contributes neutral min/max and no candidates

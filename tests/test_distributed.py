@@ -134,6 +134,14 @@ class _CpuOps:
                                 .astype(np.float32))
 
     @staticmethod
+    def operand(x, dtype):
+        return x.to(dtype).to(torch.float32)  # bf16 rounding of the operand, CPU stand-in
+
+    @staticmethod
+    def dot_scores(U, V):
+        return torch.from_numpy((U.numpy().astype(np.float64) @ V.numpy().T.astype(np.float64)).astype(np.float32))
+
+    @staticmethod
     def rows_minmax(x):
         a = x.numpy()
         return torch.from_numpy(np.stack([np.nanmin(a, axis=1), np.nanmax(a, axis=1)]).astype(np.float32))
@@ -181,7 +189,7 @@ def _hybrid_data():
     return U, V, uv, iv, k
 
 
-def _hybrid_run(world, rank, U, V, uv, iv, k, group=None):
+def _hybrid_run(world, rank, U, V, uv, iv, k, group=None, precision="exact"):
     from src.als_engine import shard_range
     from src.recommend import ShardedRecommender
 
@@ -189,27 +197,27 @@ def _hybrid_run(world, rank, U, V, uv, iv, k, group=None):
     Vl = V[i0: i0 + per]
     rec = ShardedRecommender(torch.from_numpy(U), torch.from_numpy(np.ascontiguousarray(Vl.T)),
                              torch.from_numpy(iv[i0: i0 + per]), i0, k, world=world, rank=rank, group=group,
-                             ops=_CpuOps)
+                             ops=_CpuOps, precision=precision, V_local=torch.from_numpy(np.ascontiguousarray(Vl)))
     rows = torch.tensor([0, 3, 5, 7, 11], dtype=torch.int64)
     return [t.numpy() for t in rec.recommend(rows, torch.from_numpy(uv), True, 7)]
 
 
-def _hybrid_worker(rank, world, port, q):
+def _hybrid_worker(rank, world, port, q, precision="exact"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     U, V, uv, iv, k = _hybrid_data()
-    q.put((rank, _hybrid_run(world, rank, U, V, uv, iv, k, dist.group.WORLD)))
+    q.put((rank, _hybrid_run(world, rank, U, V, uv, iv, k, dist.group.WORLD, precision)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4, 24])
-def test_sharded_hybrid_topk_matches_single(world):
+@pytest.mark.parametrize("world,precision", [(2, "exact"), (4, "exact"), (24, "exact"), (3, "bf16")])
+def test_sharded_hybrid_topk_matches_single(world, precision):
     U, V, uv, iv, k = _hybrid_data()
-    ref_i, ref_v = _hybrid_run(1, 0, U, V, uv, iv, k)
+    ref_i, ref_v = _hybrid_run(1, 0, U, V, uv, iv, k, precision=precision)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, q, precision)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=60) for _ in range(world)]

@@ -150,3 +150,42 @@ def test_dot_topk_matches_f64_ranking_outside_ties(device):
             checked += 1
         np.testing.assert_allclose(gv.cpu().numpy()[b], r[:k], rtol=1e-4, atol=tol)
     assert checked >= B // 2
+
+
+def test_hybrid_bf16_mode_matches_f64_fusion(device):
+    """BASELINE c5 numerics: rank-200 ALS factors (kp 256) and d = 256 tower
+    vectors in bf16, both score matrices on the bf16 matrix cores, then the
+    reference fusion (per-model min-max, 0.2/0.8 weights, stable top-5).
+    Checked against the f64 fusion of the bf16-ROUNDED operands: fused
+    scores within 1e-4, indices equal wherever the oracle's consecutive
+    top-6 scores are separated by more than 1e-4."""
+    from src.recommend import ShardedRecommender
+
+    rng = np.random.default_rng(21)
+    n_users, n_items, k, kp, d = 40, 3000, 200, 256, 256
+    U = np.zeros((n_users, kp), np.float32)
+    U[:, :k] = rng.normal(size=(n_users, k)) / np.sqrt(k)
+    V = np.zeros((n_items, kp), np.float32)
+    V[:, :k] = rng.normal(size=(n_items, k)) / np.sqrt(k)
+    uv = (rng.normal(size=(8, d)) / 16).astype(np.float32)
+    iv = (rng.normal(size=(n_items, d)) / 16).astype(np.float32)
+    rows = np.array([0, 3, 5, 7, 11, 13, 17, 39])
+    rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, k,
+                             precision="bf16", V_local=torch.from_numpy(V).to(device))
+    gi, gv = rec.recommend(torch.from_numpy(rows).to(device), torch.from_numpy(uv).to(device), False, 5)
+    als = _bf16_round(U[rows]).astype(np.float64) @ _bf16_round(V).astype(np.float64).T
+    tt = _bf16_round(uv).astype(np.float64) @ _bf16_round(iv).astype(np.float64).T
+
+    def mm(x):
+        lo, hi = x.min(1, keepdims=True), x.max(1, keepdims=True)
+        return (x - lo) / (hi - lo)
+
+    fused = 0.2 * mm(als) + 0.8 * mm(tt)
+    order = np.argsort(-fused, axis=1, kind="stable")
+    gi, gv = gi.cpu().numpy(), gv.cpu().numpy()
+    for b in range(len(rows)):
+        f = fused[b, order[b, :6]]
+        np.testing.assert_allclose(gv[b], f[:5], atol=1e-4)
+        for j in range(5):
+            if (j == 0 or f[j - 1] - f[j] > 1e-4) and f[j] - f[j + 1] > 1e-4:
+                assert gi[b, j] == order[b, j], (b, j)
