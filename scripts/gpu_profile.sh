@@ -9,7 +9,13 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 A="--no-cpu-baseline --steps 3 --warmup 1 $*"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o trace -- python bench.py $A > gpurun_out/prof_bench.json 2> gpurun_out/prof_trace.err
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o fetch -- python bench.py $A --no-ingest --score-users 0 --hybrid-users 0 > /dev/null 2> gpurun_out/prof_fetch.err
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o write -- python bench.py $A --no-ingest --score-users 0 --hybrid-users 0 > /dev/null 2> gpurun_out/prof_write.err
+ALS_ONLY="--no-ingest --score-users 0 --hybrid-users 0 --c4-items 0 --c5-users 0"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o fetch -- python bench.py $A $ALS_ONLY > /dev/null 2> gpurun_out/prof_fetch.err
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o write -- python bench.py $A $ALS_ONLY > /dev/null 2> gpurun_out/prof_write.err
+# c4 two-tower scoring (dot_res_kernel): its own FETCH_SIZE pass
+C4_ONLY="--no-ingest --score-users 0 --hybrid-users 0 --c5-users 0"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_c4 -o fetchc4 -- python bench.py $A $C4_ONLY > /dev/null 2> gpurun_out/prof_fetch_c4.err
+# rank-256 ALS half-sweeps (als_half_sweep_wide_kernel): kernel trace of the probe
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_wide -o wide -- python scripts/wide_quick.py 256 300000 100000 > gpurun_out/prof_wide.log 2>&1
 python scripts/summarize_profile.py gpurun_out > gpurun_out/prof_summary.json
 cat gpurun_out/prof_summary.json

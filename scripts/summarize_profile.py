@@ -43,6 +43,39 @@ def main(base):
         per = [(2 * f[i] + w[i]) * 1024 for i in range(n)]
         res["als_half_sweep"]["hbm_bytes_per_launch_corrected"] = per
         res["als_half_sweep"]["hbm_bytes_avg_per_launch"] = sum(per) / n
+    # c4 two-tower scoring: the fused dot + filter launches (FILTER = true) of
+    # the f32 and bf16 passes, HIP-trace durations and FETCH_SIZE (x2: 16-B
+    # lane loads) per launch
+    import re
+
+    def is_filter(name):
+        m = re.search(r"dot_(res|tile)_kernel<(\w+), (\d+), (\w+)", name)
+        return m and m.group(4) == "true"
+
+    dot = {}
+    for r in trace:
+        if is_filter(r["Kernel_Name"]):
+            dt = "bf16" if "dot_res_kernel<true" in r["Kernel_Name"] or "dot_tile_kernel<true" in r["Kernel_Name"] \
+                else "f32"
+            dot.setdefault(dt, {"durations_ms": []})["durations_ms"].append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    for dt, v in dot.items():
+        v["avg_ms"] = sum(v["durations_ms"]) / len(v["durations_ms"])
+    for r in rows(os.path.join(base, "prof_fetch_c4", "**", "*counter_collection.csv")):
+        if is_filter(r.get("Kernel_Name", "")) and r.get("Counter_Name") == "FETCH_SIZE":
+            dt = "bf16" if "kernel<true" in r["Kernel_Name"] else "f32"
+            dot.setdefault(dt, {}).setdefault("FETCH_SIZE_KiB_per_launch", []).append(float(r["Counter_Value"]))
+    for dt, v in dot.items():
+        f = v.get("FETCH_SIZE_KiB_per_launch")
+        if f:
+            v["hbm_read_bytes_avg_per_launch_corrected"] = 2 * 1024 * sum(f) / len(f)
+    res["dot_topk_c4_filter"] = dot
+    wide = rows(os.path.join(base, "prof_wide", "**", "*kernel_trace.csv"))
+    wd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in wide
+          if "als_half_sweep_wide_kernel" in r["Kernel_Name"]]
+    if wd:
+        res["als_half_sweep_wide_rank256"] = {"launches": len(wd), "durations_ms": wd,
+                                              "workload": "scripts/wide_quick.py 256 300000 100000 (item, user)"}
     print(json.dumps(res, indent=1))
 
 

@@ -45,13 +45,15 @@ def _frame_csr(df):
     return u_ids, i_ids, csr(urow, irow, len(u_ids)), csr(irow, urow, len(i_ids))
 
 
-def test_als_train_matches_oracle(device):
+@pytest.mark.parametrize("k", [10, 100])
+def test_als_train_matches_oracle(device, k):
+    """rank 10 (the reference's grid, src/als_model.py:185-191) and rank 100
+    (one workgroup per row, csrc/als_wide.hip) through the drop-in API."""
     from src.als_model import ALSModel
 
     rng = np.random.default_rng(0)
     df = _ratings_frame(rng)
     u_ids, i_ids, ucsr, icsc = _frame_csr(df)
-    k = 10
     U0 = rng.normal(size=(len(u_ids), k)).astype(np.float32)
     U0 /= np.linalg.norm(U0, axis=1, keepdims=True)
     m = ALSModel(rank=k, max_iter=10, reg_param=0.1)
