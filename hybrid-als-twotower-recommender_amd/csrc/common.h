@@ -25,6 +25,9 @@ inline bool hrec_factor_ld_ok(int kp) {
   return kp == 16 || kp == 32 || kp == 64 || kp == 96 || kp == 128 || kp == 192 || kp == 256;
 }
 
+// idx[i] += off for every id >= 0 (item-shard offsets; csrc/dot_topk.hip).
+int offset_ids(int64_t* idx, int64_t n, int64_t off, hipStream_t s);
+
 // Stable descending top-k of n_rows rows (score.hip): larger first, equal
 // values -> smaller original index first (src_idx maps positions to original
 // indices; entries with index -1 are skipped). Workspace: topk_ws_bytes.

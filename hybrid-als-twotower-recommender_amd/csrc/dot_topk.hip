@@ -591,6 +591,12 @@ static int64_t dot_sample(int64_t n, int kk) {
   return s < n ? s : n;
 }
 
+int offset_ids(int64_t* idx, int64_t n, int64_t off, hipStream_t s) {
+  if (n <= 0 || off == 0) return HREC_OK;
+  hipLaunchKernelGGL(dot_offset_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx, n, off);
+  return check_launch("dot_offset_kernel");
+}
+
 static char* dot_carve(char*& p, size_t bytes) {
   char* r = p;
   p += (bytes + 255) & ~(size_t)255;
@@ -702,8 +708,6 @@ extern "C" int hrec_dot_topk(const void* user_vec, int n_users, const void* item
     // 3) exact stable top-k of the survivors (item index breaks ties)
     rc = topk_rows<float>(cv, n_users, cap, cap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
   }
-  if (rc || idx_offset == 0) return rc;
-  const int64_t tot = (int64_t)n_users * kk;
-  hipLaunchKernelGGL(dot_offset_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out_idx, tot, idx_offset);
-  return check_launch("dot_offset_kernel");
+  if (rc) return rc;
+  return offset_ids(out_idx, (int64_t)n_users * kk, idx_offset, s);
 }

@@ -48,8 +48,11 @@ class DeviceOps:
         return _hrec.dot_topk(user_vecs, item_vecs_local, top_k, idx_offset=offset)
 
     @staticmethod
-    def operand(x, dtype):
-        return _hrec.dot_operand(x, dtype)
+    def operand(x, dtype, dk=None):
+        return _hrec.dot_operand(x, dtype, dk)
+
+    hybrid_minmax = staticmethod(_hrec.hybrid_minmax)
+    hybrid_topk = staticmethod(_hrec.hybrid_topk)
 
     dot_scores = staticmethod(_hrec.dot_scores)
     rows_minmax = staticmethod(_hrec.rows_minmax)
@@ -81,21 +84,61 @@ class ShardedRecommender:
         if precision == "bf16":
             if V_local is None:
                 raise ValueError("precision='bf16' needs V_local (ALS item factor rows of the shard)")
-            self.V_op = self.ops.operand(V_local, torch.bfloat16)
-            self.iv_op = self.ops.operand(item_vecs_local, torch.bfloat16)
+            # one width for both models so the fused kernel can run them together
+            self.dk = max(64, _hrec.dot_dk(V_local.shape[1]), _hrec.dot_dk(item_vecs_local.shape[1]))
+            self.fused = hasattr(self.ops, "hybrid_topk")
+            self.V_op = self.ops.operand(V_local, torch.bfloat16, self.dk)
+            self.iv_op = self.ops.operand(item_vecs_local, torch.bfloat16, self.dk)
+
+    def _user_ops(self, user_rows, user_vecs):
+        o = self.ops
+        return (o.operand(self.U.index_select(0, user_rows), torch.bfloat16, self.dk),
+                o.operand(user_vecs, torch.bfloat16, self.dk))
 
     def _scores(self, user_rows, user_vecs):
         o = self.ops
         if self.precision == "exact":
             return (o.als_scores(self.U, user_rows, self.Vt, self.n_local, self.k),
                     o.tt_scores(user_vecs, self.iv))
-        u_als = o.operand(self.U.index_select(0, user_rows), torch.bfloat16)
-        u_tt = o.operand(user_vecs, torch.bfloat16)
+        u_als, u_tt = self._user_ops(user_rows, user_vecs)
         return o.dot_scores(u_als, self.V_op), o.dot_scores(u_tt, self.iv_op)
+
+    def _recommend_fused(self, user_rows, user_vecs, als_wins, top_k):
+        """bf16 path on the fused kernels (hrec_hybrid_minmax / _topk): no
+        score matrix is written; same results as the unfused path, which
+        answers a batch whose survivor list overflowed."""
+        o = self.ops
+        B = int(user_rows.shape[0])
+        dev = user_vecs.device
+        if self.n_local > 0:
+            u_als, u_tt = self._user_ops(user_rows, user_vecs)
+            a_mm, t_mm = o.hybrid_minmax(u_als, u_tt, self.V_op, self.iv_op)
+        else:
+            inf = float("inf")
+            a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
+            t_mm = a_mm.clone()
+        if self.world > 1:
+            for mm in (a_mm, t_mm):
+                dist.all_reduce(mm[0], op=dist.ReduceOp.MIN, group=self.group)
+                dist.all_reduce(mm[1], op=dist.ReduceOp.MAX, group=self.group)
+        if self.n_local > 0:
+            idx, val, over = o.hybrid_topk(u_als, u_tt, self.V_op, self.iv_op, a_mm, t_mm, als_wins, top_k,
+                                           self.offset)
+            if over:
+                idx, val = o.fuse_rows_topk(o.dot_scores(u_als, self.V_op), o.dot_scores(u_tt, self.iv_op),
+                                            a_mm, t_mm, als_wins, top_k, self.offset)
+        else:
+            idx = torch.empty((B, 0), dtype=torch.int64, device=dev)
+            val = torch.empty((B, 0), dtype=torch.float64, device=dev)
+        if self.world == 1:
+            return idx, val
+        return merge_candidates(idx, val, top_k, self.world, self.group, o)
 
     def recommend(self, user_rows, user_vecs, als_wins, top_k):
         """user_rows: [B] int64 ALS rows; user_vecs: [B, d] two-tower user
         vectors. Returns (global item ids [B, k], fused scores f64 [B, k])."""
+        if self.precision == "bf16" and self.fused:
+            return self._recommend_fused(user_rows, user_vecs, als_wins, top_k)
         o = self.ops
         B = int(user_rows.shape[0])
         dev = user_vecs.device

@@ -324,6 +324,31 @@ int hrec_dot_topk(const void* user_vec, int n_users, const void* item_vec, int64
                   float* out_val, int* overflow, void* workspace, size_t workspace_bytes,
                   void* stream);
 
+/* ---------------------------------------------------------------------
+ * Fused hybrid recommendation on bf16 operands (csrc/hybrid_fused.hip,
+ * BASELINE config c5): ALS scores <als_user[b], als_item[j]> and two-tower
+ * scores <tt_user[b], tt_item[j]> (both operands [*, dk] bf16, dk in
+ * {64, 128, 256}, zero-padded), the reference's per-model MinMaxScaler
+ * fusion and stable top-k (src/hybrid_system.py:57-75, :108) without writing
+ * either score matrix. Same results as hrec_dot_scores x2 +
+ * hrec_fuse_rows_topk. */
+size_t hrec_hybrid_minmax_workspace_bytes(int n_users);
+/* Per-user [min | max] of both score rows over items [0, n_items):
+ * als_mm / tt_mm are [2, n_users] f32 (the hrec_rows_minmax_f32 layout). */
+int hrec_hybrid_minmax(const void* als_user, const void* tt_user, int n_users, const void* als_item,
+                       const void* tt_item, int64_t n_items, int dk, float* als_mm, float* tt_mm,
+                       void* workspace, size_t workspace_bytes, void* stream);
+size_t hrec_hybrid_topk_workspace_bytes(int n_users, int64_t n_items, int top_k);
+/* Fused scores with the scaler coefficients of als_mm / tt_mm (global
+ * min/max when the items are sharded), weights (0.8, 0.2) if als_wins else
+ * (0.2, 0.8); top_k per user, ties -> smaller item index; ids + idx_offset.
+ * thr_in (optional, [n_users] f64): lower bound of each user's k-th best;
+ * *overflow as hrec_dot_topk. */
+int hrec_hybrid_topk(const void* als_user, const void* tt_user, int n_users, const void* als_item,
+                     const void* tt_item, int64_t n_items, int dk, const float* als_mm, const float* tt_mm,
+                     int als_wins, int top_k, const double* thr_in, int64_t idx_offset, int64_t* out_idx,
+                     double* out_val, int* overflow, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -134,7 +134,7 @@ class _CpuOps:
                                 .astype(np.float32))
 
     @staticmethod
-    def operand(x, dtype):
+    def operand(x, dtype, dk=None):
         return x.to(dtype).to(torch.float32)  # bf16 rounding of the operand, CPU stand-in
 
     @staticmethod
@@ -179,6 +179,20 @@ class _CpuOps:
         return torch.from_numpy(np.array(out_i)), torch.from_numpy(np.array(out_v))
 
 
+class _CpuFusedOps(_CpuOps):
+    """Stand-ins for the fused kernels (same results as the unfused ops)."""
+
+    @staticmethod
+    def hybrid_minmax(ua, ut, va, vt):
+        return _CpuOps.rows_minmax(_CpuOps.dot_scores(ua, va)), _CpuOps.rows_minmax(_CpuOps.dot_scores(ut, vt))
+
+    @staticmethod
+    def hybrid_topk(ua, ut, va, vt, a_mm, t_mm, als_wins, top_k, offset):
+        i, v = _CpuOps.fuse_rows_topk(_CpuOps.dot_scores(ua, va), _CpuOps.dot_scores(ut, vt), a_mm, t_mm, als_wins,
+                                      top_k, offset)
+        return i, v, False
+
+
 def _hybrid_data():
     rng = np.random.default_rng(7)
     n_users, n_items, k, d = 12, 101, 8, 6
@@ -197,7 +211,9 @@ def _hybrid_run(world, rank, U, V, uv, iv, k, group=None, precision="exact"):
     Vl = V[i0: i0 + per]
     rec = ShardedRecommender(torch.from_numpy(U), torch.from_numpy(np.ascontiguousarray(Vl.T)),
                              torch.from_numpy(iv[i0: i0 + per]), i0, k, world=world, rank=rank, group=group,
-                             ops=_CpuOps, precision=precision, V_local=torch.from_numpy(np.ascontiguousarray(Vl)))
+                             ops=_CpuFusedOps if precision == "bf16-fused" else _CpuOps,
+                             precision="bf16" if precision.startswith("bf16") else precision,
+                             V_local=torch.from_numpy(np.ascontiguousarray(Vl)))
     rows = torch.tensor([0, 3, 5, 7, 11], dtype=torch.int64)
     return [t.numpy() for t in rec.recommend(rows, torch.from_numpy(uv), True, 7)]
 
@@ -210,7 +226,8 @@ def _hybrid_worker(rank, world, port, q, precision="exact"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,precision", [(2, "exact"), (4, "exact"), (24, "exact"), (3, "bf16")])
+@pytest.mark.parametrize("world,precision", [(2, "exact"), (4, "exact"), (24, "exact"), (3, "bf16"),
+                                             (3, "bf16-fused"), (24, "bf16-fused")])
 def test_sharded_hybrid_topk_matches_single(world, precision):
     U, V, uv, iv, k = _hybrid_data()
     ref_i, ref_v = _hybrid_run(1, 0, U, V, uv, iv, k, precision=precision)

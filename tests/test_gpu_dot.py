@@ -189,3 +189,58 @@ def test_hybrid_bf16_mode_matches_f64_fusion(device):
         for j in range(5):
             if (j == 0 or f[j - 1] - f[j] > 1e-4) and f[j] - f[j + 1] > 1e-4:
                 assert gi[b, j] == order[b, j], (b, j)
+
+
+@pytest.mark.parametrize("n_users,n_items,k,d,B,wins", [(40, 3000, 200, 256, 8, False), (300, 40000, 50, 64, 130, True),
+                                                       (64, 70001, 120, 100, 33, False)])
+def test_hybrid_fused_equals_unfused(device, n_users, n_items, k, d, B, wins):
+    """The fused hybrid kernels (hrec_hybrid_minmax + hrec_hybrid_topk: no
+    score matrix written) return exactly what the unfused bf16 path (two
+    hrec_dot_scores + hrec_rows_minmax + hrec_fuse_rows_topk) returns — same
+    MFMA k order, same fusion arithmetic — incl. the sample-bound filter
+    (n_items > 16384), a user count that is not a multiple of the 128-user
+    block and widths padded to one dk."""
+    from src.recommend import ShardedRecommender
+
+    rng = np.random.default_rng(n_items)
+    kp = 256 if k > 128 else (128 if k > 64 else 64)
+    U = np.zeros((n_users, kp), np.float32)
+    U[:, :k] = rng.normal(size=(n_users, k)) / np.sqrt(k)
+    V = np.zeros((n_items, kp), np.float32)
+    V[:, :k] = rng.normal(size=(n_items, k)) / np.sqrt(k)
+    iv = (rng.normal(size=(n_items, d)) / 8).astype(np.float32)
+    uv = (rng.normal(size=(B, d)) / 8).astype(np.float32)
+    rows = torch.as_tensor(rng.integers(0, n_users, B), dtype=torch.int64, device=device)
+    rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, k,
+                             precision="bf16", V_local=torch.from_numpy(V).to(device))
+    assert rec.fused
+    fi, fv = rec.recommend(rows, torch.from_numpy(uv).to(device), wins, 7)
+    rec.fused = False
+    ui, uv_ = rec.recommend(rows, torch.from_numpy(uv).to(device), wins, 7)
+    np.testing.assert_array_equal(fi.cpu().numpy(), ui.cpu().numpy())
+    np.testing.assert_array_equal(fv.cpu().numpy(), uv_.cpu().numpy())
+
+
+def test_hybrid_fused_minmax_and_overflow(device):
+    """hrec_hybrid_minmax == hrec_rows_minmax of the two score matrices; a
+    catalogue of identical items (every fused score ties) overflows the
+    survivor list and the recommender falls back to the exact unfused path."""
+    h = _h()
+    from src.recommend import ShardedRecommender
+
+    rng = np.random.default_rng(5)
+    ua = h.dot_operand(torch.from_numpy(_vecs(70, 128, 1)).to(device), torch.bfloat16)
+    ut = h.dot_operand(torch.from_numpy(_vecs(70, 128, 2)).to(device), torch.bfloat16)
+    va = h.dot_operand(torch.from_numpy(_vecs(20001, 128, 3)).to(device), torch.bfloat16)
+    vt = h.dot_operand(torch.from_numpy(_vecs(20001, 128, 4)).to(device), torch.bfloat16)
+    a_mm, t_mm = h.hybrid_minmax(ua, ut, va, vt)
+    np.testing.assert_array_equal(a_mm.cpu().numpy(), h.rows_minmax(h.dot_scores(ua, va)).cpu().numpy())
+    np.testing.assert_array_equal(t_mm.cpu().numpy(), h.rows_minmax(h.dot_scores(ut, vt)).cpu().numpy())
+    V = np.tile(rng.normal(size=(1, 64)).astype(np.float32), (30000, 1))
+    iv = np.tile(rng.normal(size=(1, 64)).astype(np.float32), (30000, 1))
+    U = rng.normal(size=(10, 64)).astype(np.float32)
+    rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, 64,
+                             precision="bf16", V_local=torch.from_numpy(V).to(device))
+    rows = torch.arange(4, dtype=torch.int64, device=device)
+    i, v = rec.recommend(rows, torch.from_numpy(U[:4]).to(device), False, 5)
+    np.testing.assert_array_equal(i.cpu().numpy(), np.tile(np.arange(5), (4, 1)))
