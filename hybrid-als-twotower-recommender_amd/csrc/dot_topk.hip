@@ -310,11 +310,23 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   const int64_t n_it = (n_items + kItems - 1) / kItems;
   if (ig >= n_it) return;  // block-uniform
   const int b0 = ut * UB;
-  for (int o = threadIdx.x; o < UB * S::kChunks; o += kDotThreads) {
-    const int r = o / S::kChunks, q = o % S::kChunks;
-    int4 v = {0, 0, 0, 0};
-    if (b0 + r < B) v = *reinterpret_cast<const int4*>(U + (int64_t)(b0 + r) * (DK * S::kElem) + 16 * q);
-    *reinterpret_cast<int4*>(us + r * kRowB + 16 * (kSwz ? q ^ (r & 15) : q)) = v;
+  // batches of 8 independent 16-B loads per thread in flight
+  for (int o0 = threadIdx.x; o0 < UB * S::kChunks; o0 += 8 * kDotThreads) {
+    int4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = o0 + j * kDotThreads;
+      const int r = o / S::kChunks, q = o % S::kChunks;
+      v[j] = int4{0, 0, 0, 0};
+      if (o < UB * S::kChunks && b0 + r < B)
+        v[j] = *reinterpret_cast<const int4*>(U + (int64_t)(b0 + r) * (DK * S::kElem) + 16 * q);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = o0 + j * kDotThreads;
+      const int r = o / S::kChunks, q = o % S::kChunks;
+      if (o < UB * S::kChunks) *reinterpret_cast<int4*>(us + r * kRowB + 16 * (kSwz ? q ^ (r & 15) : q)) = v[j];
+    }
   }
   if (FILTER) {
     for (int o = threadIdx.x; o < UB; o += kDotThreads) {

@@ -26,6 +26,12 @@
 
 #include "common.h"
 
+// Item-fragment ring depth (steps in flight; one step = 8 MFMAs = 128
+// cycles): the min/max and sample passes have registers to spare.
+#ifndef HREC_HY_RING
+#define HREC_HY_RING(MODE) ((MODE) == 2 ? 4 : 8)
+#endif
+
 namespace hrec {
 
 typedef float hy_f4 __attribute__((ext_vector_type(4)));
@@ -72,7 +78,8 @@ __global__ __launch_bounds__(kHyThreads) void hybrid_tile_kernel(
     int64_t idx_offset) {
 #pragma clang fp contract(off)
   using S = HyShape<DK>;
-  constexpr int NU = kHyNU, NI = kHyNI, KS = S::KS, P = 2;
+  constexpr int NU = kHyNU, NI = kHyNI, KS = S::KS;
+  constexpr int P = HREC_HY_RING(MODE) < 2 * KS ? HREC_HY_RING(MODE) : 2 * KS;
   static_assert((2 * KS) % P == 0, "ring depth must divide the steps of a tile");
   __shared__ __attribute__((aligned(16))) char us[S::kLds];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -86,12 +93,28 @@ __global__ __launch_bounds__(kHyThreads) void hybrid_tile_kernel(
   const int b0 = ut * kHyUsers;
   const bool active = ig < n_it;  // block-uniform; idle blocks still reach the final reduction
   if (active) {
-    for (int o = threadIdx.x; o < 2 * kHyUsers * S::kChunks; o += kHyThreads) {
-      const int m = o / (kHyUsers * S::kChunks);
-      const int r = (o / S::kChunks) % kHyUsers, q = o % S::kChunks;
-      int4 v = {0, 0, 0, 0};
-      if (b0 + r < B) v = *reinterpret_cast<const int4*>((m ? Ut : Ua) + (int64_t)(b0 + r) * (DK * 2) + 16 * q);
-      *reinterpret_cast<int4*>(us + (m * kHyUsers + r) * S::kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v;
+    // stage both user blocks: batches of 8 independent 16-B loads per thread
+    // in flight (a plain loop would wait out one load latency per chunk)
+    constexpr int NCH = 2 * kHyUsers * S::kChunks, PER = NCH / kHyThreads, BAT = PER < 8 ? PER : 8;
+    static_assert(NCH % kHyThreads == 0 && PER % BAT == 0, "staging split");
+#pragma unroll
+    for (int q0 = 0; q0 < PER; q0 += BAT) {
+      int4 v[BAT];
+#pragma unroll
+      for (int j = 0; j < BAT; ++j) {
+        const int o = threadIdx.x + (q0 + j) * kHyThreads;
+        const int m = o / (kHyUsers * S::kChunks);
+        const int r = (o / S::kChunks) % kHyUsers, q = o % S::kChunks;
+        v[j] = int4{0, 0, 0, 0};
+        if (b0 + r < B) v[j] = *reinterpret_cast<const int4*>((m ? Ut : Ua) + (int64_t)(b0 + r) * (DK * 2) + 16 * q);
+      }
+#pragma unroll
+      for (int j = 0; j < BAT; ++j) {
+        const int o = threadIdx.x + (q0 + j) * kHyThreads;
+        const int m = o / (kHyUsers * S::kChunks);
+        const int r = (o / S::kChunks) % kHyUsers, q = o % S::kChunks;
+        *reinterpret_cast<int4*>(us + (m * kHyUsers + r) * S::kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v[j];
+      }
     }
   }
   // this lane's users: ub + 16 u (u < NU)

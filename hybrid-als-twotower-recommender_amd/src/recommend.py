@@ -69,7 +69,7 @@ class ShardedRecommender:
     here; pass V_local (the shard's ALS item factor rows) instead of Vt_local."""
 
     def __init__(self, U, Vt_local, item_vecs_local, item_offset, k, world=1, rank=0, group=None, ops=None,
-                 precision="exact", V_local=None):
+                 precision="exact", V_local=None, fused=False):
         self.U = U                          # [n_users, kp] ALS user factors (replicated)
         self.Vt = Vt_local                  # [kp, ld] transposed ALS item factors of this shard
         self.iv = item_vecs_local           # [n_local, d] two-tower item vectors of this shard
@@ -86,7 +86,11 @@ class ShardedRecommender:
                 raise ValueError("precision='bf16' needs V_local (ALS item factor rows of the shard)")
             # one width for both models so the fused kernel can run them together
             self.dk = max(64, _hrec.dot_dk(V_local.shape[1]), _hrec.dot_dk(item_vecs_local.shape[1]))
-            self.fused = hasattr(self.ops, "hybrid_topk")
+            # fused kernels: no score matrix in HBM (bit-identical results);
+            # off by default — at c5's 1e5-item shards the two score matrices
+            # are cheap and the fused path's per-batch overflow check (a host
+            # sync) costs more than it saves
+            self.fused = bool(fused) and hasattr(self.ops, "hybrid_topk")
             self.V_op = self.ops.operand(V_local, torch.bfloat16, self.dk)
             self.iv_op = self.ops.operand(item_vecs_local, torch.bfloat16, self.dk)
 

@@ -213,7 +213,7 @@ def _hybrid_run(world, rank, U, V, uv, iv, k, group=None, precision="exact"):
                              torch.from_numpy(iv[i0: i0 + per]), i0, k, world=world, rank=rank, group=group,
                              ops=_CpuFusedOps if precision == "bf16-fused" else _CpuOps,
                              precision="bf16" if precision.startswith("bf16") else precision,
-                             V_local=torch.from_numpy(np.ascontiguousarray(Vl)))
+                             V_local=torch.from_numpy(np.ascontiguousarray(Vl)), fused=precision == "bf16-fused")
     rows = torch.tensor([0, 3, 5, 7, 11], dtype=torch.int64)
     return [t.numpy() for t in rec.recommend(rows, torch.from_numpy(uv), True, 7)]
 

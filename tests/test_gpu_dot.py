@@ -212,7 +212,7 @@ def test_hybrid_fused_equals_unfused(device, n_users, n_items, k, d, B, wins):
     uv = (rng.normal(size=(B, d)) / 8).astype(np.float32)
     rows = torch.as_tensor(rng.integers(0, n_users, B), dtype=torch.int64, device=device)
     rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, k,
-                             precision="bf16", V_local=torch.from_numpy(V).to(device))
+                             precision="bf16", V_local=torch.from_numpy(V).to(device), fused=True)
     assert rec.fused
     fi, fv = rec.recommend(rows, torch.from_numpy(uv).to(device), wins, 7)
     rec.fused = False
@@ -240,7 +240,7 @@ def test_hybrid_fused_minmax_and_overflow(device):
     iv = np.tile(rng.normal(size=(1, 64)).astype(np.float32), (30000, 1))
     U = rng.normal(size=(10, 64)).astype(np.float32)
     rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, 64,
-                             precision="bf16", V_local=torch.from_numpy(V).to(device))
+                             precision="bf16", V_local=torch.from_numpy(V).to(device), fused=True)
     rows = torch.arange(4, dtype=torch.int64, device=device)
     i, v = rec.recommend(rows, torch.from_numpy(U[:4]).to(device), False, 5)
     np.testing.assert_array_equal(i.cpu().numpy(), np.tile(np.arange(5), (4, 1)))
