@@ -227,11 +227,15 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
       // (zero fragments) are rejected there.
       uint64_t any = 0;
 #pragma unroll
-      for (int u = 0; u < NU; ++u)
+      for (int u = 0; u < NU; ++u) {
+        float mx = acc[u][0][0];
 #pragma unroll
         for (int t = 0; t < NI; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) any |= __ballot(acc[u][t][r] >= th[u]);
+          for (int r = 0; r < 4; ++r)
+            if (t || r) mx = fmaxf(mx, acc[u][t][r]);
+        any |= __ballot(mx >= th[u]);
+      }
       if (any) {
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
@@ -284,8 +288,11 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ in, int64_t n, uint
 // of the 128-user tiling were the stall). During the last chunk each item
 // fragment is refilled with the next tile's as soon as its step has used it
 // the last time, so the loads have a whole chunk plus a step to land.
+#ifndef HREC_RES_NU
+#define HREC_RES_NU 4
+#endif
 constexpr int kResUserBytes = 128 * 1024;
-constexpr int kResNU = 4;  // user tiles per chunk (64 users): leaves VGPRs for the prefetches
+constexpr int kResNU = HREC_RES_NU;  // user tiles per chunk (64 users): leaves VGPRs for the prefetches
 
 template <bool BF16, int DK, bool FILTER>
 __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
@@ -390,6 +397,12 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
       for (int u = 0; u < NU; ++u)
 #pragma unroll
         for (int t = 0; t < NI; ++t) acc[u][t] = dot_f4{0.f, 0.f, 0.f, 0.f};
+      float th[NU];  // this chunk's bounds, read before the MFMAs (latency hidden)
+      if constexpr (FILTER) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+          th[u] = CU * ch + 16 * u + c < UB ? ths[CU * ch + 16 * u + c] : __builtin_nanf("");
+      }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         DotFrag a[NU];
@@ -435,16 +448,19 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
           }
         }
       } else {
-        float th[NU];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) th[u] = CU * ch + 16 * u + c < UB ? ths[CU * ch + 16 * u + c] : __builtin_nanf("");
+        // one compare per user tile: the lane's max over its 8 items (fmaxf
+        // drops NaN scores, which never pass anyway; a NaN bound never passes)
         uint64_t any = 0;
 #pragma unroll
-        for (int u = 0; u < NU; ++u)
+        for (int u = 0; u < NU; ++u) {
+          float mx = acc[u][0][0];
 #pragma unroll
           for (int t = 0; t < NI; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) any |= __ballot(acc[u][t][r] >= th[u]);
+            for (int r = 0; r < 4; ++r)
+              if (t || r) mx = fmaxf(mx, acc[u][t][r]);
+          any |= __ballot(mx >= th[u]);
+        }
         if (any) {
 #pragma unroll
           for (int u = 0; u < NU; ++u) {
