@@ -47,6 +47,27 @@
 
 namespace hrec {
 
+#ifdef HREC_WIDE_STAMPS
+// Diagnostic build only: per-phase cycle sums (s_memtime) of wave 0 of every
+// block: [0] Gramian, [1] panel write + barrier, [2] panels, [3] trailing
+// updates (+ barrier), [4] substitutions.
+__device__ unsigned long long g_wide_stamps[8];
+#define WSTAMP_DECL unsigned long long _ws_prev = 0
+#define WSTAMP(i)                                                                              \
+  do {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    if (threadIdx.x == 0 && (i) >= 0) atomicAdd(&g_wide_stamps[(i) >= 0 ? (i) : 0], _t - _ws_prev); \
+    _ws_prev = _t;                                                                             \
+  } while (0)
+#else
+#define WSTAMP_DECL
+#define WSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 typedef double wd4 __attribute__((ext_vector_type(4)));
 
 // Waves per row: 8 for kp <= 128; 16 for kp >= 192, so that each wave's
@@ -124,6 +145,8 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   const int64_t n = end - beg;
 
   // ---------------------------------------------------------------- phase 1
+  WSTAMP_DECL;
+  WSTAMP(-1);
   wd4 acc[S::SLOTS];
   int pij[S::SLOTS];  // (I | J << 8) of each slot's tile pair, -1 = none (wave-uniform)
 #pragma unroll
@@ -240,6 +263,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   }
 #endif
 
+  WSTAMP(0);
   // ---------------------------------------------------------------- phase 2
 #pragma unroll 1
   for (int J = 0; J < NT; ++J) {
@@ -256,6 +280,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       }
     }
     __syncthreads();
+    WSTAMP(1);
     // (b) panel: wave w < n_act takes the diagonal block (lanes 0..15,
     //     redundantly) and 48 columns beyond it (lanes 16..63)
     const int rest = KP - 16 * (J + 1);
@@ -272,16 +297,20 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       double a[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) a[m] = pc[m * LD];
+      if (lane < 32) tri[w][16 + lane + 16 * (lane >> 4)] = 0.0;  // entries 16..31 of both buffers
+      wave_sync_lds();
 #pragma unroll 1
       for (int i = 0; i < 16; ++i) {
-        double ai = a[0];
-#pragma unroll
-        for (int m = 1; m < 16; ++m) ai = i == m ? a[m] : ai;
+        // a[] is kept shifted: a[0] is always the column's row 16 J + i, so
+        // the rolled loop indexes registers at compile time only
+        const double ai = a[0];
         const double piv = wbcast(ai, i);  // lane i: column 16 J + i, row 16 J + i
         const double r0 = __builtin_amdgcn_rcp(piv);
         const double rp = fma(r0, fma(-piv, r0, 1.0), r0);
         const double ut = ai * rp;  // U[16 J + i][c]
-        double* cbw = tri[w] + 16 * (i & 1);  // pivot row inside the diagonal block (alternating)
+        // pivot row inside the diagonal block: 32-entry buffers whose upper
+        // half stays zero, so the shifted reads below never leave them
+        double* cbw = tri[w] + 32 * (i & 1);
         if (lane < 16) cbw[lane] = ai;
         if (own && lane >= 16) P[i * LD + c] = ut;  // the panel column's row i becomes U
         if (w == 0 && lane < 16) udg[i * 17 + lane] = lane > i ? ut : (lane == i ? 1.0 : 0.0);
@@ -290,15 +319,15 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
           rdsh[16 * J + i] = rp;
         }
         wave_sync_lds();
+        double u[15];
 #pragma unroll
-        for (int m = 0; m < 16; m += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(cbw + m);
-          if (m > i) a[m] = fma(-u.x, ut, a[m]);
-          if (m + 1 > i) a[m + 1] = fma(-u.y, ut, a[m + 1]);
-        }
+        for (int j = 0; j < 15; ++j) u[j] = cbw[i + 1 + j];
+#pragma unroll
+        for (int j = 0; j < 15; ++j) a[j] = fma(-u[j], ut, a[j + 1]);
       }
     }
     __syncthreads();
+    WSTAMP(2);
     // (c) trailing update A_KM -= U_JK^T D_J U_JM; owners of row J take U_JK.
     // Slot rows K grow with the slot index, so the tiles still to update
     // (K > J) are a suffix of the slots: walk it from the end, reading the
@@ -360,6 +389,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     return;
   }
 #endif
+  WSTAMP(3);
   // ---------------------------------------------------------------- phase 3
   // The owner of diagonal tile (J, J) stages it in its scratch: T[q][c].
   auto stage_diag = [&](int s) {
@@ -458,11 +488,23 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     __syncthreads();
   }
   if (tid < KP) out[tid] = (float)xsh[tid];
+  WSTAMP(4);
 }
 
 }  // namespace hrec
 
 using namespace hrec;
+
+#ifdef HREC_WIDE_STAMPS
+extern "C" int hrec_debug_wide_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wide_stamps), sizeof(g_wide_stamps)) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wide_stamps), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
 
 int hrec_als_half_sweep_wide(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
                              const float* src_factors, int64_t n_src, int k, int kp, double reg_param,
