@@ -325,9 +325,37 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 #pragma unroll
         for (int j = 0; j < 15; ++j) a[j] = fma(-u[j], ut, a[j + 1]);
       }
+      // forward substitution of block J (U_JJ^T w_J = b_J, b_J final: every
+      // earlier block already subtracted its part) by wave 0, which has just
+      // written U_JJ to udg; v_J = w_J / D
+      if (w == 0) {
+        wave_sync_lds();
+        double tc[16];  // column `lane` of U_JJ
+#pragma unroll
+        for (int q = 0; q < 16; ++q) tc[q] = udg[q * 17 + col];
+        double bi = lane < 16 ? bsh[16 * J + lane] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const double wq = wbcast(bi, q);
+          if (lane > q && lane < 16) bi = fma(-tc[q], wq, bi);
+        }
+        if (lane < 16) {
+          xsh[16 * J + lane] = bi;                        // w_J
+          bsh[16 * J + lane] = bi * rdsh[16 * J + lane];  // v_J
+        }
+      }
     }
     __syncthreads();
     WSTAMP(2);
+    // b_K -= U_JK^T w_J for every later column, one thread per column (the
+    // panel still holds U_J); runs beside the trailing MFMAs below
+    if (tid < KP - 16 * (J + 1)) {
+      const int cc = 16 * (J + 1) + tid;
+      double part = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) part = fma(P[q * LD + cc], xsh[16 * J + q], part);
+      bsh[cc] -= part;
+    }
     // (c) trailing update A_KM -= U_JK^T D_J U_JM; owners of row J take U_JK.
     // Slot rows K grow with the slot index, so the tiles still to update
     // (K > J) are a suffix of the slots: walk it from the end, reading the
@@ -398,49 +426,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     for (int r = 0; r < 4; ++r) T[(sub + 4 * r) * 17 + col] = acc[s][r];
     wave_sync_lds();
   };
-  // forward: U^T w = b, then v = w / D (in bsh)
-#pragma unroll 1
-  for (int J = 0; J < NT; ++J) {
-#pragma unroll
-    for (int s = 0; s < S::SLOTS; ++s) {
-      if (pij[s] >= 0) {
-        const int I = pij[s] & 255, K = pij[s] >> 8;
-        if (I == J && K == J) {
-          stage_diag(s);
-          const double* T = tri[w];
-          double tc[16];  // column `lane` of U_JJ
-#pragma unroll
-          for (int q = 0; q < 16; ++q) tc[q] = T[q * 17 + col];
-          double bi = lane < 16 ? bsh[16 * J + lane] : 0.0;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const double wq = wbcast(bi, q);
-            if (lane > q && lane < 16) bi = fma(-tc[q], wq, bi);
-          }
-          if (lane < 16) {
-            xsh[16 * J + lane] = bi;                          // w_J
-            bsh[16 * J + lane] = bi * rdsh[16 * J + lane];    // v_J = w_J / D
-          }
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < S::SLOTS; ++s) {
-      if (pij[s] >= 0) {
-        const int I = pij[s] & 255, K = pij[s] >> 8;
-        if (I == J && K > J) {  // b_K -= U_JK^T w_J
-          double part = 0.0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) part = fma(acc[s][r], xsh[16 * J + sub + 4 * r], part);
-          part += __shfl_xor(part, 16, kWave);
-          part += __shfl_xor(part, 32, kWave);
-          if (lane < 16) bsh[16 * K + lane] -= part;
-        }
-      }
-    }
-    __syncthreads();
-  }
+  // (the forward substitution ran inside the factorisation: bsh holds v)
   // backward: U x = v (v in bsh, x -> xsh)
 #pragma unroll 1
   for (int M = NT - 1; M >= 0; --M) {
