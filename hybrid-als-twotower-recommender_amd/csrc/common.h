@@ -30,11 +30,13 @@ int offset_ids(int64_t* idx, int64_t n, int64_t off, hipStream_t s);
 
 // Stable descending top-k of n_rows rows (score.hip): larger first, equal
 // values -> smaller original index first (src_idx maps positions to original
-// indices; entries with index -1 are skipped). Workspace: topk_ws_bytes.
+// indices; entries with index -1 are skipped; row_n, if given, bounds row r
+// to its first min(n, row_n[r]) entries). Workspace: topk_ws_bytes.
 size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem);
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
-              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr);
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr,
+              const int* row_n = nullptr);
 
 // splitmix64 finaliser; host and device identical (integer only).
 __host__ __device__ inline uint64_t mix64(uint64_t z) {

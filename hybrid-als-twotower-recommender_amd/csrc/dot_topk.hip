@@ -724,8 +724,7 @@ extern "C" int hrec_dot_topk(const void* user_vec, int n_users, const void* item
       thr_stride = kk;
     }
     // 2) fused score + survivor filter over every item
-    if (hipMemsetAsync(ci, 0xff, (size_t)n_users * cap * 8, s) != hipSuccess ||
-        hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
+    if (hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
       return check_launch("dot_topk: memset");
     rc = dot_launch<true>(user_vec, n_users, item_vec, n_items, n_items, 1, dk, dtype, nullptr, 0, thr, thr_stride, (int)cap,
                           cv, ci, cn, 0, s);
@@ -734,7 +733,7 @@ extern "C" int hrec_dot_topk(const void* user_vec, int n_users, const void* item
     rc = check_launch("dot_overflow_kernel");
     if (rc) return rc;
     // 3) exact stable top-k of the survivors (item index breaks ties)
-    rc = topk_rows<float>(cv, n_users, cap, cap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
+    rc = topk_rows<float>(cv, n_users, cap, cap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci, cn);
   }
   if (rc) return rc;
   return offset_ids(out_idx, (int64_t)n_users * kk, idx_offset, s);

@@ -498,8 +498,7 @@ extern "C" int hrec_hybrid_topk(const void* als_user, const void* tt_user, int n
       thr = sv + (kk - 1);
       thr_stride = kk;
     }
-    if (hipMemsetAsync(ci, 0xff, (size_t)n_users * cap * 8, s) != hipSuccess ||
-        hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
+    if (hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
       return check_launch("hybrid_topk: memset");
     rc = hy_launch<kHyFilter>(als_user, tt_user, n_users, als_item, tt_item, n_items, n_items, 1, dk, als_mm, tt_mm,
                               w0, w1, nullptr, nullptr, 0, thr, thr_stride, (int)cap, cv, ci, cn, 0, s);
@@ -507,7 +506,7 @@ extern "C" int hrec_hybrid_topk(const void* als_user, const void* tt_user, int n
     hipLaunchKernelGGL(hy_overflow_kernel, dim3(64), dim3(256), 0, s, cn, n_users, (int)cap, overflow);
     rc = check_launch("hy_overflow_kernel");
     if (rc) return rc;
-    rc = topk_rows<double>(cv, n_users, cap, cap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
+    rc = topk_rows<double>(cv, n_users, cap, cap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci, cn);
   }
   if (rc || idx_offset == 0) return rc;
   // shift the (non-empty) ids of this item shard

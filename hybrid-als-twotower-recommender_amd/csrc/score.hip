@@ -65,6 +65,9 @@ __global__ __launch_bounds__(256) void als_score_kernel(const float* __restrict_
 // FILTER: instead of writing the scores, append (score, item) pairs with
 // score >= thr[b] to a per-user candidate list (wave-aggregated atomics).
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+// buffer_load_dwordx2 ... offen (raw: base + voffset, range-checked)
+__device__ f2v rbuf_load_f2(i4v rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
 
 template <int UB, bool FILTER>
 __global__ __launch_bounds__(256) void als_score_fast_kernel(
@@ -73,42 +76,85 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
     const float* __restrict__ thr, int thr_stride, int cap, float* __restrict__ cand_v,
     int64_t* __restrict__ cand_i, int* __restrict__ cand_n) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) float us[kScoreKMax][UB];
+  __shared__ __attribute__((aligned(16))) float us[kScoreKMax + 1][UB];  // + the row read ahead past the end
   __shared__ int uok[UB];
   // grid: x = user group (fastest-varying), y = 1024-item slice, so the
   // blocks of one item slice are dispatched back to back and share it in L2
   const int b0 = blockIdx.x * UB;
+  const int64_t j0 = (int64_t)blockIdx.y * 1024 + 2 * threadIdx.x;
+  const int64_t j1 = j0 + 512;
+  // Rank-step c reads row c of Vt through a raw buffer resource spanning
+  // [0, ld) of that row (rows c >= k span nothing): columns past the row end
+  // read as zero without a branch, and rank steps c + 1 ... c + P - 1 are
+  // already in flight while step c computes. ld is even, so both items of a
+  // pair are in range together; items in [n_items, ld) are dropped below.
+  constexpr int P = 4;
+  const uint64_t vbase = (uint64_t)Vt;
+  const int rec = (int)(ld * 4);
+  auto rsrc_of = [&](int c) {
+    const uint64_t a = vbase + (uint64_t)c * (uint64_t)ld * 4u;
+    i4v r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    r.z = __builtin_amdgcn_readfirstlane(c < k ? rec : 0);
+    r.w = 0x00020000;
+    return r;
+  };
+  const int o0 = (int)(j0 * 4), o1 = (int)(j1 * 4);
+  f2v r0[P], r1[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) {  // issued before the user staging: independent of it
+    const i4v rs = rsrc_of(q);
+    r0[q] = rbuf_load_f2(rs, o0, 0, 0);
+    r1[q] = rbuf_load_f2(rs, o1, 0, 0);
+  }
   for (int t = threadIdx.x; t < UB * kp; t += blockDim.x) {
     const int b = t / kp, c = t % kp;
     const int64_t ur = (b0 + b < n_users) ? user_rows[b0 + b] : -1;
-    us[c][b] = ur >= 0 ? U[ur * kp + c] : 0.f;
+    us[c][b] = (ur >= 0 && c < k) ? U[ur * kp + c] : 0.f;
     if (c == 0) uok[b] = ur >= 0;
   }
+  float tb[UB];  // survivor thresholds, read ahead of the loop
+#pragma unroll
+  for (int b = 0; b < UB; ++b) tb[b] = (FILTER && b0 + b < n_users) ? thr[(int64_t)(b0 + b) * thr_stride] : 0.f;
   __syncthreads();
-  const int64_t j0 = (int64_t)blockIdx.y * 1024 + 2 * threadIdx.x;
-  const int64_t j1 = j0 + 512;
   f2v acc0[UB], acc1[UB];
 #pragma unroll
   for (int b = 0; b < UB; ++b) {
     acc0[b] = f2v{0.f, 0.f};
     acc1[b] = f2v{0.f, 0.f};
   }
-  const bool in0 = j0 < ld, in1 = j1 < ld;
-  for (int c = 0; c < k; ++c) {
-    const float* vr = Vt + (int64_t)c * ld;
-    const f2v v0 = in0 ? *reinterpret_cast<const f2v*>(vr + j0) : f2v{0.f, 0.f};
-    const f2v v1 = in1 ? *reinterpret_cast<const f2v*>(vr + j1) : f2v{0.f, 0.f};
+  // user values for rank step c + 1 are read from LDS while step c computes
+  // (two register sets, alternating with the parity of the unrolled step)
+  float4 ub[2][UB / 4];
 #pragma unroll
-    for (int b = 0; b < UB; b += 4) {
-      const float4 u4 = *reinterpret_cast<const float4*>(&us[c][b]);
-      const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
+  for (int b = 0; b < UB; b += 4) ub[0][b / 4] = *reinterpret_cast<const float4*>(&us[0][b]);
+  for (int c0 = 0; c0 < k; c0 += P) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f2v us2 = f2v{uu[q], uu[q]};
-        const f2v p0 = us2 * v0;
-        const f2v p1 = us2 * v1;
-        acc0[b + q] = acc0[b + q] + p0;
-        acc1[b + q] = acc1[b + q] + p1;
+    for (int q = 0; q < P; ++q) {
+      const int c = c0 + q;  // may pass k by < P: zero factors there (us staged 0)
+#pragma unroll
+      for (int b = 0; b < UB; b += 4) ub[(q + 1) & 1][b / 4] = *reinterpret_cast<const float4*>(&us[c + 1][b]);
+      {
+        const f2v v0 = r0[q], v1 = r1[q];
+#pragma unroll
+        for (int b = 0; b < UB; b += 4) {
+          const float4 u4 = ub[q & 1][b / 4];
+          const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f2v us2 = f2v{uu[e], uu[e]};
+            const f2v p0 = us2 * v0;
+            const f2v p1 = us2 * v1;
+            acc0[b + e] = acc0[b + e] + p0;
+            acc1[b + e] = acc1[b + e] + p1;
+          }
+        }
+        // refill the slot only once its values are dead, so the load lands in
+        // the slot's own registers (no copy waiting on it at the back edge)
+        const i4v rs = rsrc_of(c + P);
+        r0[q] = rbuf_load_f2(rs, o0, 0, 0);
+        r1[q] = rbuf_load_f2(rs, o1, 0, 0);
       }
     }
   }
@@ -129,9 +175,14 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       if (b0 + b >= n_users || !uok[b]) continue;  // block-uniform
-      const float t = thr[(int64_t)(b0 + b) * thr_stride];
+      const float t = tb[b];
       const float sv[4] = {acc0[b].x, acc0[b].y, acc1[b].x, acc1[b].y};
       const int64_t sj[4] = {j0, j0 + 1, j1, j1 + 1};
+      // one compare per user in the common case: nothing of this wave passes
+      // (NaN scores fail >= like the per-item test; columns >= n_items may
+      // pass here and are dropped by the exact test below)
+      const float mx = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
+      if (__ballot(mx >= t) == 0) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool pass = sj[e] < n_items && sv[e] >= t;
@@ -200,6 +251,7 @@ constexpr int kTopkSeg = kTopkBlock * kTopkPer;
 template <typename T>
 __global__ __launch_bounds__(kTopkBlock) void topk_segment_kernel(const T* __restrict__ vals,
                                                                   const int64_t* __restrict__ src_idx,
+                                                                  const int* __restrict__ row_n,
                                                                   int64_t n, int64_t row_stride, int kk,
                                                                   T* __restrict__ out_v,
                                                                   int64_t* __restrict__ out_i,
@@ -210,6 +262,10 @@ __global__ __launch_bounds__(kTopkBlock) void topk_segment_kernel(const T* __res
   const int64_t seg0 = (int64_t)blockIdx.x * kTopkSeg;
   const T* __restrict__ rv = vals + row * row_stride;
   const int64_t* __restrict__ ri = src_idx ? src_idx + row * row_stride : nullptr;
+  if (row_n) {
+    const int64_t rn = row_n[row];
+    n = rn < n ? rn : n;
+  }
   T v[kTopkPer];
   int64_t id[kTopkPer];
 #pragma unroll
@@ -252,6 +308,112 @@ __global__ __launch_bounds__(kTopkBlock) void topk_segment_kernel(const T* __res
       if (id[e] == wi) id[e] = -1;
     __syncthreads();
   }
+}
+
+// Small top-k (kk <= 16) of rows of at most kTopkWaveMax elements: one wave
+// per row. Each lane streams its elements (p = lane, lane + 64, ...) through a
+// sorted register list of its KK best (a compare-exchange chain, no
+// branches), then kk rounds of wave arg-best over the list heads, the winner
+// popping its head. Same order, same output as topk_segment_kernel, without
+// its block barriers.
+constexpr int kTopkWaveMax = 8192;
+
+template <typename T, int KK>
+__global__ __launch_bounds__(256) void topk_wave_kernel(const T* __restrict__ vals,
+                                                        const int64_t* __restrict__ src_idx,
+                                                        const int* __restrict__ row_n, int64_t n_rows, int64_t n,
+                                                        int64_t row_stride, int kk, T* __restrict__ out_v,
+                                                        int64_t* __restrict__ out_i, int64_t out_row_stride) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;  // wave-uniform
+  if (row_n) {
+    const int64_t rn = row_n[row];
+    n = rn < n ? rn : n;
+  }
+  const T* __restrict__ rv = vals + row * row_stride;
+  const int64_t* __restrict__ ri = src_idx ? src_idx + row * row_stride : nullptr;
+  T lv[KK];
+  int64_t li[KK];
+#pragma unroll
+  for (int j = 0; j < KK; ++j) {
+    lv[j] = (T)0;
+    li[j] = INT64_MAX;  // empty slot: loses to every element
+  }
+  constexpr int B = 8;  // loads in flight per lane before the first insertion
+  for (int64_t p0 = lane; p0 < n; p0 += 64 * B) {
+    T bv[B];
+    int64_t bi[B];
+#pragma unroll
+    for (int e = 0; e < B; ++e) {
+      const int64_t p = p0 + 64 * e;
+      const bool in = p < n;
+      bv[e] = in ? rv[p] : (T)0;
+      bi[e] = in ? (ri ? ri[p] : p) : -1;
+    }
+#pragma unroll
+    for (int e = 0; e < B; ++e) {
+      T xv = bv[e];
+      int64_t xi = bi[e] < 0 ? INT64_MAX : bi[e];  // absent: an empty slot, inserts as a no-op
+#pragma unroll
+      for (int j = 0; j < KK; ++j) {
+        const bool sw = xi != INT64_MAX && (li[j] == INT64_MAX || better(xv, xi, lv[j], li[j]));
+        const T tv = lv[j];
+        const int64_t ti = li[j];
+        lv[j] = sw ? xv : tv;
+        li[j] = sw ? xi : ti;
+        xv = sw ? tv : xv;
+        xi = sw ? ti : xi;
+      }
+    }
+  }
+  for (int r = 0; r < kk; ++r) {
+    const KV<T> w = wave_best(KV<T>{lv[0], li[0]});
+    if (lane == 0) {
+      const int64_t o = row * out_row_stride + r;
+      out_v[o] = w.i == INT64_MAX ? (T)0 : w.v;
+      out_i[o] = w.i == INT64_MAX ? -1 : w.i;
+    }
+    if (w.i != INT64_MAX && li[0] == w.i) {  // the (unique) owner pops its head
+#pragma unroll
+      for (int j = 0; j + 1 < KK; ++j) {
+        lv[j] = lv[j + 1];
+        li[j] = li[j + 1];
+      }
+      li[KK - 1] = INT64_MAX;
+    }
+  }
+}
+
+// Survivor threshold from a sample row (one wave per row, kk <= 64): the
+// kk-th largest of the 64 lane maxima (lane l: elements l, l + 64, ...). Those
+// are kk distinct sample elements, so the value bounds the row's kk-th best
+// from below, which is all the filter needs (the final top-k is exact). NaN
+// elements are ignored (fmaxf); a row without a number yields -inf.
+__global__ __launch_bounds__(256) void sample_threshold_kernel(const float* __restrict__ vals, int64_t n_rows,
+                                                               int64_t n, int kk, float* __restrict__ thr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;  // wave-uniform
+  const float* __restrict__ rv = vals + row * n;
+  float m = -__builtin_inff();
+  int64_t p = lane;
+  for (; p + 64 * 3 < n; p += 64 * 4) {  // four loads in flight per lane
+    const float a = rv[p], b = rv[p + 64], c = rv[p + 128], d = rv[p + 192];
+    m = fmaxf(m, fmaxf(fmaxf(a, b), fmaxf(c, d)));
+  }
+  for (; p < n; p += 64) m = fmaxf(m, rv[p]);
+  float t = -__builtin_inff();
+  for (int r = 0; r < kk; ++r) {
+    float w = m;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) w = fmaxf(w, __shfl_xor(w, off, kWave));
+    t = w;
+    // retire one lane holding the maximum (the lowest such lane)
+    const uint64_t hold = __ballot(m == w);
+    if (hold && lane == __builtin_ctzll(hold)) m = -__builtin_inff();
+  }
+  if (lane == 0) thr[row] = t;
 }
 
 // ---------------------------------------------------------------- fusion
@@ -658,7 +820,7 @@ size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
 namespace hrec {
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
-              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx) {
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx, const int* row_n) {
   // Multi-pass: segments -> candidates (kk per segment) -> ... -> one segment.
   const T* cur_v = vals;
   const int64_t* cur_i = src_idx;
@@ -667,9 +829,25 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
   size_t used = 0;
   while (true) {
     const int64_t segs = (m + kTopkSeg - 1) / kTopkSeg;
-    if (segs <= 1) {
+    if (segs <= 1 || (m <= kTopkWaveMax && kk <= 16)) {
+      if (kk <= 16 && m <= kTopkWaveMax) {
+        const dim3 g((unsigned)((n_rows + 3) / 4));
+#define HREC_TOPK_WAVE(KK)                                                                                    \
+  hipLaunchKernelGGL((topk_wave_kernel<T, KK>), g, dim3(256), 0, s, cur_v, cur_i, row_n, n_rows, m, stride, kk, \
+                     out_val, out_idx, (int64_t)kk)
+        if (kk <= 2)
+          HREC_TOPK_WAVE(2);
+        else if (kk <= 4)
+          HREC_TOPK_WAVE(4);
+        else if (kk <= 8)
+          HREC_TOPK_WAVE(8);
+        else
+          HREC_TOPK_WAVE(16);
+#undef HREC_TOPK_WAVE
+        return check_launch("topk_wave_kernel");
+      }
       hipLaunchKernelGGL((topk_segment_kernel<T>), dim3(1, (unsigned)n_rows), dim3(kTopkBlock), 0, s, cur_v,
-                         cur_i, m, stride, kk, out_val, out_idx, (int64_t)kk);
+                         cur_i, row_n, m, stride, kk, out_val, out_idx, (int64_t)kk);
       return check_launch("topk_segment_kernel");
     }
     const int64_t cand = segs * kk;
@@ -682,19 +860,20 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
     T* nv = (T*)(w + used + ib);
     used += vb + ib;
     hipLaunchKernelGGL((topk_segment_kernel<T>), dim3((unsigned)segs, (unsigned)n_rows), dim3(kTopkBlock), 0, s,
-                       cur_v, cur_i, m, stride, kk, nv, ni, cand);
+                       cur_v, cur_i, row_n, m, stride, kk, nv, ni, cand);
     int rc = check_launch("topk_segment_kernel");
     if (rc) return rc;
     cur_v = nv;
     cur_i = ni;
+    row_n = nullptr;  // later passes: every row holds segs * kk entries
     m = cand;
     stride = cand;
   }
 }
 template int topk_rows<float>(const float*, int64_t, int64_t, int64_t, int, int64_t*, float*, void*, size_t,
-                              hipStream_t, const int64_t*);
+                              hipStream_t, const int64_t*, const int*);
 template int topk_rows<double>(const double*, int64_t, int64_t, int64_t, int, int64_t*, double*, void*, size_t,
-                               hipStream_t, const int64_t*);
+                               hipStream_t, const int64_t*, const int*);
 }  // namespace hrec
 
 extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_rows, int n_users,
@@ -707,7 +886,8 @@ extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_row
   HREC_REQUIRE(user_factors && user_rows && item_factors_t && out, "als_score: null pointer");
   HREC_REQUIRE(item_rows != nullptr || n_items <= ld_items, "als_score: n_items > ld_items");
   constexpr int UB = 16;
-  if (item_rows == nullptr && ld_items % 2 == 0 && (reinterpret_cast<uintptr_t>(item_factors_t) & 7) == 0) {
+  if (item_rows == nullptr && ld_items % 2 == 0 && ld_items < ((int64_t)1 << 29) &&
+      (reinterpret_cast<uintptr_t>(item_factors_t) & 7) == 0) {
     // every item in order: the packed-f32 kernel (same JVM-exact chain)
     const dim3 grid((unsigned)((n_users + UB - 1) / UB), (unsigned)((n_items + 1023) / 1024));
     hipLaunchKernelGGL((als_score_fast_kernel<UB, false>), grid, dim3(256), 0, as_stream(stream), user_factors,
@@ -830,7 +1010,8 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
   HREC_REQUIRE(hrec_factor_ld_ok(kp), "als_score_topk: kp must be 16, 32, 64, 96, 128, 192 or 256");
   HREC_REQUIRE(k >= 1 && k <= kp, "als_score_topk: need 1 <= k <= kp");
   HREC_REQUIRE(n_users >= 0 && n_users < 65536 && n_items >= 0, "als_score_topk: bad shape");
-  HREC_REQUIRE(ld_items >= n_items && ld_items % 4 == 0, "als_score_topk: ld_items must be >= n_items and %% 4");
+  HREC_REQUIRE(ld_items >= n_items && ld_items % 4 == 0 && ld_items < ((int64_t)1 << 29),
+               "als_score_topk: ld_items must be >= n_items, %% 4 and < 2^29");
   HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "als_score_topk: top_k must be in [1, 1024]");
   if (n_users == 0 || n_items == 0) return HREC_OK;
   HREC_REQUIRE(user_factors && user_rows && item_factors_t && out_idx && out_val && overflow && workspace,
@@ -866,22 +1047,31 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
                      nullptr, nullptr, nullptr);
   int rc = check_launch("als_score_fast_kernel(sample)");
   if (rc) return rc;
-  rc = topk_rows<float>(samp, n_users, S, S, kk, si, sv, tws, (size_t)1 << 62, s);
+  const float* thr = sv + (kk - 1);
+  int thr_stride = kk;
+  if (kk <= 64) {  // a lower bound suffices: the 64 lane maxima's kk-th
+    hipLaunchKernelGGL(sample_threshold_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, samp,
+                       (int64_t)n_users, S, kk, sv);
+    rc = check_launch("sample_threshold_kernel");
+    thr = sv;
+    thr_stride = 1;
+  } else {
+    rc = topk_rows<float>(samp, n_users, S, S, kk, si, sv, tws, (size_t)1 << 62, s);
+  }
   if (rc) return rc;
   // 2) fused score + filter over all items
-  if (hipMemsetAsync(ci, 0xff, (size_t)n_users * kCap * 8, s) != hipSuccess ||
-      hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
+  if (hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
     return check_launch("score_topk memset");
   hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, true>), dim3(gy, (unsigned)((n_items + 1023) / 1024)), blk, 0,
                      s, user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, nullptr,
-                     sv + (kk - 1), kk, kCap, cv, ci, cn);
+                     thr, thr_stride, kCap, cv, ci, cn);
   rc = check_launch("als_score_fast_kernel(filter)");
   if (rc) return rc;
   hipLaunchKernelGGL(cand_overflow_kernel, dim3(64), dim3(256), 0, s, cn, n_users, kCap, overflow);
   rc = check_launch("cand_overflow_kernel");
   if (rc) return rc;
   // 3) exact stable top-k over the candidates (original item index breaks ties)
-  return topk_rows<float>(cv, n_users, kCap, kCap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci);
+  return topk_rows<float>(cv, n_users, kCap, kCap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci, cn);
 }
 
 extern "C" int hrec_rows_minmax_f32(const float* x, int64_t n_rows, int64_t n, int64_t ld, float* out, void* stream) {

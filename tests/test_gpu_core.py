@@ -199,6 +199,30 @@ def test_topk_stable(device, n, k, dtype):
         assert idx[r].cpu().tolist() == exp
 
 
+@pytest.mark.parametrize("n", [1, 64, 65, 2048, 8192, 8193])
+@pytest.mark.parametrize("k", [1, 2, 3, 8, 16, 17])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_topk_wave_path_ties_nan(device, n, k, dtype):
+    """kk <= 16 over rows of <= 8192 run the wave-per-row kernel (csrc/score.hip
+    topk_wave_kernel); kk = 17 and n = 8193 the block kernel: same order
+    (larger first, ties -> smaller index, NaN last) either way."""
+    h = _hrec()
+    rng = np.random.default_rng(7 * n + k)
+    vals = np.round(rng.normal(size=(9, n)), 1)
+    vals[1, ::3] = np.nan
+    vals[2, :] = 0.5  # one big tie
+    vals[3, :] = np.nan
+    npdt = np.float32 if dtype == torch.float32 else np.float64
+    vals = vals.astype(npdt)
+    idx, v = h.topk(torch.as_tensor(vals, device=device), k)
+    kk = min(k, n)
+    for r in range(vals.shape[0]):
+        row = vals[r]
+        exp = np.lexsort((np.arange(n), -np.nan_to_num(row, nan=0.0), np.isnan(row)))[:kk]
+        assert idx[r].cpu().tolist() == exp.tolist(), r
+        np.testing.assert_array_equal(v[r].cpu().numpy(), row[exp])
+
+
 # ----------------------------------------------------------------- fusion
 def _fuse_gpu(device, als_scores, tt_scores, als_wins, top_k):
     h = _hrec()
