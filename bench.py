@@ -124,10 +124,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    # HREC_BENCH_BACKEND=gloo + HREC_BENCH_DEVICE=0: rehearsal of the W > 1
+    # flow with every rank on one GPU (RCCL refuses two ranks per device);
+    # the driver's multi-GPU runs use the defaults (RCCL, one GPU per rank).
+    backend = os.environ.get("HREC_BENCH_BACKEND", "nccl")
+    dev = int(os.environ.get("HREC_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
 
     cfg = CONFIGS[args.config]
