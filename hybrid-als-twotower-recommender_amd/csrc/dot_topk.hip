@@ -293,14 +293,20 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ in, int64_t n, uint
 #endif
 constexpr int kResUserBytes = 128 * 1024;
 constexpr int kResNU = HREC_RES_NU;  // user tiles per chunk (64 users): leaves VGPRs for the prefetches
+#ifndef HREC_RES_NI_BF16
+#define HREC_RES_NI_BF16 4
+#endif
+constexpr int kResNIbf16 = HREC_RES_NI_BF16;  // item tiles per wave, bf16 at d <= 128 (2 or 4)
 
-template <bool BF16, int DK, bool FILTER>
+template <bool BF16, int DK, bool FILTER, int NI_>
 __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
     const char* __restrict__ U, int B, int UB, const char* __restrict__ V, int64_t n_rows, int64_t n_items,
     int64_t item_step, int n_ut, float* __restrict__ out, int64_t ldo, const float* __restrict__ thr, int thr_stride,
     int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n, int64_t idx_offset) {
   using S = DotShape<BF16, DK>;
-  constexpr int NU = kResNU, NI = 2, KS = S::kSteps;
+  // NI = 4: 32-user chunks (8 MFMAs per 2 user-fragment reads, as 4 x 4
+  // would be, at the register budget of two waves per SIMD)
+  constexpr int NI = NI_, NU = NI_ == 4 ? 2 : kResNU, KS = S::kSteps;
   constexpr int CU = 16 * NU;  // users per chunk
   constexpr int kItems = 8 * 16 * NI;  // per block tile
   constexpr bool kSwz = S::kChunks >= 16;
@@ -545,6 +551,14 @@ static int dot_launch_t(const void* U, int B, const void* V, int64_t n_rows, int
   return check_launch("dot_tile_kernel");
 }
 
+template <bool BF16, int DK, bool FILTER>
+static auto dot_res_pick(int ni) {
+  if constexpr (BF16 && DK <= 128) {
+    if (ni == 4) return dot_res_kernel<BF16, DK, FILTER, 4>;
+  }
+  return dot_res_kernel<BF16, DK, FILTER, 2>;
+}
+
 template <bool FILTER>
 static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
                           int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
@@ -557,12 +571,16 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
   int UB = (B + n_ut - 1) / n_ut;
   UB = (UB + 16 * kResNU - 1) / (16 * kResNU) * (16 * kResNU);
   const size_t lds = (size_t)UB * row_lds + (size_t)UB * 4;
-  const dim3 grid(dot_grid(n_ut, n_items, 256)), block(kDotThreads);
+  // bf16 at d <= 128: 64 items per wave (4 item tiles), so each user fragment
+  // read from LDS feeds 4 MFMAs instead of 2 (the LDS read chain, not the
+  // matrix cores, was what the waves waited on); f32 and d = 256 keep 32
+  const int ni = (bf16 && dk <= 128) ? kResNIbf16 : 2;
+  const dim3 grid(dot_grid(n_ut, n_items, 128 * ni)), block(kDotThreads);
   const char* u = (const char*)U;
   const char* v = (const char*)V;
 #define HREC_DOTR(BF, DK)                                                                                      \
   do {                                                                                                         \
-    auto kfn = dot_res_kernel<BF, DK, FILTER>;                                                                 \
+    auto kfn = dot_res_pick<BF, DK, FILTER>(ni);                                                               \
     if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
       return check_launch("dot_res_kernel: LDS attribute");                                                   \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, u, B, UB, v, n_rows, n_items, step, n_ut, out, ldo, thr,         \
