@@ -26,7 +26,7 @@
 #define HREC_ALS_CH0 8
 #endif
 #ifndef HREC_ALS_ABLATE
-#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip factor+solve, 3 = skip the substitutions
+#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip factor+solve, 3 = skip the substitutions, 4 = skip the Gramian
 #endif
 #ifndef HREC_ALS_SOLVE_UNROLL
 #define HREC_ALS_SOLVE_UNROLL 8  // unroll of the two 64-step triangular-solve loops
@@ -36,6 +36,9 @@
 #endif
 #ifndef HREC_ALS_SPLIT
 #define HREC_ALS_SPLIT 0  // 1 = producer/consumer kernel (Gramian waves hand rows to factor/solve waves)
+#endif
+#ifndef HREC_ALS_INTCVT
+#define HREC_ALS_INTCVT 0  // 1 = Gramian operands f32 -> f64 by 32-bit integer ops (measured slower)
 #endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
@@ -121,6 +124,25 @@ __device__ unsigned long long g_als_stamps[8];
 #define STAMP_DECL
 #endif
 
+// f32 -> f64 from the bit fields with 32-bit integer ops only: v_cvt_f64_f32
+// runs on the f64 pipe, which the Gramian's f64 MFMAs keep busy (f64 VALU ops
+// do not co-execute with them; integer ops do). Exact for normal numbers and
+// zeros; f32 subnormals (|x| < 2^-126) become zero; inf/NaN are not factor
+// values (Spark's factors are finite).
+__device__ __forceinline__ double f32_to_f64_int(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const uint32_t em = u & 0x7fffffffu;
+  const bool normal = (u & 0x7f800000u) != 0u;
+  const uint32_t hi = (u & 0x80000000u) | (normal ? (em >> 3) + 0x38000000u : 0u);
+  const uint32_t lo = normal ? em << 29 : 0u;
+  return __hiloint2double((int)hi, (int)lo);
+}
+
+__device__ __forceinline__ double gram_cvt(float x) {
+  if constexpr (HREC_ALS_INTCVT) return f32_to_f64_int(x);
+  return (double)x;
+}
+
 // Wave-uniform broadcast of lane `src`'s double (two v_readlane_b32).
 __device__ __forceinline__ double bcast(double v, int src) {
   const long long x = __double_as_longlong(v);
@@ -171,6 +193,15 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   STAMP(0);
 #pragma unroll
   for (int p = 0; p < NPAIR; ++p) acc[p] = d4{0.0, 0.0, 0.0, 0.0};
+  if constexpr (HREC_ALS_ABLATE == 4) {  // timing-only: factor/solve without the Gramian (SPD stand-in)
+#pragma unroll
+    for (int I = 0, p = 0; I < NT; p += NT - I, ++I)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[p][rr] = (sub + 4 * rr == col) ? 1.0 + reg * (double)n : 0.0;
+    if (lane < KP) bsh[lane] = 1.0;
+    wave_lds_sync();
+    return;
+  }
   f4 fa[NPAIR];
   double bp[NT];
 #pragma unroll
@@ -249,11 +280,11 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
       const Vec<NT> cur = ring[s % PF];
       double a[NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) a[t] = (double)cur.x[t];
+      for (int t = 0; t < NT; ++t) a[t] = gram_cvt(cur.x[t]);
       ring[s % PF] = struct_load<NT>(rsrc, nidx, voff);
       nidx = (s + 1 + PF < 16) ? bperm(iw0, s + 1 + PF) : bperm(iw1, s + 1 + PF - 16);
       const float rf = __int_as_float(__builtin_amdgcn_ds_bpermute(bp_addr + 16 * s, __float_as_int(rw0)));
-      const double rv = (double)rf;
+      const double rv = gram_cvt(rf);
       if (MODE == 1 && (s % HREC_ALS_CH1) == 0) {
 #pragma unroll
         for (int p = 0; p < NPAIR; ++p) fa[p] = f4{0.f, 0.f, 0.f, 0.f};

@@ -1,7 +1,7 @@
 # A/B the ALS half-sweep variants on one GPU (two interleaved rounds).
 set -e
 mkdir -p gpurun_out/ab
-V=hybrid-als-twotower-recommender_amd/lib/variants
+V=hybrid-als-twotower-recommender_amd/lib/ab
 for round in 1 2; do
   for lib in $V/*.so; do
     n=$(basename $lib .so)

@@ -1,11 +1,11 @@
-# Build A/B variants of libhrec into hybrid-als-twotower-recommender_amd/lib/variants/
+# Build A/B variants of libhrec into hybrid-als-twotower-recommender_amd/lib/ab/
 # usage: bash scripts/build_variants.sh "NAME:-DFLAG=1 -DOTHER=2" ...
 set -e
 D=hybrid-als-twotower-recommender_amd
-mkdir -p $D/lib/variants
+mkdir -p $D/lib/ab
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags $D/csrc/*.hip -o $D/lib/variants/libhrec_$name.so &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags $D/csrc/*.hip -o $D/lib/ab/libhrec_$name.so &
 done
 wait
-ls -la $D/lib/variants
+ls -la $D/lib/ab

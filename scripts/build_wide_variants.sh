@@ -1,5 +1,5 @@
 # Timing-only builds of libhrec with HREC_WIDE_CUT=1 (Gramian only) and 2
-# (no substitutions) -> hybrid-als-twotower-recommender_amd/lib/variants/
+# (no substitutions) -> hybrid-als-twotower-recommender_amd/lib/ab/
 set -e
 L=hybrid-als-twotower-recommender_amd/lib
 mkdir -p $L/variants
