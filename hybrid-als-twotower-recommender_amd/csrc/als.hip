@@ -40,6 +40,9 @@
 #ifndef HREC_ALS_INTCVT
 #define HREC_ALS_INTCVT 0  // 1 = Gramian operands f32 -> f64 by 32-bit integer ops (measured slower)
 #endif
+#ifndef HREC_ALS_RLPANEL
+#define HREC_ALS_RLPANEL 0  // 1 = panel pivot entries by v_readlane from the pivot lane (measured slower)
+#endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
 #endif
@@ -473,7 +476,13 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int q = 16 * J + m;
-      a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
+      if constexpr (HREC_ALS_RLPANEL) {
+        // the diagonal block's lanes also hold its lower triangle (A[c][q] by
+        // symmetry), so column pv carries the pivot row of the block
+        a[m] = !own ? 0.0 : q <= c ? Up[tri(c) + q] : c < 16 * J + 16 ? Up[tri(q) + c] : 0.0;
+      } else {
+        a[m] = (own && q <= c) ? Up[tri(c) + q] : 0.0;
+      }
     }
     // (c) 16 pivots of A = Ut^T D Ut (LDL^T: no square roots), right-looking,
     //     columns on lanes. The unscaled pivot row goes to LDS (alternating
@@ -482,6 +491,33 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
     //     needs only the lane's own entries), so the per-pivot critical path is
     //     rcp -> Newton -> scale -> fma -> readlane.
     double piv = bcast(a[0], 16 * J);
+    if constexpr (HREC_ALS_RLPANEL) {
+      // Pivot pv's row within the block, A[pv][16J + m] (m > i), is lane pv's
+      // own column entries A[16J + m][pv] (the Schur complement stays
+      // symmetric): read by v_readlane at the start of the pivot, so the
+      // per-pivot critical path is rcp -> Newton -> scale -> fma -> readlane,
+      // with no LDS store/load round trip.
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int pv = 16 * J + i;
+        double u[16];
+#pragma unroll
+        for (int m0 = i + 1; m0 < 16; ++m0) u[m0] = bcast(a[m0], pv);
+        const double r0 = __builtin_amdgcn_rcp(piv);
+        const double r = fma(r0, fma(-piv, r0, 1.0), r0);
+        const double ut = a[i] * r;  // Ut[pv][c]
+        if (own && c > pv) Up[tri(c) + pv] = ut;
+        if (c == pv) {
+          dsh[pv] = piv;
+          rdsh[pv] = r;
+        }
+        if (i < 15) {
+#pragma unroll
+          for (int m0 = i + 1; m0 < 16; ++m0) a[m0] = fma(-u[m0], ut, a[m0]);
+          piv = bcast(a[i + 1], pv + 1);
+        }
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int pv = 16 * J + i;
