@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
     const float* __restrict__ U, const int64_t* __restrict__ user_rows, int n_users,
     const float* __restrict__ Vt, int64_t ld, int64_t n_items, int k, int kp, float* __restrict__ out,
     const float* __restrict__ thr, int thr_stride, int cap, float* __restrict__ cand_v,
-    int64_t* __restrict__ cand_i, int* __restrict__ cand_n) {
+    int64_t* __restrict__ cand_i, int* __restrict__ cand_n, int* __restrict__ overflow) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float us[kScoreKMax + 1][UB];  // + the row read ahead past the end
   __shared__ int uok[UB];
@@ -190,7 +190,10 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
         if (m == 0) continue;
         int base = 0;
         const int leader = __builtin_ctzll(m);
-        if (lane == leader) base = atomicAdd(&cand_n[b0 + b], __popcll(m));
+        if (lane == leader) {
+          base = atomicAdd(&cand_n[b0 + b], __popcll(m));
+          if (base + __popcll(m) > cap) *overflow = 1;  // this user's survivors exceed the list
+        }
         base = __shfl(base, leader, kWave);
         if (pass) {
           const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -203,11 +206,6 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
       }
     }
   }
-}
-
-__global__ void cand_overflow_kernel(const int* __restrict__ cand_n, int n_users, int cap, int* __restrict__ flag) {
-  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < n_users; b += gridDim.x * blockDim.x)
-    if (cand_n[b] > cap) atomicOr(flag, 1);
 }
 
 // ----------------------------------------------------------------- top-k
@@ -391,7 +389,8 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const T* __restrict__ va
 // from below, which is all the filter needs (the final top-k is exact). NaN
 // elements are ignored (fmaxf); a row without a number yields -inf.
 __global__ __launch_bounds__(256) void sample_threshold_kernel(const float* __restrict__ vals, int64_t n_rows,
-                                                               int64_t n, int kk, float* __restrict__ thr) {
+                                                               int64_t n, int kk, float* __restrict__ thr,
+                                                               int* __restrict__ zero_cnt) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_rows) return;  // wave-uniform
@@ -413,7 +412,10 @@ __global__ __launch_bounds__(256) void sample_threshold_kernel(const float* __re
     const uint64_t hold = __ballot(m == w);
     if (hold && lane == __builtin_ctzll(hold)) m = -__builtin_inff();
   }
-  if (lane == 0) thr[row] = t;
+  if (lane == 0) {
+    thr[row] = t;
+    if (zero_cnt) zero_cnt[row] = 0;
+  }
 }
 
 // ---------------------------------------------------------------- fusion
@@ -892,7 +894,7 @@ extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_row
     const dim3 grid((unsigned)((n_users + UB - 1) / UB), (unsigned)((n_items + 1023) / 1024));
     hipLaunchKernelGGL((als_score_fast_kernel<UB, false>), grid, dim3(256), 0, as_stream(stream), user_factors,
                        user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, out, nullptr, 0, 0, nullptr,
-                       nullptr, nullptr);
+                       nullptr, nullptr, nullptr);
     return check_launch("als_score_fast_kernel");
   }
   const dim3 grid((unsigned)((n_items + 255) / 256), (unsigned)((n_users + UB - 1) / UB));
@@ -983,6 +985,7 @@ extern "C" int hrec_cosine_sim(const double* feats, int64_t n_items, int dim, co
 
 static constexpr int kScoreUB = 16;
 static constexpr int kSample = 2048;
+static constexpr int kSampleUB = 4;
 static constexpr int kCap = 4096;
 
 extern "C" size_t hrec_als_score_topk_workspace_bytes(int n_users, int64_t n_items, int top_k) {
@@ -1036,39 +1039,40 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
   if (n_items <= kSample) {  // small: score everything, exact top-k
     hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, false>), dim3(gy, (unsigned)((n_items + 1023) / 1024)), blk,
                        0, s, user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, samp,
-                       nullptr, 0, 0, nullptr, nullptr, nullptr);
+                       nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr);
     int rc = check_launch("als_score_fast_kernel");
     if (rc) return rc;
     return topk_rows<float>(samp, n_users, n_items, n_items, kk, out_idx, out_val, tws, (size_t)1 << 62, s);
   }
   // 1) thresholds: the kk-th best of the first S items bounds the final kk-th from below
-  hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, false>), dim3(gy, (unsigned)((S + 1023) / 1024)), blk, 0, s,
-                     user_factors, user_rows, n_users, item_factors_t, ld_items, S, k, kp, samp, nullptr, 0, 0,
-                     nullptr, nullptr, nullptr);
+  //    (4 users per block: the sample is too small to fill the chip with 16)
+  hipLaunchKernelGGL((als_score_fast_kernel<kSampleUB, false>),
+                     dim3((unsigned)((n_users + kSampleUB - 1) / kSampleUB), (unsigned)((S + 1023) / 1024)), blk, 0,
+                     s, user_factors, user_rows, n_users, item_factors_t, ld_items, S, k, kp, samp, nullptr, 0, 0,
+                     nullptr, nullptr, nullptr, nullptr);
   int rc = check_launch("als_score_fast_kernel(sample)");
   if (rc) return rc;
   const float* thr = sv + (kk - 1);
   int thr_stride = kk;
   if (kk <= 64) {  // a lower bound suffices: the 64 lane maxima's kk-th
+    // (also zeroes the survivor counters: no separate memset launch)
     hipLaunchKernelGGL(sample_threshold_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, samp,
-                       (int64_t)n_users, S, kk, sv);
+                       (int64_t)n_users, S, kk, sv, cn);
     rc = check_launch("sample_threshold_kernel");
     thr = sv;
     thr_stride = 1;
   } else {
     rc = topk_rows<float>(samp, n_users, S, S, kk, si, sv, tws, (size_t)1 << 62, s);
+    if (rc == HREC_OK && hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
+      return check_launch("score_topk memset");
   }
   if (rc) return rc;
-  // 2) fused score + filter over all items
-  if (hipMemsetAsync(cn, 0, (size_t)n_users * 4, s) != hipSuccess)
-    return check_launch("score_topk memset");
+  // 2) fused score + filter over all items; a user whose survivors exceed
+  //    kCap raises *overflow from inside the filter (the caller falls back)
   hipLaunchKernelGGL((als_score_fast_kernel<kScoreUB, true>), dim3(gy, (unsigned)((n_items + 1023) / 1024)), blk, 0,
                      s, user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, nullptr,
-                     thr, thr_stride, kCap, cv, ci, cn);
+                     thr, thr_stride, kCap, cv, ci, cn, overflow);
   rc = check_launch("als_score_fast_kernel(filter)");
-  if (rc) return rc;
-  hipLaunchKernelGGL(cand_overflow_kernel, dim3(64), dim3(256), 0, s, cn, n_users, kCap, overflow);
-  rc = check_launch("cand_overflow_kernel");
   if (rc) return rc;
   // 3) exact stable top-k over the candidates (original item index breaks ties)
   return topk_rows<float>(cv, n_users, kCap, kCap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci, cn);

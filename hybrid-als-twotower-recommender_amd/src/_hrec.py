@@ -274,17 +274,21 @@ def als_score(user_factors, user_rows, item_factors_t, item_rows, n_items, k, ou
     return out
 
 
-def als_score_topk(user_factors, user_rows, item_factors_t, n_items, k, top_k, check_overflow=True):
+def als_score_topk(user_factors, user_rows, item_factors_t, n_items, k, top_k, check_overflow=True,
+                   overflow_out=None):
     """Top-k of the JVM-exact ALS scores over items [0, n_items) for each
     (known) user, without materialising the score matrix. Falls back to the
-    full score matrix + top-k when a user's survivor list overflowed."""
+    full score matrix + top-k when a user's survivor list overflowed.
+    overflow_out (device int32 [1], optional) receives the library's overflow
+    flag (with check_overflow=False the caller resolves it later)."""
     kp = user_factors.shape[1]
     B = user_rows.numel()
     kk = min(int(top_k), int(n_items))
     dev = user_factors.device
     out_i = torch.empty((B, kk), dtype=torch.int64, device=dev)
     out_v = torch.empty((B, kk), dtype=torch.float32, device=dev)
-    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    # zeroed by the library on the stream
+    flag = overflow_out if overflow_out is not None else torch.empty(1, dtype=torch.int32, device=dev)
     need = int(lib().hrec_als_score_topk_workspace_bytes(B, n_items, kk))
     ws = torch.empty(need, dtype=torch.uint8, device=dev)
     _check("hrec_als_score_topk", lib().hrec_als_score_topk(

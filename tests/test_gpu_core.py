@@ -325,6 +325,36 @@ def test_als_score_topk_fused_matches_full(device, n_items, quant):
     np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(full, exp_i, 1))
 
 
+def test_als_score_topk_overflow_flag(device):
+    """The filter kernel raises the overflow flag itself when a user's
+    survivors exceed the candidate list (constant scores: every item ties
+    with the sampled bound) and leaves it 0 on random factors; the wrapper's
+    fallback then still returns the exact stable top-k."""
+    h = _hrec()
+    n_items, k, kp, B = 100_000, 64, 64, 8
+    rng = np.random.default_rng(3)
+    U = np.zeros((B, kp), np.float32)
+    U[:, :k] = rng.normal(size=(B, k))
+    users = torch.arange(B, dtype=torch.int64, device=device)
+    flag = torch.full((1,), 7, dtype=torch.int32, device=device)
+    V = np.zeros((n_items, kp), np.float32)
+    V[:, :k] = rng.normal(size=(n_items, k))
+    Vt = h.transpose(torch.as_tensor(V, device=device))
+    h.als_score_topk(torch.as_tensor(U, device=device), users, Vt, n_items, k, 5, check_overflow=False,
+                     overflow_out=flag)
+    assert int(flag.item()) == 0
+    Vc = np.zeros((n_items, kp), np.float32)
+    Vc[:, :k] = 0.25
+    Vt = h.transpose(torch.as_tensor(Vc, device=device))
+    idx, val = h.als_score_topk(torch.as_tensor(U, device=device), users, Vt, n_items, k, 5,
+                                overflow_out=flag)
+    assert int(flag.item()) == 1
+    full = oals.score_matrix(U[:, :k], Vc[:, :k])
+    exp_i = _np_stable_topk(full, 5)
+    np.testing.assert_array_equal(idx.cpu().numpy(), exp_i)
+    np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(full, exp_i, 1))
+
+
 # ------------------------------------------------ multi-rank on one device
 def _chunked_worker(rank, world, port, chunks, q):
     import os
