@@ -41,7 +41,7 @@
 #define HREC_ALS_INTCVT 0  // 1 = Gramian operands f32 -> f64 by 32-bit integer ops (measured slower)
 #endif
 #ifndef HREC_ALS_RLPANEL
-#define HREC_ALS_RLPANEL 0  // 1 = panel pivot entries by v_readlane from the pivot lane (measured slower)
+#define HREC_ALS_RLPANEL 0  // 1 = pivot-row entries by v_readlane, 2 = only the next pivot's (both measured slower)
 #endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
@@ -523,6 +523,11 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
       const int pv = 16 * J + i;
       double* cb = colbuf + 64 * (i & 1);
       if (c < KP) cb[c] = a[i];  // A[pv][c] (lane pv: the pivot)
+      // RLPANEL 2: the one pivot-row entry the NEXT pivot depends on,
+      // A[pv][pv + 1], comes by v_readlane (final since the previous pivot),
+      // so the LDS round trip of the rest has a whole pivot of slack
+      constexpr bool kRl2 = HREC_ALS_RLPANEL == 2;
+      const double u1 = (kRl2 && i < 15) ? bcast(a[i], pv + 1) : 0.0;
       // 1 / piv: v_rcp_f64 (~2^-24 relative) + one Newton step
       const double r0 = __builtin_amdgcn_rcp(piv);
       const double r = fma(r0, fma(-piv, r0, 1.0), r0);
@@ -533,13 +538,18 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
         rdsh[pv] = r;
       }
       if (i < 15) {
-        piv = bcast(fma(-a[i], ut, a[i + 1]), pv + 1);
+        if constexpr (kRl2) {  // bit-identical: u1 is the value lane pv + 1 stored to cb
+          a[i + 1] = fma(-u1, ut, a[i + 1]);
+          piv = bcast(a[i + 1], pv + 1);
+        } else {
+          piv = bcast(fma(-a[i], ut, a[i + 1]), pv + 1);
+        }
         wave_lds_sync();
 #pragma unroll
         for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
           const double2 u = *reinterpret_cast<const double2*>(cb + 16 * J + m0);
-          if (m0 > i) a[m0] = fma(-u.x, ut, a[m0]);
-          a[m0 + 1] = fma(-u.y, ut, a[m0 + 1]);
+          if (m0 > i + (kRl2 ? 1 : 0)) a[m0] = fma(-u.x, ut, a[m0]);
+          if (!kRl2 || m0 > i) a[m0 + 1] = fma(-u.y, ut, a[m0 + 1]);
         }
       }
     }
