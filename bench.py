@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=4,
                     help="W > 1: user-side ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")
+    ap.add_argument("--tt-steps", type=int, default=50,
+                    help="two-tower training steps timed (c2 tables, d = 64, batch 256; 0 = skip)")
     ap.add_argument("--no-ingest", dest="ingest", action="store_false",
                     help="skip the COO -> CSR/CSC ingest measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_prof_summary.json"),
@@ -384,6 +386,52 @@ def main():
         del V4, U4
         torch.cuda.empty_cache()
 
+    # Two-tower training (Keras fit step, src/two_tower_model.py:111): c2's
+    # tables at d = 64 (1M users, 100k items, 2651 manufacturers, 255
+    # categories), batch 256, one step = forward + MSE + backward + Keras-exact
+    # Adam. Keras' sparse Adam decays m and v of the WHOLE table every step
+    # [ext: optimizer_v2/adam.py], so a step is bound by that HBM sweep:
+    # 6 x 4 B (var, m, v read + write) per table element. W > 1 trains
+    # replicas (sharding would change Keras' batch semantics): rank 0 only.
+    tt_train = None
+    if rank == 0 and world == 1 and args.tt_steps > 0:
+        dtt = 64
+        n_man, n_cat = 2651, 255
+        tt = DeviceTwoTower(n_users, n_items, n_man, n_cat, dtt, seed=3)
+        Bt = 256
+        gt = torch.Generator(device="cuda").manual_seed(11)
+        nb = 16  # distinct pre-generated batches, cycled
+        bu = torch.randint(0, n_users, (nb, Bt), device="cuda", generator=gt, dtype=torch.int32)
+        bi = torch.randint(0, n_items, (nb, Bt), device="cuda", generator=gt, dtype=torch.int32)
+        bm = torch.randint(0, n_man, (nb, Bt), device="cuda", generator=gt, dtype=torch.int32)
+        bc = torch.randint(0, n_cat, (nb, Bt), device="cuda", generator=gt, dtype=torch.int32)
+        bx = torch.rand((nb, Bt, 2), device="cuda", generator=gt)
+        by = torch.randint(0, 19, (nb, Bt), device="cuda", generator=gt).to(torch.float32)
+        for j in range(3):
+            tt.train_step(bu[j], bi[j], bm[j], bc[j], bx[j], by[j])
+        torch.cuda.synchronize()
+        te0, te1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0t = time.perf_counter()
+        te0.record(stream)
+        for j in range(args.tt_steps):
+            q = j % nb
+            tt.train_step(bu[q], bi[q], bm[q], bc[q], bx[q], by[q])
+        te1.record(stream)
+        torch.cuda.synchronize()
+        tts = (time.perf_counter() - t0t) / args.tt_steps
+        dev_s = te0.elapsed_time(te1) / args.tt_steps / 1e3
+        tab_elems = n_users * dtt + n_items * dtt + (n_man + n_cat) * 8
+        step_bytes = 6 * 4 * (tab_elems + tt.n_dense)
+        tt_train = {"samples_per_s": Bt / tts, "ms_per_step": tts * 1e3, "batch": Bt, "d": dtt,
+                    "tables": {"users": n_users, "items": n_items, "manufacturers": n_man, "categories": n_cat},
+                    "steps": args.tt_steps,
+                    "step": "hrec_tt_forward_backward + hrec_adam_dense + 4 x hrec_adam_sparse (Keras-exact)",
+                    "roofline": {"bound": "hbm", "achieved": step_bytes / dev_s / 1e9, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": step_bytes / dev_s / 1e9 / HBM_PEAK_GBS,
+                                 "algorithmic_bytes_per_step": step_bytes}}
+        del tt, bu, bi, bm, bc, bx, by
+        torch.cuda.empty_cache()
+
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.accum_mode == 0:
         with open(args.traffic_json) as f:
@@ -439,6 +487,7 @@ def main():
             "ingest": ingest,
             "tt_scoring_c4": tt_c4,
             "hybrid_top5_c5": hybrid_c5,
+            "tt_train": tt_train,
         }
         print(json.dumps(line))
     if world > 1:

@@ -13,7 +13,7 @@
 
 namespace hrec {
 
-constexpr int kTR = 32;     // rows (samples / candidates) per workgroup
+constexpr int kTR = 8;      // rows (samples / candidates) per workgroup: 32 workgroups at a batch of 256
 constexpr int kBlock = 256;
 constexpr float kLnEps = 1e-3f;
 
@@ -388,32 +388,38 @@ __global__ __launch_bounds__(kBlock) void adam_dense_kernel(float* __restrict__ 
 }
 
 // IndexedSlices dedup (tf.unique order = first occurrence, segment sums in
-// sample order). One block; gsum row q is the summed grad of sample q when q
-// is the first occurrence of its index; mark[idx] = q.
-__global__ __launch_bounds__(1024) void sparse_dedup_kernel(const int32_t* __restrict__ idx, int B, int dim,
-                                                            const float* __restrict__ g, float* __restrict__ gsum,
-                                                            int32_t* __restrict__ mark) {
-  for (int s = threadIdx.x; s < B; s += blockDim.x) {
-    const int32_t key = idx[s];
-    bool first = true;
-    for (int t = 0; t < s; ++t)
-      if (idx[t] == key) {
-        first = false;
-        break;
-      }
-    if (!first) continue;
-    for (int c = 0; c < dim; ++c) {
-      float acc = 0.f;
-      bool any = false;
-      for (int t = s; t < B; ++t)
-        if (idx[t] == key) {
-          acc = any ? acc + g[(int64_t)t * dim + c] : g[(int64_t)t * dim + c];
-          any = true;
-        }
-      gsum[(int64_t)s * dim + c] = acc;
-    }
-    mark[key] = s;
+// sample order): gsum row q is the summed grad of sample q when q is the
+// first occurrence of its index; mark[idx] = q.
+// One wave per batch slot s. Slots whose key already occurred earlier exit;
+// the first occurrence sums its key's gradient rows in batch order (g[s],
+// then + g[t] for each later t with the same key: the order of TF's
+// unsorted_segment_sum over the deduplicated IndexedSlices) and publishes
+// its slot in mark[key]. Occurrences are found 64 slots per ballot.
+__global__ __launch_bounds__(64) void sparse_dedup_kernel(const int32_t* __restrict__ idx, int B, int dim,
+                                                          const float* __restrict__ g, float* __restrict__ gsum,
+                                                          int32_t* __restrict__ mark) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  const int32_t key = idx[s];
+  for (int t0 = 0; t0 < s; t0 += kWave) {
+    const int t = t0 + lane;
+    if (__ballot(t < s && idx[t] == key)) return;  // wave-uniform: not the first occurrence
   }
+  for (int c0 = 0; c0 < dim; c0 += kWave) {
+    const int c = c0 + lane;
+    const bool on = c < dim;
+    float acc = on ? g[(int64_t)s * dim + c] : 0.f;
+    for (int t0 = s + 1; t0 < B; t0 += kWave) {
+      const int t = t0 + lane;
+      uint64_t m = __ballot(t < B && idx[t] == key);
+      while (m) {  // ascending slot order
+        const int u = t0 + __builtin_ctzll(m);
+        m &= m - 1;
+        if (on) acc = acc + g[(int64_t)u * dim + c];
+      }
+    }
+    if (on) gsum[(int64_t)s * dim + c] = acc;
+  }
+  if (lane == 0) mark[key] = s;
 }
 
 // Keras OptimizerV2 Adam._resource_apply_sparse: whole-table decay of m and
@@ -439,6 +445,46 @@ __global__ __launch_bounds__(kBlock) void adam_sparse_table_kernel(float* __rest
   m[o] = mo;
   v[o] = vo;
   var[o] = var[o] - (lr * mo) / (sqrtf(vo) + eps);
+}
+
+// The same update, 4 consecutive elements of one row per thread (dim % 4 ==
+// 0): 16-B loads and stores for the whole-table sweep, identical arithmetic.
+__global__ __launch_bounds__(kBlock) void adam_sparse_table4_kernel(float* __restrict__ var, float* __restrict__ m,
+                                                                     float* __restrict__ v, int64_t n_rows, int dim,
+                                                                     const int32_t* __restrict__ mark,
+                                                                     const float* __restrict__ gsum, float lr,
+                                                                     float b1, float omb1, float b2, float omb2,
+                                                                     float eps) {
+  const int64_t o4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o4 * 4 >= n_rows * dim) return;
+  const int64_t o = o4 * 4;
+  const int64_t r = o / dim;
+  const int c = (int)(o - r * dim);
+  const int32_t q = mark[r];
+  float4 mo = reinterpret_cast<const float4*>(m)[o4];
+  float4 vo = reinterpret_cast<const float4*>(v)[o4];
+  float4 xo = reinterpret_cast<const float4*>(var)[o4];
+  float* mp = &mo.x;
+  float* vp = &vo.x;
+  float* xp = &xo.x;
+  float4 gr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q >= 0) gr = *reinterpret_cast<const float4*>(gsum + (int64_t)q * dim + c);
+  const float* gp = &gr.x;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float me = mp[e] * b1;
+    float ve = vp[e] * b2;
+    if (q >= 0) {
+      me = me + gp[e] * omb1;
+      ve = ve + (gp[e] * gp[e]) * omb2;
+    }
+    mp[e] = me;
+    vp[e] = ve;
+    xp[e] = xp[e] - (lr * me) / (sqrtf(ve) + eps);
+  }
+  reinterpret_cast<float4*>(m)[o4] = mo;
+  reinterpret_cast<float4*>(v)[o4] = vo;
+  reinterpret_cast<float4*>(var)[o4] = xo;
 }
 
 __global__ void sparse_unmark_kernel(const int32_t* __restrict__ idx, int B, int32_t* __restrict__ mark) {
@@ -592,14 +638,22 @@ extern "C" int hrec_adam_sparse(float* var, float* m, float* v, int64_t n_rows, 
   HREC_REQUIRE(batch == 0 || (indices && grad_rows && gsum), "adam_sparse: null slices");
   hipStream_t s = as_stream(stream);
   if (batch > 0) {
-    hipLaunchKernelGGL(sparse_dedup_kernel, dim3(1), dim3(1024), 0, s, indices, batch, dim, grad_rows, gsum, mark);
+    hipLaunchKernelGGL(sparse_dedup_kernel, dim3((unsigned)batch), dim3(kWave), 0, s, indices, batch, dim, grad_rows,
+                       gsum, mark);
     int rc = check_launch("sparse_dedup_kernel");
     if (rc) return rc;
   }
   const int64_t total = n_rows * dim;
-  hipLaunchKernelGGL(adam_sparse_table_kernel, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                     var, m, v, n_rows, dim, mark, gsum, lr, beta1, one_minus_beta1, beta2, one_minus_beta2,
-                     epsilon);
+  const bool vec4 = dim % 4 == 0 && (((uintptr_t)var | (uintptr_t)m | (uintptr_t)v | (uintptr_t)gsum) & 15) == 0;
+  if (vec4) {
+    hipLaunchKernelGGL(adam_sparse_table4_kernel, dim3((unsigned)((total / 4 + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, s, var, m, v, n_rows, dim, mark, gsum, lr, beta1, one_minus_beta1, beta2, one_minus_beta2,
+                       epsilon);
+  } else {
+    hipLaunchKernelGGL(adam_sparse_table_kernel, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       var, m, v, n_rows, dim, mark, gsum, lr, beta1, one_minus_beta1, beta2, one_minus_beta2,
+                       epsilon);
+  }
   int rc = check_launch("adam_sparse_table_kernel");
   if (rc || batch == 0) return rc;
   hipLaunchKernelGGL(sparse_unmark_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, indices, batch,

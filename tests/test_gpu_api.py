@@ -259,6 +259,33 @@ def test_tt_adam_steps_match_oracle(device):
                                    err_msg=name)
 
 
+@pytest.mark.parametrize("B,dim,n_rows", [(300, 80, 7), (257, 8, 2651), (64, 64, 1)])
+def test_sparse_adam_dedup_order(device, B, dim, n_rows):
+    """Duplicate ids of a batch are summed in batch order (TF's
+    unsorted_segment_sum over the IndexedSlices) before the slot update: with
+    beta_1 = 0, m of a touched row is exactly that ordered f32 sum. Covers
+    batches past one 64-slot ballot, rows wider than a wave and all-equal ids."""
+    from src import _hrec as h
+
+    rng = np.random.default_rng(B + dim)
+    idx = rng.integers(0, n_rows, B).astype(np.int32)
+    g = rng.normal(size=(B, dim)).astype(np.float32)
+    exp = {}
+    for t in range(B):  # sequential f32 sums in batch order
+        exp[idx[t]] = g[t].copy() if idx[t] not in exp else (exp[idx[t]] + g[t]).astype(np.float32)
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    var = T(np.zeros((n_rows, dim), np.float32))
+    m = T(np.full((n_rows, dim), 5.0, np.float32))
+    v = T(np.ones((n_rows, dim), np.float32))
+    mark = T(np.full(n_rows, -1, np.int32))
+    gsum = torch.empty((B, dim), dtype=torch.float32, device=device)
+    h.adam_sparse(var, m, v, T(idx), T(g), mark, gsum, 0.0, 0.0, 1.0, 0.0, 1.0, 1.0)
+    mh = m.cpu().numpy()
+    for r in range(n_rows):
+        np.testing.assert_array_equal(mh[r], exp[r] if r in exp else np.zeros(dim, np.float32), err_msg=str(r))
+    assert (mark.cpu().numpy() == -1).all()  # unmarked again for the next step
+
+
 def _tt_frame(rng, n, nu, ni, nm, nc):
     return pd.DataFrame({
         "userId": rng.integers(0, nu, n), "itemId": rng.integers(0, ni, n),
