@@ -425,7 +425,7 @@ def main():
         tt_train = {"samples_per_s": Bt / tts, "ms_per_step": tts * 1e3, "batch": Bt, "d": dtt,
                     "tables": {"users": n_users, "items": n_items, "manufacturers": n_man, "categories": n_cat},
                     "steps": args.tt_steps,
-                    "step": "hrec_tt_forward_backward + hrec_adam_dense + 4 x hrec_adam_sparse (Keras-exact)",
+                    "step": "hrec_tt_forward_backward + hrec_adam_dense + hrec_adam_sparse_tables (4 tables, Keras-exact)",
                     "roofline": {"bound": "hbm", "achieved": step_bytes / dev_s / 1e9, "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": step_bytes / dev_s / 1e9 / HBM_PEAK_GBS,
                                  "algorithmic_bytes_per_step": step_bytes}}

@@ -983,7 +983,10 @@ extern "C" int hrec_cosine_sim(const double* feats, int64_t n_items, int dim, co
   return check_launch("cosine_kernel");
 }
 
-static constexpr int kScoreUB = 16;
+#ifndef HREC_SCORE_UB
+#define HREC_SCORE_UB 16
+#endif
+static constexpr int kScoreUB = HREC_SCORE_UB;
 static constexpr int kSample = 2048;
 static constexpr int kSampleUB = 4;
 static constexpr int kCap = 4096;

@@ -487,6 +487,97 @@ __global__ __launch_bounds__(kBlock) void adam_sparse_table4_kernel(float* __res
   reinterpret_cast<float4*>(var)[o4] = xo;
 }
 
+// Grouped form (hrec_adam_sparse_tables): one launch per phase for all
+// tables. Work item ranges per table are prefix sums in the kernel argument.
+struct SparseGroup {
+  hrec_sparse_table t[HREC_MAX_SPARSE_TABLES];
+  int64_t start[HREC_MAX_SPARSE_TABLES + 1];  // first work item (slot / block) of table i
+  int n;
+};
+
+__device__ __forceinline__ int group_of(const SparseGroup& G, int64_t x) {
+  int i = 0;
+  while (i + 1 < G.n && x >= G.start[i + 1]) ++i;
+  return i;
+}
+
+// blocks of one wave: block b is slot (b - start[i]) of table i
+__global__ __launch_bounds__(64) void sparse_dedup_group_kernel(const SparseGroup G) {
+  const int i = group_of(G, blockIdx.x);
+  const hrec_sparse_table& T = G.t[i];
+  const int s = (int)(blockIdx.x - G.start[i]), lane = threadIdx.x;
+  const int32_t* __restrict__ idx = T.indices;
+  const float* __restrict__ g = T.grad_rows;
+  const int B = T.batch, dim = T.dim;
+  const int32_t key = idx[s];
+  for (int t0 = 0; t0 < s; t0 += kWave) {
+    const int t = t0 + lane;
+    if (__ballot(t < s && idx[t] == key)) return;
+  }
+  for (int c0 = 0; c0 < dim; c0 += kWave) {
+    const int c = c0 + lane;
+    const bool on = c < dim;
+    float acc = on ? g[(int64_t)s * dim + c] : 0.f;
+    for (int t0 = s + 1; t0 < B; t0 += kWave) {
+      const int t = t0 + lane;
+      uint64_t msk = __ballot(t < B && idx[t] == key);
+      while (msk) {
+        const int u = t0 + __builtin_ctzll(msk);
+        msk &= msk - 1;
+        if (on) acc = acc + g[(int64_t)u * dim + c];
+      }
+    }
+    if (on) T.gsum[(int64_t)s * dim + c] = acc;
+  }
+  if (lane == 0) T.mark[key] = s;
+}
+
+// blocks of kBlock threads x 4 elements (every dim % 4 == 0, 16-B aligned)
+__global__ __launch_bounds__(kBlock) void adam_sparse_group4_kernel(const SparseGroup G, float lr, float b1,
+                                                                     float omb1, float b2, float omb2, float eps) {
+  const int i = group_of(G, blockIdx.x);
+  const hrec_sparse_table& T = G.t[i];
+  const int64_t o4 = (blockIdx.x - G.start[i]) * (int64_t)kBlock + threadIdx.x;
+  const int dim = T.dim;
+  if (o4 * 4 >= T.n_rows * dim) return;
+  const int64_t o = o4 * 4;
+  const int64_t r = o / dim;
+  const int c = (int)(o - r * dim);
+  const int32_t q = T.mark[r];
+  float4 mo = reinterpret_cast<const float4*>(T.m)[o4];
+  float4 vo = reinterpret_cast<const float4*>(T.v)[o4];
+  float4 xo = reinterpret_cast<const float4*>(T.var)[o4];
+  float* mp = &mo.x;
+  float* vp = &vo.x;
+  float* xp = &xo.x;
+  float4 gr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q >= 0) gr = *reinterpret_cast<const float4*>(T.gsum + (int64_t)q * dim + c);
+  const float* gp = &gr.x;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float me = mp[e] * b1;
+    float ve = vp[e] * b2;
+    if (q >= 0) {
+      me = me + gp[e] * omb1;
+      ve = ve + (gp[e] * gp[e]) * omb2;
+    }
+    mp[e] = me;
+    vp[e] = ve;
+    xp[e] = xp[e] - (lr * me) / (sqrtf(ve) + eps);
+  }
+  reinterpret_cast<float4*>(T.m)[o4] = mo;
+  reinterpret_cast<float4*>(T.v)[o4] = vo;
+  reinterpret_cast<float4*>(T.var)[o4] = xo;
+}
+
+__global__ void sparse_unmark_group_kernel(const SparseGroup G) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= G.start[G.n]) return;
+  const int i = group_of(G, x);
+  const hrec_sparse_table& T = G.t[i];
+  T.mark[T.indices[x - G.start[i]]] = -1;
+}
+
 __global__ void sparse_unmark_kernel(const int32_t* __restrict__ idx, int B, int32_t* __restrict__ mark) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < B) mark[idx[s]] = -1;
@@ -659,6 +750,69 @@ extern "C" int hrec_adam_sparse(float* var, float* m, float* v, int64_t n_rows, 
   hipLaunchKernelGGL(sparse_unmark_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, indices, batch,
                      mark);
   return check_launch("sparse_unmark_kernel");
+}
+
+extern "C" int hrec_adam_sparse_tables(const hrec_sparse_table* tables, int n_tables, float lr, float beta1,
+                                       float one_minus_beta1, float beta2, float one_minus_beta2, float epsilon,
+                                       void* stream) {
+  HREC_REQUIRE(n_tables >= 0 && n_tables <= HREC_MAX_SPARSE_TABLES, "adam_sparse_tables: 0..%d tables",
+               HREC_MAX_SPARSE_TABLES);
+  if (n_tables == 0) return HREC_OK;
+  HREC_REQUIRE(tables, "adam_sparse_tables: null table list");
+  bool vec4 = true;
+  for (int i = 0; i < n_tables; ++i) {
+    const hrec_sparse_table& T = tables[i];
+    HREC_REQUIRE(T.n_rows >= 0 && T.dim >= 1 && T.batch >= 0, "adam_sparse_tables: table %d: bad shape", i);
+    HREC_REQUIRE(T.n_rows == 0 || (T.var && T.m && T.v && T.mark), "adam_sparse_tables: table %d: null pointer", i);
+    HREC_REQUIRE(T.batch == 0 || (T.indices && T.grad_rows && T.gsum),
+                 "adam_sparse_tables: table %d: null slices", i);
+    vec4 = vec4 && T.dim % 4 == 0 &&
+           (((uintptr_t)T.var | (uintptr_t)T.m | (uintptr_t)T.v | (uintptr_t)T.gsum) & 15) == 0;
+  }
+  hipStream_t s = as_stream(stream);
+  if (!vec4) {  // per table (rare shapes: d % 4 != 0)
+    for (int i = 0; i < n_tables; ++i) {
+      const hrec_sparse_table& T = tables[i];
+      const int rc = hrec_adam_sparse(T.var, T.m, T.v, T.n_rows, T.dim, T.indices, T.grad_rows, T.batch, T.mark,
+                                      T.gsum, lr, beta1, one_minus_beta1, beta2, one_minus_beta2, epsilon, stream);
+      if (rc) return rc;
+    }
+    return HREC_OK;
+  }
+  SparseGroup G{};
+  // phase 1: slots; tables with no rows keep their (empty) batch out
+  G.n = 0;
+  int64_t acc = 0;
+  for (int i = 0; i < n_tables; ++i) {
+    if (tables[i].n_rows == 0) continue;
+    G.t[G.n] = tables[i];
+    G.start[G.n] = acc;
+    acc += tables[i].batch;
+    ++G.n;
+  }
+  G.start[G.n] = acc;
+  if (G.n == 0) return HREC_OK;
+  const int64_t n_slots = acc;
+  if (n_slots > 0) {
+    hipLaunchKernelGGL(sparse_dedup_group_kernel, dim3((unsigned)n_slots), dim3(kWave), 0, s, G);
+    const int rc = check_launch("sparse_dedup_group_kernel");
+    if (rc) return rc;
+  }
+  // phase 2: whole-table sweeps, each table starting on a block boundary
+  SparseGroup H = G;
+  acc = 0;
+  for (int i = 0; i < H.n; ++i) {
+    H.start[i] = acc;
+    acc += (H.t[i].n_rows * H.t[i].dim / 4 + kBlock - 1) / kBlock;
+  }
+  H.start[H.n] = acc;
+  hipLaunchKernelGGL(adam_sparse_group4_kernel, dim3((unsigned)acc), dim3(kBlock), 0, s, H, lr, beta1,
+                     one_minus_beta1, beta2, one_minus_beta2, epsilon);
+  int rc = check_launch("adam_sparse_group4_kernel");
+  if (rc || n_slots == 0) return rc;
+  // phase 3: restore mark = -1
+  hipLaunchKernelGGL(sparse_unmark_group_kernel, dim3((unsigned)((n_slots + 255) / 256)), dim3(256), 0, s, G);
+  return check_launch("sparse_unmark_group_kernel");
 }
 
 extern "C" int hrec_tt_pair_score(const float* user_vec, const float* item_vec, int64_t n, int d, float* out,

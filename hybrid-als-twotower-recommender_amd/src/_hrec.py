@@ -67,6 +67,13 @@ class TTParams(ctypes.Structure):
                                  "ln_user_gamma", "ln_user_beta", "ln_item_gamma", "ln_item_beta")]
 
 
+class SparseTable(ctypes.Structure):
+    """hrec_sparse_table (include/hrec.h)."""
+    _fields_ = [("var", _vp), ("m", _vp), ("v", _vp), ("n_rows", ctypes.c_int64), ("dim", ctypes.c_int32),
+                ("batch", ctypes.c_int32), ("indices", _vp), ("grad_rows", _vp), ("mark", _vp), ("gsum", _vp)]
+
+
+MAX_SPARSE_TABLES = 8
 _PP = ctypes.POINTER(TTParams)
 _SIGNATURES.update({
     "hrec_tt_item_forward": (_c_i32, [_PP, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp]),
@@ -91,6 +98,7 @@ _SIGNATURES.update({
                                   _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
                          [ctypes.c_float] * 6 + [_vp]),
+    "hrec_adam_sparse_tables": (_c_i32, [ctypes.POINTER(SparseTable), _c_i32] + [ctypes.c_float] * 6 + [_vp]),
 })
 
 ABI_VERSION = 1
@@ -613,6 +621,22 @@ def adam_sparse(var, m, v, indices, grad_rows, mark, gsum, lr, beta1, omb1, beta
         _dev(indices, torch.int32, "indices"), _dev(grad_rows, torch.float32, "grad_rows"), indices.numel(),
         _dev(mark, torch.int32, "mark"), _dev(gsum, torch.float32, "gsum"), float(lr), float(beta1),
         float(omb1), float(beta2), float(omb2), float(eps), _stream()))
+
+
+def adam_sparse_tables(tables, lr, beta1, omb1, beta2, omb2, eps):
+    """hrec_adam_sparse over several tables in 3 launches. tables: list of
+    (var, m, v, indices, grad_rows, mark, gsum) tuples, as adam_sparse takes."""
+    if len(tables) > MAX_SPARSE_TABLES:
+        raise HrecError(f"adam_sparse_tables: at most {MAX_SPARSE_TABLES} tables")
+    arr = (SparseTable * max(1, len(tables)))()
+    for j, (var, m, v, indices, grad_rows, mark, gsum) in enumerate(tables):
+        n_rows, dim = var.shape
+        arr[j] = SparseTable(_dev(var, torch.float32, "var"), _dev(m, torch.float32, "m"),
+                             _dev(v, torch.float32, "v"), n_rows, dim, indices.numel(),
+                             _dev(indices, torch.int32, "indices"), _dev(grad_rows, torch.float32, "grad_rows"),
+                             _dev(mark, torch.int32, "mark"), _dev(gsum, torch.float32, "gsum"))
+    _check("hrec_adam_sparse_tables", lib().hrec_adam_sparse_tables(
+        arr, len(tables), float(lr), float(beta1), float(omb1), float(beta2), float(omb2), float(eps), _stream()))
 
 
 # --------------------------------------------------------- batched fusion

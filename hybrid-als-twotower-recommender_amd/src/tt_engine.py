@@ -132,11 +132,13 @@ class DeviceTwoTower:
         c = self.opt.coefficients(self.iterations)
         _hrec.adam_dense(self.dense, self.m_dense, self.v_dense, gd[: self.n_dense], c["dense_alpha"],
                          self.opt.b1, self.opt.b2, self.opt.eps)
-        for name, idx, g in (("user_emb", user, gu), ("item_emb", item, gi), ("man_emb", man, gm),
-                             ("cat_emb", cat, gc)):
-            gsum = torch.empty_like(g)
-            _hrec.adam_sparse(self.tensors[name], self.m_tab[name], self.v_tab[name], idx, g, self.mark[name],
-                              gsum, c["sparse_lr"], self.opt.b1, c["omb1"], self.opt.b2, c["omb2"], self.opt.eps)
+        # the four embedding tables' IndexedSlices updates in one grouped call
+        tabs = [(self.tensors[name], self.m_tab[name], self.v_tab[name], idx, g, self.mark[name],
+                 torch.empty_like(g))
+                for name, idx, g in (("user_emb", user, gu), ("item_emb", item, gi), ("man_emb", man, gm),
+                                     ("cat_emb", cat, gc))]
+        _hrec.adam_sparse_tables(tabs, c["sparse_lr"], self.opt.b1, c["omb1"], self.opt.b2, c["omb2"],
+                                 self.opt.eps)
         self.iterations += 1
         return gd[self.n_dense:]
 

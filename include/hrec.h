@@ -296,6 +296,28 @@ int hrec_adam_sparse(float* var, float* m, float* v, int64_t n_rows, int dim,
                      float one_minus_beta1, float beta2, float one_minus_beta2,
                      float epsilon, void* stream);
 
+/* hrec_adam_sparse over several tables in one set of launches (the four
+ * embedding tables of one Keras train step, src/two_tower_model.py:85,111):
+ * per table exactly hrec_adam_sparse's arithmetic; 3 launches in total
+ * instead of 3 per table. At most HREC_MAX_SPARSE_TABLES tables. */
+#define HREC_MAX_SPARSE_TABLES 8
+typedef struct hrec_sparse_table {
+  float* var;
+  float* m;
+  float* v;
+  int64_t n_rows;
+  int32_t dim;
+  int32_t batch;
+  const int32_t* indices;
+  const float* grad_rows;
+  int32_t* mark;
+  float* gsum;
+} hrec_sparse_table;
+
+int hrec_adam_sparse_tables(const hrec_sparse_table* tables, int n_tables, float lr,
+                            float beta1, float one_minus_beta1, float beta2,
+                            float one_minus_beta2, float epsilon, void* stream);
+
 /* ---------------------------------------------------------------------
  * Matrix-core dot-product scoring + fused top-k (csrc/dot_topk.hip).
  * Replaces Keras Dot(axes=1) over every candidate in model.predict

@@ -286,6 +286,35 @@ def test_sparse_adam_dedup_order(device, B, dim, n_rows):
     assert (mark.cpu().numpy() == -1).all()  # unmarked again for the next step
 
 
+def test_sparse_adam_grouped_matches_per_table(device):
+    """hrec_adam_sparse_tables (3 launches for all tables) == hrec_adam_sparse
+    per table, bit for bit, incl. an empty batch and mixed row widths."""
+    from src import _hrec as h
+
+    rng = np.random.default_rng(21)
+    shapes = [(1000, 64, 256), (300, 64, 256), (40, 8, 256), (7, 8, 0)]
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    runs = []
+    for _ in range(2):
+        runs.append([])
+    for n_rows, dim, B in shapes:
+        var = rng.normal(size=(n_rows, dim)).astype(np.float32)
+        m = rng.normal(size=(n_rows, dim)).astype(np.float32)
+        v = rng.uniform(0, 1, size=(n_rows, dim)).astype(np.float32)
+        idx = rng.integers(0, n_rows, B).astype(np.int32)
+        g = rng.normal(size=(B, dim)).astype(np.float32)
+        for run in runs:
+            run.append((T(var), T(m), T(v), T(idx), T(g), T(np.full(n_rows, -1, np.int32)),
+                        torch.empty((B, dim), dtype=torch.float32, device=device)))
+    coef = (1e-3, 0.9, 0.1, 0.999, 1e-3, 1e-7)
+    for tab in runs[0]:
+        h.adam_sparse(*tab, *coef)
+    h.adam_sparse_tables(runs[1], *coef)
+    for a_, b_ in zip(runs[0], runs[1]):
+        for j in (0, 1, 2, 5):  # var, m, v, mark
+            assert torch.equal(a_[j], b_[j])
+
+
 def _tt_frame(rng, n, nu, ni, nm, nc):
     return pd.DataFrame({
         "userId": rng.integers(0, nu, n), "itemId": rng.integers(0, ni, n),
