@@ -437,6 +437,14 @@ def main():
         with open(args.traffic_json) as f:
             traffic = json.load(f)["als_half_sweep"].get("hbm_bytes_avg_per_launch")
 
+    if tt_train is not None and args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tsw = json.load(f).get("tt_adam_sweep", {})
+        tt_train["roofline"]["traffic"] = tsw.get("hbm_bytes_avg_per_launch_corrected")
+        tt_train["roofline"]["traffic_note"] = (
+            "HBM bytes per launch of the grouped whole-table Adam sweep (adam_sparse_group4_kernel, rocprofv3 "
+            "FETCH_SIZE x2 + WRITE_SIZE, scripts/gpu_profile.sh); achieved above is the whole step's")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(eng, cfg, min(args.cpu_user_rows, n_users), min(args.cpu_item_rows, n_items))

@@ -70,6 +70,25 @@ def main(base):
         if f:
             v["hbm_read_bytes_avg_per_launch_corrected"] = 2 * 1024 * sum(f) / len(f)
     res["dot_topk_c4_filter"] = dot
+    # two-tower train step: grouped whole-table Adam sweep (all 4 tables per
+    # launch; 1.69 GB algorithmic per launch at c2's tables, d = 64)
+    tk = "adam_sparse_group4_kernel"
+    td = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace if tk in r["Kernel_Name"]]
+    tt = {"launches": len(td), "avg_ms": sum(td) / max(len(td), 1)}
+    for name, sub in (("FETCH_SIZE", "prof_fetch_tt"), ("WRITE_SIZE", "prof_write_tt")):
+        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(base, sub, "**", "*counter_collection.csv"))
+                if tk in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+        if vals:
+            tt[name + "_KiB_avg_per_launch"] = sum(vals) / len(vals)
+    if "FETCH_SIZE_KiB_avg_per_launch" in tt and "WRITE_SIZE_KiB_avg_per_launch" in tt:
+        tt["hbm_bytes_avg_per_launch_corrected"] = 1024 * (2 * tt["FETCH_SIZE_KiB_avg_per_launch"] +
+                                                           tt["WRITE_SIZE_KiB_avg_per_launch"])
+    res["tt_adam_sweep"] = tt
+    # JVM-exact ALS score + filter (the scoring half of the metric)
+    sd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace
+          if "als_score_fast_kernel<16, true>" in r["Kernel_Name"]]
+    if sd:
+        res["als_score_filter"] = {"launches": len(sd), "avg_ms": sum(sd) / len(sd)}
     wide = rows(os.path.join(base, "prof_wide", "**", "*kernel_trace.csv"))
     wd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in wide
           if "als_half_sweep_wide_kernel" in r["Kernel_Name"]]
