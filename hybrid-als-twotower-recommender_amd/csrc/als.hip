@@ -43,6 +43,9 @@
 #ifndef HREC_ALS_RLPANEL
 #define HREC_ALS_RLPANEL 0  // 1 = pivot-row entries by v_readlane, 2 = only the next pivot's (both measured slower)
 #endif
+#ifndef HREC_ALS_DIAG4
+#define HREC_ALS_DIAG4 0  // 1/2: diagonal Gramian tiles as 3 x v_mfma_f64_4x4x4_4b (measured slower)
+#endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
 #endif
@@ -144,6 +147,16 @@ __device__ __forceinline__ double f32_to_f64_int(float x) {
 __device__ __forceinline__ double gram_cvt(float x) {
   if constexpr (HREC_ALS_INTCVT) return f32_to_f64_int(x);
   return (double)x;
+}
+
+// x of lane (l & 48) | ((l + 16 - N) & 15): a rotation inside each 16-lane
+// row (DPP row_ror:N on both halves of the double).
+template <int N>
+__device__ __forceinline__ double row_ror(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)v, 0x120 + N, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), 0x120 + N, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
 // Wave-uniform broadcast of lane `src`'s double (two v_readlane_b32).
@@ -268,6 +281,37 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
 #pragma unroll
   for (int s = 0; s < PF; ++s) ring[s] = struct_load<NT>(rsrc, bperm(iw0, s), voff);
   int nidx = bperm(iw0, PF);  // source row of the next gather (one step ahead)
+  // DIAG4: a diagonal tile's 16 x 16 block is 16 sub-blocks of 4 x 4, of
+  // which 10 are distinct (symmetry). v_mfma_f64_4x4x4_4b runs 4 independent
+  // 4 x 4 x 4 blocks at the 16x16x4 rate (16 vs 64 cycles, measured:
+  // scripts/micro/mfma_f64_rate.hip); with A = B = the lane's operand it
+  // yields the 4 diagonal sub-blocks (b, b), with B rotated by 4 / 8 lanes
+  // inside each 16-lane row the sub-blocks (b, b + 1) and (b, b + 2) mod 4:
+  // all 10, in 3/4 of the 16x16x4 time.
+  // DIAG4 = 1 rotates with DPP moves at the step itself; DIAG4 = 2 converts
+  // the next step's operands one step ahead and rotates them by ds_bpermute
+  // (LDS path), so the rotations have a whole step to land.
+  constexpr bool kDiag4 = HREC_ALS_DIAG4 && MODE == 0;
+  constexpr bool kAhead = HREC_ALS_DIAG4 == 2 && MODE == 0;
+  double dg[NT][3];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dg[t][0] = dg[t][1] = dg[t][2] = 0.0;
+  const int ra1 = 4 * ((lane & 48) | ((lane + 4) & 15)), ra2 = 4 * ((lane & 48) | ((lane + 8) & 15));
+  auto bperm64 = [](double x, int addr) {
+    const long long v = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)v);
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(v >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+  };
+  double an[NT], r1n[NT], r2n[NT];  // kAhead: the next step's operands
+  if constexpr (kAhead) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      an[t] = gram_cvt(ring[0].x[t]);
+      r1n[t] = bperm64(an[t], ra1);
+      r2n[t] = bperm64(an[t], ra2);
+    }
+  }
   for (int64_t w = 0;; ++w) {
     int iw2;
     float rw2;
@@ -281,10 +325,28 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         break;
       }
       const Vec<NT> cur = ring[s % PF];
-      double a[NT];
+      double a[NT], ar1[NT], ar2[NT];
+      if constexpr (kAhead) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) a[t] = gram_cvt(cur.x[t]);
+        for (int t = 0; t < NT; ++t) {
+          a[t] = an[t];
+          ar1[t] = r1n[t];
+          ar2[t] = r2n[t];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) a[t] = gram_cvt(cur.x[t]);
+      }
       ring[s % PF] = struct_load<NT>(rsrc, nidx, voff);
+      if constexpr (kAhead) {
+        const Vec<NT> nx = ring[(s + 1) % PF];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          an[t] = gram_cvt(nx.x[t]);
+          r1n[t] = bperm64(an[t], ra1);
+          r2n[t] = bperm64(an[t], ra2);
+        }
+      }
       nidx = (s + 1 + PF < 16) ? bperm(iw0, s + 1 + PF) : bperm(iw1, s + 1 + PF - 16);
       const float rf = __int_as_float(__builtin_amdgcn_ds_bpermute(bp_addr + 16 * s, __float_as_int(rw0)));
       const double rv = gram_cvt(rf);
@@ -297,10 +359,19 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
       for (int I = 0; I < NT; ++I) {
 #pragma unroll
         for (int J = I; J < NT; ++J) {
-          if (MODE == 0)
-            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
-          else
+          if (MODE == 0) {
+            if (kDiag4 && I == J) {
+              dg[I][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], a[I], dg[I][0], 0, 0, 0);
+              dg[I][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], kAhead ? ar1[I] : row_ror<12>(a[I]), dg[I][1], 0,
+                                                            0, 0);
+              dg[I][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], kAhead ? ar2[I] : row_ror<8>(a[I]), dg[I][2], 0,
+                                                            0, 0);
+            } else {
+              acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
+            }
+          } else {
             fa[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x[I], cur.x[J], fa[p], 0, 0, 0);
+          }
           ++p;
         }
       }
@@ -319,6 +390,26 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
     rw0 = rw1;
     iw1 = iw2;
     rw1 = rw2;
+  }
+  if constexpr (kDiag4) {
+    // 4x4x4 block C[i][j] of block q sits at lane 16 i + 4 q + j and holds
+    // G[4q + i][4((q + s) & 3) + j] for rotation s; write it and its mirror
+    // into a 16 x 16 LDS image, read back the 16x16x4 C layout (one pass per
+    // diagonal tile and row)
+    const int i4 = lane >> 4, q4 = (lane >> 2) & 3, j4 = lane & 3;
+#pragma unroll
+    for (int I = 0, p = 0; I < NT; p += NT - I, ++I) {
+#pragma unroll
+      for (int sh = 0; sh < 3; ++sh) {
+        const int r = 4 * q4 + i4, c = 4 * ((q4 + sh) & 3) + j4;
+        stage[r * 16 + c] = dg[I][sh];
+        stage[c * 16 + r] = dg[I][sh];
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[p][rr] = stage[(sub + 4 * rr) * 16 + col];
+      wave_lds_sync();
+    }
   }
   } else {
   int i0, i1;
