@@ -632,7 +632,10 @@ __global__ __launch_bounds__(256) void fuse_rows_kernel(const float* __restrict_
 //   3. kk rounds of a wave arg-best over the candidates (key desc, index asc)
 //      -> [row][seg*kk] (value, index).
 constexpr int kFuseK = 8;
-constexpr int kFusePer = 16;
+#ifndef HREC_FUSE_PER
+#define HREC_FUSE_PER 16
+#endif
+constexpr int kFusePer = HREC_FUSE_PER;  // items per lane per segment
 constexpr int kFuseSeg = 64 * kFusePer;
 
 __device__ __forceinline__ uint64_t order_key(double v) {
