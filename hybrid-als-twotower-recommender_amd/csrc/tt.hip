@@ -140,6 +140,9 @@ __global__ __launch_bounds__(kBlock) void tt_score_kernel(const float* __restric
 // items per 256-thread block, the d axis staged through LDS in chunks of 64
 // (rows padded to 65 floats: conflict-free column reads).
 typedef float f4v __attribute__((ext_vector_type(4)));
+#ifndef HREC_TT_SCORE_DIRECT
+#define HREC_TT_SCORE_DIRECT 0  // 1 = scores stored from the MFMA C layout (measured slower: hybrid 0.31 -> 0.32 ms)
+#endif
 __global__ __launch_bounds__(256) void tt_score_mfma_kernel(const float* __restrict__ U, int B,
                                                             const float* __restrict__ V, int64_t N, int d,
                                                             float* __restrict__ out) {
@@ -172,6 +175,20 @@ __global__ __launch_bounds__(256) void tt_score_mfma_kernel(const float* __restr
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
         }
       }
+    }
+    if constexpr (HREC_TT_SCORE_DIRECT) {
+      // straight from the C layout: lane holds users 16w + 4(lane>>4) + r,
+      // item 16t + (lane & 15) -> 64-B runs per user row, no LDS round trip
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int64_t j = j0 + 16 * t + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int b = b0 + 16 * w + 4 * (lane >> 4) + r;
+          if (b < B && j < N) out[(int64_t)b * N + j] = acc[t][r];
+        }
+      }
+      continue;
     }
     // stage the 64 x 64 tile in LDS (over Us), then write each user's 64
     // items as 256 contiguous bytes (16 lanes x float4)
