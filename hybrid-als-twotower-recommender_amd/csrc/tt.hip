@@ -230,6 +230,81 @@ __global__ __launch_bounds__(256) void tt_score_mfma_kernel(const float* __restr
   }
 }
 
+// The same products in the same k order (one exact f32 fma chain over k per
+// score, so bit-identical), staged with 16-B loads (d % 4 == 0, 16-B aligned
+// rows): 4 instead of 16 staging iterations per tile and array, and rows
+// padded to 66 floats so the operand reads (row + 4 ks + g) hit 32 distinct
+// banks per 32-lane half.
+#ifndef HREC_TT_SCORE_V2
+#define HREC_TT_SCORE_V2 1
+#endif
+constexpr int kTs2 = 66;
+__global__ __launch_bounds__(256) void tt_score_mfma2_kernel(const float* __restrict__ U, int B,
+                                                             const float* __restrict__ V, int64_t N, int d,
+                                                             float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float Us[64 * kTs2];
+  __shared__ __attribute__((aligned(16))) float Vs[64 * kTs2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * 64;
+  const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  auto stage = [&](float* dst, const float* __restrict__ src, int64_t row0, int64_t nrows, int k0) {
+    for (int o = threadIdx.x; o < 64 * 16; o += 256) {
+      const int r = o >> 4, c4 = (o & 15) * 4;
+      const int kk = k0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row0 + r < nrows && kk < d) v = *reinterpret_cast<const float4*>(src + (row0 + r) * d + kk);
+      float2* p = reinterpret_cast<float2*>(dst + r * kTs2 + c4);
+      p[0] = make_float2(v.x, v.y);
+      p[1] = make_float2(v.z, v.w);
+    }
+  };
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    f4v acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < d; k0 += 64) {
+      __syncthreads();  // the previous tile's readers are done with Us/Vs
+      stage(Us, U, b0, B, k0);
+      if (b0 == 0 || d > 64) stage(Vs, V, j0, N, k0);
+      __syncthreads();
+#pragma unroll 4
+      for (int ks = 0; ks < 16; ++ks) {
+        const float a = Us[(16 * w + (lane & 15)) * kTs2 + 4 * ks + (lane >> 4)];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float b = Vs[(16 * t + (lane & 15)) * kTs2 + 4 * ks + (lane >> 4)];
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Us[(16 * w + 4 * (lane >> 4) + r) * kTs2 + 16 * t + (lane & 15)] = acc[t][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = q * 256 + threadIdx.x;
+      const int row = o >> 4, c4 = (o & 15) * 4;
+      const int b = b0 + row;
+      const int64_t j = j0 + c4;
+      if (b >= B) continue;
+      const float2* p = reinterpret_cast<const float2*>(Us + row * kTs2 + c4);
+      const float2 x0 = p[0], x1 = p[1];
+      float* dst = out + (int64_t)b * N + j;
+      if (vec && j + 3 < N) {
+        *reinterpret_cast<float4*>(dst) = make_float4(x0.x, x0.y, x1.x, x1.y);
+      } else {
+        const float xs[4] = {x0.x, x0.y, x1.x, x1.y};
+        for (int e = 0; e < 4; ++e)
+          if (j + e < N) dst[e] = xs[e];
+      }
+    }
+  }
+}
+
 // Paired dot: out[r] = <U[r], V[r]> (model.predict on per-row inputs).
 __global__ __launch_bounds__(kBlock) void tt_pair_score_kernel(const float* __restrict__ U,
                                                                const float* __restrict__ V, int64_t n, int d,
@@ -679,6 +754,11 @@ extern "C" int hrec_tt_score(const float* user_vec, int n_users, const float* it
     return check_launch("tt_score_kernel");
   }
   HREC_REQUIRE((n_items + 63) / 64 < (1ll << 32), "tt_score: grid too large");
+  if (HREC_TT_SCORE_V2 && d % 4 == 0 && (((uintptr_t)user_vec | (uintptr_t)item_vec) & 15) == 0) {
+    hipLaunchKernelGGL(tt_score_mfma2_kernel, dim3((unsigned)((n_items + 63) / 64)), dim3(256), 0,
+                       as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
+    return check_launch("tt_score_mfma2_kernel");
+  }
   hipLaunchKernelGGL(tt_score_mfma_kernel, dim3((unsigned)((n_items + 63) / 64)),
                      dim3(256), 0, as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
   return check_launch("tt_score_mfma_kernel");

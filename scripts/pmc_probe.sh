@@ -1,0 +1,26 @@
+# PMC passes (one rocprofv3 --pmc run per counter group) over a probe script,
+# averaged per dispatch of one kernel:  bash scripts/pmc_probe.sh <kernel-substring> <python script> [args]
+set -e
+K=$1; shift
+mkdir -p gpurun_out/pmcp
+export TMPDIR=/tmp
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmcp/p$i -o p$i -- python "$@" > gpurun_out/pmcp/p$i.log 2>&1
+done
+python - "$K" <<'PY'
+import csv, glob, sys, collections
+k = sys.argv[1]
+agg = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/pmcp/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if k in r.get("Kernel_Name", ""):
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for c in sorted(agg):
+    v = agg[c]
+    print(f"{c:28s} n={len(v):3d} avg={sum(v)/len(v):.4g}")
+PY
