@@ -637,6 +637,10 @@ constexpr int kFuseK = 8;
 #endif
 constexpr int kFusePer = HREC_FUSE_PER;  // items per lane per segment
 constexpr int kFuseSeg = 64 * kFusePer;
+#ifndef HREC_FUSE_RANK
+#define HREC_FUSE_RANK 1  // selections by rank among <= 64 entries (LDS broadcast reads) instead of arg-best rounds
+#endif
+constexpr bool kFuseRank = HREC_FUSE_RANK;
 
 __device__ __forceinline__ uint64_t order_key(double v) {
   if (v != v) return 0;  // NaN ranks below every number
@@ -729,11 +733,42 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
   }
   KI mine{bk, nmine > 0 ? seg0 + (int64_t)be * 64 + lane : INT64_MAX};
   KI t{0, INT64_MAX};
-  for (int q = 0; q < KK; ++q) {
-    const KI w = wave_best_ki(mine);
-    if (w.i == INT64_MAX) break;
-    t = w;
-    if (w.i == mine.i) mine.i = INT64_MAX;
+  if constexpr (kFuseRank) {
+    // t = the min(kk, live lanes)-th best lane maximum, by each lane's RANK
+    // among the 64 maxima (one pass of broadcast LDS reads, no dependent
+    // cross-lane rounds); in-segment positions order equal keys
+    const int mpos = nmine > 0 ? be * 64 + lane : -1;
+    ck_sh[wv][64 + lane] = bk;
+    ce_sh[wv][64 + lane] = mpos;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int rank = 0;
+#pragma unroll 8
+    for (int q = 0; q < 64; ++q) {
+      const uint64_t ok = ck_sh[wv][64 + q];
+      const int op = ce_sh[wv][64 + q];
+      rank += (op >= 0 && (mpos < 0 || ok > bk || (ok == bk && op < mpos))) ? 1 : 0;
+    }
+    const int nvl = __popcll(__ballot(mpos >= 0));
+    const int target = (nvl < KK ? nvl : KK) - 1;
+    const uint64_t hit = __ballot(mpos >= 0 && rank == target);
+    if (hit) {
+      const int src = __builtin_ctzll(hit);
+      t.k = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(bk >> 32), src) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)bk, src);
+      t.i = seg0 + __builtin_amdgcn_readlane(mpos, src);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    for (int q = 0; q < KK; ++q) {
+      const KI w = wave_best_ki(mine);
+      if (w.i == INT64_MAX) break;
+      t = w;
+      if (w.i == mine.i) mine.i = INT64_MAX;
+    }
   }
   // 2. candidates: items not worse than t (no t: fewer than kk items, take all)
   int nc = 0;
@@ -760,6 +795,26 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (kFuseRank) {
+      // each candidate's rank among the nc candidates = its output slot
+      const uint64_t mk = lane < nc ? ck_sh[wv][lane] : 0;
+      const int mp = lane < nc ? ce_sh[wv][lane] : 0;
+      int rank = 0;
+      for (int q = 0; q < nc; ++q) {
+        const uint64_t ok = ck_sh[wv][q];
+        const int op = ce_sh[wv][q];
+        rank += (ok > mk || (ok == mk && op < mp)) ? 1 : 0;
+      }
+      if (lane < nc && rank < KK) {
+        cand_v[obase + rank] = key_value(mk);
+        cand_i[obase + rank] = seg0 + mp;
+      }
+      if (lane >= nc && lane < KK) {  // fewer candidates than kk: empty slots
+        cand_v[obase + lane] = key_value(0);
+        cand_i[obase + lane] = -1;
+      }
+      return;
+    }
     KI c{0, INT64_MAX};
     if (lane < nc) c = KI{ck_sh[wv][lane], seg0 + ce_sh[wv][lane]};
     for (int q = 0; q < KK; ++q) {
