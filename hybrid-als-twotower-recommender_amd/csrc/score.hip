@@ -1045,7 +1045,10 @@ extern "C" int hrec_cosine_sim(const double* feats, int64_t n_items, int dim, co
 #define HREC_SCORE_UB 16
 #endif
 static constexpr int kScoreUB = HREC_SCORE_UB;
-static constexpr int kSample = 2048;
+#ifndef HREC_SCORE_SAMPLE
+#define HREC_SCORE_SAMPLE 2048
+#endif
+static constexpr int kSample = HREC_SCORE_SAMPLE;  // items scored for the survivor bound
 static constexpr int kSampleUB = 4;
 static constexpr int kCap = 4096;
 
