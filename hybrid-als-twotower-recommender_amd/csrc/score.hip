@@ -7,6 +7,9 @@
 
 namespace hrec {
 
+#ifndef HREC_SCORE_PAIR_STORE
+#define HREC_SCORE_PAIR_STORE 1  // full-row JVM-exact scores: 8-B stores of item pairs
+#endif
 constexpr int kScoreKMax = 256;  // widest factor row (rank 256)
 
 // --------------------------------------------------------------- ALS score
@@ -160,11 +163,21 @@ __global__ __launch_bounds__(256) void als_score_fast_kernel(
   }
   if (!FILTER) {
     const float qnan = __builtin_nanf("");
+    // pairs (j, j + 1) as one 8-B store when rows are 8-B aligned: a wave
+    // then writes 512 contiguous bytes per instruction
+    const bool pair = HREC_SCORE_PAIR_STORE && (n_items % 2 == 0) && ((reinterpret_cast<uintptr_t>(out) & 7) == 0);
 #pragma unroll
     for (int b = 0; b < UB; ++b) {
       if (b0 + b >= n_users) break;
       float* o = out + (int64_t)(b0 + b) * n_items;
       const bool ok = uok[b];
+      if (pair) {
+        if (j0 + 1 < n_items) *reinterpret_cast<float2*>(o + j0) = ok ? make_float2(acc0[b].x, acc0[b].y)
+                                                                        : make_float2(qnan, qnan);
+        if (j1 + 1 < n_items) *reinterpret_cast<float2*>(o + j1) = ok ? make_float2(acc1[b].x, acc1[b].y)
+                                                                        : make_float2(qnan, qnan);
+        continue;
+      }
       if (j0 < n_items) o[j0] = ok ? acc0[b].x : qnan;
       if (j0 + 1 < n_items) o[j0 + 1] = ok ? acc0[b].y : qnan;
       if (j1 < n_items) o[j1] = ok ? acc1[b].x : qnan;
