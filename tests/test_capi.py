@@ -45,6 +45,14 @@ def test_invalid_arguments_fail_loudly_without_gpu():
                                  ctypes.c_double(0.1), 0, None, None)
     assert rc == -1
     assert b"kp must be 16, 32, 64, 96, 128, 192 or 256" in lib.hrec_last_error()
+    # grouped sparse Adam: the table count is checked before any device work
+    f = lib.hrec_adam_sparse_tables
+    f.restype = ctypes.c_int
+    args = [ctypes.c_float(0.001), ctypes.c_float(0.9), ctypes.c_float(0.1), ctypes.c_float(0.999),
+            ctypes.c_float(0.001), ctypes.c_float(1e-7), None]
+    assert f(None, 9, *args) == -1
+    assert b"tables" in lib.hrec_last_error()
+    assert f(None, 0, *args) == 0  # nothing to update
 
 
 def test_product_has_no_oracle_imports():
