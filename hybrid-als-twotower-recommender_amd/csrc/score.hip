@@ -912,6 +912,8 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
           HREC_TOPK_WAVE(2);
         else if (kk <= 4)
           HREC_TOPK_WAVE(4);
+        else if (kk == 5)  // the reference's default top_k: 5-deep lane lists
+          HREC_TOPK_WAVE(5);
         else if (kk <= 8)
           HREC_TOPK_WAVE(8);
         else
