@@ -38,6 +38,13 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
               T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr,
               const int* row_n = nullptr);
 
+// Stable descending top-k by a full per-row radix sort (csrc/sort_topk.hip),
+// for top_k above the selection kernels' 1024; rows * n < 2^31.
+size_t sort_topk_ws_bytes(int64_t n_rows, int64_t n);
+template <typename T>
+int sort_topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
+                   T* out_val, void* ws, size_t ws_bytes, hipStream_t s);
+
 // splitmix64 finaliser; host and device identical (integer only).
 __host__ __device__ inline uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;

@@ -255,6 +255,7 @@ __device__ __forceinline__ KV<T> wave_best(KV<T> x) {
 constexpr int kTopkBlock = 256;
 constexpr int kTopkPer = 16;  // elements per thread per segment
 constexpr int kTopkSeg = kTopkBlock * kTopkPer;
+constexpr int kTopkSelectMax = 1024;  // larger top_k: the sort path (csrc/sort_topk.hip)
 
 // Stage 1: rows x segments; each block selects the top `kk` of its segment
 // of one row by kk rounds of block arg-best over elements held in registers.
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(256) void minmax_partial_kernel(const double* __res
 // coef = {als_scale, als_min_, tt_scale, tt_min_} as doubles (the tt pair is
 // the exact f32 values widened when tt_f32).
 __global__ void minmax_final_kernel(const double* __restrict__ part, int nparts, int tt_f32,
-                                    double* __restrict__ coef) {
+                                    double* __restrict__ coef, double* __restrict__ out_minmax) {
   if (threadIdx.x != 0) return;
   double amin = DBL_MAX, amax = -DBL_MAX, tmin = DBL_MAX, tmax = -DBL_MAX;
   for (int q = 0; q < nparts; ++q) {
@@ -476,6 +477,12 @@ __global__ void minmax_final_kernel(const double* __restrict__ part, int nparts,
     amax = fmax(amax, part[4 * q + 1]);
     tmin = fmin(tmin, part[4 * q + 2]);
     tmax = fmax(tmax, part[4 * q + 3]);
+  }
+  if (out_minmax) {  // the fitted MinMaxScalers' data_min_ / data_max_ (src/hybrid_system.py:66-67)
+    out_minmax[0] = amin;
+    out_minmax[1] = amax;
+    out_minmax[2] = tmin;
+    out_minmax[3] = tmax;
   }
   double arange = amax - amin;
   if (arange < 10.0 * DBL_EPSILON) arange = 1.0;
@@ -874,15 +881,21 @@ __global__ void add_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t 
 
 using namespace hrec;
 
-// Workspace for a stable top-k of n_rows rows of n elements (bytes).
+// Workspace for a stable top-k of n_rows rows of n elements (bytes) by the
+// segment selections (kk <= kTopkSelectMax). Each pass keeps kk of every
+// kTopkSeg elements, so it shrinks the row only while kk < kTopkSeg / 2; the
+// loop stops as soon as a pass would not shrink it (larger kk go through the
+// sort path, csrc/sort_topk.hip).
 namespace hrec {
 size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
   size_t total = 0;
   int64_t m = n;
+  if (kk < 1 || kk > kTopkSelectMax) return 256;
   while (true) {
     const int64_t segs = (m + kTopkSeg - 1) / kTopkSeg;
     if (segs <= 1) break;
     const int64_t cand = segs * kk;
+    if (cand >= m) break;
     total += (size_t)n_rows * (size_t)cand * (elem + 8);
     m = cand;
   }
@@ -977,18 +990,24 @@ extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_row
 }
 
 extern "C" size_t hrec_topk_workspace_bytes(int64_t n_rows, int64_t n, int top_k, int is_f64) {
-  return topk_ws_bytes(n_rows, n, top_k, is_f64 ? 8 : 4);
+  const int64_t kk = top_k < n ? top_k : n;
+  if (kk > kTopkSelectMax) return sort_topk_ws_bytes(n_rows, n);
+  return topk_ws_bytes(n_rows, n, (int)kk, is_f64 ? 8 : 4);
 }
 
 extern "C" int hrec_topk_f32(const float* vals, int64_t n_rows, int64_t n, int64_t row_stride, int top_k,
                              int64_t* out_idx, float* out_val, void* workspace, size_t workspace_bytes,
                              void* stream) {
   HREC_REQUIRE(n_rows >= 0 && n >= 0 && row_stride >= n, "topk_f32: bad shape");
-  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "topk_f32: top_k must be in [1, 1024]");
-  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(top_k >= 1, "topk_f32: top_k must be >= 1");
+  if (n_rows == 0 || n == 0) return HREC_OK;
   HREC_REQUIRE(n_rows < 65536, "topk_f32: at most 65535 rows per call");
   HREC_REQUIRE(vals && out_idx && out_val, "topk_f32: null pointer");
-  return topk_rows<float>(vals, n_rows, n, row_stride, top_k, out_idx, out_val, workspace, workspace_bytes,
+  const int kk = (int)(top_k < n ? top_k : n);
+  if (kk > kTopkSelectMax)
+    return sort_topk_rows<float>(vals, n_rows, n, row_stride, kk, out_idx, out_val, workspace, workspace_bytes,
+                                as_stream(stream));
+  return topk_rows<float>(vals, n_rows, n, row_stride, kk, out_idx, out_val, workspace, workspace_bytes,
                           as_stream(stream));
 }
 
@@ -996,25 +1015,31 @@ extern "C" int hrec_topk_f64(const double* vals, int64_t n_rows, int64_t n, int6
                              int64_t* out_idx, double* out_val, void* workspace, size_t workspace_bytes,
                              void* stream) {
   HREC_REQUIRE(n_rows >= 0 && n >= 0 && row_stride >= n, "topk_f64: bad shape");
-  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "topk_f64: top_k must be in [1, 1024]");
-  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(top_k >= 1, "topk_f64: top_k must be >= 1");
+  if (n_rows == 0 || n == 0) return HREC_OK;
   HREC_REQUIRE(n_rows < 65536, "topk_f64: at most 65535 rows per call");
   HREC_REQUIRE(vals && out_idx && out_val, "topk_f64: null pointer");
-  return topk_rows<double>(vals, n_rows, n, row_stride, top_k, out_idx, out_val, workspace, workspace_bytes,
+  const int kk = (int)(top_k < n ? top_k : n);
+  if (kk > kTopkSelectMax)
+    return sort_topk_rows<double>(vals, n_rows, n, row_stride, kk, out_idx, out_val, workspace, workspace_bytes,
+                                as_stream(stream));
+  return topk_rows<double>(vals, n_rows, n, row_stride, kk, out_idx, out_val, workspace, workspace_bytes,
                            as_stream(stream));
 }
 
 static constexpr int kMinmaxParts = 256;
 
 extern "C" size_t hrec_fuse_workspace_bytes(int64_t n, int top_k) {
-  return (size_t)kMinmaxParts * 4 * 8 + 64 + (size_t)n * 8 + topk_ws_bytes(1, n, top_k, 8);
+  const int64_t kk = top_k < n ? top_k : n;
+  const size_t t = kk > kTopkSelectMax ? sort_topk_ws_bytes(1, n) : topk_ws_bytes(1, n, (int)kk, 8);
+  return (size_t)kMinmaxParts * 4 * 8 + 64 + (size_t)n * 8 + t;
 }
 
 extern "C" int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, int64_t n, int als_wins,
                               int top_k, int64_t* out_idx, double* out_score, double* out_fused,
-                              void* workspace, size_t workspace_bytes, void* stream) {
+                              double* out_minmax, void* workspace, size_t workspace_bytes, void* stream) {
   HREC_REQUIRE(n >= 0, "fuse_topk: negative n");
-  HREC_REQUIRE(top_k >= 0 && top_k <= 1024, "fuse_topk: top_k must be in [0, 1024]");
+  HREC_REQUIRE(top_k >= 0, "fuse_topk: top_k must be >= 0");
   if (n == 0) return HREC_OK;
   HREC_REQUIRE(als && tt, "fuse_topk: null input");
   HREC_REQUIRE(top_k == 0 || (out_idx && out_score), "fuse_topk: null output");
@@ -1031,7 +1056,8 @@ extern "C" int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, 
   hipLaunchKernelGGL(minmax_partial_kernel, dim3(parts), dim3(256), 0, s, als, tt, tt_is_f32, n, part);
   int rc = check_launch("minmax_partial_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(minmax_final_kernel, dim3(1), dim3(64), 0, s, part, parts, tt_is_f32, coef);
+  hipLaunchKernelGGL(minmax_final_kernel, dim3(1), dim3(64), 0, s, part, parts, tt_is_f32, coef,
+                     out_minmax);
   rc = check_launch("minmax_final_kernel");
   if (rc) return rc;
   // src/hybrid_system.py:69 — strict '>' picks (0.8, 0.2), else (0.2, 0.8).
@@ -1041,6 +1067,7 @@ extern "C" int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, 
   rc = check_launch("fuse_kernel");
   if (rc || top_k == 0) return rc;
   const int kk = (int)(top_k < n ? top_k : n);
+  if (kk > kTopkSelectMax) return sort_topk_rows<double>(fused, 1, n, n, kk, out_idx, out_score, tws, tws_bytes, s);
   rc = topk_rows<double>(fused, 1, n, n, kk, out_idx, out_score, tws, tws_bytes, s);
   return rc;
 }

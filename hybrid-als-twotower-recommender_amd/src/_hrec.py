@@ -54,8 +54,8 @@ _SIGNATURES = {
                                      _vp, _c_sz, _vp]),
     "hrec_topk_f64_keyed": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_fuse_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
-    "hrec_fuse_topk": (_c_i32, [_vp, _vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_sz,
-                                _vp]),
+    "hrec_fuse_topk": (_c_i32, [_vp, _vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp,
+                                _c_sz, _vp]),
 }
 
 
@@ -333,8 +333,9 @@ def topk(vals, top_k):
 
 
 # ----------------------------------------------------------------- fusion
-def fuse_topk(als, tt, als_wins, top_k, want_fused=True):
-    """als: f64 [n]; tt: f32 or f64 [n] (device). Returns (idx, score, fused)."""
+def fuse_topk(als, tt, als_wins, top_k, want_fused=True, minmax=None):
+    """als: f64 [n]; tt: f32 or f64 [n] (device). Returns (idx, score, fused).
+    minmax (optional f64 [4] device tensor) receives (als min, als max, tt min, tt max)."""
     n = als.numel()
     dev = als.device
     tt_f32 = tt.dtype == torch.float32
@@ -347,7 +348,8 @@ def fuse_topk(als, tt, als_wins, top_k, want_fused=True):
     _check("hrec_fuse_topk", lib().hrec_fuse_topk(
         _dev(als, torch.float64, "als"), _dev(tt, tt.dtype, "tt"), int(tt_f32), n, int(bool(als_wins)),
         kk, _dev(out_i, torch.int64, "out_idx"), _dev(out_s, torch.float64, "out_score"),
-        _dev(fused, torch.float64, "out_fused"), _dev(ws, torch.uint8, "ws"), ws_bytes, _stream()))
+        _dev(fused, torch.float64, "out_fused"), _dev(minmax, torch.float64, "out_minmax"),
+        _dev(ws, torch.uint8, "ws"), ws_bytes, _stream()))
     return out_i[:kk], out_s[:kk], fused
 
 

@@ -25,9 +25,6 @@ from .two_tower_model import TwoTowerModel
 
 warnings.filterwarnings("ignore")
 
-_TOPK_MAX = 1024  # hrec_fuse_topk's top-k bound
-
-
 def _as_scores(values):
     """np.array(list) as the reference builds it, then the dtype
     MinMaxScaler computes in (ints/bools -> float64, float32 stays)."""
@@ -44,20 +41,39 @@ def _as_scores(values):
     return out
 
 
-def fuse_device(als_scores, tt_scores, als_wins, top_k, device=None, want_fused=True):
+def _set_fitted(scaler, lo, hi, n, dtype):
+    """Leave `scaler` in the state MinMaxScaler.fit_transform of an [n, 1]
+    column of `dtype` with min lo / max hi leaves it (the reference refits both
+    scalers per fusion, src/hybrid_system.py:66-67); the O(1) attribute
+    arithmetic is sklearn's (_data.py partial_fit, feature_range (0, 1))."""
+    dmin = np.array([lo], dtype=dtype)
+    dmax = np.array([hi], dtype=dtype)
+    drange = dmax - dmin
+    safe = drange.copy()
+    safe[safe < 10 * np.finfo(safe.dtype).eps] = 1.0
+    scaler.n_features_in_ = 1
+    scaler.n_samples_seen_ = int(n)
+    scaler.data_min_, scaler.data_max_, scaler.data_range_ = dmin, dmax, drange
+    scaler.scale_ = (1 - 0) / safe
+    scaler.min_ = 0 - dmin * scaler.scale_
+
+
+def fuse_device(als_scores, tt_scores, als_wins, top_k, device=None, want_fused=True, scalers=None):
     """Fusion + stable top-k on the device. Returns (fused f64 [n] or None,
-    top indices, top scores) as numpy arrays."""
+    top indices, top scores) as numpy arrays. `scalers` = (als_scaler,
+    tt_scaler) are left fitted as the reference's fit_transform leaves them."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     a = torch.as_tensor(als_scores, device=device)
     t = torch.as_tensor(tt_scores, device=device)
     n = a.numel()
     kk = n if top_k is None else (max(n + top_k, 0) if top_k < 0 else min(top_k, n))
-    dev_k = kk if kk <= _TOPK_MAX else 0
-    idx, sc, fused = _hrec.fuse_topk(a, t, als_wins, dev_k, want_fused=want_fused or kk > _TOPK_MAX)
+    mm = torch.empty(4, dtype=torch.float64, device=device) if scalers is not None else None
+    idx, sc, fused = _hrec.fuse_topk(a, t, als_wins, kk, want_fused=want_fused, minmax=mm)
     fused_np = fused.cpu().numpy() if fused is not None else None
-    if kk > _TOPK_MAX:  # beyond the device top-k bound: order the device-fused scores stably
-        order = np.argsort(-fused_np, kind="stable")[:kk]
-        return fused_np, order, fused_np[order]
+    if scalers is not None:
+        m = mm.cpu().numpy()
+        _set_fitted(scalers[0], m[0], m[1], n, np.float64)
+        _set_fitted(scalers[1], m[2], m[3], n, np.dtype(tt_scores.dtype))
     return fused_np, idx.cpu().numpy(), sc.cpu().numpy()
 
 
@@ -107,7 +123,8 @@ class HybridRecommendationSystem:
     def adaptive_fusion(self, als_predictions, twotower_predictions):
         try:
             items, als_scores, tt_scores = self._union(als_predictions, twotower_predictions)
-            fused, _, _ = fuse_device(als_scores, tt_scores, self.als_f1_score > self.twotower_f1_score, 0)
+            fused, _, _ = fuse_device(als_scores, tt_scores, self.als_f1_score > self.twotower_f1_score, 0,
+                                      scalers=(self.als_scaler, self.twotower_scaler))
             return [(item, fused[i]) for i, item in enumerate(items)]
         except Exception as e:
             print(f"Error in adaptive fusion: {str(e)}")
@@ -143,7 +160,8 @@ class HybridRecommendationSystem:
             try:
                 items, als_scores, tt_scores = self._union(als_preds, tt_preds)
                 fused, idx, sc = fuse_device(als_scores, tt_scores, self.als_f1_score > self.twotower_f1_score,
-                                             top_k, want_fused=save_predictions)
+                                             top_k, want_fused=save_predictions,
+                                             scalers=(self.als_scaler, self.twotower_scaler))
             except Exception as e:  # adaptive_fusion's own guard (:73-75) -> []
                 print(f"Error in adaptive fusion: {str(e)}")
                 items, fused, idx, sc = [], None, [], []

@@ -148,6 +148,25 @@ class DeviceTwoTower:
         out["__iterations__"] = np.array(self.iterations)
         return out
 
+    def optimizer_state(self):
+        """Adam slots (Keras save_model's include_optimizer=True part)."""
+        out = {"__opt_m_dense__": self.m_dense.cpu().numpy(), "__opt_v_dense__": self.v_dense.cpu().numpy()}
+        for n in TABLES:
+            out[f"__opt_m_{n}__"] = self.m_tab[n].cpu().numpy()
+            out[f"__opt_v_{n}__"] = self.v_tab[n].cpu().numpy()
+        return out
+
+    def load_optimizer_state(self, state):
+        """Restore what optimizer_state() saved (absent keys: slots stay zero)."""
+        if "__opt_m_dense__" not in state:
+            return False
+        self.m_dense.copy_(torch.as_tensor(state["__opt_m_dense__"]))
+        self.v_dense.copy_(torch.as_tensor(state["__opt_v_dense__"]))
+        for n in TABLES:
+            self.m_tab[n].copy_(torch.as_tensor(state[f"__opt_m_{n}__"]))
+            self.v_tab[n].copy_(torch.as_tensor(state[f"__opt_v_{n}__"]))
+        return True
+
     def snapshot(self):
         return {n: t.detach().clone() for n, t in self.tensors.items()}
 

@@ -173,6 +173,7 @@ class TwoTowerModel:
     def save_model(self, model_path="models/twotower.keras"):
         os.makedirs(os.path.dirname(model_path) or ".", exist_ok=True)
         state = self.model.state_dict()
+        state.update(self.model.optimizer_state())  # Keras saves the optimizer too (include_optimizer=True)
         meta = np.array([self.num_users, self.num_items, self.num_manufacturers, self.num_categories,
                          self.embedding_size], dtype=np.int64)
         with open(model_path, "wb") as f:
@@ -190,6 +191,7 @@ class TwoTowerModel:
         loaded_model = cls(nu, ni, nm, nc, d, float(state["__lr__"]))
         loaded_model.build_model(init={k: v for k, v in state.items() if not k.startswith("__")})
         loaded_model.model.iterations = int(state["__iterations__"])
+        loaded_model.model.load_optimizer_state(state)
         loaded_model.scaler = scaler
         loaded_model.is_trained = True
         return loaded_model
@@ -206,6 +208,12 @@ def hyperparameter_tuning(train_data, param_grid, val_size=0.2, random_state=42)
     val_users = rng.choice(train_users, size=int(len(train_users) * val_size), replace=False)
     train_sub = train_data[~train_data["userId"].isin(val_users)]
     val_sub = train_data[train_data["userId"].isin(val_users)]
+    # D4b: the reference sizes the tables by train_sub's distinct counts
+    # (:186-189), but ids index the tables: once the validation users are
+    # removed the largest user id is (almost surely) >= that count, Keras'
+    # lookup raises, every grid point is skipped (:232-234) and the function
+    # can only return None. Tables sized max(id) + 1 over train_data let the
+    # loop do what it is written for.
     num_users = int(train_data["userId"].max()) + 1
     num_items = int(train_data["itemId"].max()) + 1
     num_man = int(train_data["manufacturer_id"].max()) + 1

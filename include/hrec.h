@@ -166,7 +166,9 @@ int hrec_als_score_topk(const float* user_factors, const int64_t* user_rows,
  * vals + i*row_stride, n elements): larger value first, equal values keep
  * input order (smaller index first), NaN last — Python's
  * sorted(..., key=score, reverse=True)[:k] as used at
- * src/hybrid_system.py:108 and src/als_model.py:173. */
+ * src/hybrid_system.py:108 and src/als_model.py:173. Any top_k >= 1 (clamped
+ * to n): up to 1024 by segment selections, above by a stable per-row radix
+ * sort on the device (then n_rows * n < 2^31). */
 size_t hrec_topk_workspace_bytes(int64_t n_rows, int64_t n, int top_k, int is_f64);
 int hrec_topk_f32(const float* vals, int64_t n_rows, int64_t n, int64_t row_stride,
                   int top_k, int64_t* out_idx, float* out_val, void* workspace,
@@ -183,12 +185,15 @@ int hrec_topk_f64(const double* vals, int64_t n_rows, int64_t n, int64_t row_str
  * fused = w0*als_norm + w1*tt_norm in f64 with (w0,w1) = (0.8,0.2) when
  * als_wins (the strict als_f1 > tt_f1 of :69) else (0.2,0.8).
  * out_fused (optional, n doubles) receives every fused score; out_idx /
- * out_score receive the stable top min(top_k, n). */
+ * out_score receive the stable top min(top_k, n) (any top_k >= 0; 0 = no
+ * top-k). out_minmax (optional, 4 doubles) receives (als min, als max,
+ * tt min, tt max): the two scalers' data_min_ / data_max_ after the
+ * reference's fit_transform (src/hybrid_system.py:66-67). */
 size_t hrec_fuse_workspace_bytes(int64_t n, int top_k);
 int hrec_fuse_topk(const double* als, const void* tt, int tt_is_f32, int64_t n,
                    int als_wins, int top_k, int64_t* out_idx, double* out_score,
-                   double* out_fused, void* workspace, size_t workspace_bytes,
-                   void* stream);
+                   double* out_fused, double* out_minmax, void* workspace,
+                   size_t workspace_bytes, void* stream);
 
 /* Batched fusion for many users over one item range (a shard of the item
  * set when the item rows are split across GPUs):

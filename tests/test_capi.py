@@ -63,3 +63,38 @@ def test_product_has_no_oracle_imports():
                 with open(os.path.join(dirpath, f)) as fh:
                     src = fh.read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+
+
+def test_facade_reexports_reference_classes():
+    """src/__init__.py:39-42 of the reference: `from src import ...` works."""
+    import src
+    from src import ALSModel, HybridRecommendationSystem, RecommenderEvaluator, TwoTowerModel
+
+    assert src.__all__ == ["HybridRecommendationSystem", "ALSModel", "TwoTowerModel", "RecommenderEvaluator"]
+    assert ALSModel.__module__ == "src.als_model"
+    assert TwoTowerModel.__module__ == "src.two_tower_model"
+    assert HybridRecommendationSystem.__module__ == "src.hybrid_system"
+    assert RecommenderEvaluator.__module__ == "src.evaluation"
+
+
+def test_topk_workspace_query_terminates_for_large_k():
+    """the workspace query looped forever for top_k > 2048; any
+    top_k is now accepted (above 1024 by the device sort path)."""
+    import __graft_entry__ as g
+
+    lib = ctypes.CDLL(g.build_lib())
+    for fn in ("hrec_topk_workspace_bytes",):
+        f = getattr(lib, fn)
+        f.restype = ctypes.c_size_t
+        f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+        for n, k in ((5000, 3000), (100000, 3000), (100000, 5000), (100000, 1500), (100000, 1024), (10, 3000)):
+            assert f(1, n, k, 1) > 0
+            assert f(4, n, k, 0) > 0
+    f = lib.hrec_fuse_workspace_bytes
+    f.restype = ctypes.c_size_t
+    f.argtypes = [ctypes.c_int64, ctypes.c_int]
+    assert f(100000, 5000) > 100000 * 8
+    f = lib.hrec_fuse_rows_workspace_bytes
+    f.restype = ctypes.c_size_t
+    f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+    assert f(2, 100000, 3000) > 0
