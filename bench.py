@@ -42,6 +42,9 @@ F64_MFMA_PEAK_TFLOPS = 78.6  # AMD MI355X spec (FP64 matrix); not in MI355X_MICR
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA = f32 VALU peak (64 flop/clk/SIMD)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+# JVM-exact scoring forbids FMA: one v_pk_mul_f32 + one v_pk_add_f32 per 2
+# products -> half the 157.3 TF FMA rate (measured issue rate 60 T)
+F32_VALU_MULADD_TFLOPS = 78.6
 
 CONFIGS = {
     "c2": dict(users=1_000_000, items=100_000, density=0.005, rank=64),
@@ -59,11 +62,72 @@ def algo_bytes(nnz, n_dst, k):
     return nnz * (4 + 4 + 4 * k) + (n_dst + 1) * 8 + n_dst * k * 4
 
 
+def ev_time(fn, reps, stream):
+    """Average ms of fn() over reps, HIP events on the stream fn launches on."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def roofline(bound, work, ms, peak, unit, kernel, **extra):
+    """work = algorithmic flops or bytes of ONE launch of `kernel`; ms = its
+    average launch duration (HIP events)."""
+    ach = work / (ms / 1e3) / (1e12 if unit == "TFLOP/s" else 1e9)
+    out = {"kernel": kernel, "bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
+           "avg_launch_ms": ms, ("algorithmic_flops" if unit == "TFLOP/s" else "algorithmic_bytes"): work}
+    out.update(extra)
+    return out
+
+
+def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
+    """W = 1: each step of ShardedRecommender.recommend timed on its own
+    (HIP events), with the roofline of each; the dominant one is the line's
+    roofline. Same calls recommend() makes, in the same order."""
+    o = rec.ops
+    B, N = int(hu.shape[0]), rec.n_local
+    if rec.precision == "exact":
+        als = o.als_scores(rec.U, hu, rec.Vt, N, rec.k)
+        tt = o.tt_scores(uvec, rec.iv)
+        d = rec.iv.shape[1]
+        st = [("als_score (JVM-exact f32 mul+add, no FMA)",
+               lambda: o.als_scores(rec.U, hu, rec.Vt, N, rec.k),
+               dict(bound="valu", work=2.0 * rec.k * B * N, peak=F32_VALU_MULADD_TFLOPS, unit="TFLOP/s")),
+              ("tt_score (f32 MFMA Dot)", lambda: o.tt_scores(uvec, rec.iv),
+               dict(bound="mfma", work=2.0 * d * B * N, peak=F32_MFMA_PEAK_TFLOPS, unit="TFLOP/s"))]
+    else:
+        u_als, u_tt = rec._user_ops(hu, uvec)
+        als, tt = o.dot_scores(u_als, rec.V_op), o.dot_scores(u_tt, rec.iv_op)
+        st = [("als_score (bf16 MFMA, dk %d)" % rec.dk, lambda: o.dot_scores(u_als, rec.V_op),
+               dict(bound="mfma", work=2.0 * rec.dk * B * N, peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s")),
+              ("tt_score (bf16 MFMA, dk %d)" % rec.dk, lambda: o.dot_scores(u_tt, rec.iv_op),
+               dict(bound="mfma", work=2.0 * rec.dk * B * N, peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s"))]
+    a_mm, t_mm = o.rows_minmax(als), o.rows_minmax(tt)
+    st += [("rows_minmax x2 (per-user min/max of both score rows)",
+            lambda: (o.rows_minmax(als), o.rows_minmax(tt)),
+            dict(bound="hbm", work=2 * 4.0 * B * N, peak=HBM_PEAK_GBS, unit="GB/s")),
+           ("fuse_rows_topk (min-max fusion f64 + stable top-k)",
+            lambda: o.fuse_rows_topk(als, tt, a_mm, t_mm, False, top_k, rec.offset),
+            dict(bound="hbm", work=8.0 * B * N, peak=HBM_PEAK_GBS, unit="GB/s"))]
+    out = []
+    for name, fn, rf in st:
+        fn()
+        ms = ev_time(fn, reps, stream)
+        out.append(roofline(rf["bound"], rf["work"], ms, rf["peak"], rf["unit"], name))
+    dom = max(out, key=lambda r: r["avg_launch_ms"])
+    return dict(dom, stages=out)
+
+
 def cpu_baseline(eng, cfg, n_user_rows, n_item_rows):
     """C oracle on a bounded sample of the same matrix (rank 0, N=1)."""
     import numpy as np
 
     from oracle import build as obuild
+
+    from oracle.cpu_baseline import cpu_model
 
     obuild.build()
     k = cfg["rank"]
@@ -85,11 +149,92 @@ def cpu_baseline(eng, cfg, n_user_rows, n_item_rows):
     epoch_s = t_item * cfg["items"] / n_item_rows + t_user * cfg["users"] / n_user_rows
     return {
         "value": 1.0 / epoch_s, "unit": "epochs/s", "cores": int(obuild.load().oracle_max_threads()),
-        "kind": "port",
+        "kind": "port", "cpu_model": cpu_model(),
         "sample": (f"C oracle (Spark 3.5.1 ALS restated: f64 dspr Gramian + dpptrf/dpptrs, OpenMP) on "
                    f"{n_item_rows} item rows + {n_user_rows} user rows of the same c2 matrix, "
                    f"{t_item + t_user:.1f} s measured, extrapolated to one full epoch"),
     }
+
+
+def latest_profile():
+    import glob
+
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_prof_summary.json")))
+    return c[-1] if c else None
+
+
+def source_sha256(name):
+    import hashlib
+
+    with open(os.path.join(ROOT, "hybrid-als-twotower-recommender_amd", "csrc", name), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def api_line(eng, n_users, n_items, k, reps):
+    import contextlib
+    import io
+
+    import numpy as np
+    import pandas as pd
+    from sklearn.preprocessing import MinMaxScaler
+
+    from src.als_model import ALSModel, DeviceALSFactors, DeviceSession
+    from src.hybrid_system import HybridRecommendationSystem, fuse_device
+    from src.two_tower_model import TwoTowerModel
+
+    als = ALSModel(rank=k)
+    als.spark = DeviceSession()
+    als.model = DeviceALSFactors(np.arange(n_users), np.arange(n_items), eng.U[:n_users], eng.V[:n_items], k)
+    als.item_features = {}
+    tt = TwoTowerModel(n_users, n_items, 2651, 255, embedding_size=64, seed=4)
+    tt.build_model()
+    rng = np.random.default_rng(9)
+    items = pd.DataFrame({"itemId": np.arange(n_items), "manufacturer_id": rng.integers(0, 2651, n_items),
+                          "category_id": rng.integers(0, 255, n_items), "price": rng.random(n_items) * 100,
+                          "average_review_rating": rng.integers(0, 19, n_items).astype(np.float64)})
+    tt.scaler = MinMaxScaler().fit(items[["price", "average_review_rating"]])
+    h = HybridRecommendationSystem()
+    h.als_model, h.twotower_model, h.models_loaded = als, tt, True
+    ids = [int(i) for i in items["itemId"]]
+    uids = [int(u) for u in rng.integers(0, n_users, reps + 1)]
+    sink = io.StringIO()
+
+    def timed(fn):
+        fn(uids[0])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for u in uids[1:]:
+            fn(u)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    parts = {}
+    with contextlib.redirect_stdout(sink):
+        ref_ms = timed(lambda u: h.get_hybrid_recommendations(u, items, top_k=5))
+        parts["als.predict_for_user (id list)"] = timed(lambda u: als.predict_for_user(u, ids))
+        parts["twotower.predict_for_user (item frame)"] = timed(lambda u: tt.predict_for_user(u, items))
+        a, t = als.predict_for_user(uids[0], ids), tt.predict_for_user(uids[0], items)
+
+        def fuse(_u):
+            its, sa, st = h._union(a, t)
+            _, idx, sc = fuse_device(sa, st, h.als_f1_score > h.twotower_f1_score, 5,
+                                     scalers=(h.als_scaler, h.twotower_scaler))
+            return [(its[i], np.float64(x)) for i, x in zip(idx, sc)]
+
+        parts["_union + fuse_device top-5"] = timed(fuse)
+        top = fuse(0)
+    work = sum(parts.values())
+    return {"users_per_s": 1e3 / work, "pairs_per_s": n_items * 1e3 / work, "working_call_ms": work,
+            "reference_call_ms": ref_ms, "parts_ms": parts, "items": n_items, "top_k": 5, "reps": reps,
+            "top5_nonempty": len(top) == 5,
+            "note": ("one user per call (the reference API); reference_call = get_hybrid_recommendations(uid, "
+                     "item_frame) as the reference wires it (ALS side -> [] by SURVEY D9); working_call = ALS "
+                     "on an id list + two-tower on the frame + the call's own fusion/top-5")}
+
+
+def WANT_CPU(args, rank, world):
+    """CPU baselines run on rank 0 at N = 1 only (a bounded sample each)."""
+    return rank == 0 and world == 1 and not args.no_cpu_baseline
 
 
 def main():
@@ -109,14 +254,21 @@ def main():
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-score-users", type=int, default=1024,
+                    help="users of the scoring batch timed by the C JVM-exact scoring baseline")
+    ap.add_argument("--rank256-epochs", type=int, default=1,
+                    help="timed rank-256 ALS epochs on the same matrix (BASELINE c5's ALS half; 0 = skip)")
+    ap.add_argument("--api-reps", type=int, default=5,
+                    help="users timed through HybridRecommendationSystem.get_hybrid_recommendations (0 = skip)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="W > 1: user-side ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")
     ap.add_argument("--tt-steps", type=int, default=50,
                     help="two-tower training steps timed (c2 tables, d = 64, batch 256; 0 = skip)")
     ap.add_argument("--no-ingest", dest="ingest", action="store_false",
                     help="skip the COO -> CSR/CSC ingest measurement")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_prof_summary.json"),
-                    help="rocprofv3 PMC summary (scripts/gpu_profile.sh) for roofline.traffic")
+    ap.add_argument("--traffic-json", default=None,
+                    help="rocprofv3 PMC summary (scripts/gpu_profile.sh) for roofline.traffic "
+                         "(default: the newest profiles/r*_prof_summary.json)")
     ap.add_argument("--accum-mode", type=int, default=0, choices=[0, 1],
                     help="0: f64 matrix-core Gramian; 1: f32 matrix cores, f64 across 16-rating chunks")
     args = ap.parse_args()
@@ -222,7 +374,13 @@ def main():
                    # JVM-exact: k rounded products + k rounded sums per pair, no FMA/MFMA
                    # -> bound by the f32 VALU (packed mul/add: half the 157.3 TF FMA peak)
                    "roofline": {"bound": "valu-f32 (mul+add, no FMA)", "achieved": pps * 2 * k / 1e12,
-                                "peak": 78.6, "unit": "TFLOP/s", "frac": pps * 2 * k / 1e12 / 78.6}}
+                                "peak": F32_VALU_MULADD_TFLOPS, "unit": "TFLOP/s",
+                                "frac": pps * 2 * k / 1e12 / F32_VALU_MULADD_TFLOPS}}
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import cpu_baseline as cb
+
+            su = users[: args.cpu_score_users].cpu().numpy()
+            scoring["cpu_baseline"] = cb.als_scoring(eng.U[su].cpu().numpy(), eng.V[:n_items].cpu().numpy(), k, 5, B)
 
     # End-to-end hybrid top-5 (HybridRecommendationSystem.get_hybrid_recommendations
     # for a batch of users): JVM-exact ALS scores + two-tower Dot (d=64, Keras
@@ -261,6 +419,13 @@ def main():
         hybrid = {"pairs_per_s": Bh * n_items / hs, "ms_per_batch": hs * 1e3, "users": Bh, "items": n_items,
                   "top_k": 5, "d": d, "items_sharded_over": world,
                   "steps": "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5"}
+        if world == 1:
+            hybrid["roofline"] = hybrid_stages(rec, hu, uvec, 5, 10, stream)
+        if WANT_CPU(args, rank, world):
+            from oracle import cpu_baseline as cb
+
+            hybrid["cpu_baseline"] = cb.hybrid(Bh, n_items, k, d, 5)
+        del rec, tt
 
     # BASELINE c5: rank-256 ALS factors + d = 256 two-tower vectors in bf16,
     # end-to-end hybrid top-5 over c2's items (sharded): both score matrices
@@ -306,8 +471,64 @@ def main():
                      "top_k": 5, "rank": k5, "d": d5, "dtype": "bf16 operands, f32 accumulation",
                      "items_sharded_over": world,
                      "steps": "ALS + two-tower scores on bf16 MFMA (hrec_dot_scores) + min-max fusion + stable top-5"}
+        if world == 1:
+            hybrid_c5["roofline"] = hybrid_stages(rec5, hu5, uv5, 5, 10, stream)
+        if WANT_CPU(args, rank, world):
+            from oracle import cpu_baseline as cb
+
+            hybrid_c5["cpu_baseline"] = cb.hybrid(B5, n_items, k5, d5, 5)
         del U5, V5, tt5, rec5, iv5
         torch.cuda.empty_cache()
+
+    # BASELINE c5's ALS half: rank 256 on c2's matrix (K1w,
+    # als_half_sweep_wide_kernel, one 8-wave workgroup per row), same shards
+    # and all-gathers as the headline; one untimed + E timed epochs.
+    als256 = None
+    if args.rank256_epochs > 0:
+        k256 = 256
+        e256 = DeviceALS(n_users, n_items, k256, 0.1, csr, csc, world=world, rank=rank, group=group, chunks=chunks)
+        e256.init_user_factors(synthetic.SEED_INIT)
+        e256.epoch()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev256 = []
+        w0 = time.perf_counter()
+        for _ in range(args.rank256_epochs):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(stream)
+            e256.item_half_sweep()
+            e[1].record(stream)
+            e256.user_half_sweep()
+            e[2].record(stream)
+            ev256.append(e)
+        torch.cuda.synchronize()
+        wt = torch.tensor([(time.perf_counter() - w0) / args.rank256_epochs], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+        it_ms = sum(e[0].elapsed_time(e[1]) for e in ev256) / len(ev256)
+        ut_ms = sum(e[1].elapsed_time(e[2]) for e in ev256) / len(ev256)
+        fl256 = algo_flops(csc.nnz, i_per, k256) + algo_flops(csr.nnz, u_per, k256)
+        als256 = {"epochs_per_s": 1.0 / float(wt.item()), "ms_per_epoch": float(wt.item()) * 1e3, "rank": k256,
+                  "epochs": args.rank256_epochs, "kernel_ms_per_epoch": {"item": it_ms, "user": ut_ms},
+                  "roofline": roofline("mfma", fl256 / 2, (it_ms + ut_ms) / 2, F64_MFMA_PEAK_TFLOPS, "TFLOP/s",
+                                       "als_half_sweep_wide_kernel (item + user launches)")}
+        del e256
+        torch.cuda.empty_cache()
+
+    # The drop-in API call itself: HybridRecommendationSystem.
+    # get_hybrid_recommendations for ONE user over c2's 100k candidate items,
+    # models in memory (ALS factors of this run, a d = 64 two-tower on c2's
+    # tables). The reference hands the same `all_items` object to both models
+    # (src/hybrid_system.py:100-101): with the item DataFrame the ALS side
+    # fails as the reference's does -> "reference_call"; the
+    # "working_call" feeds ALS an id list and the two-tower side the frame,
+    # then _union + device fusion + stable top-5 — what the call does once
+    # both models answer. Host-side Python (dicts / sets over 100k items)
+    # dominates; the device kernels are in the lines above.
+    api = None
+    if rank == 0 and world == 1 and args.api_reps > 0:
+        api = api_line(eng, n_users, n_items, k, args.api_reps)
 
     # Ingest (§8(f) row 1, ALSModel.train's DataFrame -> CSR/CSC step): the
     # rank's user shard as COO columns (int64 ids, ratings) -> id codes +
@@ -380,6 +601,10 @@ def main():
                            "roofline": {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
                                         "frac": tf / peak}}
             del Vd, Ud
+        if WANT_CPU(args, rank, world):
+            from oracle import cpu_baseline as cb
+
+            tt_c4["cpu_baseline"] = cb.tt_scoring(args.c4_items // 100, args.c4_items, args.c4_users, d4, 5)
         tt_c4.update({"users": args.c4_users, "items": args.c4_items, "d": d4, "top_k": 5,
                       "items_sharded_over": world,
                       "kernel": "hrec_dot_topk (sample bound + fused matrix-core dot + survivor filter + exact top-k)"})
@@ -430,20 +655,33 @@ def main():
                                  "unit": "GB/s", "frac": step_bytes / dev_s / 1e9 / HBM_PEAK_GBS,
                                  "algorithmic_bytes_per_step": step_bytes}}
         del tt, bu, bi, bm, bc, bx, by
+        if not args.no_cpu_baseline:
+            from oracle import cpu_baseline as cb
+
+            tt_train["cpu_baseline"] = cb.tt_train(n_users, n_items, n_man, n_cat, dtt, Bt, 5)
         torch.cuda.empty_cache()
 
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.accum_mode == 0:
-        with open(args.traffic_json) as f:
-            traffic = json.load(f)["als_half_sweep"].get("hbm_bytes_avg_per_launch")
-
-    if tt_train is not None and args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tsw = json.load(f).get("tt_adam_sweep", {})
-        tt_train["roofline"]["traffic"] = tsw.get("hbm_bytes_avg_per_launch_corrected")
+    # roofline.traffic: PMC bytes per launch from the newest committed
+    # rocprofv3 summary (scripts/gpu_profile.sh), used only when the kernel
+    # source it profiled is the one this tree runs (sha256 stamped by
+    # scripts/summarize_profile.py); otherwise null + the reason.
+    traffic, traffic_src, tsw = None, None, None
+    prof = args.traffic_json or latest_profile()
+    if prof and os.path.exists(prof) and args.accum_mode == 0:
+        with open(prof) as f:
+            pj = json.load(f)
+        fresh = {src: pj.get("sources_sha256", {}).get(src) == source_sha256(src) for src in ("als.hip", "tt.hip")}
+        traffic_src = {"profile": os.path.relpath(prof, ROOT), "kernel_source_matches": fresh["als.hip"]}
+        if fresh["als.hip"] and world == 1:
+            traffic = pj["als_half_sweep"].get("hbm_bytes_avg_per_launch")
+        if fresh["tt.hip"]:
+            tsw = pj.get("tt_adam_sweep", {})
+    if tt_train is not None:
+        tt_train["roofline"]["traffic"] = tsw.get("hbm_bytes_avg_per_launch_corrected") if tsw else None
         tt_train["roofline"]["traffic_note"] = (
             "HBM bytes per launch of the grouped whole-table Adam sweep (adam_sparse_group4_kernel, rocprofv3 "
-            "FETCH_SIZE x2 + WRITE_SIZE, scripts/gpu_profile.sh); achieved above is the whole step's")
+            "FETCH_SIZE x2 + WRITE_SIZE, scripts/gpu_profile.sh; null when the profile predates csrc/tt.hip); "
+            "achieved above is the whole step's")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -481,6 +719,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / F64_MFMA_PEAK_TFLOPS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "traffic_note": ("HBM-side bytes per launch from rocprofv3 FETCH_SIZE(x2, gfx950) + WRITE_SIZE, "
                                  "separate PMC passes of this command (scripts/gpu_profile.sh -> profiles/)"),
                 "algorithmic_flops_per_launch": flops / 2,
@@ -496,6 +735,8 @@ def main():
             "tt_scoring_c4": tt_c4,
             "hybrid_top5_c5": hybrid_c5,
             "tt_train": tt_train,
+            "api_hybrid_call": api,
+            "als_rank256": als256,
         }
         print(json.dumps(line))
     if world > 1:

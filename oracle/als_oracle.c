@@ -141,3 +141,45 @@ int oracle_max_threads(void) {
   return 1;
 #endif
 }
+
+/* Spark ALSModel.transform's predict [ext: ALSModel.scala, called from
+ * src/als_model.py:75]: `dot = 0f; for i < rank: dot += a(i) * b(i)` in f32,
+ * product and sum each rounded (no FMA: built with -ffp-contract=off), then
+ * Python's stable sorted(reverse=True)[:top_k] (src/hybrid_system.py:108):
+ * ties keep the earlier item. One user row per OpenMP iteration; 8 items are
+ * scored side by side (same per-item operation order, so still exact).
+ * U: [n_sel rows gathered by `rows`, ld_u], V: [n_items, ld_v]. */
+void oracle_score_topk(const float* U, int64_t ld_u, const int64_t* rows, int64_t n_sel, const float* V,
+                       int64_t ld_v, int64_t n_items, int k, int top_k, int64_t* out_idx, float* out_val) {
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t s = 0; s < n_sel; ++s) {
+    const float* u = U + rows[s] * ld_u;
+    int64_t* oi = out_idx + s * top_k;
+    float* ov = out_val + s * top_k;
+    int filled = 0;
+    for (int64_t j0 = 0; j0 < n_items; j0 += 8) {
+      const int nb = (int)((n_items - j0) < 8 ? (n_items - j0) : 8);
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < k; ++c) {
+        const float a = u[c];
+        for (int t = 0; t < nb; ++t) acc[t] = acc[t] + a * V[(j0 + t) * ld_v + c];
+      }
+      for (int t = 0; t < nb; ++t) {
+        const float x = acc[t];
+        if (filled == top_k && !(x > ov[top_k - 1])) continue;
+        int p = filled < top_k ? filled++ : top_k - 1;
+        while (p > 0 && x > ov[p - 1]) {
+          ov[p] = ov[p - 1];
+          oi[p] = oi[p - 1];
+          --p;
+        }
+        ov[p] = x;
+        oi[p] = j0 + t;
+      }
+    }
+    for (int p = filled; p < top_k; ++p) {
+      ov[p] = -INFINITY;
+      oi[p] = -1;
+    }
+  }
+}

@@ -40,6 +40,8 @@ def load():
         lib.oracle_half_sweep.restype = None
         lib.oracle_half_sweep.argtypes = [vp, vp, vp, i64, vp, i64, i32, dbl, vp, i64]
         lib.oracle_max_threads.restype = i32
+        lib.oracle_score_topk.restype = None
+        lib.oracle_score_topk.argtypes = [vp, i64, vp, i64, vp, i64, i64, i32, i32, vp, vp]
         _lib = lib
     return _lib
 
@@ -89,3 +91,19 @@ def half_sweep(indptr, indices, values, src, k, reg):
     vv = np.ascontiguousarray(values, np.float32)
     lib.oracle_half_sweep(_p(ip), _p(ix), _p(vv), n_rows, _p(src), src.shape[1], k, float(reg), _p(out), k)
     return out
+
+
+def score_topk(U, rows, V, k, top_k):
+    """JVM-exact ALS scores of U[rows] against every row of V + stable top-k
+    (oracle_score_topk). Returns (idx int64 [n, top_k], val f32 [n, top_k])."""
+    import numpy as np
+
+    lib = load()
+    U = np.ascontiguousarray(U, dtype=np.float32)
+    V = np.ascontiguousarray(V, dtype=np.float32)
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    idx = np.empty((len(rows), top_k), dtype=np.int64)
+    val = np.empty((len(rows), top_k), dtype=np.float32)
+    lib.oracle_score_topk(_p(U), U.shape[1], _p(rows), len(rows), _p(V), V.shape[1], V.shape[0], int(k),
+                          int(top_k), _p(idx), _p(val))
+    return idx, val

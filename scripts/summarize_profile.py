@@ -21,6 +21,22 @@ def rows(pattern):
     return out
 
 
+def source_hashes():
+    """sha256 of every kernel source at profile time: bench.py compares the
+    entry of the kernel it reports against the tree it runs from, so a
+    roofline.traffic read from a stale profile is flagged, not silently used."""
+    import hashlib
+
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hybrid-als-twotower-recommender_amd",
+                        "csrc")
+    out = {}
+    for f in sorted(os.listdir(root)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(root, f), "rb") as fh:
+                out[f] = hashlib.sha256(fh.read()).hexdigest()
+    return out
+
+
 def main(base):
     stats = rows(os.path.join(base, "prof_trace", "**", "*kernel_stats.csv"))
     top = sorted(stats, key=lambda r: -float(r["TotalDurationNs"]))[:8]
@@ -95,6 +111,7 @@ def main(base):
     if wd:
         res["als_half_sweep_wide_rank256"] = {"launches": len(wd), "durations_ms": wd,
                                               "workload": "scripts/wide_quick.py 256 300000 100000 (item, user)"}
+    res["sources_sha256"] = source_hashes()
     print(json.dumps(res, indent=1))
 
 

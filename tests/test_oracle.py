@@ -216,3 +216,52 @@ def test_tt_oracle_gradcheck():
             q2[name][ix] -= h
             fd = (loss(q1) - loss(q2)) / (2 * h)
             assert abs(fd - grads[name][ix]) <= 1e-5 * max(1.0, abs(fd)), (name, ix, fd, grads[name][ix])
+
+
+def test_c_score_topk_matches_jvm_predict():
+    """oracle_score_topk (bench's scoring cpu_baseline): the JVM-exact f32 dot
+    of oracle/als.score_matrix + Python's stable sorted(reverse=True)[:k],
+    ties included."""
+    obuild.build()
+    rng = np.random.default_rng(4)
+    U = rng.normal(size=(40, 24)).astype(np.float32)
+    V = rng.normal(size=(517, 24)).astype(np.float32)
+    V[200] = V[7]  # exact tie: the earlier item wins
+    rows = np.array([0, 3, 39, 17])
+    idx, val = obuild.score_topk(U, rows, V, 24, 9)
+    S = oals.score_matrix(U[rows], V)
+    for r in range(len(rows)):
+        order = sorted(range(V.shape[0]), key=lambda j: S[r, j], reverse=True)[:9]
+        assert idx[r].tolist() == order
+        assert np.array_equal(val[r], S[r, order])
+
+
+def test_cpu_baseline_keras_step_matches_oracle():
+    """The torch-CPU Keras train step timed as bench's tt_train cpu_baseline
+    computes what the f64 two-tower oracle computes (3 steps, rtol 1e-4)."""
+    import torch
+
+    from oracle import cpu_baseline as cb
+
+    d, sizes = 16, (30, 25, 6, 5)
+    g = torch.Generator().manual_seed(2)
+    p = cb._init(sizes, d, g)
+    p["gi"] += 0.1 * torch.rand(d, generator=g)
+    p["b2"] += 0.1 * torch.rand(d, generator=g)
+    names = {"gi": "ln_item_gamma", "bi": "ln_item_beta", "gu": "ln_user_gamma", "bu": "ln_user_beta"}
+    po = {names.get(n, n): t.numpy().astype(np.float32).copy() for n, t in p.items()}
+    slots = {n: (torch.zeros_like(t), torch.zeros_like(t)) for n, t in p.items()}
+    so = {n: (np.zeros_like(t), np.zeros_like(t)) for n, t in po.items()}
+    rng = np.random.default_rng(3)
+    for it in range(3):
+        B = 12
+        u, i = rng.integers(0, sizes[0], B), rng.integers(0, sizes[1], B)
+        m, c = rng.integers(0, sizes[2], B), rng.integers(0, sizes[3], B)
+        u[1] = u[0]  # a duplicated row (IndexedSlices dedup)
+        x = rng.random((B, 2)).astype(np.float32)
+        y = rng.integers(0, 19, B).astype(np.float32)
+        t = [torch.as_tensor(a) for a in (u, i, m, c, x, y)]
+        cb.keras_step(p, slots, it, *t)
+        ott.train_step(po, so, u, i, m, c, x, y, it)
+    for n, t in p.items():
+        np.testing.assert_allclose(t.numpy(), po[names.get(n, n)], rtol=1e-4, atol=1e-6, err_msg=n)
