@@ -561,19 +561,50 @@ def main():
         del uid, iid, out
         torch.cuda.empty_cache()
 
-    # Two-tower scoring at BASELINE c4: d = 128 item vectors (N(0, 1/d),
-    # generated on the device), items sharded over the ranks; one batch of
-    # users ranked top-5 against every item (fused dot + filter + top-k;
-    # the [B, N] score matrix is never written), C3 merge across ranks.
-    tt_c4 = None
+    # Two-tower scoring at BASELINE c4: d = 128, 50M candidate items, items
+    # sharded over the ranks. First the catalogue's item vectors are
+    # precomputed by the item tower (Keras graph, src/two_tower_model.py:38-66,
+    # K4m on the f32 matrix cores; random Keras init of a 50M-row item table,
+    # c2's 2651 manufacturers / 255 categories) — its own line,
+    # tt_item_vectors_c4; then one batch of user-tower vectors is ranked
+    # top-5 against every item (fused dot + filter + top-k; the [B, N] score
+    # matrix is never written), C3 merge across ranks.
+    tt_c4, tt_iv = None, None
     if args.c4_items > 0:
         tt_c4 = {}
         d4 = 128
         c0, c_per = shard_range(args.c4_items, world, rank)
         c_loc = max(0, min(c_per, args.c4_items - c0))
-        g4 = torch.Generator(device="cuda").manual_seed(1000 + rank)
-        V4 = torch.randn((c_loc, d4), device="cuda", generator=g4).mul_(d4 ** -0.5)
-        U4 = torch.randn((args.c4_users, d4), device="cuda", generator=torch.Generator(device="cuda").manual_seed(7))
+        tt4 = DeviceTwoTower(args.c4_users, c_loc, 2651, 255, d4, seed=1000 + rank, device_init=True)
+        g4 = torch.Generator(device="cuda").manual_seed(2000 + rank)
+        it4 = torch.arange(c_loc, dtype=torch.int32, device="cuda")
+        mn4 = torch.randint(0, 2651, (c_loc,), device="cuda", generator=g4, dtype=torch.int32)
+        ct4 = torch.randint(0, 255, (c_loc,), device="cuda", generator=g4, dtype=torch.int32)
+        nu4 = torch.rand((c_loc, 2), device="cuda", generator=g4)
+        V4 = tt4.item_vectors(it4, mn4, ct4, nu4)  # warm
+        torch.cuda.synchronize()
+        reps4 = 3
+        q0 = time.perf_counter()
+        iv_ms = ev_time(lambda: tt4.item_vectors(it4, mn4, ct4, nu4), reps4, stream)
+        it_t = torch.tensor([(time.perf_counter() - q0) / reps4], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(it_t, op=dist.ReduceOp.MAX)
+        iv_bytes = c_loc * (4 * d4 + 64 + 8 + 12 + 4 * d4)
+        tt_iv = {"items_per_s": args.c4_items / float(it_t.item()), "ms": float(it_t.item()) * 1e3,
+                 "items": args.c4_items, "d": d4, "items_sharded_over": world,
+                 "kernel": "tt_item_forward_mfma_kernel (Dense(16, relu) + concat + Dense(d) on f32 MFMA + LN)",
+                 "roofline": roofline("mfma", 2.0 * (d4 + 32) * d4 * c_loc, iv_ms, F32_MFMA_PEAK_TFLOPS, "TFLOP/s",
+                                      "tt_item_forward_mfma_kernel",
+                                      hbm_view={"algorithmic_bytes": iv_bytes,
+                                                "GBps": iv_bytes / (iv_ms / 1e3) / 1e9,
+                                                "frac": iv_bytes / (iv_ms / 1e3) / 1e9 / HBM_PEAK_GBS})}
+        if WANT_CPU(args, rank, world):
+            from oracle import cpu_baseline as cb
+
+            tt_iv["cpu_baseline"] = cb.item_vectors(args.c4_items // 100, args.c4_items, d4)
+        U4 = tt4.user_vectors(torch.arange(args.c4_users, dtype=torch.int32, device="cuda"))
+        del tt4, it4, mn4, ct4, nu4
+        torch.cuda.empty_cache()
         for name, dt, peak in (("f32", torch.float32, F32_MFMA_PEAK_TFLOPS),
                                ("bf16", torch.bfloat16, BF16_MFMA_PEAK_TFLOPS)):
             Vd = _hrec.dot_operand(V4, dt)
@@ -732,6 +763,7 @@ def main():
             "scoring": scoring,
             "hybrid_top5": hybrid,
             "ingest": ingest,
+            "tt_item_vectors_c4": tt_iv,
             "tt_scoring_c4": tt_c4,
             "hybrid_top5_c5": hybrid_c5,
             "tt_train": tt_train,

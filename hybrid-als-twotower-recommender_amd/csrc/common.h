@@ -65,6 +65,14 @@ int hrec_als_half_sweep_wide(const int64_t* indptr, const int32_t* indices, cons
                              const float* src_factors, int64_t n_src, int k, int kp, double reg_param,
                              float* dst_factors, void* stream);
 
+// csrc/tt_mfma.hip: the item tower on the f32 matrix cores for d <= 256
+// (returns 1 when d needs the scalar kernel of csrc/tt.hip instead).
+int hrec_tt_item_forward_mfma(int d, const float* ie, const float* me, const float* ce, const float* w1,
+                              const float* b1, const float* w2, const float* b2, const float* gamma,
+                              const float* beta, const int32_t* item, const int32_t* man, const int32_t* cat,
+                              const float* numeric, int64_t n, float* out, float* z_save, float* xhat_save,
+                              float* rstd_save, void* stream);
+
 #define HREC_REQUIRE(cond, ...)          \
   do {                                   \
     if (!(cond)) {                       \

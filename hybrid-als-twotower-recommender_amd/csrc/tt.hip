@@ -714,6 +714,15 @@ static bool params_ok(const hrec_tt_params* p) {
 
 using namespace hrec;
 
+// the matrix-core item tower (csrc/tt_mfma.hip) for d <= 256; 1 = use the
+// scalar kernel below
+static int item_forward(const hrec_tt_params& p, const int32_t* item, const int32_t* man, const int32_t* cat,
+                        const float* numeric, int64_t n, float* out, float* z, float* xh, float* rs, void* stream) {
+  if (getenv("HREC_TT_SCALAR_FWD")) return 1;  // A/B against the scalar kernel (scripts only)
+  return hrec_tt_item_forward_mfma(p.d, p.item_emb, p.man_emb, p.cat_emb, p.w1, p.b1, p.w2, p.b2, p.ln_item_gamma,
+                                   p.ln_item_beta, item, man, cat, numeric, n, out, z, xh, rs, stream);
+}
+
 static size_t item_fwd_smem(int d) { return (size_t)kTR * (2 * d + 32) * sizeof(float); }
 
 extern "C" int hrec_tt_item_forward(const hrec_tt_params* params, const int32_t* item, const int32_t* manufacturer,
@@ -723,6 +732,9 @@ extern "C" int hrec_tt_item_forward(const hrec_tt_params* params, const int32_t*
   HREC_REQUIRE(n >= 0, "tt_item_forward: negative n");
   if (n == 0) return HREC_OK;
   HREC_REQUIRE(item && manufacturer && category && numeric && item_vec, "tt_item_forward: null pointer");
+  const int rc = item_forward(*params, item, manufacturer, category, numeric, n, item_vec, nullptr, nullptr, nullptr,
+                              stream);
+  if (rc <= 0) return rc;
   const size_t sm = item_fwd_smem(params->d);
   HREC_REQUIRE(sm <= 160 * 1024, "tt_item_forward: embedding_size too large for one LDS tile");
   hipLaunchKernelGGL(tt_item_forward_kernel, dim3((unsigned)((n + kTR - 1) / kTR)), dim3(kBlock), sm,
@@ -803,10 +815,14 @@ extern "C" int hrec_tt_forward_backward(const hrec_tt_params* params, const int3
                      uvec, uxh, urs);
   int rc = check_launch("tt_user_forward_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(tt_item_forward_kernel, dim3((unsigned)nblk), dim3(kBlock), item_fwd_smem(d), s, P, item,
-                     manufacturer, category, numeric, batch, ivec, zs, ixh, irs);
-  rc = check_launch("tt_item_forward_kernel");
-  if (rc) return rc;
+  rc = item_forward(*params, item, manufacturer, category, numeric, batch, ivec, zs, ixh, irs, stream);
+  if (rc < 0) return rc;
+  if (rc == 1) {
+    hipLaunchKernelGGL(tt_item_forward_kernel, dim3((unsigned)nblk), dim3(kBlock), item_fwd_smem(d), s, P, item,
+                       manufacturer, category, numeric, batch, ivec, zs, ixh, irs);
+    rc = check_launch("tt_item_forward_kernel");
+    if (rc) return rc;
+  }
   const size_t bsm = ((size_t)kTR * d + kTR * 16 + kTR + 8) * sizeof(float);
   hipLaunchKernelGGL(tt_backward_kernel, dim3((unsigned)nblk), dim3(kBlock), bsm, s, P, y, batch, uvec, uxh, urs,
                      ivec, ixh, irs, zs, numeric, g_user, g_item, g_man, g_cat, part);

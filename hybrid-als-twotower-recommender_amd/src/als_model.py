@@ -57,7 +57,7 @@ class DeviceALSFactors:
 
     @staticmethod
     def _lookup(ids, keys):
-        keys = np.asarray(keys)
+        keys = np.fromiter(keys, np.int64, len(keys)) if isinstance(keys, list) else np.asarray(keys)
         if len(ids) == 0:
             return np.full(keys.shape, -1, dtype=np.int64)
         pos = np.searchsorted(ids, keys)
@@ -221,23 +221,35 @@ class ALSModel:
             return False
 
     # --------------------------------------------------------------- predict
+    @staticmethod
+    def _check_int_ids(values):
+        """Spark's createDataFrame(pairs, IntegerType schema) at :71-75
+        rejects non-integer ids (e.g. the column names of a DataFrame, SURVEY
+        D9). One pass over the distinct element types; the slow per-item scan
+        only runs to name the offending value."""
+        def ok(t):
+            return issubclass(t, (int, np.integer)) and not issubclass(t, (bool, np.bool_))
+
+        if all(ok(t) for t in set(map(type, values))):
+            return
+        for x in values:
+            if not ok(type(x)):
+                raise TypeError(f"field itemId: IntegerType() can not accept object {x!r} in type {type(x)}")
+
     def predict_for_user(self, user_id, all_items):
         try:
             items = list(all_items)
-            # Spark's createDataFrame(pairs, IntegerType schema) at :71-75 rejects
-            # non-integer ids (e.g. the column names of a DataFrame).
-            for x in [user_id] + items:
-                if isinstance(x, (bool, np.bool_)) or not isinstance(x, (int, np.integer)):
-                    raise TypeError(f"field itemId: IntegerType() can not accept object {x!r} in type {type(x)}")
+            self._check_int_ids([user_id])
+            self._check_int_ids(items)
             scores = self.model.score([user_id], items)[0].cpu().numpy() if items else np.zeros(0, np.float32)
-            missing = [n for n in range(len(items)) if np.isnan(scores[n])]
-            sims = self._similar_batch([items[n] for n in missing]) if missing else []
-            fallback = {}
-            for n, sim in zip(missing, sims):
-                fallback[n] = (np.mean([self.item_features[s]["rating"] for s in sim]) if sim
-                               else self.global_mean)
-            return [(item, float(scores[n])) if n not in fallback else (item, fallback[n])
-                    for n, item in enumerate(items)]
+            out = list(zip(items, scores.tolist()))  # (item, float(prediction)) as :84
+            missing = np.flatnonzero(np.isnan(scores)).tolist()
+            if missing:  # cold-start fallback (:78-86): mean rating of <= 3 similar items, else the global mean
+                sims = self._similar_batch([items[n] for n in missing])
+                for n, sim in zip(missing, sims):
+                    out[n] = (items[n], np.mean([self.item_features[s]["rating"] for s in sim]) if sim
+                              else self.global_mean)
+            return out
         except Exception as e:
             print(f"Prediction error: {str(e)}")
             return []

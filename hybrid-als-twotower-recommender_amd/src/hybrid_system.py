@@ -10,6 +10,7 @@ Python's sorted(..., reverse=True) tie order. The item order of the fused
 list is the iteration order of set(als).union(set(tt)) (:61), built on the
 host exactly as the reference builds it.
 """
+import itertools
 import os
 import warnings
 
@@ -116,8 +117,9 @@ class HybridRecommendationSystem:
         als_dict = dict(als_predictions)
         tt_dict = dict(twotower_predictions)
         items = list(set(als_dict.keys()).union(set(tt_dict.keys())))
-        als_scores = _as_scores([als_dict.get(item, 0) for item in items])
-        tt_scores = _as_scores([tt_dict.get(item, 0) for item in items])
+        # [d.get(item, 0) for item in items] (:62-63), via map (same values)
+        als_scores = _as_scores(list(map(als_dict.get, items, itertools.repeat(0))))
+        tt_scores = _as_scores(list(map(tt_dict.get, items, itertools.repeat(0))))
         return items, als_scores, tt_scores
 
     def adaptive_fusion(self, als_predictions, twotower_predictions):

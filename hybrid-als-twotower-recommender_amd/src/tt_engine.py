@@ -79,15 +79,25 @@ class DeviceTwoTower:
     """Parameters + Adam slots on one HIP device."""
 
     def __init__(self, num_users, num_items, num_man, num_cat, d, learning_rate=0.001, seed=0, device=None,
-                 init=None):
+                 init=None, device_init=False):
+        """device_init=True draws the embedding tables' Keras
+        uniform(-0.05, 0.05) init on the device (catalogue-sized tables, e.g.
+        BASELINE c4's 50M x 128) instead of on the host."""
         _hrec.require_device()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.d = int(d)
         self.sizes = {"user_emb": int(num_users), "item_emb": int(num_items), "man_emb": int(num_man),
                       "cat_emb": int(num_cat)}
         self.layout, self.n_dense = dense_layout(self.d)
-        init = init if init is not None else keras_init(num_users, num_items, num_man, num_cat, d, seed)
         dev = self.device
+        if init is None:
+            init = keras_init(0 if device_init else num_users, 0 if device_init else num_items, num_man, num_cat, d,
+                              seed)
+            if device_init:
+                g = torch.Generator(device=dev).manual_seed(int(seed))
+                for name, rows in (("user_emb", num_users), ("item_emb", num_items)):
+                    t = torch.empty((int(rows), self.d), dtype=torch.float32, device=dev)
+                    init[name] = t.uniform_(-0.05, 0.05, generator=g)
         self.dense = torch.zeros(self.n_dense, dtype=torch.float32, device=dev)
         self.tensors = {}
         for name, (off, shape) in self.layout.items():
@@ -95,7 +105,9 @@ class DeviceTwoTower:
             view.copy_(torch.as_tensor(np.asarray(init[name], np.float32).reshape(shape)))
             self.tensors[name] = view
         for name in TABLES:
-            self.tensors[name] = torch.as_tensor(np.asarray(init[name], np.float32), device=dev).contiguous()
+            t = init[name]
+            self.tensors[name] = (t if isinstance(t, torch.Tensor) else
+                                  torch.as_tensor(np.asarray(t, np.float32), device=dev)).contiguous()
         self.opt = AdamConfig(learning_rate)
         self.iterations = 0
         self.m_dense = torch.zeros_like(self.dense)

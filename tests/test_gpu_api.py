@@ -211,7 +211,7 @@ def _tt_batch(rng, B, nu, ni, nm, nc):
             rng.uniform(0, 1, (B, 2)).astype(np.float32), rng.integers(0, 19, B).astype(np.float32))
 
 
-@pytest.mark.parametrize("d", [50, 64, 128])
+@pytest.mark.parametrize("d", [16, 50, 64, 128, 256])
 def test_tt_forward_backward_matches_oracle(device, d):
     from src import _hrec
     from src.tt_engine import DeviceTwoTower
@@ -239,6 +239,52 @@ def test_tt_forward_backward_matches_oracle(device, d):
         scale = np.abs(rows[name]).max() + 1e-12
         np.testing.assert_allclose(g.cpu().numpy(), rows[name], rtol=1e-4, atol=1e-4 * scale, err_msg=name)
     np.testing.assert_allclose(gd[eng.n_dense:], [sq, ab], rtol=1e-5)
+
+
+@pytest.mark.parametrize("d,n", [(16, 1), (50, 77), (64, 1000), (100, 333), (128, 4099), (256, 530)])
+def test_tt_item_tower_mfma_matches_oracle(device, d, n, monkeypatch):
+    """K4m (csrc/tt_mfma.hip, f32 matrix cores, permuted-k Dense + fused LN)
+    against the f64 Keras graph at rtol 1e-5, ragged tails and padded d
+    included, and against the scalar K4 kernel it replaces."""
+    from src import _hrec
+    from src.tt_engine import DeviceTwoTower
+
+    rng = np.random.default_rng(d * 7 + n)
+    nu, ni, nm, nc = 5, 3000, 11, 6
+    p = _tt_params(rng, nu, ni, nm, nc, d)
+    eng = DeviceTwoTower(nu, ni, nm, nc, d, init=p)
+    u, i, m, c, x, _ = _tt_batch(rng, n, nu, ni, nm, nc)
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    got = eng.item_vectors(T(i), T(m), T(c), T(x)).cpu().numpy()
+    want = ott.forward(p, u, i, m, c, x)["ivec"]
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-5)
+    monkeypatch.setenv("HREC_TT_SCALAR_FWD", "1")
+    scalar = eng.item_vectors(T(i), T(m), T(c), T(x)).cpu().numpy()
+    np.testing.assert_allclose(got, scalar, rtol=1e-5, atol=2e-5)
+
+
+def test_tt_item_tower_mfma_catalogue_sample(device):
+    """A catalogue-sized call (1M items, d = 128, many persistent-loop trips
+    per wave): sampled rows against the f64 graph, every row LayerNormed
+    (mean = mean(beta) when gamma = 1)."""
+    from src.tt_engine import DeviceTwoTower
+
+    rng = np.random.default_rng(5)
+    n, d, nm, nc = 1_000_000, 128, 2651, 255
+    p = _tt_params(rng, 2, n, nm, nc, d)
+    p["ln_item_gamma"][:] = 1.0
+    eng = DeviceTwoTower(2, n, nm, nc, d, init=p)
+    i = torch.arange(n, dtype=torch.int32, device=device)
+    m = torch.as_tensor(rng.integers(0, nm, n).astype(np.int32), device=device)
+    c = torch.as_tensor(rng.integers(0, nc, n).astype(np.int32), device=device)
+    x = torch.as_tensor(rng.uniform(0, 1, (n, 2)).astype(np.float32), device=device)
+    iv = eng.item_vectors(i, m, c, x)
+    mu = iv.double().mean(1).cpu().numpy()
+    np.testing.assert_allclose(mu, float(p["ln_item_beta"].astype(np.float64).mean()), atol=1e-5)
+    rows = np.unique(np.concatenate([rng.integers(0, n, 500), [0, 15, 16, n - 17, n - 1]]))
+    want = ott.forward(p, np.zeros(len(rows), np.int64), rows, m.cpu().numpy()[rows], c.cpu().numpy()[rows],
+                       x.cpu().numpy()[rows])["ivec"]
+    np.testing.assert_allclose(iv[torch.as_tensor(rows, device=device)].cpu().numpy(), want, rtol=1e-5, atol=2e-5)
 
 
 def test_tt_adam_steps_match_oracle(device):
