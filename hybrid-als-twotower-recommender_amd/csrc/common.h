@@ -73,6 +73,15 @@ int hrec_tt_item_forward_mfma(int d, const float* ie, const float* me, const flo
                               const float* numeric, int64_t n, float* out, float* z_save, float* xhat_save,
                               float* rstd_save, void* stream);
 
+// csrc/tt_mfma.hip: the train step's backward with both Dense GEMMs on the
+// f32 matrix cores (returns 1 when d needs the scalar kernels instead).
+// scratch: B·(d + 19) floats.
+int hrec_tt_backward_mfma(int d, const float* w2, const float* gamma_u, const float* gamma_i, const float* y,
+                          int64_t B, const float* uvec, const float* uxhat, const float* urstd, const float* ivec,
+                          const float* ixhat, const float* irstd, const float* zsave, const float* numeric,
+                          float* g_user, float* g_item, float* g_man, float* g_cat, float* grad, float* scratch,
+                          void* stream);
+
 #define HREC_REQUIRE(cond, ...)          \
   do {                                   \
     if (!(cond)) {                       \

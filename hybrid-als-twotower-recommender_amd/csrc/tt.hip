@@ -718,7 +718,7 @@ using namespace hrec;
 // scalar kernel below
 static int item_forward(const hrec_tt_params& p, const int32_t* item, const int32_t* man, const int32_t* cat,
                         const float* numeric, int64_t n, float* out, float* z, float* xh, float* rs, void* stream) {
-  if (getenv("HREC_TT_SCALAR_FWD")) return 1;  // A/B against the scalar kernel (scripts only)
+  if (getenv("HREC_TT_SCALAR_FWD")) return 1;  // A/B against the scalar kernel (scripts, tests)
   return hrec_tt_item_forward_mfma(p.d, p.item_emb, p.man_emb, p.cat_emb, p.w1, p.b1, p.w2, p.b2, p.ln_item_gamma,
                                    p.ln_item_beta, item, man, cat, numeric, n, out, z, xh, rs, stream);
 }
@@ -780,7 +780,9 @@ static size_t partial_len(int d) { return (size_t)(d + 32) * d + 5 * (size_t)d +
 
 extern "C" size_t hrec_tt_train_workspace_bytes(int d, int64_t batch) {
   const int64_t nblk = (batch + kTR - 1) / kTR;
-  const size_t f = (size_t)batch * (4 * (size_t)d + (d + 32) + 2) + (size_t)nblk * partial_len(d);
+  const size_t scalar_part = (size_t)nblk * partial_len(d), mfma_scratch = (size_t)batch * (d + 19);
+  const size_t f = (size_t)batch * (4 * (size_t)d + (d + 32) + 2) +
+                   (scalar_part > mfma_scratch ? scalar_part : mfma_scratch);
   return f * sizeof(float) + 256;
 }
 
@@ -822,6 +824,13 @@ extern "C" int hrec_tt_forward_backward(const hrec_tt_params* params, const int3
                        manufacturer, category, numeric, batch, ivec, zs, ixh, irs);
     rc = check_launch("tt_item_forward_kernel");
     if (rc) return rc;
+  }
+  // backward with both Dense GEMMs on the matrix cores (csrc/tt_mfma.hip);
+  // the scratch (B·(d + 19) floats) reuses the partials region
+  if (!getenv("HREC_TT_SCALAR_BWD")) {  // set: the scalar kernels below (A/B, tests)
+    rc = hrec_tt_backward_mfma(d, P.w2, P.gu, P.gi, y, batch, uvec, uxh, urs, ivec, ixh, irs, zs, numeric, g_user,
+                               g_item, g_man, g_cat, grad_dense, part, stream);
+    if (rc <= 0) return rc;
   }
   const size_t bsm = ((size_t)kTR * d + kTR * 16 + kTR + 8) * sizeof(float);
   hipLaunchKernelGGL(tt_backward_kernel, dim3((unsigned)nblk), dim3(kBlock), bsm, s, P, y, batch, uvec, uxh, urs,

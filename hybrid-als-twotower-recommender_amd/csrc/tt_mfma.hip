@@ -72,7 +72,7 @@ __device__ __forceinline__ int wq_index(int kb, int c, int q, int dp) {
 // every output column and applies the LayerNorm epilogue; otherwise it
 // writes the pre-LN Dense output (z @ W2 + b2) of its columns (d = 256: two
 // passes, then tt_ln_rows_kernel).
-template <int NTI, int NT, bool kLN, bool kSave, int kFwdWaves>
+template <int NTI, int NT, bool kLN, bool kSave, int kFwdWaves, bool kLds>
 __global__ __launch_bounds__(64 * kFwdWaves) void tt_item_forward_mfma_kernel(
     TTFwd P, const int32_t* __restrict__ item, const int32_t* __restrict__ man, const int32_t* __restrict__ cat,
     const float* __restrict__ numeric, int64_t n, int col0, float* __restrict__ out, float* __restrict__ z_save,
@@ -80,8 +80,7 @@ __global__ __launch_bounds__(64 * kFwdWaves) void tt_item_forward_mfma_kernel(
   constexpr int dp = 16 * NT;
   constexpr int KB = NTI + 2;
   constexpr int kTG = NT >= 2 ? 2 : 1;
-  constexpr bool kLds = true;
-  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [KB][dp][16]
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [KB][dp][16] (kLds)
   const int d = P.d, dz = P.d + 32;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = lane >> 4, m = lane & 15;
@@ -187,7 +186,15 @@ __global__ __launch_bounds__(64 * kFwdWaves) void tt_item_forward_mfma_kernel(
 #pragma unroll
         for (int u = 0; u < kTG; ++u) {
           const int c = 16 * (t0 + u) + m;
-          b[u] = *reinterpret_cast<const f4m*>(Ws + wq_index(kb, c, q, dp));
+          if constexpr (kLds) {
+            b[u] = *reinterpret_cast<const f4m*>(Ws + wq_index(kb, c, q, dp));
+          } else {  // small calls: straight from W2 (L2-resident), no staging
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int wr = w2_row(16 * kb + 4 * q + j, d, NTI);
+              b[u][j] = (wr >= 0 && col0 + c < d) ? P.w2[(int64_t)wr * d + col0 + c] : 0.f;
+            }
+          }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -291,20 +298,32 @@ static int nt_of(int d) {
   return 0;
 }
 
+template <int NTI, int NT, bool kLN, bool kSave, int kW, bool kLds>
+static int launch_fwd_w(const TTFwd& P, const int32_t* item, const int32_t* man, const int32_t* cat,
+                        const float* numeric, int64_t n, int col0, float* out, float* z, float* xh, float* rs,
+                        hipStream_t s) {
+  const size_t sm = ((kLds ? (size_t)(NTI + 2) * 16 * NT * 16 : 0) + 3 * 16 * NT) * sizeof(float);
+  const int64_t tiles = (n + 15) / 16;
+  int64_t grid = (tiles + kW - 1) / kW;
+  const int64_t cap = kW == 16 ? 256 : 4096;
+  if (grid > cap) grid = cap;
+  hipLaunchKernelGGL((tt_item_forward_mfma_kernel<NTI, NT, kLN, kSave, kW, kLds>), dim3((unsigned)grid), dim3(64 * kW),
+                     sm, s, P, item, man, cat, numeric, n, col0, out, z, xh, rs);
+  return check_launch("tt_item_forward_mfma_kernel");
+}
+
+// W2 (the pass's columns) + b2/gamma/beta in LDS. Catalogue-sized calls: one
+// persistent 1024-thread workgroup per CU (81.5 KB at d = 128, 149 KB per
+// d = 256 pass); small calls (a training batch): one wave per workgroup
+// reading W2 straight from L2 (no staging), so the tiles spread over many
+// CUs instead of queueing on one.
 template <int NTI, int NT, bool kLN, bool kSave>
 static int launch_fwd(const TTFwd& P, const int32_t* item, const int32_t* man, const int32_t* cat,
                       const float* numeric, int64_t n, int col0, float* out, float* z, float* xh, float* rs,
                       hipStream_t s) {
-  // W2 (the pass's columns) + b2/gamma/beta in LDS, one persistent
-  // 1024-thread workgroup per CU (81.5 KB at d = 128, 149 KB per d = 256 pass)
-  constexpr int kW = 16;
-  const size_t sm = ((size_t)(NTI + 2) * 16 * NT * 16 + 3 * 16 * NT) * sizeof(float);
-  const int64_t tiles = (n + 15) / 16;
-  int64_t grid = (tiles + kW - 1) / kW;
-  if (grid > 256) grid = 256;
-  hipLaunchKernelGGL((tt_item_forward_mfma_kernel<NTI, NT, kLN, kSave, kW>), dim3((unsigned)grid), dim3(64 * kW),
-                     sm, s, P, item, man, cat, numeric, n, col0, out, z, xh, rs);
-  return check_launch("tt_item_forward_mfma_kernel");
+  if ((n + 15) / 16 >= 4096)
+    return launch_fwd_w<NTI, NT, kLN, kSave, 16, true>(P, item, man, cat, numeric, n, col0, out, z, xh, rs, s);
+  return launch_fwd_w<NTI, NT, kLN, kSave, 1, false>(P, item, man, cat, numeric, n, col0, out, z, xh, rs, s);
 }
 
 // LayerNorm of pre-LN rows in place (d = 256 path), one wave per row; same
@@ -378,4 +397,269 @@ int hrec_tt_item_forward_mfma(int d, const float* ie, const float* me, const flo
   }
 #undef HREC_FWD_CASE
   return 1;
+}
+
+// ------------------------------------------------------------------------
+// K6m: the backward pass of one Keras train step (MSE loss, batch B) with
+// its two Dense(d) GEMMs on the f32 matrix cores. Three launches:
+//   rows : per sample (one wave): score, dL/dscore = 2 (yhat - y) / B, the
+//          LayerNorm backward of both towers -> dp [B, d] (grad of the item
+//          Dense output) and the user-embedding row grads; squared / abs
+//          error per sample;
+//   dz   : dz = dp · W2^T [B, d+32] -> item / manufacturer / category row
+//          grads and relu'(h) · dh = dpre [B, 16]   (MFMA, K = d);
+//   dense: dW2 = z^T · dp [d+32, d]                    (MFMA, K = B) and
+//          the column sums (db2, LN gamma/beta of both towers, dW1, db1,
+//          loss sums) straight into the gradient block — no per-block
+//          partials, one fixed summation order (deterministic).
+// The k order inside the MFMA GEMMs is permuted as in K4m (16-B operand
+// loads feed 4 k-steps).
+
+namespace hrec {
+
+struct TTBwd {
+  int d;
+  const float *w2, *gu, *gi;
+};
+
+// one wave per sample row
+__global__ __launch_bounds__(256) void tt_bwd_rows_kernel(TTBwd P, const float* __restrict__ y, int64_t B,
+                                                          const float* __restrict__ uvec,
+                                                          const float* __restrict__ uxhat,
+                                                          const float* __restrict__ urstd,
+                                                          const float* __restrict__ ivec,
+                                                          const float* __restrict__ ixhat,
+                                                          const float* __restrict__ irstd, float* __restrict__ dp,
+                                                          float* __restrict__ g_user, float* __restrict__ dyh,
+                                                          float* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= B) return;
+  const int d = P.d;
+  const float* u = uvec + g * d;
+  const float* v = ivec + g * d;
+  float s = 0.f;
+  for (int c = lane; c < d; c += kWave) s = fmaf(u[c], v[c], s);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+  const float e = s - y[g];
+  const float dy = 2.0f * e / (float)B;
+  // item LN backward: dxh = dy·u·gamma ; dx = rstd·(dxh - mean(dxh) - xh·mean(dxh·xh))
+  float m1 = 0.f, m2 = 0.f, u1 = 0.f, u2 = 0.f;
+  for (int c = lane; c < d; c += kWave) {
+    const float di = dy * u[c] * P.gi[c];
+    m1 += di;
+    m2 += di * ixhat[g * d + c];
+    const float du = dy * v[c] * P.gu[c];
+    u1 += du;
+    u2 += du * uxhat[g * d + c];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m1 += __shfl_xor(m1, off, kWave);
+    m2 += __shfl_xor(m2, off, kWave);
+    u1 += __shfl_xor(u1, off, kWave);
+    u2 += __shfl_xor(u2, off, kWave);
+  }
+  m1 /= (float)d;
+  m2 /= (float)d;
+  u1 /= (float)d;
+  u2 /= (float)d;
+  const float ir = irstd[g], ur = urstd[g];
+  for (int c = lane; c < d; c += kWave) {
+    const float di = dy * u[c] * P.gi[c];
+    dp[g * d + c] = ir * (di - m1 - ixhat[g * d + c] * m2);
+    const float du = dy * v[c] * P.gu[c];
+    g_user[g * d + c] = ur * (du - u1 - uxhat[g * d + c] * u2);
+  }
+  if (lane == 0) {
+    dyh[g] = dy;
+    err[2 * g] = e * e;
+    err[2 * g + 1] = fabsf(e);
+  }
+}
+
+// dz = dp · W2^T, transposed on the matrix cores: C[z col][sample] =
+// W2 · dp^T, so lane (q, m) holds z columns 16t + 4q + i of sample 16·tile
+// + m. One wave per 16 samples x all z columns (dz <= 288: NTZ <= 18).
+template <int NTZ>
+__global__ __launch_bounds__(64) void tt_bwd_dz_kernel(TTBwd P, int64_t B, const float* __restrict__ dp,
+                                                       const float* __restrict__ zsave, float* __restrict__ g_item,
+                                                       float* __restrict__ g_man, float* __restrict__ g_cat,
+                                                       float* __restrict__ dpre) {
+  const int d = P.d, dz = d + 32;
+  const int lane = threadIdx.x, q = lane >> 4, m = lane & 15;
+  const int64_t row = (int64_t)blockIdx.x * 16 + m;
+  const bool live = row < B;
+  const int64_t rr = live ? row : B - 1;
+  f4m acc[NTZ];
+#pragma unroll
+  for (int t = 0; t < NTZ; ++t) acc[t] = f4m{0.f, 0.f, 0.f, 0.f};
+  const int nkb = (d + 15) / 16;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = 16 * kb + 4 * q;
+    f4m a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = k0 + j < d ? dp[rr * d + k0 + j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < NTZ; ++t) {
+      const int zc = 16 * t + m;  // A row = z column
+      f4m b;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (zc < dz && k0 + j < d) ? P.w2[(int64_t)zc * d + k0 + j] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j], a[j], acc[t], 0, 0, 0);
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int t = 0; t < NTZ; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 16 * t + 4 * q + i;
+      const float x = acc[t][i];
+      if (c < d) {
+        g_item[row * d + c] = x;
+      } else if (c < d + 8) {
+        g_man[row * 8 + (c - d)] = x;
+      } else if (c < d + 16) {
+        g_cat[row * 8 + (c - d - 8)] = x;
+      } else if (c < dz) {
+        const float h = zsave[row * dz + c];
+        dpre[row * 16 + (c - d - 16)] = h > 0.f ? x : 0.f;  // relu'
+      }
+    }
+  }
+}
+
+// dW2 = z^T · dp over the batch, then the column sums. 1024-thread blocks:
+// blocks [0, tiles) each own one 16 x 16 tile of dW2, its 16 waves split the
+// batch (MFMA, K = the wave's samples in order 16kb + 4q + j) and the 16
+// partial tiles are summed in LDS in wave order; the remaining blocks take
+// 64 columns each of [db2 | dgi | dbi | dgu | dbu | dW1 | db1 | loss sums],
+// 16 sample stripes per column summed the same way. Fixed orders throughout
+// (deterministic), no per-block partials in HBM. Grad layout =
+// tt_engine.dense_layout: W2[(d+32)·d] | b2 | gamma_i | beta_i | gamma_u |
+// beta_u | W1[32] | b1[16] | sum sq err | sum abs err.
+constexpr int kBwdWaves = 16;
+__global__ __launch_bounds__(64 * kBwdWaves) void tt_bwd_dense_kernel(
+    TTBwd P, int64_t B, const float* __restrict__ zsave, const float* __restrict__ dp,
+    const float* __restrict__ uvec, const float* __restrict__ uxhat, const float* __restrict__ ivec,
+    const float* __restrict__ ixhat, const float* __restrict__ dyh, const float* __restrict__ numeric,
+    const float* __restrict__ dpre, const float* __restrict__ err, float* __restrict__ grad) {
+  __shared__ float red[kBwdWaves][256];
+  const int d = P.d, dz = d + 32;
+  const int tz = (dz + 15) / 16, td = (d + 15) / 16;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int blk = blockIdx.x;
+  if (blk < tz * td) {
+    const int q = lane >> 4, m = lane & 15;
+    const int zt = blk / td, dt = blk % td;
+    const int zc = 16 * zt + m, dc = 16 * dt + m;
+    const int64_t per = ((B + kBwdWaves - 1) / kBwdWaves + 15) / 16 * 16;  // samples per wave
+    const int64_t sb = w * per, se = sb + per < B ? sb + per : B;
+    f4m acc = f4m{0.f, 0.f, 0.f, 0.f};
+    for (int64_t s0 = sb; s0 < se; s0 += 16) {
+      f4m a, b;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t s = s0 + 4 * q + j;
+        a[j] = (s < se && zc < dz) ? zsave[s * dz + zc] : 0.f;
+        b[j] = (s < se && dc < d) ? dp[s * d + dc] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[w][(4 * q + i) * 16 + m] = acc[i];  // C[z 4q + i][d m]
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      const int zr = 16 * zt + (threadIdx.x >> 4), c = 16 * dt + (threadIdx.x & 15);
+      float sum = 0.f;
+#pragma unroll
+      for (int v = 0; v < kBwdWaves; ++v) sum += red[v][threadIdx.x];
+      if (zr < dz && c < d) grad[(int64_t)zr * d + c] = sum;
+    }
+    return;
+  }
+  float* tail = grad + (int64_t)dz * d;
+  const int ncol = 5 * d + 48 + 2;
+  const int o = (blk - tz * td) * 64 + lane;  // column of this lane; w = sample stripe
+  float acc = 0.f;
+  if (o < 5 * d) {
+    const int kind = o / d, j = o % d;
+    for (int64_t s = w; s < B; s += kBwdWaves) {
+      const float dy = dyh[s];
+      if (kind == 0) {
+        acc += dp[s * d + j];
+      } else if (kind == 1 || kind == 2) {
+        const float dvi = dy * uvec[s * d + j];  // d item_vec
+        acc = kind == 1 ? fmaf(dvi, ixhat[s * d + j], acc) : acc + dvi;
+      } else {
+        const float dvu = dy * ivec[s * d + j];  // d user_vec
+        acc = kind == 3 ? fmaf(dvu, uxhat[s * d + j], acc) : acc + dvu;
+      }
+    }
+  } else if (o < 5 * d + 32) {  // dW1[i][j] = sum_s x_i · dpre_j
+    const int i = (o - 5 * d) / 16, j = (o - 5 * d) % 16;
+    for (int64_t s = w; s < B; s += kBwdWaves) acc = fmaf(numeric[s * 2 + i], dpre[s * 16 + j], acc);
+  } else if (o < 5 * d + 48) {
+    const int j = o - 5 * d - 32;
+    for (int64_t s = w; s < B; s += kBwdWaves) acc += dpre[s * 16 + j];
+  } else if (o < ncol) {
+    const int k = o - 5 * d - 48;
+    for (int64_t s = w; s < B; s += kBwdWaves) acc += err[2 * s + k];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64 && o < ncol) {
+    float sum = 0.f;
+#pragma unroll
+    for (int v = 0; v < kBwdWaves; ++v) sum += red[v][threadIdx.x];
+    tail[o] = sum;
+  }
+}
+
+}  // namespace hrec
+
+// Called by hrec_tt_forward_backward (csrc/tt.hip) after both forwards:
+// returns 1 when d needs the scalar backward instead (d > 256).
+int hrec_tt_backward_mfma(int d, const float* w2, const float* gamma_u, const float* gamma_i, const float* y,
+                          int64_t B, const float* uvec, const float* uxhat, const float* urstd, const float* ivec,
+                          const float* ixhat, const float* irstd, const float* zsave, const float* numeric,
+                          float* g_user, float* g_item, float* g_man, float* g_cat, float* grad, float* scratch,
+                          void* stream) {
+  using namespace hrec;
+  if (d > 256) return 1;
+  hipStream_t s = as_stream(stream);
+  TTBwd P{d, w2, gamma_u, gamma_i};
+  float* dp = scratch;               // [B, d]
+  float* dpre = dp + B * d;          // [B, 16]
+  float* dyh = dpre + B * 16;        // [B]
+  float* err = dyh + B;              // [B, 2]
+  hipLaunchKernelGGL(tt_bwd_rows_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, P, y, B, uvec, uxhat, urstd,
+                     ivec, ixhat, irstd, dp, g_user, dyh, err);
+  int rc = check_launch("tt_bwd_rows_kernel");
+  if (rc) return rc;
+  const int ntz = (d + 32 + 15) / 16;
+  const dim3 gz((unsigned)((B + 15) / 16));
+#define HREC_DZ_CASE(N)                                                                                          \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL(tt_bwd_dz_kernel<N>, gz, dim3(64), 0, s, P, B, dp, zsave, g_item, g_man, g_cat, dpre); \
+    break;
+  switch (ntz) {
+    HREC_DZ_CASE(3) HREC_DZ_CASE(4) HREC_DZ_CASE(5) HREC_DZ_CASE(6) HREC_DZ_CASE(7) HREC_DZ_CASE(8)
+    HREC_DZ_CASE(9) HREC_DZ_CASE(10) HREC_DZ_CASE(11) HREC_DZ_CASE(12) HREC_DZ_CASE(13) HREC_DZ_CASE(14)
+    HREC_DZ_CASE(15) HREC_DZ_CASE(16) HREC_DZ_CASE(17) HREC_DZ_CASE(18)
+    default:
+      return 1;
+  }
+#undef HREC_DZ_CASE
+  rc = check_launch("tt_bwd_dz_kernel");
+  if (rc) return rc;
+  const int tiles = ntz * ((d + 15) / 16);
+  const int sums = (5 * d + 48 + 2 + 63) / 64;
+  hipLaunchKernelGGL(tt_bwd_dense_kernel, dim3((unsigned)(tiles + sums)), dim3(64 * kBwdWaves), 0, s, P, B, zsave, dp, uvec,
+                     uxhat, ivec, ixhat, dyh, numeric, dpre, err, grad);
+  return check_launch("tt_bwd_dense_kernel");
 }

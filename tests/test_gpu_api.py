@@ -287,6 +287,27 @@ def test_tt_item_tower_mfma_catalogue_sample(device):
     np.testing.assert_allclose(iv[torch.as_tensor(rows, device=device)].cpu().numpy(), want, rtol=1e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("d,B", [(16, 1), (64, 256), (50, 77), (128, 300), (256, 40)])
+def test_tt_backward_mfma_matches_scalar(device, d, B, monkeypatch):
+    """K6m (dz and dW2 on the f32 matrix cores, column sums in one pass)
+    against the scalar backward kernels it replaces, at rtol 1e-5 (both are
+    f32; the summation orders differ)."""
+    from src import _hrec
+    from src.tt_engine import DeviceTwoTower
+
+    rng = np.random.default_rng(d + B)
+    nu, ni, nm, nc = 40, 30, 7, 5
+    p = _tt_params(rng, nu, ni, nm, nc, d)
+    eng = DeviceTwoTower(nu, ni, nm, nc, d, init=p)
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    batch = [T(a) for a in _tt_batch(rng, B, nu, ni, nm, nc)]
+    got = [g.cpu().numpy() for g in _hrec.tt_forward_backward(eng.params, *batch)]
+    monkeypatch.setenv("HREC_TT_SCALAR_BWD", "1")
+    ref = [g.cpu().numpy() for g in _hrec.tt_forward_backward(eng.params, *batch)]
+    for a, b in zip(got, ref):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5 * (np.abs(b).max() + 1e-12))
+
+
 def test_tt_adam_steps_match_oracle(device):
     from src.tt_engine import TABLES, DeviceTwoTower
 
