@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 from src import _hrec, synthetic  # noqa: E402
 from src.als_engine import DeviceALS, shard_chunks, shard_range  # noqa: E402
-from src.recommend import ShardedRecommender, ShardedScorer  # noqa: E402
+from src.recommend import CapturedRecommend, ShardedRecommender, ShardedScorer  # noqa: E402
 from src.tt_engine import DeviceTwoTower  # noqa: E402
 
 METRIC = "ALS epochs/sec + scored user-item pairs/sec at rank=64, 1/2/4/8 MI355X"
@@ -81,6 +81,45 @@ def roofline(bound, work, ms, peak, unit, kernel, **extra):
            "avg_launch_ms": ms, ("algorithmic_flops" if unit == "TFLOP/s" else "algorithmic_bytes"): work}
     out.update(extra)
     return out
+
+
+def time_recommend(rec, hu, uvec, world, reps=20):
+    """Seconds per batch (max over ranks): at W = 1 the batch replayed as one
+    HIP graph (CapturedRecommend), at W > 1 eager (the C2/C3 collectives run
+    between the kernels). Returns (seconds, eager seconds or None)."""
+    def run_timed(fn):
+        for _ in range(2):
+            fn()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        ht = torch.tensor([(time.perf_counter() - h0) / reps], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
+        return float(ht.item())
+
+    eager = run_timed(lambda: rec.recommend(hu, uvec, False, 5))
+    if world > 1:
+        return eager, None
+    cap = CapturedRecommend(rec, hu, uvec, False, 5)
+    ei, ev = rec.recommend(hu, uvec, False, 5)
+    gi, gv = cap()
+    if not (torch.equal(ei, gi) and torch.equal(ev, gv)):
+        raise RuntimeError("captured recommend differs from eager")
+    return run_timed(cap), eager
+
+
+def recommend_line_timing(hs_graph, hs_eager):
+    """ms_per_batch = the faster of graph replay / eager launch (both timed)."""
+    if hs_eager is None:
+        return hs_graph, "eager (W > 1: collectives between kernels)"
+    if hs_graph < hs_eager:
+        return hs_graph, "one HIP graph per batch (CapturedRecommend)"
+    return hs_eager, "eager launches (HIP-graph replay measured no faster)"
 
 
 def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
@@ -402,21 +441,11 @@ def main():
         Bh = args.hybrid_users
         hu = (torch.arange(Bh, dtype=torch.int64) * (n_users // Bh)).cuda()
         uvec = tt.user_vectors(hu.to(torch.int32))
-        for _ in range(2):
-            rec.recommend(hu, uvec, False, 5)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        reps = 5
-        h0 = time.perf_counter()
-        for _ in range(reps):
-            rec.recommend(hu, uvec, False, 5)
-        torch.cuda.synchronize()
-        ht = torch.tensor([(time.perf_counter() - h0) / reps], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
-        hs = float(ht.item())
+        hs_g, hs_eager = time_recommend(rec, hu, uvec, world)
+        hs, how = recommend_line_timing(hs_g, hs_eager)
         hybrid = {"pairs_per_s": Bh * n_items / hs, "ms_per_batch": hs * 1e3, "users": Bh, "items": n_items,
+                  "eager_ms_per_batch": (hs_eager if hs_eager else hs_g) * 1e3,
+                  "graph_ms_per_batch": hs_g * 1e3 if hs_eager else None, "launch": how,
                   "top_k": 5, "d": d, "items_sharded_over": world,
                   "steps": "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5"}
         if world == 1:
@@ -453,21 +482,11 @@ def main():
         B5 = args.c5_users
         hu5 = (torch.arange(B5, dtype=torch.int64) * (n_users // B5)).cuda()
         uv5 = tt5.user_vectors(hu5.to(torch.int32))
-        for _ in range(2):
-            rec5.recommend(hu5, uv5, False, 5)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        reps = 5
-        h0 = time.perf_counter()
-        for _ in range(reps):
-            rec5.recommend(hu5, uv5, False, 5)
-        torch.cuda.synchronize()
-        ht = torch.tensor([(time.perf_counter() - h0) / reps], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
-        hs = float(ht.item())
+        hs_g, hs_eager = time_recommend(rec5, hu5, uv5, world)
+        hs, how = recommend_line_timing(hs_g, hs_eager)
         hybrid_c5 = {"pairs_per_s": B5 * n_items / hs, "ms_per_batch": hs * 1e3, "users": B5, "items": n_items,
+                     "eager_ms_per_batch": (hs_eager if hs_eager else hs_g) * 1e3,
+                     "graph_ms_per_batch": hs_g * 1e3 if hs_eager else None, "launch": how,
                      "top_k": 5, "rank": k5, "d": d5, "dtype": "bf16 operands, f32 accumulation",
                      "items_sharded_over": world,
                      "steps": "ALS + two-tower scores on bf16 MFMA (hrec_dot_scores) + min-max fusion + stable top-5"}
@@ -585,7 +604,7 @@ def main():
         torch.cuda.synchronize()
         reps4 = 3
         q0 = time.perf_counter()
-        iv_ms = ev_time(lambda: tt4.item_vectors(it4, mn4, ct4, nu4), reps4, stream)
+        iv_ms = ev_time(lambda: tt4.item_vectors(it4, mn4, ct4, nu4, out=V4), reps4, stream)
         it_t = torch.tensor([(time.perf_counter() - q0) / reps4], dtype=torch.float64, device="cuda")
         if world > 1:
             dist.all_reduce(it_t, op=dist.ReduceOp.MAX)

@@ -33,10 +33,12 @@ int offset_ids(int64_t* idx, int64_t n, int64_t off, hipStream_t s);
 // indices; entries with index -1 are skipped; row_n, if given, bounds row r
 // to its first min(n, row_n[r]) entries). Workspace: topk_ws_bytes.
 size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem);
+// gate (optional): a device flag; the launches do nothing while *gate == 0
+// (a device-side fallback that needs no host round trip).
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
               T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx = nullptr,
-              const int* row_n = nullptr);
+              const int* row_n = nullptr, const int* gate = nullptr);
 
 // Stable descending top-k by a full per-row radix sort (csrc/sort_topk.hip),
 // for top_k above the selection kernels' 1024; rows * n < 2^31.

@@ -267,9 +267,11 @@ __global__ __launch_bounds__(kTopkBlock) void topk_segment_kernel(const T* __res
                                                                   int64_t n, int64_t row_stride, int kk,
                                                                   T* __restrict__ out_v,
                                                                   int64_t* __restrict__ out_i,
-                                                                  int64_t out_row_stride) {
+                                                                  int64_t out_row_stride,
+                                                                  const int* __restrict__ gate) {
   __shared__ KV<T> red[kTopkBlock / 64];
   __shared__ int64_t win;
+  if (gate && *gate == 0) return;
   const int64_t row = blockIdx.y;
   const int64_t seg0 = (int64_t)blockIdx.x * kTopkSeg;
   const T* __restrict__ rv = vals + row * row_stride;
@@ -335,10 +337,11 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const T* __restrict__ va
                                                         const int64_t* __restrict__ src_idx,
                                                         const int* __restrict__ row_n, int64_t n_rows, int64_t n,
                                                         int64_t row_stride, int kk, T* __restrict__ out_v,
-                                                        int64_t* __restrict__ out_i, int64_t out_row_stride) {
+                                                        int64_t* __restrict__ out_i, int64_t out_row_stride,
+                                                        const int* __restrict__ gate) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n_rows) return;  // wave-uniform
+  if (row >= n_rows || (gate && *gate == 0)) return;  // wave-uniform
   if (row_n) {
     const int64_t rn = row_n[row];
     n = rn < n ? rn : n;
@@ -695,13 +698,13 @@ template <int KK>
 __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
     const float* __restrict__ als, const float* __restrict__ tt, int64_t n, int64_t ld, int64_t segs,
     const float* __restrict__ als_mm, const float* __restrict__ tt_mm, double w0, double w1,
-    double* __restrict__ cand_v, int64_t* __restrict__ cand_i) {
+    double* __restrict__ cand_v, int64_t* __restrict__ cand_i, const int* __restrict__ gate) {
 #pragma clang fp contract(off)
   __shared__ uint64_t ck_sh[4][128];  // [64, 128): scratch slots of non-candidates
   __shared__ int ce_sh[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t seg = (int64_t)blockIdx.x * 4 + wv;
-  if (seg >= segs) return;
+  if (seg >= segs || (gate && *gate == 0)) return;
   const int64_t r = blockIdx.y;
   const int64_t R = gridDim.y;
   const double amin = (double)als_mm[r], amax = (double)als_mm[R + r];
@@ -872,6 +875,113 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
   }
 }
 
+// Threshold filter for the batched fusion top-k (kk <= kFuseK): the same
+// fused f64 keys as fuse_segment_topk_kernel, one wave per segment, but each
+// row first takes a threshold key tk = the best of its sample segments'
+// kk-th best keys (fuse_segment_topk_kernel over the row's first G segments
+// -> samp). Those are kk distinct items of the row, so at least kk items have
+// key >= tk and the row's top kk all do. Per item: the fusion, one compare
+// and a ballot; the (few) items with key >= tk are compacted into LDS and
+// the segment's stable top-kk among them is taken by rank (each candidate
+// counts the better ones, a handful of broadcast LDS reads) -> [row][seg*kk]
+// like fuse_segment_topk_kernel, and the same merge follows. A segment with
+// more than kFuseSlots candidates (heavy ties, or a row whose best items
+// cluster) raises *overflow, which gates the exact segment path on the
+// device (clear_flag_kernel resets it first).
+constexpr int kFuseSlots = 64;
+__global__ __launch_bounds__(256) void fuse_filter_kernel(
+    const float* __restrict__ als, const float* __restrict__ tt, int64_t n, int64_t ld, int64_t segs,
+    const float* __restrict__ als_mm, const float* __restrict__ tt_mm, double w0, double w1,
+    const double* __restrict__ samp, int G, int kk, double* __restrict__ cand_v, int64_t* __restrict__ cand_i,
+    int* __restrict__ overflow) {
+#pragma clang fp contract(off)
+  __shared__ uint64_t ck_sh[4][kFuseSlots];
+  __shared__ int ce_sh[4][kFuseSlots];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wv;
+  if (seg >= segs) return;
+  const int64_t r = blockIdx.y;
+  const int64_t R = gridDim.y;
+  uint64_t tk = 0;
+  for (int g = 0; g < G; ++g) {
+    const uint64_t k = order_key(samp[(r * G + g) * kk + kk - 1]);
+    tk = k > tk ? k : tk;
+  }
+  const double amin = (double)als_mm[r], amax = (double)als_mm[R + r];
+  double arange = amax - amin;
+  if (arange < 10.0 * DBL_EPSILON) arange = 1.0;
+  const double ascale = 1.0 / arange;
+  const double amin_ = 0.0 - amin * ascale;
+  const float tmin = tt_mm[r], tmax = tt_mm[R + r];
+  float trange = tmax - tmin;
+  if (trange < 10.0f * FLT_EPSILON) trange = 1.0f;
+  const float tscale = 1.0f / trange;
+  const float tmin_ = 0.0f - tmin * tscale;
+  const int64_t seg0 = seg * kFuseSeg;
+  const float* __restrict__ ar = als + r * ld + seg0 + lane;
+  const float* __restrict__ tr = tt + r * ld + seg0 + lane;
+  const int nvalid = (int)((n - seg0) < kFuseSeg ? (n - seg0) : kFuseSeg);
+  float av[kFusePer], tv[kFusePer];
+  if (nvalid == kFuseSeg) {
+#pragma unroll
+    for (int e = 0; e < kFusePer; ++e) {
+      av[e] = ar[e * 64];
+      tv[e] = tr[e * 64];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < kFusePer; ++e) {
+      const int off = e * 64 + lane < nvalid ? e * 64 : 0;
+      av[e] = ar[off];
+      tv[e] = tr[off];
+    }
+  }
+  int nc = 0;
+#pragma unroll
+  for (int e = 0; e < kFusePer; ++e) {
+    const double an = (double)av[e] * ascale + amin_;
+    const float tn = tv[e] * tscale + tmin_;
+    const uint64_t key = order_key(w0 * an + w1 * (double)tn);
+    const bool c = e * 64 + lane < nvalid && key >= tk;
+    const uint64_t m = __ballot(c);
+    if (m == 0) continue;  // wave-uniform
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const int slot = nc + below;
+    if (c && slot < kFuseSlots) {
+      ck_sh[wv][slot] = key;
+      ce_sh[wv][slot] = e * 64 + lane;
+    }
+    nc += __popcll(m);
+  }
+  if (nc > kFuseSlots) {
+    if (lane == 0) *overflow = 1;
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // each candidate's rank among the nc (key desc, position asc) = its slot
+  const uint64_t mk = lane < nc ? ck_sh[wv][lane] : 0;
+  const int mp = lane < nc ? ce_sh[wv][lane] : 0;
+  int rank = 0;
+  for (int q = 0; q < nc; ++q) {
+    const uint64_t ok = ck_sh[wv][q];
+    const int op = ce_sh[wv][q];
+    rank += (ok > mk || (ok == mk && op < mp)) ? 1 : 0;
+  }
+  const int64_t obase = (r * segs + seg) * kk;
+  if (lane < nc && rank < kk) {
+    cand_v[obase + rank] = key_value(mk);
+    cand_i[obase + rank] = seg0 + mp;
+  }
+  if (lane >= nc && lane < kk) {  // fewer candidates than kk: empty slots
+    cand_v[obase + lane] = key_value(0);
+    cand_i[obase + lane] = -1;
+  }
+}
+
+__global__ void clear_flag_kernel(int* __restrict__ flag) { *flag = 0; }
+
 __global__ void add_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t off) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n && idx[i] >= 0) idx[i] += off;
@@ -906,7 +1016,8 @@ size_t topk_ws_bytes(int64_t n_rows, int64_t n, int kk, size_t elem) {
 namespace hrec {
 template <typename T>
 int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
-              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx, const int* row_n) {
+              T* out_val, void* ws, size_t ws_bytes, hipStream_t s, const int64_t* src_idx, const int* row_n,
+              const int* gate) {
   // Multi-pass: segments -> candidates (kk per segment) -> ... -> one segment.
   const T* cur_v = vals;
   const int64_t* cur_i = src_idx;
@@ -920,7 +1031,7 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
         const dim3 g((unsigned)((n_rows + 3) / 4));
 #define HREC_TOPK_WAVE(KK)                                                                                    \
   hipLaunchKernelGGL((topk_wave_kernel<T, KK>), g, dim3(256), 0, s, cur_v, cur_i, row_n, n_rows, m, stride, kk, \
-                     out_val, out_idx, (int64_t)kk)
+                     out_val, out_idx, (int64_t)kk, gate)
         if (kk <= 2)
           HREC_TOPK_WAVE(2);
         else if (kk <= 4)
@@ -935,7 +1046,7 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
         return check_launch("topk_wave_kernel");
       }
       hipLaunchKernelGGL((topk_segment_kernel<T>), dim3(1, (unsigned)n_rows), dim3(kTopkBlock), 0, s, cur_v,
-                         cur_i, row_n, m, stride, kk, out_val, out_idx, (int64_t)kk);
+                         cur_i, row_n, m, stride, kk, out_val, out_idx, (int64_t)kk, gate);
       return check_launch("topk_segment_kernel");
     }
     const int64_t cand = segs * kk;
@@ -948,7 +1059,7 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
     T* nv = (T*)(w + used + ib);
     used += vb + ib;
     hipLaunchKernelGGL((topk_segment_kernel<T>), dim3((unsigned)segs, (unsigned)n_rows), dim3(kTopkBlock), 0, s,
-                       cur_v, cur_i, row_n, m, stride, kk, nv, ni, cand);
+                       cur_v, cur_i, row_n, m, stride, kk, nv, ni, cand, gate);
     int rc = check_launch("topk_segment_kernel");
     if (rc) return rc;
     cur_v = nv;
@@ -959,9 +1070,9 @@ int topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int 
   }
 }
 template int topk_rows<float>(const float*, int64_t, int64_t, int64_t, int, int64_t*, float*, void*, size_t,
-                              hipStream_t, const int64_t*, const int*);
+                              hipStream_t, const int64_t*, const int*, const int*);
 template int topk_rows<double>(const double*, int64_t, int64_t, int64_t, int, int64_t*, double*, void*, size_t,
-                               hipStream_t, const int64_t*, const int*);
+                               hipStream_t, const int64_t*, const int*, const int*);
 }  // namespace hrec
 
 extern "C" int hrec_als_score(const float* user_factors, const int64_t* user_rows, int n_users,
@@ -1195,7 +1306,22 @@ extern "C" int hrec_rows_minmax_f32(const float* x, int64_t n_rows, int64_t n, i
   return check_launch("rows_minmax_kernel");
 }
 
+// Threshold-filter path (kk <= kFuseK): sample segments per row
+static int64_t fuse_sample_segs(int64_t n, int /*kk*/) {
+  // ~kk / G expected candidates per segment (the bound is the best of G
+  // segments' kk-th best) against kFuseSlots
+  const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg;
+  return segs < 4 ? segs : 4;
+}
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
 extern "C" size_t hrec_fuse_rows_workspace_bytes(int64_t n_rows, int64_t n, int top_k) {
+  const int kk = (int)(top_k < n ? top_k : n);
+  if (kk >= 1 && kk <= kFuseK) {
+    const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg, G = fuse_sample_segs(n, kk);
+    const size_t seg_path = 2 * al256((size_t)n_rows * segs * kk * 8) + topk_ws_bytes(n_rows, segs * kk, kk, 8);
+    return 2 * al256((size_t)n_rows * G * kk * 8) + al256(4) + 2 * seg_path + 256;
+  }
   return (size_t)n_rows * n * 8 + 256 + topk_ws_bytes(n_rows, n, top_k, 8);
 }
 
@@ -1215,25 +1341,56 @@ extern "C" int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_
   const int kk = (int)(top_k < n ? top_k : n);
   int rc;
   if (kk <= kFuseK) {
-    // fused values never hit HBM: segment candidates, then the merge
-    const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg;
-    double* cv = (double*)workspace;
-    int64_t* ci = (int64_t*)((char*)workspace + (((size_t)n_rows * segs * kk * 8 + 255) & ~(size_t)255));
-    char* tws = (char*)ci + (((size_t)n_rows * segs * kk * 8 + 255) & ~(size_t)255);
-    const dim3 g((unsigned)((segs + 3) / 4), (unsigned)n_rows);
-#define HREC_FUSE_K(K)                                                                                        \
-  case K:                                                                                                     \
-    hipLaunchKernelGGL(fuse_segment_topk_kernel<K>, g, dim3(256), 0, s, als, tt, n, ld, segs, als_minmax, tt_minmax, \
-                       w0, w1, cv, ci);                                                                      \
+    // 1. sample: the exact top-kk of each row's first G segments
+    // 2. filter: every item whose fused key reaches the sample bound -> row list
+    // 3. exact keyed top-kk of the lists
+    // 4. (gated on overflow) the exact segment path over every segment
+    const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg, G = fuse_sample_segs(n, kk);
+    char* p = (char*)workspace;
+    auto take = [&](size_t b) { char* q = p; p += al256(b); return q; };
+    double* sv = (double*)take((size_t)n_rows * G * kk * 8);
+    int64_t* si = (int64_t*)take((size_t)n_rows * G * kk * 8);
+    int* over = (int*)take(4);
+    double* cv = (double*)take((size_t)n_rows * segs * kk * 8);
+    int64_t* ci = (int64_t*)take((size_t)n_rows * segs * kk * 8);
+    char* tws = take(topk_ws_bytes(n_rows, segs * kk, kk, 8));
+    double* gv = (double*)take((size_t)n_rows * segs * kk * 8);
+    int64_t* gi = (int64_t*)take((size_t)n_rows * segs * kk * 8);
+    char* gws = p;
+    hipLaunchKernelGGL(clear_flag_kernel, dim3(1), dim3(1), 0, s, over);
+    rc = check_launch("clear_flag_kernel");
+    if (rc) return rc;
+#define HREC_FUSE_K(K, GRID, SEGS, V, I, GATE)                                                                  \
+  case K:                                                                                                       \
+    hipLaunchKernelGGL(fuse_segment_topk_kernel<K>, GRID, dim3(256), 0, s, als, tt, n, ld, SEGS, als_minmax,   \
+                       tt_minmax, w0, w1, V, I, GATE);                                                          \
     break;
-    switch (kk) {
-      HREC_FUSE_K(1) HREC_FUSE_K(2) HREC_FUSE_K(3) HREC_FUSE_K(4) HREC_FUSE_K(5) HREC_FUSE_K(6) HREC_FUSE_K(7)
-      default: HREC_FUSE_K(8)
-    }
-#undef HREC_FUSE_K
-    rc = check_launch("fuse_segment_topk_kernel");
+#define HREC_FUSE_SWITCH(GRID, SEGS, V, I, GATE)                                                                 \
+  switch (kk) {                                                                                                 \
+    HREC_FUSE_K(1, GRID, SEGS, V, I, GATE) HREC_FUSE_K(2, GRID, SEGS, V, I, GATE)                              \
+    HREC_FUSE_K(3, GRID, SEGS, V, I, GATE) HREC_FUSE_K(4, GRID, SEGS, V, I, GATE)                              \
+    HREC_FUSE_K(5, GRID, SEGS, V, I, GATE) HREC_FUSE_K(6, GRID, SEGS, V, I, GATE)                              \
+    HREC_FUSE_K(7, GRID, SEGS, V, I, GATE) default : HREC_FUSE_K(8, GRID, SEGS, V, I, GATE)                    \
+  }
+    const dim3 gs((unsigned)((G + 3) / 4), (unsigned)n_rows);
+    HREC_FUSE_SWITCH(gs, G, sv, si, nullptr)
+    rc = check_launch("fuse_segment_topk_kernel (sample)");
+    if (rc) return rc;
+    const dim3 gf((unsigned)((segs + 3) / 4), (unsigned)n_rows);
+    hipLaunchKernelGGL(fuse_filter_kernel, gf, dim3(256), 0, s, als, tt, n, ld, segs, als_minmax, tt_minmax, w0, w1,
+                       sv, (int)G, kk, cv, ci, over);
+    rc = check_launch("fuse_filter_kernel");
     if (rc) return rc;
     rc = topk_rows<double>(cv, n_rows, segs * kk, segs * kk, kk, out_idx, out_val, tws, (size_t)1 << 62, s, ci);
+    if (rc) return rc;
+    // exact path, run only if some row overflowed its list
+    HREC_FUSE_SWITCH(gf, segs, gv, gi, over)
+#undef HREC_FUSE_SWITCH
+#undef HREC_FUSE_K
+    rc = check_launch("fuse_segment_topk_kernel (gated)");
+    if (rc) return rc;
+    rc = topk_rows<double>(gv, n_rows, segs * kk, segs * kk, kk, out_idx, out_val, gws, (size_t)1 << 62, s, gi,
+                           nullptr, over);
   } else {
     double* fused = (double*)workspace;
     char* tws = (char*)workspace + (((size_t)n_rows * n * 8 + 255) & ~(size_t)255);

@@ -375,9 +375,12 @@ def tt_params(d, tensors):
     return p
 
 
-def tt_item_forward(params, item, man, cat, numeric):
+def tt_item_forward(params, item, man, cat, numeric, out=None):
     n = item.numel()
-    out = torch.empty((n, params.d), dtype=torch.float32, device=item.device)
+    if out is None:
+        out = torch.empty((n, params.d), dtype=torch.float32, device=item.device)
+    elif tuple(out.shape) != (n, params.d):
+        raise HrecError(f"tt_item_forward: out must be [{n}, {params.d}], got {tuple(out.shape)}")
     _check("hrec_tt_item_forward", lib().hrec_tt_item_forward(
         ctypes.byref(params), _dev(item, torch.int32, "item"), _dev(man, torch.int32, "manufacturer"),
         _dev(cat, torch.int32, "category"), _dev(numeric, torch.float32, "numeric"), n,

@@ -213,3 +213,40 @@ class ShardedScorer:
         if self.world == 1:
             return idx, val
         return merge_candidates(idx, val.double(), top_k, self.world, self.group, self.ops)
+
+
+class CapturedRecommend:
+    """One ShardedRecommender.recommend batch captured as a HIP graph and
+    replayed: a serving loop with a fixed batch size launches the whole
+    hybrid (operand conversion, two score GEMMs, row min/max, fusion
+    threshold filter, merge) as one graph instead of ~15 kernel launches
+    from Python. Every step is device-side (no host round trip: the fusion's
+    overflow fallback is gated on the device), so the graph holds the exact
+    eager computation. Single rank only (W > 1 runs the collectives eagerly).
+
+        cap = CapturedRecommend(rec, user_rows, user_vecs, als_wins, top_k)
+        idx, val = cap(new_user_rows, new_user_vecs)   # same shapes
+    """
+
+    def __init__(self, rec, user_rows, user_vecs, als_wins, top_k, warmup=2):
+        if rec.world != 1:
+            raise ValueError("CapturedRecommend: single-rank recommenders only")
+        self.rows = user_rows.clone()
+        self.vecs = user_vecs.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm up allocator / lazy init outside the capture
+            for _ in range(warmup):
+                rec.recommend(self.rows, self.vecs, als_wins, top_k)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = rec.recommend(self.rows, self.vecs, als_wins, top_k)
+
+    def __call__(self, user_rows=None, user_vecs=None):
+        if user_rows is not None:
+            self.rows.copy_(user_rows)
+        if user_vecs is not None:
+            self.vecs.copy_(user_vecs)
+        self.graph.replay()
+        return self.out

@@ -122,8 +122,10 @@ class DeviceTwoTower:
         self.params = _hrec.tt_params(self.d, self.tensors)
 
     # ---------------------------------------------------------- forward
-    def item_vectors(self, item, man, cat, numeric):
-        return _hrec.tt_item_forward(self.params, item, man, cat, numeric)
+    def item_vectors(self, item, man, cat, numeric, out=None):
+        """Item tower over candidate rows; `out` ([n, d] f32) is written in
+        place when given (catalogue precompute without a fresh allocation)."""
+        return _hrec.tt_item_forward(self.params, item, man, cat, numeric, out=out)
 
     def user_vectors(self, user):
         return _hrec.tt_user_forward(self.params, user)

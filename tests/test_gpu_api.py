@@ -684,3 +684,63 @@ def test_twotower_hyperparameter_tuning(device):
         if np.mean(f1s) > best_f1:
             best_f1, want = np.mean(f1s), params.copy()
     assert best == want
+
+
+def _fuse_rows_reference(als, tt, als_wins, kk):
+    """numpy restatement of hrec_fuse_rows_topk's row fusion (MinMaxScaler per
+    model and row: ALS in f64, two-tower in f32; f64 weighted sum with numpy
+    1.21 promotion) + Python's stable sorted(reverse=True)[:kk]."""
+    w0, w1 = (0.8, 0.2) if als_wins else (0.2, 0.8)
+    idx, val = [], []
+    for a, t in zip(als, tt):
+        amin, amax = float(np.nanmin(a)), float(np.nanmax(a))
+        ar = amax - amin
+        ar = 1.0 if ar < 10 * np.finfo(np.float64).eps else ar
+        asc = 1.0 / ar
+        amn = 0.0 - amin * asc
+        tmin, tmax = np.float32(np.nanmin(t)), np.float32(np.nanmax(t))
+        tr = np.float32(tmax - tmin)
+        tr = np.float32(1.0) if tr < 10 * np.finfo(np.float32).eps else tr
+        tsc = np.float32(np.float32(1.0) / tr)
+        tmn = np.float32(np.float32(0.0) - tmin * tsc)
+        an = a.astype(np.float64) * asc + amn
+        tn = (t * tsc + tmn).astype(np.float32)
+        f = w0 * an + w1 * tn.astype(np.float64)
+        order = sorted(range(len(f)), key=lambda j: f[j], reverse=True)[:kk]
+        idx.append(order)
+        val.append(f[order])
+    return np.array(idx), np.array(val)
+
+
+@pytest.mark.parametrize("n,kk,pattern", [(100_000, 5, "random"), (100_000, 1, "random"), (37_000, 8, "quantised"),
+                                          (5000, 5, "constant"), (3000, 3, "two_levels"), (70, 5, "random"),
+                                          (6_000_000, 5, "random"), (20_000, 10, "random")])
+def test_fuse_rows_topk_filter_matches_reference(device, n, kk, pattern):
+    """hrec_fuse_rows_topk's threshold-filter path (sample bound -> candidate
+    lists -> keyed top-k; overflowing rows take the exact segment path on the
+    device) returns the reference's fused top-k: indices bit-exact, values
+    bit-exact (same f64 arithmetic). Covers ties (quantised scores, two
+    levels), constant rows (every item a candidate -> overflow), short rows,
+    a 6M-item shard and kk above the filter path's 8."""
+    from src import _hrec
+
+    rng = np.random.default_rng(n + kk)
+    B = 3 if n > 1_000_000 else 7
+    a = rng.normal(size=(B, n)).astype(np.float32)
+    t = rng.normal(size=(B, n)).astype(np.float32)
+    if pattern == "quantised":
+        a, t = np.round(a, 1), np.round(t, 1)
+    elif pattern == "constant":
+        a[:] = 2.0
+        t[1:] = 0.5
+    elif pattern == "two_levels":
+        a = (rng.random((B, n)) < 0.5).astype(np.float32)
+        t = (rng.random((B, n)) < 0.5).astype(np.float32)
+    A, T = torch.as_tensor(a, device=device), torch.as_tensor(t, device=device)
+    amm, tmm = _hrec.rows_minmax(A), _hrec.rows_minmax(T)
+    rows = range(B) if n <= 1_000_000 else range(1)
+    for wins in (True, False):
+        gi, gv = _hrec.fuse_rows_topk(A, T, amm, tmm, wins, kk, idx_offset=11)
+        ei, ev = _fuse_rows_reference(a[list(rows)], t[list(rows)], wins, kk)
+        np.testing.assert_array_equal(gi.cpu().numpy()[list(rows)], ei + 11)
+        np.testing.assert_array_equal(gv.cpu().numpy()[list(rows)], ev)

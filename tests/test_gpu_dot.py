@@ -244,3 +244,30 @@ def test_hybrid_fused_minmax_and_overflow(device):
     rows = torch.arange(4, dtype=torch.int64, device=device)
     i, v = rec.recommend(rows, torch.from_numpy(U[:4]).to(device), False, 5)
     np.testing.assert_array_equal(i.cpu().numpy(), np.tile(np.arange(5), (4, 1)))
+
+
+@pytest.mark.parametrize("precision", ["exact", "bf16"])
+def test_captured_recommend_matches_eager(device, precision):
+    """CapturedRecommend (HIP graph replay of one recommend batch) returns the
+    eager results bit for bit, for new user batches copied into the
+    captured inputs."""
+    from src import _hrec
+    from src.recommend import CapturedRecommend, ShardedRecommender
+
+    rng = np.random.default_rng(41)
+    n_users, n_items, k, d, B = 500, 20_000, 32, 48, 64
+    U = torch.as_tensor(rng.normal(size=(n_users, k)).astype(np.float32), device=device)
+    V = torch.as_tensor(rng.normal(size=(n_items, k)).astype(np.float32), device=device)
+    iv = torch.as_tensor(rng.normal(size=(n_items, d)).astype(np.float32), device=device)
+    if precision == "exact":
+        rec = ShardedRecommender(U, _hrec.transpose(V), iv, 0, k)
+    else:
+        rec = ShardedRecommender(U, None, iv, 0, k, precision="bf16", V_local=V)
+    rows = [torch.as_tensor(rng.choice(n_users, B, replace=False), device=device) for _ in range(3)]
+    vecs = [torch.as_tensor(rng.normal(size=(B, d)).astype(np.float32), device=device) for _ in range(3)]
+    for wins in (True, False):
+        cap = CapturedRecommend(rec, rows[0], vecs[0], wins, 5)
+        for r, v in zip(rows, vecs):
+            gi, gv = (t.clone() for t in cap(r, v))
+            ei, ev = rec.recommend(r, v, wins, 5)
+            assert torch.equal(gi, ei) and torch.equal(gv, ev)
