@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "hybrid-als-twotower-recommender_amd"))
 sys.path.insert(0, ROOT)
 
 from src import _hrec, synthetic  # noqa: E402
-from src.als_engine import DeviceALS, shard_chunks, shard_range  # noqa: E402
+from src.als_engine import DeviceALS, RowLayout, shard_range  # noqa: E402
 from src.recommend import CapturedRecommend, ShardedRecommender, ShardedScorer  # noqa: E402
 from src.tt_engine import DeviceTwoTower  # noqa: E402
 
@@ -337,14 +337,22 @@ def main():
     u0, u_per = shard_range(n_users, world, rank)
     i0, i_per = shard_range(n_items, world, rank)
     # ALS shards: chunk-interleaved when W > 1 so each chunk's all-gather
-    # overlaps the next chunk's half-sweep (src/als_engine.py)
+    # overlaps the next chunk's half-sweep, users and items in contiguous
+    # parts balanced on cost = nnz + a per-row solve term (RowLayout.balanced
+    # over every row's rating count; src/als_engine.py)
     chunks = args.chunks if world > 1 else 1
-    u_ranges, _ = shard_chunks(n_users, world, rank, chunks)
-    i_ranges, _ = shard_chunks(n_items, world, rank, 1)
-    csr = synthetic.generate_ranges(n_users, n_items, cfg["density"], False, u_ranges)
-    csc = synthetic.generate_ranges(n_users, n_items, cfg["density"], True, i_ranges)
+    if world > 1:
+        u_lay = RowLayout.balanced(synthetic.row_counts(n_users, n_items, cfg["density"], False).cpu().numpy(),
+                                   world, chunks)
+        i_lay = RowLayout.balanced(synthetic.row_counts(n_users, n_items, cfg["density"], True).cpu().numpy(),
+                                   world, 1)
+    else:
+        u_lay, i_lay = RowLayout.equal(n_users, 1, 1), RowLayout.equal(n_items, 1, 1)
+    csr = synthetic.generate_layout(n_users, n_items, cfg["density"], False, u_lay, rank)
+    csc = synthetic.generate_layout(n_users, n_items, cfg["density"], True, i_lay, rank)
+    shard_nnz = torch.tensor([csr.nnz + csc.nnz], dtype=torch.int64, device="cuda")
     eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group,
-                    accum_mode=args.accum_mode, chunks=chunks)
+                    accum_mode=args.accum_mode, chunks=chunks, user_layout=u_lay, item_layout=i_lay)
     eng.init_user_factors(synthetic.SEED_INIT)
     torch.cuda.synchronize()
 
@@ -352,6 +360,11 @@ def main():
     if world > 1:
         dist.all_reduce(nnz_local)
     nnz_user, nnz_item = (int(x) for x in nnz_local.tolist())
+    per_rank_nnz = [int(shard_nnz.item())]
+    if world > 1:
+        allr = torch.zeros(world, dtype=torch.int64, device="cuda")
+        dist.all_gather_into_tensor(allr, shard_nnz)
+        per_rank_nnz = allr.tolist()
 
     for _ in range(args.warmup):
         eng.epoch()
@@ -394,9 +407,9 @@ def main():
     # (hrec_als_score_topk: the score matrix is never written).
     scoring = None
     if rank == 0 and args.score_users > 0:
-        Vt = _hrec.transpose(eng.V[:n_items].contiguous())
+        Vt = _hrec.transpose(eng.item_factor_rows(0, n_items).contiguous())
         B = args.score_users
-        users = torch.arange(B, dtype=torch.int64, device="cuda") * (n_users // B)
+        users = eng.user_rows(torch.arange(B, dtype=torch.int64, device="cuda") * (n_users // B))
         for _ in range(2):
             _hrec.als_score_topk(eng.U, users, Vt, n_items, k, 5)
         torch.cuda.synchronize()
@@ -419,7 +432,8 @@ def main():
             from oracle import cpu_baseline as cb
 
             su = users[: args.cpu_score_users].cpu().numpy()
-            scoring["cpu_baseline"] = cb.als_scoring(eng.U[su].cpu().numpy(), eng.V[:n_items].cpu().numpy(), k, 5, B)
+            scoring["cpu_baseline"] = cb.als_scoring(eng.U[su].cpu().numpy(), eng.item_factor_rows(0, n_items).cpu().numpy(),
+                                                     k, 5, B)
 
     # End-to-end hybrid top-5 (HybridRecommendationSystem.get_hybrid_recommendations
     # for a batch of users): JVM-exact ALS scores + two-tower Dot (d=64, Keras
@@ -436,11 +450,12 @@ def main():
         cat = torch.randint(0, 255, (n_items,), generator=g, dtype=torch.int32)[i0: i0 + n_loc]
         num = torch.rand((n_items, 2), generator=g)[i0: i0 + n_loc].contiguous()
         ivec = tt.item_vectors(items.cuda(), man.cuda(), cat.cuda(), num.cuda())
-        Vt_loc = _hrec.transpose(eng.V[i0: i0 + n_loc].contiguous())
+        Vt_loc = _hrec.transpose(eng.item_factor_rows(i0, n_loc).contiguous())
         rec = ShardedRecommender(eng.U, Vt_loc, ivec, i0, k, world=world, rank=rank, group=group)
         Bh = args.hybrid_users
-        hu = (torch.arange(Bh, dtype=torch.int64) * (n_users // Bh)).cuda()
-        uvec = tt.user_vectors(hu.to(torch.int32))
+        hu_ids = (torch.arange(Bh, dtype=torch.int64) * (n_users // Bh)).cuda()
+        hu = eng.user_rows(hu_ids)  # rows of the (layout-ordered) user factor buffer
+        uvec = tt.user_vectors(hu_ids.to(torch.int32))
         hs_g, hs_eager = time_recommend(rec, hu, uvec, world)
         hs, how = recommend_line_timing(hs_g, hs_eager)
         hybrid = {"pairs_per_s": Bh * n_items / hs, "ms_per_batch": hs * 1e3, "users": Bh, "items": n_items,
@@ -505,7 +520,8 @@ def main():
     als256 = None
     if args.rank256_epochs > 0:
         k256 = 256
-        e256 = DeviceALS(n_users, n_items, k256, 0.1, csr, csc, world=world, rank=rank, group=group, chunks=chunks)
+        e256 = DeviceALS(n_users, n_items, k256, 0.1, csr, csc, world=world, rank=rank, group=group, chunks=chunks,
+                         user_layout=u_lay, item_layout=i_lay)
         e256.init_user_factors(synthetic.SEED_INIT)
         e256.epoch()
         if world > 1:
@@ -757,8 +773,10 @@ def main():
                              f"rank {k}, reg 0.1; step = one ALS epoch (item + user half-sweep)"),
                 "users": n_users, "items": n_items, "density": cfg["density"], "rank": k,
                 "nnz": nnz_user, "nnz_check_csc": nnz_item,
-                "parallelism": (f"dp{world} (row-sharded users/items; user side in {chunks} chunks per rank, "
-                                f"each chunk's RCCL all-gather overlapping the next chunk's half-sweep)"
+                "shard_nnz_max_over_min": max(per_rank_nnz) / max(1, min(per_rank_nnz)),
+                "parallelism": (f"dp{world} (users/items in contiguous parts balanced on nnz + per-row solve cost; "
+                                f"user side in {chunks} chunks per rank, each chunk's RCCL all-gather overlapping "
+                                f"the next chunk's half-sweep)"
                                 if world > 1 else "dp1 (single GPU, no collectives)"),
             },
             "roofline": {

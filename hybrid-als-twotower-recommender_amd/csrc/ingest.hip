@@ -257,3 +257,28 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
                      indptr);
   return check_launch("coo_to_csr");
 }
+
+// ------------------------------------------------------- shard layouts
+// x[i] = table[x[i]] in place (the CSR/CSC column ids of an nnz-balanced
+// ALS shard -> rows of the padded replicated factor buffer,
+// src/als_engine.py:RowLayout). Ids outside [0, table_n) become -1 (the
+// half-sweep's structured loads read those as zero rows).
+namespace hrec {
+__global__ __launch_bounds__(256) void remap_i32_kernel(int32_t* __restrict__ x, int64_t n,
+                                                        const int32_t* __restrict__ table, int64_t table_n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int32_t v = x[i];
+    x[i] = (v >= 0 && v < table_n) ? table[v] : -1;
+  }
+}
+}  // namespace hrec
+
+extern "C" int hrec_remap_i32(int32_t* x, int64_t n, const int32_t* table, int64_t table_n, void* stream) {
+  HREC_REQUIRE(n >= 0 && table_n >= 0, "remap_i32: bad shape");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(x && table, "remap_i32: null pointer");
+  int64_t grid = (n + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(remap_i32_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), x, n, table, table_n);
+  return check_launch("remap_i32_kernel");
+}

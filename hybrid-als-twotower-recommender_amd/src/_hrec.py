@@ -35,6 +35,7 @@ _SIGNATURES = {
     "hrec_minmax_i64": (_c_i32, [_vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "hrec_coo_to_csr_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "hrec_coo_to_csr": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_remap_i32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp]),
     "hrec_als_init_factors": (_c_i32, [_c_u64, _c_i64, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_als_half_sweep": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl,
                                      _c_i32, _vp, _vp]),
@@ -237,6 +238,13 @@ def coo_to_csr(rows, cols, vals, n_rows):
         nnz, n_rows, _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
         _dev(values, torch.float32, "values"), _dev(ws, torch.uint8, "ws"), ws.numel(), _stream()))
     return indptr, indices, values
+
+
+def remap_i32(x, table):
+    """x[i] = table[x[i]] in place on the device (ids outside the table -> -1)."""
+    _check("hrec_remap_i32", lib().hrec_remap_i32(
+        _dev(x, torch.int32, "x"), x.numel(), _dev(table, torch.int32, "table"), table.numel(), _stream()))
+    return x
 
 
 # -------------------------------------------------------------------- ALS

@@ -53,13 +53,90 @@ def shard_chunks(n, world, rank, chunks):
     return [(c * world * cs + rank * cs, cs) for c in range(chunks)], cs
 
 
+class RowLayout:
+    """How one side's rows (users or items) sit in the replicated factor
+    buffer across W ranks and C chunks per rank ("partitioned by
+    nnz-balanced contiguous ranges"). Part p = c·W + r (chunk c of rank r)
+    owns the contiguous global rows [bounds[p], bounds[p+1]) and stores them
+    at buffer rows [p·cs, p·cs + count_p): every part has cs slots, so each
+    chunk's RCCL all-gather moves equal-sized shards (the padding rows stay
+    zero and are never referenced).
+
+    equal(): count-balanced parts with bounds[p] = p·cs — buffer row ==
+    global row (the CSR ids need no remap). balanced(): bounds chosen on the
+    row costs nnz + row_cost (Gramian work per rating + a per-row solve
+    term), so skewed degree distributions (power-law items) give every rank
+    the same work; the shards' column ids are then remapped to buffer rows
+    (hrec_remap_i32) once, at setup."""
+
+    def __init__(self, n, world, chunks, bounds):
+        self.n, self.world, self.chunks = int(n), int(world), int(chunks)
+        self.bounds = [int(b) for b in bounds]
+        if len(self.bounds) != self.world * self.chunks + 1 or self.bounds[0] != 0 or self.bounds[-1] != self.n:
+            raise ValueError("RowLayout: bounds must run 0 .. n over world * chunks parts")
+        counts = [b - a for a, b in zip(self.bounds, self.bounds[1:])]
+        if min(counts) < 0:
+            raise ValueError("RowLayout: bounds must be non-decreasing")
+        self.cs = max(1, max(counts))
+
+    @classmethod
+    def equal(cls, n, world, chunks=1):
+        per = math.ceil(n / world) if n else 0
+        cs = math.ceil(per / chunks) if per else 0
+        return cls(n, world, chunks, [min(p * cs, n) for p in range(world * chunks + 1)])
+
+    @classmethod
+    def balanced(cls, row_nnz, world, chunks=1, row_cost=128):
+        """Contiguous parts of (near) equal cost, cost(row) = nnz + row_cost."""
+        import numpy as np
+
+        w = np.asarray(row_nnz, dtype=np.float64) + float(row_cost)
+        n, P = len(w), world * chunks
+        cum = np.concatenate([[0.0], np.cumsum(w)])
+        # part p starts at the first row whose preceding cost reaches p/P of the total
+        starts = np.searchsorted(cum, cum[-1] * np.arange(P + 1) / P, side="left")
+        starts = np.minimum(np.maximum.accumulate(starts), n)
+        starts[0], starts[-1] = 0, n
+        return cls(n, world, chunks, starts.tolist())
+
+    @property
+    def identity(self):
+        """Buffer row == global row for every real row."""
+        return all(self.bounds[p] == min(p * self.cs, self.n) for p in range(len(self.bounds)))
+
+    @property
+    def slots(self):
+        return self.world * self.chunks * self.cs
+
+    def part_rows(self, rank):
+        """[(global row_begin, count)] of this rank's chunks, in chunk order."""
+        return [(self.bounds[c * self.world + rank], self.bounds[c * self.world + rank + 1] -
+                 self.bounds[c * self.world + rank]) for c in range(self.chunks)]
+
+    def positions(self):
+        """int32 [n]: buffer row of each global row."""
+        import numpy as np
+
+        pos = np.empty(self.n, dtype=np.int32)
+        for p in range(len(self.bounds) - 1):
+            a, b = self.bounds[p], self.bounds[p + 1]
+            pos[a:b] = p * self.cs + np.arange(b - a, dtype=np.int32)
+        return pos
+
+
 class DeviceALS:
     """Holds one rank's CSR shard (user rows), CSC shard (item rows) and the
     replicated factor matrices."""
 
     def __init__(self, n_users, n_items, rank_k, reg_param, user_csr: DeviceCSR,
                  item_csc: DeviceCSR, world=1, rank=0, group=None, accum_mode=0, sweep=None, chunks=1,
-                 item_chunks=1):
+                 item_chunks=1, user_layout=None, item_layout=None, remap=None):
+        """user_layout / item_layout (RowLayout): the shards' row layout;
+        default RowLayout.equal(n, world, chunks). With a non-identity layout
+        the shards are this rank's parts padded to cs rows each (see
+        synthetic.generate_layout) with GLOBAL column ids; they are remapped
+        here (remap, default hrec_remap_i32) to rows of the other side's
+        buffer."""
         self.n_users, self.n_items = int(n_users), int(n_items)
         self.k = int(rank_k)
         self.kp = padded_k(self.k)
@@ -76,17 +153,32 @@ class DeviceALS:
         # row chunks per side (user side: `chunks`, item side: `item_chunks`)
         self.u_chunks = int(chunks) if self.world > 1 else 1
         self.i_chunks = int(item_chunks) if self.world > 1 else 1
-        self.u_cs, self.i_cs = self.u_per, self.i_per
-        if self.world > 1:
-            ur, self.u_cs = shard_chunks(self.n_users, self.world, self.rank, self.u_chunks)
-            ir, self.i_cs = shard_chunks(self.n_items, self.world, self.rank, self.i_chunks)
-            assert self.u_per == self.u_chunks * self.u_cs and self.i_per == self.i_chunks * self.i_cs
-            assert user_csr.row_begin == ur[0][0] and item_csc.row_begin == ir[0][0]
+        self.u_layout = user_layout or RowLayout.equal(self.n_users, self.world, self.u_chunks)
+        self.i_layout = item_layout or RowLayout.equal(self.n_items, self.world, self.i_chunks)
+        for lay, ch, per, csr in ((self.u_layout, self.u_chunks, self.u_per, user_csr),
+                                  (self.i_layout, self.i_chunks, self.i_per, item_csc)):
+            if lay.world != self.world or lay.chunks != ch or per != ch * lay.cs:
+                raise ValueError("DeviceALS: shard rows do not match the row layout")
+            if self.world > 1 and csr.row_begin != lay.part_rows(self.rank)[0][0]:
+                raise ValueError("DeviceALS: shard does not start at the layout's first row for this rank")
+        self.u_cs, self.i_cs = self.u_layout.cs, self.i_layout.cs
+        self._u_pos = self._i_pos = None  # global row -> buffer row (non-identity layouts)
+        if not self.u_layout.identity or not self.i_layout.identity:
+            remap = remap or _hrec.remap_i32
+            self._u_pos = torch.as_tensor(self.u_layout.positions(), device=dev)
+            self._i_pos = torch.as_tensor(self.i_layout.positions(), device=dev)
+            for csr, lay, pos in ((user_csr, self.i_layout, self._i_pos), (item_csc, self.u_layout, self._u_pos)):
+                if lay.identity or csr.col_layout is lay:
+                    continue  # global ids are buffer rows / already remapped for this layout
+                if csr.col_layout is not None:
+                    raise ValueError("DeviceALS: shard ids were remapped to another layout")
+                remap(csr.indices, pos)  # user rows hold item ids, item rows user ids
+                csr.col_layout = lay
         chunked = max(self.u_chunks, self.i_chunks) > 1
         self.comm = torch.cuda.Stream(device=dev) if chunked and dev.type == "cuda" else None
-        # Replicated factors, padded to world * per rows for the all-gather.
-        self.U = torch.zeros((self.u_per * self.world, self.kp), dtype=torch.float32, device=dev)
-        self.V = torch.zeros((self.i_per * self.world, self.kp), dtype=torch.float32, device=dev)
+        # Replicated factors in the layouts' padded buffers (world * per rows).
+        self.U = torch.zeros((self.u_layout.slots, self.kp), dtype=torch.float32, device=dev)
+        self.V = torch.zeros((self.i_layout.slots, self.kp), dtype=torch.float32, device=dev)
         if self.world > 1:
             self.U_local = torch.zeros((self.u_per, self.kp), dtype=torch.float32, device=dev)
             self.V_local = torch.zeros((self.i_per, self.kp), dtype=torch.float32, device=dev)
@@ -96,13 +188,25 @@ class DeviceALS:
     # -------------------------------------------------------------- init
     def init_user_factors(self, seed):
         """Spark-style init of the user side (the item init is never read in
-        explicit mode: items are solved first)."""
-        _hrec.als_init_factors(seed, 0, self.n_users, self.k, self.kp, self.U)
+        explicit mode: items are solved first). Counter-based per global row,
+        so every layout holds the same vectors."""
+        if self._u_pos is None:
+            _hrec.als_init_factors(seed, 0, self.n_users, self.k, self.kp, self.U)
+            return
+        lay = self.u_layout
+        for p in range(len(lay.bounds) - 1):
+            a, b = lay.bounds[p], lay.bounds[p + 1]
+            if b > a:
+                _hrec.als_init_factors(seed, a, b - a, self.k, self.kp, self.U[p * lay.cs: p * lay.cs + b - a])
 
     def set_user_factors(self, U0):
         """Inject initial user factors ([n_users, k] float32, any device)."""
         self.U.zero_()
-        self.U[: self.n_users, : self.k].copy_(torch.as_tensor(U0, dtype=torch.float32))
+        U0 = torch.as_tensor(U0, dtype=torch.float32).to(self.U.device)
+        if self._u_pos is None:
+            self.U[: self.n_users, : self.k].copy_(U0)
+        else:
+            self.U[self._u_pos.long(), : self.k] = U0
 
     # ------------------------------------------------------------- sweeps
     def _gather(self, full, local):
@@ -148,10 +252,25 @@ class DeviceALS:
         for _ in range(int(max_iter)):
             self.epoch()
 
+    def user_rows(self, ids):
+        """Buffer rows of U for global user ids (a device int64 tensor)."""
+        return ids if self._u_pos is None else self._u_pos[ids].to(torch.int64)
+
+    def item_factor_rows(self, start, count):
+        """[count, kp] item factors of global items [start, start + count)."""
+        if self._i_pos is None:
+            return self.V[start: start + count]
+        return self.V[self._i_pos[start: start + count].long()]
+
     @property
     def user_factors(self):
-        return self.U[: self.n_users, : self.k]
+        """[n_users, k] in global row order."""
+        if self._u_pos is None:
+            return self.U[: self.n_users, : self.k]
+        return self.U[self._u_pos.long(), : self.k]
 
     @property
     def item_factors(self):
-        return self.V[: self.n_items, : self.k]
+        if self._i_pos is None:
+            return self.V[: self.n_items, : self.k]
+        return self.V[self._i_pos.long(), : self.k]

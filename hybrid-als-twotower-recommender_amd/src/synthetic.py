@@ -43,6 +43,7 @@ class DeviceCSR:
     row_begin: int
     n_rows: int
     n_cols: int
+    col_layout: object = None  # RowLayout the column ids were remapped to (None: global ids)
 
     @property
     def nnz(self):
@@ -50,10 +51,11 @@ class DeviceCSR:
 
 
 def generate(n_users, n_items, density, transposed, row_begin=0, n_rows=None, seed=SEED,
-             seed2=SEED2, n_levels=N_LEVELS, device=None):
+             seed2=SEED2, n_levels=N_LEVELS, device=None, n_real=None):
     """Generate rows [row_begin, row_begin+n_rows) of R (transposed=False:
     user rows over items) or of R^T (transposed=True: item rows over users).
-    Rows past the end of the matrix are empty (shard padding)."""
+    Rows past the end of the matrix, or past the first n_real rows, are empty
+    (shard padding)."""
     _hrec.require_device()
     device = device or torch.device("cuda", torch.cuda.current_device())
     total_rows = n_items if transposed else n_users
@@ -61,6 +63,8 @@ def generate(n_users, n_items, density, transposed, row_begin=0, n_rows=None, se
     if n_rows is None:
         n_rows = total_rows - row_begin
     real = max(0, min(n_rows, total_rows - row_begin))
+    if n_real is not None:
+        real = min(real, int(n_real))
     thr = threshold(density)
     counts = torch.zeros(n_rows, dtype=torch.int64, device=device)
     if real > 0:
@@ -91,3 +95,32 @@ def generate_ranges(n_users, n_items, density, transposed, ranges, **kw):
     values = torch.cat([p.values for p in parts])
     return DeviceCSR(indptr, indices, values, ranges[0][0], sum(n for _, n in ranges), parts[0].n_cols)
 
+
+
+def generate_layout(n_users, n_items, density, transposed, layout, rank, **kw):
+    """This rank's shard under an als_engine.RowLayout: its parts (chunk
+    order), each part's rows followed by empty rows up to the layout's cs,
+    with GLOBAL column ids (DeviceALS remaps them)."""
+    parts = [generate(n_users, n_items, density, transposed, b, layout.cs, n_real=cnt, **kw)
+             for b, cnt in layout.part_rows(rank)]
+    if len(parts) == 1:
+        return parts[0]
+    offs, ips = 0, [parts[0].indptr[:1]]
+    for p in parts:
+        ips.append(p.indptr[1:] + offs)
+        offs += p.nnz
+    return DeviceCSR(torch.cat(ips), torch.cat([p.indices for p in parts]), torch.cat([p.values for p in parts]),
+                     parts[0].row_begin, layout.cs * len(parts), parts[0].n_cols)
+
+
+def row_counts(n_users, n_items, density, transposed, seed=SEED, device=None):
+    """Ratings per row of R (or R^T) for every row: the input of
+    als_engine.RowLayout.balanced."""
+    _hrec.require_device()
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    n_rows = n_items if transposed else n_users
+    counts = torch.zeros(n_rows, dtype=torch.int64, device=device)
+    if n_rows:
+        _hrec.synth_row_counts(seed, threshold(density), 0, n_rows, n_users if transposed else n_items, transposed,
+                               counts)
+    return counts

@@ -104,6 +104,13 @@ int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const float* vals,
                     float* values, void* workspace, size_t workspace_bytes,
                     void* stream);
 
+/* hrec_remap_i32: x[i] = table[x[i]] in place (ids outside [0, table_n)
+ * -> -1). Maps an ALS shard's column ids (global user / item rows) to rows
+ * of an nnz-balanced, padded factor layout (src/als_engine.py RowLayout;
+ * Spark partitions users/items into numUserBlocks/numItemBlocks blocks
+ * [ext: ALS.scala] — here contiguous row ranges balanced by ratings). */
+int hrec_remap_i32(int32_t* x, int64_t n, const int32_t* table, int64_t table_n, void* stream);
+
 /* ------------------------------------------------------------------ ALS --
  * Initial factors (Spark ALS.initialize [ext: pyspark 3.5.1 ALS.scala]:
  * per row a Gaussian-like vector, L2-normalised, f32). Counter-based on

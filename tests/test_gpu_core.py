@@ -356,7 +356,7 @@ def test_als_score_topk_overflow_flag(device):
 
 
 # ------------------------------------------------ multi-rank on one device
-def _chunked_worker(rank, world, port, chunks, q):
+def _chunked_worker(rank, world, port, chunks, q, balanced=False):
     import os
 
     import torch.distributed as dist
@@ -368,11 +368,21 @@ def _chunked_worker(rank, world, port, chunks, q):
     from src.als_engine import DeviceALS, shard_chunks
 
     n_u, n_i, dens, k = 700, 300, 0.05, 32
-    ur, _ = shard_chunks(n_u, world, rank, chunks)
-    ir, _ = shard_chunks(n_i, world, rank, 2)
-    eng = DeviceALS(n_u, n_i, k, 0.1, synthetic.generate_ranges(n_u, n_i, dens, False, ur),
-                    synthetic.generate_ranges(n_u, n_i, dens, True, ir), world=world, rank=rank,
-                    group=dist.group.WORLD, chunks=chunks, item_chunks=2)
+    if balanced:  # nnz-balanced parts: padded shards, ids remapped on the device (hrec_remap_i32)
+        from src.als_engine import RowLayout
+
+        ul = RowLayout.balanced(synthetic.row_counts(n_u, n_i, dens, False).cpu().numpy(), world, chunks)
+        il = RowLayout.balanced(synthetic.row_counts(n_u, n_i, dens, True).cpu().numpy(), world, 2)
+        assert not ul.identity and not il.identity
+        eng = DeviceALS(n_u, n_i, k, 0.1, synthetic.generate_layout(n_u, n_i, dens, False, ul, rank),
+                        synthetic.generate_layout(n_u, n_i, dens, True, il, rank), world=world, rank=rank,
+                        group=dist.group.WORLD, chunks=chunks, item_chunks=2, user_layout=ul, item_layout=il)
+    else:
+        ur, _ = shard_chunks(n_u, world, rank, chunks)
+        ir, _ = shard_chunks(n_i, world, rank, 2)
+        eng = DeviceALS(n_u, n_i, k, 0.1, synthetic.generate_ranges(n_u, n_i, dens, False, ur),
+                        synthetic.generate_ranges(n_u, n_i, dens, True, ir), world=world, rank=rank,
+                        group=dist.group.WORLD, chunks=chunks, item_chunks=2)
     eng.init_user_factors(synthetic.SEED_INIT)
     eng.fit(3)
     torch.cuda.synchronize()
@@ -381,9 +391,11 @@ def _chunked_worker(rank, world, port, chunks, q):
     dist.destroy_process_group()
 
 
-def test_chunked_overlapped_allgather_on_device(device):
+@pytest.mark.parametrize("balanced", [False, True])
+def test_chunked_overlapped_allgather_on_device(device, balanced):
     """Two ranks on one GPU (gloo carries the all-gathers of device tensors):
-    the chunk-interleaved shards, HIP half-sweeps on the compute stream and
+    the chunk-interleaved shards (equal-count, or nnz-balanced with padded
+    parts and device-remapped ids), HIP half-sweeps on the compute stream and
     per-chunk all-gathers on the side stream reproduce the single-rank fit
     bit for bit."""
     import socket
@@ -403,7 +415,7 @@ def test_chunked_overlapped_allgather_on_device(device):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_chunked_worker, args=(r, 2, port, 3, q)) for r in range(2)]
+    procs = [ctx.Process(target=_chunked_worker, args=(r, 2, port, 3, q, balanced)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(2)]
