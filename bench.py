@@ -731,17 +731,23 @@ def main():
     # rocprofv3 summary (scripts/gpu_profile.sh), used only when the kernel
     # source it profiled is the one this tree runs (sha256 stamped by
     # scripts/summarize_profile.py); otherwise null + the reason.
-    traffic, traffic_src, tsw = None, None, None
+    traffic, traffic_src, tsw, pj, fresh = None, None, None, {}, {}
     prof = args.traffic_json or latest_profile()
     if prof and os.path.exists(prof) and args.accum_mode == 0:
         with open(prof) as f:
             pj = json.load(f)
-        fresh = {src: pj.get("sources_sha256", {}).get(src) == source_sha256(src) for src in ("als.hip", "tt.hip")}
+        fresh = {src: pj.get("sources_sha256", {}).get(src) == source_sha256(src)
+                 for src in ("als.hip", "tt.hip", "tt_mfma.hip")}
         traffic_src = {"profile": os.path.relpath(prof, ROOT), "kernel_source_matches": fresh["als.hip"]}
         if fresh["als.hip"] and world == 1:
             traffic = pj["als_half_sweep"].get("hbm_bytes_avg_per_launch")
         if fresh["tt.hip"]:
             tsw = pj.get("tt_adam_sweep", {})
+    if tt_iv is not None:
+        tiv = pj.get("tt_item_forward_c4", {}) if traffic_src and fresh["tt_mfma.hip"] and world == 1 else {}
+        tt_iv["roofline"]["traffic"] = tiv.get("hbm_bytes_avg_per_launch_corrected")
+        tt_iv["roofline"]["traffic_note"] = ("HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                                             "scripts/gpu_profile.sh; null when the profile predates csrc/tt_mfma.hip)")
     if tt_train is not None:
         tt_train["roofline"]["traffic"] = tsw.get("hbm_bytes_avg_per_launch_corrected") if tsw else None
         tt_train["roofline"]["traffic_note"] = (

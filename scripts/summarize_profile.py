@@ -111,6 +111,21 @@ def main(base):
     if wd:
         res["als_half_sweep_wide_rank256"] = {"launches": len(wd), "durations_ms": wd,
                                               "workload": "scripts/wide_quick.py 256 300000 100000 (item, user)"}
+    # c4 item-vector precompute (K4m, tt_item_forward_mfma_kernel at d = 128
+    # over 50M items): trace durations + FETCH/WRITE passes (x2 on FETCH:
+    # 16-B lane loads)
+    kf = "tt_item_forward_mfma_kernel<8, 8, true, false, 16, true>"
+    fd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace if kf in r["Kernel_Name"]]
+    tf = {"launches": len(fd), "avg_ms": sum(fd) / max(len(fd), 1)}
+    for name, sub in (("FETCH_SIZE", "prof_fetch_c4"), ("WRITE_SIZE", "prof_write_c4")):
+        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(base, sub, "**", "*counter_collection.csv"))
+                if kf in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+        if vals:
+            tf[name + "_KiB_avg_per_launch"] = sum(vals) / len(vals)
+    if "FETCH_SIZE_KiB_avg_per_launch" in tf and "WRITE_SIZE_KiB_avg_per_launch" in tf:
+        tf["hbm_bytes_avg_per_launch_corrected"] = 1024 * (2 * tf["FETCH_SIZE_KiB_avg_per_launch"] +
+                                                           tf["WRITE_SIZE_KiB_avg_per_launch"])
+    res["tt_item_forward_c4"] = tf
     res["sources_sha256"] = source_hashes()
     print(json.dumps(res, indent=1))
 
