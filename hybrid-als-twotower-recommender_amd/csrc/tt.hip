@@ -766,6 +766,13 @@ extern "C" int hrec_tt_score(const float* user_vec, int n_users, const float* it
     return check_launch("tt_score_kernel");
   }
   HREC_REQUIRE((n_items + 63) / 64 < (1ll << 32), "tt_score: grid too large");
+  // widths the K8 matrix-core dot handles natively: its f32 path (exact f32
+  // fma chains per k-step, item fragments kept in registers across the
+  // user chunks, XCD-aware tile order; csrc/dot_topk.hip) — 0.91 of the f32
+  // peak at c4 against ~0.33 for the LDS-staged tile kernel below
+  if ((d == 32 || d == 64 || d == 128 || d == 256) && (((uintptr_t)user_vec | (uintptr_t)item_vec) & 15) == 0 &&
+      !getenv("HREC_TT_SCORE_TILE"))
+    return hrec_dot_scores(user_vec, n_users, item_vec, n_items, d, 0, out, n_items, stream);
   if (HREC_TT_SCORE_V2 && d % 4 == 0 && (((uintptr_t)user_vec | (uintptr_t)item_vec) & 15) == 0) {
     hipLaunchKernelGGL(tt_score_mfma2_kernel, dim3((unsigned)((n_items + 63) / 64)), dim3(256), 0,
                        as_stream(stream), user_vec, n_users, item_vec, n_items, d, out);
