@@ -1,0 +1,441 @@
+// K9s: both score matrices of the bf16 hybrid (BASELINE c5: rank-256 ALS
+// factors and d = 256 tower vectors) in ONE launch, with the per-user
+// min / max of each matrix reduced in the epilogue.
+//
+// Replaces, for precision "bf16", the chain the reference's
+// get_hybrid_recommendations implies per user (src/hybrid_system.py:95-116:
+// ALS transform + Keras Dot over every candidate, then a MinMaxScaler
+// fit_transform per model, src/hybrid_system.py:57-75) up to the fusion:
+// the gather of the batch's ALS user rows, their f32 -> bf16 conversion
+// (round to nearest even, as hrec_f32_to_bf16), the two [B, d] x [d, N]
+// GEMMs on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16, f32
+// accumulation, the k order of hrec_dot_scores: bit-identical scores) and
+// the per-row min / max of hrec_rows_minmax_f32 (fminf / fmaxf: NaN-free
+// minimum and maximum — exact under any grouping). The score matrices still
+// go to HBM: the fusion's exact min-max scaling needs every row's extremes
+// before any fused score exists (hrec_fuse_rows_topk reads them back).
+//
+// Work split: block (model, user tile, item group) stages its <= 256 users
+// (128 KB at d = 256) in LDS once and owns a contiguous item range; each
+// wave walks its own 16 NI-item slices of that range (no block barrier in
+// the main loop, so waves of a short range simply finish early), keeping
+// the slice's item fragments for the whole d in registers and sweeping the
+// users in chunks of 64. The epilogue stores the tile (16-B stores) and
+// folds each lane's min / max into per-user LDS slots (order-preserving
+// uint keys, ds_max_u32); every block writes its partials, and a tiny
+// second kernel reduces them per user (no global atomics, deterministic).
+#include <float.h>
+
+#include <type_traits>
+
+#include "common.h"
+
+namespace hrec {
+
+typedef float hs_f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 hs_bf8 __attribute__((ext_vector_type(8)));
+typedef int hs_rsrc __attribute__((ext_vector_type(4)));
+__device__ hs_f4 hs_sbuf_load(hs_rsrc rsrc, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.buffer.load.v4f32");
+
+union HsFrag {
+  int4 i;
+  hs_f4 f;
+};
+
+struct HybScoresArgs {
+  const float* users[2];   // f32 user rows: ALS factors, two-tower user vectors
+  int64_t ld[2];           // their row strides (elements)
+  const int64_t* rows[2];  // row of batch user b (nullptr: row b)
+  int width[2];            // valid columns (<= DK; the operand is zero beyond)
+  int B;
+  const char* items[2];    // bf16 item operands [N, DK]
+  int64_t N;
+  float* out[2];           // score matrices [B, ldo]
+  int64_t ldo;
+  float* part;             // [2][G][2][B]: per-block min / max
+  int G;                   // item groups per (model, user tile)
+  int UB;                  // users per tile (multiple of 64)
+  int n_ut;
+};
+
+#ifndef HREC_HS_ABLATE
+#define HREC_HS_ABLATE 0  // timing-only builds: 1 = no score stores, 2 = and no min/max, 3 = staging only
+#endif
+
+#ifndef HREC_HS_NT
+#define HREC_HS_NT 0  // 1 = non-temporal score stores
+#endif
+
+constexpr int kHsThreads = 512;
+constexpr int kHsMaxUserBytes = 128 * 1024;
+
+// f32 -> bf16 bits, round to nearest even (NaN stays NaN): hrec_f32_to_bf16.
+__device__ __forceinline__ uint32_t hs_bf16(float v) {
+  const uint32_t x = __float_as_uint(v);
+  if ((x & 0x7fffffffu) > 0x7f800000u) return (x >> 16) | 0x40u;
+  return (x + 0x7fffu + ((x >> 16) & 1u)) >> 16;
+}
+
+// Order-preserving float <-> uint keys (larger float -> larger key); the
+// LDS slots start at 0, below every key.
+__device__ __forceinline__ uint32_t hs_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float hs_unkey(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int DK>
+struct HsShape {
+  static constexpr int KS = DK / 32;           // bf16 MFMA k-steps
+  static constexpr int kChunks = DK * 2 / 16;  // 16-B chunks per user row
+  static constexpr bool kSwz = kChunks >= 16;  // XOR-swizzled rows (as dot_res_kernel)
+  static constexpr int kRowB = kSwz ? kChunks * 16 : kChunks * 16 + 16;
+#ifndef HREC_HS_NI256
+#define HREC_HS_NI256 2
+#endif
+  static constexpr int NI = DK == 64 ? 4 : (DK == 256 ? HREC_HS_NI256 : 2);  // item tiles per wave slice (VGPR budget)
+  static constexpr int NU = NI == 4 ? 2 : 4;    // user tiles per chunk (NI 4: each user fragment feeds 4 MFMAs)
+};
+
+template <int DK>
+__global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a) {
+  using S = HsShape<DK>;
+  constexpr int KS = S::KS, NI = S::NI, NU = S::NU, CU = 16 * NU;
+  constexpr int kRowB = S::kRowB;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  char* us = dsm;
+  uint32_t* mmk = reinterpret_cast<uint32_t*>(dsm + (size_t)a.UB * kRowB);  // [UB][2]: ~key(min), key(max)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int model = blockIdx.x & 1;
+  const int rest = blockIdx.x >> 1;
+  const int ut = rest % a.n_ut, grp = rest / a.n_ut;
+  const int64_t per = ((a.N + a.G - 1) / a.G + 15) / 16 * 16;
+  const int64_t i0 = (int64_t)grp * per;
+  const int64_t i1 = i0 + per < a.N ? i0 + per : a.N;
+  const int b0 = ut * a.UB;
+  const int ub = a.B - b0 < a.UB ? a.B - b0 : a.UB;
+
+  // users of the tile -> LDS as bf16 (zero rows / columns beyond the batch /
+  // width). Batches of chunks (8 floats each) per thread: all loads are
+  // issued before the first conversion (16-B loads when the row allows).
+  {
+    const float* src = a.users[model];
+    const int64_t ld = a.ld[model];
+    const int64_t* rws = a.rows[model];
+    const int wd = a.width[model];
+    const bool vec = (ld & 3) == 0 && ((uintptr_t)src & 15) == 0;
+    constexpr int kBatch = DK == 256 ? 16 : 8;  // one round of loads at UB = 256
+    const int n_chunks = a.UB * S::kChunks;
+    for (int o0 = threadIdx.x; o0 < n_chunks; o0 += kBatch * kHsThreads) {
+      float f[kBatch][8];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int o = o0 + j * kHsThreads;
+        const int r = o / S::kChunks, q = o % S::kChunks;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[j][e] = 0.f;
+        if (o < n_chunks && r < ub && 8 * q < wd) {
+          const int64_t row = rws ? rws[b0 + r] : (int64_t)(b0 + r);
+          const float* p = src + row * ld + 8 * q;
+          if (vec && 8 * q + 8 <= wd) {
+            const float4 x0 = *reinterpret_cast<const float4*>(p);
+            const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
+            f[j][0] = x0.x, f[j][1] = x0.y, f[j][2] = x0.z, f[j][3] = x0.w;
+            f[j][4] = x1.x, f[j][5] = x1.y, f[j][6] = x1.z, f[j][7] = x1.w;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (8 * q + e < wd) f[j][e] = p[e];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int o = o0 + j * kHsThreads;
+        if (o >= n_chunks) break;
+        const int r = o / S::kChunks, q = o % S::kChunks;
+        uint32_t h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = hs_bf16(f[j][e]);  // bf16(0.f) = 0
+        const int4 v = {(int)(h[0] | (h[1] << 16)), (int)(h[2] | (h[3] << 16)), (int)(h[4] | (h[5] << 16)),
+                        (int)(h[6] | (h[7] << 16))};
+        *reinterpret_cast<int4*>(us + r * kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v;
+      }
+    }
+    for (int o = threadIdx.x; o < 2 * a.UB; o += kHsThreads) mmk[o] = 0u;
+  }
+  __syncthreads();
+
+  const int xq = c ^ g;
+  const uint64_t vb = (uint64_t)a.items[model];
+  hs_rsrc rsrc;
+  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
+  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * 2) << 16));
+  rsrc.z = __builtin_amdgcn_readfirstlane((int)a.N);
+  rsrc.w = 0x00020000;
+  const int voff = 16 * g;
+  auto rows_of = [&](int64_t jb, int (&vi)[NI]) {
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int64_t j = jb + 16 * t + c;
+      vi[t] = j < i1 ? (int)j : 0x7fffffff;  // out of range: the buffer check reads zeros
+    }
+  };
+  const int n_ch = (ub + CU - 1) / CU;
+  constexpr int64_t kSlice = 16 * NI, kStride = 8 * kSlice;  // items per wave slice / per block round
+  int64_t jb = i0 + kSlice * w;
+  if (HREC_HS_ABLATE < 3 && ub > 0 && jb < i1) {
+    int vnext[NI];
+    rows_of(jb, vnext);
+    HsFrag it_f[KS][NI];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+    HsFrag ua[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int off = S::kSwz ? 16 * xq : 16 * g;
+      ua[u].i = *reinterpret_cast<const int4*>(us + (16 * u + c) * kRowB + off);
+    }
+    float* const out = a.out[model];
+    for (; jb < i1; jb += kStride) {
+      rows_of(jb + kStride, vnext);
+      auto user_frag = [&](int ch, int u, int ks) {
+        HsFrag f;
+        const int off = S::kSwz ? 16 * ((4 * ks) ^ xq) : 64 * ks + 16 * g;
+        f.i = *reinterpret_cast<const int4*>(us + (CU * ch + 16 * u + c) * kRowB + off);
+        return f;
+      };
+      // the last chunk is peeled: its item refills (the next slice) are unconditional
+      auto chunk = [&](int ch, auto last_t) {
+        constexpr bool last = decltype(last_t)::value;
+        const int ch_next = ch + 1 < n_ch ? ch + 1 : 0;
+        hs_f4 acc[NU][NI];
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int t = 0; t < NI; ++t) acc[u][t] = hs_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          HsFrag f[NU];
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            f[u] = ua[u];
+            ua[u] = ks + 1 < KS ? user_frag(ch, u, ks + 1) : user_frag(ch_next, u, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < NU; ++u)
+#pragma unroll
+            for (int t = 0; t < NI; ++t)
+              acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it_f[ks][t].i),
+                                                                  __builtin_bit_cast(hs_bf8, f[u].i), acc[u][t], 0,
+                                                                  0, 0);
+          if constexpr (last) {
+#pragma unroll
+            for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, NI, 0);  // MFMA
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // C/D: lane holds user CU ch + 16 u + c, items jb + 16 t + 4 g + r
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int bl = CU * ch + 16 * u + c;
+          float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+          for (int t = 0; t < NI; ++t) {
+            const int64_t j = jb + 16 * t + 4 * g;
+            if (j + 3 < i1) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                lo = fminf(lo, acc[u][t][r]);
+                hi = fmaxf(hi, acc[u][t][r]);
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (j + r < i1) {
+                  lo = fminf(lo, acc[u][t][r]);
+                  hi = fmaxf(hi, acc[u][t][r]);
+                }
+            }
+            if (HREC_HS_ABLATE == 0 && bl < ub) {
+              float* o = out + (int64_t)(b0 + bl) * a.ldo;
+              if (j + 3 < i1 && (a.ldo & 3) == 0) {
+                if constexpr (HREC_HS_NT) {
+                  __builtin_nontemporal_store(acc[u][t], reinterpret_cast<hs_f4*>(o + j));
+                } else {
+                  *reinterpret_cast<float4*>(o + j) =
+                      make_float4(acc[u][t][0], acc[u][t][1], acc[u][t][2], acc[u][t][3]);
+                }
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (j + r < i1) o[j + r] = acc[u][t][r];
+              }
+            }
+          }
+          lo = fminf(lo, __shfl_xor(lo, 16, kWave));
+          lo = fminf(lo, __shfl_xor(lo, 32, kWave));
+          hi = fmaxf(hi, __shfl_xor(hi, 16, kWave));
+          hi = fmaxf(hi, __shfl_xor(hi, 32, kWave));
+          if (HREC_HS_ABLATE < 2 && g == 0 && bl < ub) {
+            atomicMax(&mmk[2 * bl], ~hs_key(lo));
+            atomicMax(&mmk[2 * bl + 1], hs_key(hi));
+          }
+        }
+      };
+      for (int ch = 0; ch + 1 < n_ch; ++ch) chunk(ch, std::false_type{});
+      chunk(n_ch - 1, std::true_type{});
+    }
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < ub; o += kHsThreads) {
+    const uint32_t kmin = mmk[2 * o], kmax = mmk[2 * o + 1];
+    float* pp = a.part + ((int64_t)(model * a.G + grp) * 2) * a.B + b0 + o;
+    pp[0] = kmin ? hs_unkey(~kmin) : __builtin_inff();
+    pp[a.B] = kmax ? hs_unkey(kmax) : -__builtin_inff();
+  }
+}
+
+// mm[model][0 / 1][b] = min / max over the G item groups' partials: a block
+// of 256 threads takes 64 users of one model, 4 stripes of groups per user
+// (8 loads in flight per thread), then folds the stripes in LDS.
+__global__ __launch_bounds__(256) void hyb_mm_reduce_kernel(const float* __restrict__ part, int B, int G,
+                                                           float* __restrict__ mm0, float* __restrict__ mm1) {
+  __shared__ float slo[4][64], shi[4][64];
+  const int bl = threadIdx.x & 63, st = threadIdx.x >> 6, model = blockIdx.y;
+  const int b = blockIdx.x * 64 + bl;
+  float lo = __builtin_inff(), hi = -__builtin_inff();
+  if (b < B) {
+    const float* p = part + (int64_t)model * G * 2 * B + b;
+    for (int q0 = st; q0 < G; q0 += 4 * 8) {
+      float l[8], h[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = q0 + 4 * e;
+        l[e] = q < G ? p[(int64_t)q * 2 * B] : __builtin_inff();
+        h[e] = q < G ? p[(int64_t)q * 2 * B + B] : -__builtin_inff();
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        lo = fminf(lo, l[e]);
+        hi = fmaxf(hi, h[e]);
+      }
+    }
+  }
+  slo[st][bl] = lo;
+  shi[st][bl] = hi;
+  __syncthreads();
+  if (st == 0 && b < B) {
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      lo = fminf(lo, slo[q][bl]);
+      hi = fmaxf(hi, shi[q][bl]);
+    }
+    float* mm = model ? mm1 : mm0;
+    mm[b] = lo;
+    mm[B + b] = hi;
+  }
+}
+
+static int hs_groups(int64_t n_items) {
+  const int64_t g = (n_items + 255) / 256;
+  return (int)(g < 128 ? (g < 1 ? 1 : g) : 128);
+}
+
+template <int DK>
+static int hs_user_tile(int B) {
+  int ub_max = kHsMaxUserBytes / HsShape<DK>::kRowB;
+  ub_max = ub_max / 64 * 64;
+  if (ub_max > 256) ub_max = 256;
+  const int n_ut = (B + ub_max - 1) / ub_max;
+  int UB = (B + n_ut - 1) / n_ut;
+  return (UB + 63) / 64 * 64;
+}
+
+template <int DK>
+static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
+  a.UB = hs_user_tile<DK>(a.B);
+  a.n_ut = (a.B + a.UB - 1) / a.UB;
+  const size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * 8;
+  const auto kfn = hyb_scores_kernel<DK>;
+  if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return check_launch("hyb_scores_kernel: LDS attribute");
+  hipLaunchKernelGGL(kfn, dim3((unsigned)(2 * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
+  int rc = check_launch("hyb_scores_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((a.B + 63) / 64), 2), dim3(256), 0, s, a.part, a.B, a.G,
+                     mm0, mm1);
+  return check_launch("hyb_mm_reduce_kernel");
+}
+
+}  // namespace hrec
+
+using namespace hrec;
+
+extern "C" size_t hrec_hybrid_scores_workspace_bytes(int n_users, int64_t n_items) {
+  const size_t B = (size_t)(n_users > 0 ? n_users : 0);
+  return (size_t)2 * hs_groups(n_items) * 2 * B * sizeof(float) + 256;
+}
+
+extern "C" int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* als_rows, int als_width,
+                                  const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
+                                  const void* als_items, const void* tt_items, int64_t n_items, int dk,
+                                  float* als_out, float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  HREC_REQUIRE(dk == 64 || dk == 128 || dk == 256, "hybrid_scores: dk must be 64, 128 or 256 (got %d)", dk);
+  HREC_REQUIRE(n_users >= 0 && n_items >= 0, "hybrid_scores: negative size");
+  HREC_REQUIRE(n_items < 0x7fffffffll, "hybrid_scores: n_items must be < 2^31 - 1");
+  HREC_REQUIRE(n_users <= (1 << 20), "hybrid_scores: at most 2^20 users per call");
+  HREC_REQUIRE(als_width >= 0 && als_width <= dk && tt_width >= 0 && tt_width <= dk,
+               "hybrid_scores: user widths must be in [0, dk]");
+  HREC_REQUIRE(als_ld >= als_width && tt_ld >= tt_width, "hybrid_scores: row stride below the width");
+  HREC_REQUIRE(ld_out >= n_items, "hybrid_scores: ld_out < n_items");
+  if (n_users == 0) return HREC_OK;
+  HREC_REQUIRE(als_mm && tt_mm && workspace, "hybrid_scores: null min/max output or workspace");
+  HREC_REQUIRE(n_items == 0 || (als_users && tt_users && als_items && tt_items && als_out && tt_out),
+               "hybrid_scores: null pointer");
+  HREC_REQUIRE(((uintptr_t)als_items & 15) == 0 && ((uintptr_t)tt_items & 15) == 0,
+               "hybrid_scores: item operands must be 16-B aligned");
+  const size_t need = hrec_hybrid_scores_workspace_bytes(n_users, n_items);
+  HREC_REQUIRE(workspace_bytes >= need, "hybrid_scores: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t s = as_stream(stream);
+  if (n_items == 0) {  // no scores: min = +inf, max = -inf (hrec_rows_minmax_f32 of an empty row)
+    hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((n_users + 63) / 64), 2), dim3(256), 0, s,
+                       static_cast<const float*>(workspace), n_users, 0, als_mm, tt_mm);
+    return check_launch("hyb_mm_reduce_kernel");
+  }
+  HybScoresArgs a{};
+  a.users[0] = als_users;
+  a.users[1] = tt_users;
+  a.ld[0] = als_ld;
+  a.ld[1] = tt_ld;
+  a.rows[0] = als_rows;
+  a.rows[1] = nullptr;
+  a.width[0] = als_width;
+  a.width[1] = tt_width;
+  a.B = n_users;
+  a.items[0] = static_cast<const char*>(als_items);
+  a.items[1] = static_cast<const char*>(tt_items);
+  a.N = n_items;
+  a.out[0] = als_out;
+  a.out[1] = tt_out;
+  a.ldo = ld_out;
+  a.part = static_cast<float*>(workspace);
+  a.G = hs_groups(n_items);
+  switch (dk) {
+    case 64: return hs_launch<64>(a, als_mm, tt_mm, s);
+    case 128: return hs_launch<128>(a, als_mm, tt_mm, s);
+    default: return hs_launch<256>(a, als_mm, tt_mm, s);
+  }
+}

@@ -92,6 +92,9 @@ _SIGNATURES.update({
     "hrec_dot_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
     "hrec_dot_topk": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp,
                                _c_sz, _vp]),
+    "hrec_hybrid_scores_workspace_bytes": (_c_sz, [_c_i32, _c_i64]),
+    "hrec_hybrid_scores": (_c_i32, [_vp, _c_i64, _vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32,
+                                    _vp, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_minmax_workspace_bytes": (_c_sz, [_c_i32]),
     "hrec_hybrid_minmax": (_c_i32, [_vp, _vp, _c_i32, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
@@ -534,6 +537,38 @@ def hybrid_minmax(als_user, tt_user, als_item, tt_item):
         dk, _dev(a_mm, torch.float32, "als_mm"), _dev(t_mm, torch.float32, "tt_mm"), _dev(ws, torch.uint8, "ws"),
         need, _stream()))
     return a_mm, t_mm
+
+
+def hybrid_scores(als_users, als_rows, tt_users, als_item, tt_item):
+    """Both bf16 score matrices of a hybrid batch and their per-row min/max
+    in one launch (hrec_hybrid_scores): als_users [n, ka] f32 ALS factors
+    (rows als_rows [B] int64 are used), tt_users [B, kt] f32 two-tower user
+    vectors, als_item / tt_item bf16 [N, dk] item operands (dot_operand).
+    Returns (als [B, N] f32, tt [B, N] f32, als_mm [2, B], tt_mm [2, B]) —
+    dot_scores of the bf16 user operands and rows_minmax of each."""
+    dk = _hyb_args(als_item, tt_item)
+    B, N = int(als_rows.shape[0]), int(als_item.shape[0])
+    if tt_item.shape[0] != N or tt_users.shape[0] != B:
+        raise HrecError("hybrid_scores: item counts / batch sizes differ")
+    for t, name in ((als_users, "als_users"), (tt_users, "tt_users")):
+        if t.dtype != torch.float32 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+            raise HrecError(f"hybrid_scores: {name} must be a row-major float32 device matrix")
+        if t.shape[1] > dk:
+            raise HrecError(f"hybrid_scores: {name} width {t.shape[1]} > operand width {dk}")
+    rows = als_rows.to(torch.int64).contiguous()
+    dev = als_item.device
+    als = torch.empty((B, N), dtype=torch.float32, device=dev)
+    tt = torch.empty((B, N), dtype=torch.float32, device=dev)
+    a_mm = torch.empty((2, B), dtype=torch.float32, device=dev)
+    t_mm = torch.empty((2, B), dtype=torch.float32, device=dev)
+    need = int(lib().hrec_hybrid_scores_workspace_bytes(B, N))
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _check("hrec_hybrid_scores", lib().hrec_hybrid_scores(
+        _vp(als_users.data_ptr()), als_users.stride(0), _vp(rows.data_ptr()), als_users.shape[1],
+        _vp(tt_users.data_ptr()), tt_users.stride(0), tt_users.shape[1], B, _vp(als_item.data_ptr()),
+        _vp(tt_item.data_ptr()), N, dk, _vp(als.data_ptr()), _vp(tt.data_ptr()), N, _vp(a_mm.data_ptr()),
+        _vp(t_mm.data_ptr()), _vp(ws.data_ptr()), need, _stream()))
+    return als, tt, a_mm, t_mm
 
 
 def _hyb_args(*ops):

@@ -55,6 +55,7 @@ class DeviceOps:
     hybrid_topk = staticmethod(_hrec.hybrid_topk)
 
     dot_scores = staticmethod(_hrec.dot_scores)
+    hybrid_scores = staticmethod(_hrec.hybrid_scores)
     rows_minmax = staticmethod(_hrec.rows_minmax)
     fuse_rows_topk = staticmethod(_hrec.fuse_rows_topk)
     topk_keyed = staticmethod(_hrec.topk_keyed)
@@ -146,7 +147,11 @@ class ShardedRecommender:
         o = self.ops
         B = int(user_rows.shape[0])
         dev = user_vecs.device
-        if self.n_local > 0:
+        if self.n_local > 0 and self.precision == "bf16" and hasattr(o, "hybrid_scores"):
+            # one launch: user gather + bf16 conversion, both score GEMMs and
+            # both rows' min / max (hrec_hybrid_scores; same values as below)
+            als, tt, a_mm, t_mm = o.hybrid_scores(self.U, user_rows, user_vecs, self.V_op, self.iv_op)
+        elif self.n_local > 0:
             als, tt = self._scores(user_rows, user_vecs)
             a_mm = o.rows_minmax(als)
             t_mm = o.rows_minmax(tt)

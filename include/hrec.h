@@ -383,6 +383,25 @@ int hrec_hybrid_topk(const void* als_user, const void* tt_user, int n_users, con
                      int als_wins, int top_k, const double* thr_in, int64_t idx_offset, int64_t* out_idx,
                      double* out_val, int* overflow, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------
+ * Both score matrices of the bf16 hybrid in one launch (csrc/hybrid_scores.hip,
+ * BASELINE config c5): the scores get_hybrid_recommendations ranks per user
+ * (ALS transform + Keras Dot over every candidate, src/hybrid_system.py:95-116)
+ * and the per-model MinMaxScaler extremes it fits (src/hybrid_system.py:57-75).
+ * User rows are f32 (ALS: als_users[als_rows[b] * als_ld + c], als_rows may
+ * be NULL for row b; two-tower: tt_users[b * tt_ld + c]), converted to bf16
+ * (round to nearest even) for columns c < width and zero up to dk; item
+ * operands are bf16 [n_items, dk], dk in {64, 128, 256}. Writes
+ * als_out / tt_out [n_users, ld_out] f32 (bit-identical to hrec_dot_scores on
+ * hrec_f32_to_bf16 operands) and als_mm / tt_mm [2, n_users] f32 =
+ * hrec_rows_minmax_f32 of those rows. */
+size_t hrec_hybrid_scores_workspace_bytes(int n_users, int64_t n_items);
+int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* als_rows, int als_width,
+                       const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
+                       const void* als_items, const void* tt_items, int64_t n_items, int dk,
+                       float* als_out, float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -221,6 +221,39 @@ def test_hybrid_fused_equals_unfused(device, n_users, n_items, k, d, B, wins):
     np.testing.assert_array_equal(fv.cpu().numpy(), uv_.cpu().numpy())
 
 
+@pytest.mark.parametrize("dk,B,N,ka,kt", [(256, 256, 100_003, 256, 256), (256, 300, 1000, 200, 250),
+                                          (128, 70, 4097, 100, 50), (64, 1, 17, 64, 33), (64, 513, 2000, 48, 64),
+                                          (256, 5, 1, 256, 7)])
+def test_hybrid_scores_equals_dot_scores_and_minmax(device, dk, B, N, ka, kt):
+    """hrec_hybrid_scores (user gather + bf16 conversion + both score GEMMs
+    + per-row min/max in one launch) == hrec_f32_to_bf16 operands through
+    hrec_dot_scores and hrec_rows_minmax_f32, bit for bit: odd widths and
+    row strides, several user tiles (B > 256 at dk 256), tiny and ragged
+    item counts, repeated user rows."""
+    h = _h()
+    rng = np.random.default_rng(B * 7 + N)
+    n_users = max(B, 9)
+    U = torch.as_tensor(rng.normal(size=(n_users, ka)).astype(np.float32), device=device)
+    uv = torch.as_tensor(rng.normal(size=(B, kt)).astype(np.float32) / 4, device=device)
+    va = h.dot_operand(torch.as_tensor(rng.normal(size=(N, ka)).astype(np.float32), device=device), torch.bfloat16, dk)
+    vt = h.dot_operand(torch.as_tensor(rng.normal(size=(N, kt)).astype(np.float32), device=device), torch.bfloat16, dk)
+    rows = torch.as_tensor(rng.integers(0, n_users, B), dtype=torch.int64, device=device)
+    als, tt, a_mm, t_mm = h.hybrid_scores(U, rows, uv, va, vt)
+    ua = h.dot_operand(U.index_select(0, rows), torch.bfloat16, dk)
+    ut = h.dot_operand(uv, torch.bfloat16, dk)
+    ref_a, ref_t = h.dot_scores(ua, va), h.dot_scores(ut, vt)
+    assert torch.equal(als, ref_a) and torch.equal(tt, ref_t)
+    assert torch.equal(a_mm, h.rows_minmax(ref_a)) and torch.equal(t_mm, h.rows_minmax(ref_t))
+
+
+def test_hybrid_scores_empty_catalogue(device):
+    h = _h()
+    U = torch.ones((4, 64), device=device)
+    v = torch.empty((0, 64), dtype=torch.bfloat16, device=device)
+    als, tt, a_mm, t_mm = h.hybrid_scores(U, torch.arange(4, device=device), U, v, v)
+    assert als.shape == (4, 0) and torch.all(a_mm[0] == float("inf")) and torch.all(t_mm[1] == -float("inf"))
+
+
 def test_hybrid_fused_minmax_and_overflow(device):
     """hrec_hybrid_minmax == hrec_rows_minmax of the two score matrices; a
     catalogue of identical items (every fused score ties) overflows the
