@@ -44,13 +44,22 @@
 #define HREC_ALS_RLPANEL 0  // 1 = pivot-row entries by v_readlane, 2 = only the next pivot's (both measured slower)
 #endif
 #ifndef HREC_ALS_DIAG4
-#define HREC_ALS_DIAG4 0  // 1/2: diagonal Gramian tiles as 3 x v_mfma_f64_4x4x4_4b (measured slower)
+// diagonal Gramian tiles as 3 x v_mfma_f64_4x4x4_4b (3/4 of the 16x16x4 work):
+// 3 = rotated operands gathered from memory (default); 1 / 2 = rotated by DPP /
+// ds_bpermute (measured slower); 0 = whole 16x16x4 diagonal tiles
+#define HREC_ALS_DIAG4 3
 #endif
 #ifndef HREC_ALS_PIPE
 #define HREC_ALS_PIPE 1  // 1 = ring-prefetch gather with structured buffer loads; 0 = chunked flat loads
 #endif
 #ifndef HREC_ALS_PF
 #define HREC_ALS_PF 8  // PIPE: gather prefetch distance in steps of 4 ratings
+#endif
+#ifndef HREC_ALS_PF64
+#define HREC_ALS_PF64 4  // prefetch distance of f64-source gathers (steps)
+#endif
+#ifndef HREC_ALS_PR
+#define HREC_ALS_PR 2  // DIAG4 = 3: prefetch distance of the rotated loads (steps)
 #endif
 
 namespace hrec {
@@ -95,6 +104,22 @@ __device__ f2 sbuf_load_f2(i4v rsrc, int vindex, int voffset, int soffset, int a
     "llvm.amdgcn.struct.buffer.load.v2f32");
 __device__ float sbuf_load_f1(i4v rsrc, int vindex, int voffset, int soffset, int aux) __asm(
     "llvm.amdgcn.struct.buffer.load.f32");
+
+// Four f64 source-factor columns (32 B) of one gathered row: two 16-B
+// structured loads (S64 gathers: source factors kept in f64, no conversion).
+struct VecD {
+  double x[4];
+};
+__device__ __forceinline__ VecD struct_load_d(i4v rsrc, int vindex, int voffset) {
+  const f4 lo = sbuf_load_f4(rsrc, vindex, voffset, 0, 0);
+  const f4 hi = sbuf_load_f4(rsrc, vindex, voffset + 16, 0, 0);
+  VecD v;
+  v.x[0] = __hiloint2double(__float_as_int(lo.y), __float_as_int(lo.x));
+  v.x[1] = __hiloint2double(__float_as_int(lo.w), __float_as_int(lo.z));
+  v.x[2] = __hiloint2double(__float_as_int(hi.y), __float_as_int(hi.x));
+  v.x[3] = __hiloint2double(__float_as_int(hi.w), __float_as_int(hi.z));
+  return v;
+}
 
 template <int NT>
 __device__ __forceinline__ Vec<NT> struct_load(i4v rsrc, int vindex, int voffset) {
@@ -202,7 +227,7 @@ struct NoHook {
 // `before_lds` runs once the row's Gramian is in registers, before the first
 // LDS write (b, MODE 1 re-layout): the producer of the trio kernel waits there
 // for its hand-off slot.
-template <int NT, int CH, int MODE, typename Hook = NoHook>
+template <int NT, int CH, int MODE, typename Hook = NoHook, bool S64 = false>
 __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, const int32_t* __restrict__ indices,
                                          const float* __restrict__ values, const float* __restrict__ src,
                                          int64_t n_src, int k, double reg, d4 (&acc)[NT * (NT + 1) / 2],
@@ -263,14 +288,16 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   // voffset = this lane's 16-B column slice). Padding entries carry index -1:
   // the buffer range check returns zeros for them, so the loop has no
   // branches, masks or address arithmetic on the VALU.
-  constexpr int PF = HREC_ALS_PF;
+  constexpr int PF = S64 ? HREC_ALS_PF64 : HREC_ALS_PF;  // f64 sources sit in the MALL: shorter distance
   static_assert(16 % PF == 0, "prefetch distance must divide the window");
-  const int voff = NT * 4 * col;
+  static_assert(!S64 || (NT == 4 && MODE == 0 && (HREC_ALS_DIAG4 == 0 || HREC_ALS_DIAG4 == 3)),
+                "f64 sources: kp 64, f64 accumulation only");
+  const int voff = (S64 ? 8 : 4) * NT * col;
   const int bp_addr = 4 * sub;  // ds_bpermute byte address of nnz (4s + sub) is 16 s + 4 sub
   const uint64_t sbase = (uint64_t)src;
   i4v rsrc;
   rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
-  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(sbase >> 32) | ((KP * 4) << 16));
+  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(sbase >> 32) | ((KP * (S64 ? 8 : 4)) << 16));
   rsrc.z = __builtin_amdgcn_readfirstlane((int)n_src);
   rsrc.w = 0x00020000;
   auto load_win = [&](int64_t w, int& ii, float& vv) {
@@ -287,9 +314,14 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   float rw0, rw1;
   load_win(0, iw0, rw0);
   load_win(1, iw1, rw1);
-  Vec<NT> ring[PF];
+  using RingT = std::conditional_t<S64, VecD, Vec<NT>>;
+  auto ring_load = [&](int vi) -> RingT {
+    if constexpr (S64) return struct_load_d(rsrc, vi, voff);
+    else return struct_load<NT>(rsrc, vi, voff);
+  };
+  RingT ring[PF];
 #pragma unroll
-  for (int s = 0; s < PF; ++s) ring[s] = struct_load<NT>(rsrc, bperm(iw0, s), voff);
+  for (int s = 0; s < PF; ++s) ring[s] = ring_load(bperm(iw0, s));
   int nidx = bperm(iw0, PF);  // source row of the next gather (one step ahead)
   // DIAG4: a diagonal tile's 16 x 16 block is 16 sub-blocks of 4 x 4, of
   // which 10 are distinct (symmetry). v_mfma_f64_4x4x4_4b runs 4 independent
@@ -301,8 +333,28 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   // DIAG4 = 1 rotates with DPP moves at the step itself; DIAG4 = 2 converts
   // the next step's operands one step ahead and rotates them by ds_bpermute
   // (LDS path), so the rotations have a whole step to land.
+  // DIAG4 = 3 gathers the rotated operands from memory instead: two more
+  // 16-B structured loads per step (the same source rows, the column slices
+  // of lane col + 4 and col + 8), PR steps ahead — no cross-lane moves.
   constexpr bool kDiag4 = HREC_ALS_DIAG4 && MODE == 0;
   constexpr bool kAhead = HREC_ALS_DIAG4 == 2 && MODE == 0;
+  constexpr bool kMemRot = HREC_ALS_DIAG4 == 3 && MODE == 0;
+  constexpr int PR = kMemRot ? HREC_ALS_PR : 1;  // rotated-load prefetch distance (steps)
+  static_assert(PR < PF, "rotated loads are issued from the current windows");
+  const int voff1 = (S64 ? 8 : 4) * NT * ((col + 4) & 15), voff2 = (S64 ? 8 : 4) * NT * ((col + 8) & 15);
+  auto rot_load = [&](int vi, int vo) -> RingT {
+    if constexpr (S64) return struct_load_d(rsrc, vi, vo);
+    else return struct_load<NT>(rsrc, vi, vo);
+  };
+  RingT rot1[PR], rot2[PR];
+  if constexpr (kMemRot) {
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+      const int vi = bperm(iw0, q);
+      rot1[q] = rot_load(vi, voff1);
+      rot2[q] = rot_load(vi, voff2);
+    }
+  }
   double dg[NT][3];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dg[t][0] = dg[t][1] = dg[t][2] = 0.0;
@@ -334,7 +386,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         stop = true;
         break;
       }
-      const Vec<NT> cur = ring[s % PF];
+      const RingT cur = ring[s % PF];
       double a[NT], ar1[NT], ar2[NT];
       if constexpr (kAhead) {
 #pragma unroll
@@ -345,9 +397,27 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         }
       } else {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) a[t] = gram_cvt(cur.x[t]);
+        for (int t = 0; t < NT; ++t) {
+          if constexpr (S64) a[t] = cur.x[t];
+          else a[t] = gram_cvt(cur.x[t]);
+        }
       }
-      ring[s % PF] = struct_load<NT>(rsrc, nidx, voff);
+      ring[s % PF] = ring_load(nidx);
+      if constexpr (kMemRot) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          if constexpr (S64) {
+            ar1[t] = rot1[s % PR].x[t];
+            ar2[t] = rot2[s % PR].x[t];
+          } else {
+            ar1[t] = gram_cvt(rot1[s % PR].x[t]);
+            ar2[t] = gram_cvt(rot2[s % PR].x[t]);
+          }
+        }
+        const int vr = (s + PR < 16) ? bperm(iw0, s + PR) : bperm(iw1, s + PR - 16);
+        rot1[s % PR] = rot_load(vr, voff1);
+        rot2[s % PR] = rot_load(vr, voff2);
+      }
       if constexpr (kAhead) {
         const Vec<NT> nx = ring[(s + 1) % PF];
 #pragma unroll
@@ -372,10 +442,10 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
           if (MODE == 0) {
             if (kDiag4 && I == J) {
               dg[I][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], a[I], dg[I][0], 0, 0, 0);
-              dg[I][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], kAhead ? ar1[I] : row_ror<12>(a[I]), dg[I][1], 0,
-                                                            0, 0);
-              dg[I][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], kAhead ? ar2[I] : row_ror<8>(a[I]), dg[I][2], 0,
-                                                            0, 0);
+              dg[I][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], (kAhead || kMemRot) ? ar1[I] : row_ror<12>(a[I]),
+                                                            dg[I][1], 0, 0, 0);
+              dg[I][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], (kAhead || kMemRot) ? ar2[I] : row_ror<8>(a[I]),
+                                                            dg[I][2], 0, 0, 0);
             } else {
               acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
             }
@@ -823,7 +893,7 @@ __device__ __forceinline__ void factor_row_lds(int lane, double* __restrict__ Up
 }
 
 // One destination row on one wave (lane = 0..63), all scratch in `lds`.
-template <int NT, int CH, int MODE>
+template <int NT, int CH, int MODE, bool S64 = false>
 __device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __restrict__ indptr,
                                         const int32_t* __restrict__ indices, const float* __restrict__ values,
                                         const float* __restrict__ src, int64_t n_src, int k, double reg,
@@ -839,18 +909,24 @@ __device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __
   d4 acc[NT * (NT + 1) / 2];
   double* scratch = lds + RowLds<KP>::kUpPad;
   double* bsh = scratch + 128 + 2 * KP;
-  gram_row<NT, CH, MODE>(beg, end, lane, indices, values, src, n_src, k, reg, acc, bsh, lds);
+  gram_row<NT, CH, MODE, NoHook, S64>(beg, end, lane, indices, values, src, n_src, k, reg, acc, bsh, lds);
   factor_row<NT>(lane, acc, lds, scratch, bsh, out);
 }
 
-// One wave per destination row.
-template <int NT, int CH, int MODE>
+// One wave per destination row. S64: src points at f64 source factors.
+template <int NT, int CH, int MODE, bool S64 = false>
 __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
     int k, double reg, float* __restrict__ dst) {
   __shared__ __attribute__((aligned(16))) double lds[RowLds<16 * NT>::kSize];
-  als_row<NT, CH, MODE>(blockIdx.x, threadIdx.x, indptr, indices, values, src, n_src, k, reg, dst, lds);
+  als_row<NT, CH, MODE, S64>(blockIdx.x, threadIdx.x, indptr, indices, values, src, n_src, k, reg, dst, lds);
+}
+
+__global__ __launch_bounds__(256) void f32_to_f64_kernel(const float* __restrict__ in, int64_t n,
+                                                         double* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = (double)in[i];
 }
 
 // Producer/consumer variant: one block of 8 waves per CU. Wave p (0..3)
@@ -985,7 +1061,7 @@ __global__ __launch_bounds__(768) void als_half_sweep_trio_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
     int k, double reg, float* __restrict__ dst, unsigned long long* __restrict__ counter) {
-  static_assert(HREC_ALS_DIAG4 == 0, "the trio producer hands off before any DIAG4 LDS staging");
+  static_assert(HREC_ALS_DIAG4 == 0, "the trio producer hands off before any DIAG4 LDS staging: build it with -DHREC_ALS_DIAG4=0");
   constexpr int KP = 16 * NT;
   constexpr int NPAIR = NT * (NT + 1) / 2;
   using L = TrioLds<KP>;
@@ -1207,6 +1283,34 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
   }
 #undef HREC_SWEEP
   return check_launch("als_half_sweep_f64_kernel");
+}
+
+extern "C" int hrec_f32_to_f64(const float* in, int64_t n, double* out, void* stream) {
+  HREC_REQUIRE(n >= 0, "f32_to_f64: negative size");
+  if (n == 0) return HREC_OK;
+  HREC_REQUIRE(in && out, "f32_to_f64: null pointer");
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(f32_to_f64_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), in, n, out);
+  return check_launch("f32_to_f64_kernel");
+}
+
+extern "C" int hrec_als_half_sweep_src64(const int64_t* indptr, const int32_t* indices, const float* values,
+                                         int64_t n_rows, const double* src64, int64_t n_src, int k, int kp,
+                                         double reg_param, float* dst_factors, void* stream) {
+  HREC_REQUIRE(kp == 64, "als_half_sweep_src64: kp must be 64 (got %d)", kp);
+  HREC_REQUIRE(k >= 1 && k <= kp, "als_half_sweep_src64: need 1 <= k <= kp (k=%d kp=%d)", k, kp);
+  HREC_REQUIRE(n_rows >= 0 && n_src >= 0, "als_half_sweep_src64: negative size");
+  HREC_REQUIRE(n_rows < 0x7fffffffll && n_src < 0x7fffffffll, "als_half_sweep_src64: too many rows for one launch");
+  HREC_REQUIRE(reg_param >= 0.0, "als_half_sweep_src64: reg_param must be >= 0");
+  if (n_rows == 0) return HREC_OK;
+  HREC_REQUIRE(indptr && dst_factors, "als_half_sweep_src64: null pointer");
+  HREC_REQUIRE(n_src > 0 && src64 && indices && values, "als_half_sweep_src64: null source factors / CSR arrays");
+  HREC_REQUIRE(((uintptr_t)src64 & 15) == 0, "als_half_sweep_src64: src64 must be 16-B aligned");
+  hipLaunchKernelGGL((als_half_sweep_f64_kernel<4, HREC_ALS_CH0, 0, true>), dim3((unsigned)n_rows), dim3(64), 0,
+                     as_stream(stream), indptr, indices, values, n_rows, reinterpret_cast<const float*>(src64), n_src,
+                     k, reg_param, dst_factors);
+  return check_launch("als_half_sweep_f64_kernel (f64 sources)");
 }
 
 extern "C" int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, float* out, int64_t ld_out,

@@ -694,19 +694,15 @@ __device__ __forceinline__ KI wave_best_ki(KI x) {
   return x;
 }
 
+// One segment (seg of row r, R rows) on one wave; ck / ce: the wave's 128
+// LDS slots ([64, 128): scratch of non-candidates).
 template <int KK>
-__global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
-    const float* __restrict__ als, const float* __restrict__ tt, int64_t n, int64_t ld, int64_t segs,
-    const float* __restrict__ als_mm, const float* __restrict__ tt_mm, double w0, double w1,
-    double* __restrict__ cand_v, int64_t* __restrict__ cand_i, const int* __restrict__ gate) {
+__device__ __forceinline__ void fuse_segment_one(
+    int64_t seg, int64_t r, int64_t R, const float* __restrict__ als, const float* __restrict__ tt, int64_t n,
+    int64_t ld, int64_t segs, const float* __restrict__ als_mm, const float* __restrict__ tt_mm, double w0, double w1,
+    double* __restrict__ cand_v, int64_t* __restrict__ cand_i, uint64_t* __restrict__ ck, int* __restrict__ ce) {
 #pragma clang fp contract(off)
-  __shared__ uint64_t ck_sh[4][128];  // [64, 128): scratch slots of non-candidates
-  __shared__ int ce_sh[4][128];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t seg = (int64_t)blockIdx.x * 4 + wv;
-  if (seg >= segs || (gate && *gate == 0)) return;
-  const int64_t r = blockIdx.y;
-  const int64_t R = gridDim.y;
+  const int lane = threadIdx.x & 63;
   const double amin = (double)als_mm[r], amax = (double)als_mm[R + r];
   double arange = amax - amin;
   if (arange < 10.0 * DBL_EPSILON) arange = 1.0;
@@ -761,16 +757,16 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
     // among the 64 maxima (one pass of broadcast LDS reads, no dependent
     // cross-lane rounds); in-segment positions order equal keys
     const int mpos = nmine > 0 ? be * 64 + lane : -1;
-    ck_sh[wv][64 + lane] = bk;
-    ce_sh[wv][64 + lane] = mpos;
+    ck[64 + lane] = bk;
+    ce[64 + lane] = mpos;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     int rank = 0;
 #pragma unroll 8
     for (int q = 0; q < 64; ++q) {
-      const uint64_t ok = ck_sh[wv][64 + q];
-      const int op = ce_sh[wv][64 + q];
+      const uint64_t ok = ck[64 + q];
+      const int op = ce[64 + q];
       rank += (op >= 0 && (mpos < 0 || ok > bk || (ok == bk && op < mpos))) ? 1 : 0;
     }
     const int nvl = __popcll(__ballot(mpos >= 0));
@@ -809,8 +805,8 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
     }
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     const int slot = c ? nc + below : 64 + lane;  // branch-free append
-    ck_sh[wv][slot] = key[e];
-    ce_sh[wv][slot] = e * 64 + lane;
+    ck[slot] = key[e];
+    ce[slot] = e * 64 + lane;
     nc += cnt;
   }
   const int64_t obase = r * segs * KK + seg * KK;
@@ -820,12 +816,12 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if constexpr (kFuseRank) {
       // each candidate's rank among the nc candidates = its output slot
-      const uint64_t mk = lane < nc ? ck_sh[wv][lane] : 0;
-      const int mp = lane < nc ? ce_sh[wv][lane] : 0;
+      const uint64_t mk = lane < nc ? ck[lane] : 0;
+      const int mp = lane < nc ? ce[lane] : 0;
       int rank = 0;
       for (int q = 0; q < nc; ++q) {
-        const uint64_t ok = ck_sh[wv][q];
-        const int op = ce_sh[wv][q];
+        const uint64_t ok = ck[q];
+        const int op = ce[q];
         rank += (ok > mk || (ok == mk && op < mp)) ? 1 : 0;
       }
       if (lane < nc && rank < KK) {
@@ -839,7 +835,7 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
       return;
     }
     KI c{0, INT64_MAX};
-    if (lane < nc) c = KI{ck_sh[wv][lane], seg0 + ce_sh[wv][lane]};
+    if (lane < nc) c = KI{ck[lane], seg0 + ce[lane]};
     for (int q = 0; q < KK; ++q) {
       const KI w = wave_best_ki(c);
       if (lane == 0) {
@@ -875,6 +871,27 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
   }
 }
 
+template <int KK>
+__global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
+    const float* __restrict__ als, const float* __restrict__ tt, int64_t n, int64_t ld, int64_t segs,
+    const float* __restrict__ als_mm, const float* __restrict__ tt_mm, double w0, double w1,
+    double* __restrict__ cand_v, int64_t* __restrict__ cand_i, const int* __restrict__ gate, int* __restrict__ clear) {
+  // clear (the sample launch): reset the filter's overflow flag for this call
+  if (clear && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *clear = 0;
+  if (gate && *gate == 0) return;
+  __shared__ uint64_t ck_sh[4][128];
+  __shared__ int ce_sh[4][128];
+  const int wv = threadIdx.x >> 6;
+  // block-stride over the row's segment groups (a gated launch uses one block
+  // per row, so skipping it costs a small grid)
+  for (int64_t sb = blockIdx.x; sb * 4 < segs; sb += gridDim.x) {
+    const int64_t seg = sb * 4 + wv;
+    if (seg < segs)
+      fuse_segment_one<KK>(seg, blockIdx.y, gridDim.y, als, tt, n, ld, segs, als_mm, tt_mm, w0, w1, cand_v, cand_i,
+                           ck_sh[wv], ce_sh[wv]);
+  }
+}
+
 // Threshold filter for the batched fusion top-k (kk <= kFuseK): the same
 // fused f64 keys as fuse_segment_topk_kernel, one wave per segment, but each
 // row first takes a threshold key tk = the best of its sample segments'
@@ -887,7 +904,7 @@ __global__ __launch_bounds__(256) void fuse_segment_topk_kernel(
 // like fuse_segment_topk_kernel, and the same merge follows. A segment with
 // more than kFuseSlots candidates (heavy ties, or a row whose best items
 // cluster) raises *overflow, which gates the exact segment path on the
-// device (clear_flag_kernel resets it first).
+// device (the sample launch of fuse_segment_topk_kernel resets it first).
 constexpr int kFuseSlots = 64;
 __global__ __launch_bounds__(256) void fuse_filter_kernel(
     const float* __restrict__ als, const float* __restrict__ tt, int64_t n, int64_t ld, int64_t segs,
@@ -979,8 +996,6 @@ __global__ __launch_bounds__(256) void fuse_filter_kernel(
     cand_i[obase + lane] = -1;
   }
 }
-
-__global__ void clear_flag_kernel(int* __restrict__ flag) { *flag = 0; }
 
 __global__ void add_offset_kernel(int64_t* __restrict__ idx, int64_t n, int64_t off) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1357,23 +1372,20 @@ extern "C" int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_
     double* gv = (double*)take((size_t)n_rows * segs * kk * 8);
     int64_t* gi = (int64_t*)take((size_t)n_rows * segs * kk * 8);
     char* gws = p;
-    hipLaunchKernelGGL(clear_flag_kernel, dim3(1), dim3(1), 0, s, over);
-    rc = check_launch("clear_flag_kernel");
-    if (rc) return rc;
-#define HREC_FUSE_K(K, GRID, SEGS, V, I, GATE)                                                                  \
+#define HREC_FUSE_K(K, GRID, SEGS, V, I, GATE, CLEAR)                                                           \
   case K:                                                                                                       \
     hipLaunchKernelGGL(fuse_segment_topk_kernel<K>, GRID, dim3(256), 0, s, als, tt, n, ld, SEGS, als_minmax,   \
-                       tt_minmax, w0, w1, V, I, GATE);                                                          \
+                       tt_minmax, w0, w1, V, I, GATE, CLEAR);                                                   \
     break;
-#define HREC_FUSE_SWITCH(GRID, SEGS, V, I, GATE)                                                                 \
+#define HREC_FUSE_SWITCH(GRID, SEGS, V, I, GATE, CLEAR)                                                          \
   switch (kk) {                                                                                                 \
-    HREC_FUSE_K(1, GRID, SEGS, V, I, GATE) HREC_FUSE_K(2, GRID, SEGS, V, I, GATE)                              \
-    HREC_FUSE_K(3, GRID, SEGS, V, I, GATE) HREC_FUSE_K(4, GRID, SEGS, V, I, GATE)                              \
-    HREC_FUSE_K(5, GRID, SEGS, V, I, GATE) HREC_FUSE_K(6, GRID, SEGS, V, I, GATE)                              \
-    HREC_FUSE_K(7, GRID, SEGS, V, I, GATE) default : HREC_FUSE_K(8, GRID, SEGS, V, I, GATE)                    \
+    HREC_FUSE_K(1, GRID, SEGS, V, I, GATE, CLEAR) HREC_FUSE_K(2, GRID, SEGS, V, I, GATE, CLEAR)                \
+    HREC_FUSE_K(3, GRID, SEGS, V, I, GATE, CLEAR) HREC_FUSE_K(4, GRID, SEGS, V, I, GATE, CLEAR)                \
+    HREC_FUSE_K(5, GRID, SEGS, V, I, GATE, CLEAR) HREC_FUSE_K(6, GRID, SEGS, V, I, GATE, CLEAR)                \
+    HREC_FUSE_K(7, GRID, SEGS, V, I, GATE, CLEAR) default : HREC_FUSE_K(8, GRID, SEGS, V, I, GATE, CLEAR)      \
   }
     const dim3 gs((unsigned)((G + 3) / 4), (unsigned)n_rows);
-    HREC_FUSE_SWITCH(gs, G, sv, si, nullptr)
+    HREC_FUSE_SWITCH(gs, G, sv, si, nullptr, over)  // also clears the overflow flag
     rc = check_launch("fuse_segment_topk_kernel (sample)");
     if (rc) return rc;
     const dim3 gf((unsigned)((segs + 3) / 4), (unsigned)n_rows);
@@ -1383,8 +1395,9 @@ extern "C" int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_
     if (rc) return rc;
     rc = topk_rows<double>(cv, n_rows, segs * kk, segs * kk, kk, out_idx, out_val, tws, (size_t)1 << 62, s, ci);
     if (rc) return rc;
-    // exact path, run only if some row overflowed its list
-    HREC_FUSE_SWITCH(gf, segs, gv, gi, over)
+    // exact path, run only if some row overflowed its list (one block per
+    // row: a skipped launch costs a small grid)
+    HREC_FUSE_SWITCH(dim3(1, (unsigned)n_rows), segs, gv, gi, over, nullptr)
 #undef HREC_FUSE_SWITCH
 #undef HREC_FUSE_K
     rc = check_launch("fuse_segment_topk_kernel (gated)");

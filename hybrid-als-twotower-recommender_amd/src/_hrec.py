@@ -37,6 +37,8 @@ _SIGNATURES = {
     "hrec_coo_to_csr": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_remap_i32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp]),
     "hrec_als_init_factors": (_c_i32, [_c_u64, _c_i64, _c_i64, _c_i32, _c_i32, _vp, _vp]),
+    "hrec_als_half_sweep_src64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl, _vp, _vp]),
+    "hrec_f32_to_f64": (_c_i32, [_vp, _c_i64, _vp, _vp]),
     "hrec_als_half_sweep": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl,
                                      _c_i32, _vp, _vp]),
     "hrec_transpose_f32": (_c_i32, [_vp, _c_i64, _c_i64, _vp, _c_i64, _vp]),
@@ -256,17 +258,40 @@ def als_init_factors(seed, row_begin, n_rows, k, kp, out):
         seed, row_begin, n_rows, k, kp, _dev(out, torch.float32, "out"), _stream()))
 
 
-def als_half_sweep(indptr, indices, values, src_factors, k, reg_param, dst_factors, accum_mode=0):
+def als_half_sweep(indptr, indices, values, src_factors, k, reg_param, dst_factors, accum_mode=0, src64=None):
+    """K1. src64 (optional): the source factors already converted to f64
+    (f32_to_f64 of src_factors) — same results, no conversion per gathered
+    row (hrec_als_half_sweep_src64; kp 64, accum_mode 0)."""
     n_rows = indptr.numel() - 1
     kp = dst_factors.shape[1]
     if src_factors.shape[1] != kp or dst_factors.shape[0] < n_rows:
         raise HrecError("als_half_sweep: factor shapes do not match")
+    if src64 is not None:
+        if accum_mode != 0 or src64.shape != src_factors.shape:
+            raise HrecError("als_half_sweep: src64 needs accum_mode 0 and the source factors' shape")
+        _check("hrec_als_half_sweep_src64", lib().hrec_als_half_sweep_src64(
+            _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
+            _dev(values, torch.float32, "values"), n_rows, _dev(src64, torch.float64, "src64"),
+            src64.shape[0], k, kp, float(reg_param), _dev(dst_factors, torch.float32, "dst_factors"), _stream()))
+        return
     _check("hrec_als_half_sweep", lib().hrec_als_half_sweep(
         _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
         _dev(values, torch.float32, "values"), n_rows,
         _dev(src_factors, torch.float32, "src_factors"), src_factors.shape[0], k, kp,
         float(reg_param), int(accum_mode), _dev(dst_factors, torch.float32, "dst_factors"),
         _stream()))
+
+
+def f32_to_f64(x, out=None):
+    """Exact f32 -> f64 copy on the device (hrec_f32_to_f64)."""
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float64, device=x.device)
+    if out.numel() != x.numel():
+        raise HrecError("f32_to_f64: size mismatch")
+    _check("hrec_f32_to_f64", lib().hrec_f32_to_f64(_dev(x, torch.float32, "in"), x.numel(),
+                                                    _dev(out, torch.float64, "out"), _stream()))
+    return out
 
 
 def transpose(x, pad=4):

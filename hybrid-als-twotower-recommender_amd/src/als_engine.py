@@ -19,12 +19,19 @@ matrix); the item side's few long rows would lose more to per-launch tails
 than its small all-gather costs, so the two sides take separate counts.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
 
 from . import _hrec
 from .synthetic import DeviceCSR
+
+
+# f64 sources up to this size (the MI355X's 256 MB MALL holds them; larger
+# ones are gathered in f32): the c2 user side (51 MB) qualifies, its item
+# side (512 MB) does not
+SRC64_MAX_BYTES = int(os.environ.get("HREC_ALS_SRC64_MB", "128")) << 20
 
 
 def padded_k(k):
@@ -147,6 +154,11 @@ class DeviceALS:
         # the half-sweep launcher (K1); tests inject the CPU oracle here to
         # exercise the sharding/all-gather logic on gloo without a GPU
         self.sweep = sweep or _hrec.als_half_sweep
+        # f64 copies of sources that stay in the on-chip caches (the device
+        # sweep only): hrec_als_half_sweep_src64, same results, no per-row
+        # conversion in the gather
+        self._src64_ok = sweep is None and self.kp == 64 and self.accum_mode == 0
+        self._s64 = None
         dev = user_csr.indptr.device
         self.u_per = user_csr.n_rows
         self.i_per = item_csc.n_rows
@@ -213,10 +225,23 @@ class DeviceALS:
         if self.world > 1:
             dist.all_gather_into_tensor(full, local, group=self.group)
 
+    def _src64(self, src):
+        """The f64 copy of `src` for the half-sweep, or None when the source
+        is larger than SRC64_MAX_BYTES (it would stream from HBM at twice
+        the bytes: the f32 gather is faster there)."""
+        if not self._src64_ok or src.numel() * 8 > SRC64_MAX_BYTES:
+            return None
+        if self._s64 is None or self._s64.numel() < src.numel():
+            self._s64 = torch.empty(src.numel(), dtype=torch.float64, device=src.device)
+        out = self._s64[: src.numel()].view(src.shape)
+        return _hrec.f32_to_f64(src, out)
+
     def _sweep(self, csr, src, local, full, cs, chunks):
         """One half-sweep of this rank's rows + replication of the result."""
+        s64 = self._src64(src)
+        extra = {} if s64 is None else {"src64": s64}
         if chunks == 1:
-            self.sweep(csr.indptr, csr.indices, csr.values, src, self.k, self.reg, local, self.accum_mode)
+            self.sweep(csr.indptr, csr.indices, csr.values, src, self.k, self.reg, local, self.accum_mode, **extra)
             self._gather(full, local)
             return
         W = self.world
@@ -224,7 +249,7 @@ class DeviceALS:
         for c in range(chunks):
             rows = slice(c * cs, (c + 1) * cs)
             self.sweep(csr.indptr[c * cs: (c + 1) * cs + 1], csr.indices, csr.values, src, self.k, self.reg,
-                       local[rows], self.accum_mode)
+                       local[rows], self.accum_mode, **extra)
             out = full[c * W * cs: (c + 1) * W * cs]
             if self.comm is None:
                 dist.all_gather_into_tensor(out, local[rows], group=self.group)

@@ -136,6 +136,17 @@ int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices,
                         double reg_param, int accum_mode, float* dst_factors,
                         void* stream);
 
+/* The same half-sweep with the source factors given in f64
+ * (src64[n_src*kp] = the f32 factors converted exactly, hrec_f32_to_f64):
+ * identical results, no per-step f32 -> f64 conversion in the gather. For
+ * sources that stay in the MI355X's on-chip caches (the user side at
+ * BASELINE c2: 100k item rows = 51 MB in f64). kp = 64, accum_mode 0. */
+int hrec_als_half_sweep_src64(const int64_t* indptr, const int32_t* indices, const float* values,
+                              int64_t n_rows, const double* src64, int64_t n_src, int k, int kp,
+                              double reg_param, float* dst_factors, void* stream);
+/* out[i] = (double)in[i]. */
+int hrec_f32_to_f64(const float* in, int64_t n, double* out, void* stream);
+
 /* out[c*ld_out + r] = in[r*cols + c] (f32), ld_out >= rows. */
 int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, float* out,
                        int64_t ld_out, void* stream);

@@ -125,6 +125,60 @@ def test_half_sweep_window_boundaries(device, mode):
     np.testing.assert_allclose(dst.cpu().numpy(), exp, rtol=rtol, atol=atol)
 
 
+def test_half_sweep_src64_equals_f32_sources(device):
+    """hrec_als_half_sweep_src64 (source factors pre-converted to f64, the
+    user side's path at c2) returns the f32-source kernel's factors bit for
+    bit (the gather converts exactly either way), across the pipeline's
+    window boundaries and the first/last source rows; and matches the C
+    oracle."""
+    h = _hrec()
+    k, kp, n_src = 64, 64, 301
+    deg = np.array([0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65, 66, 67, 95, 96, 97,
+                    127, 128, 129, 130, 191, 192, 193, 255, 256, 257, 1000, 1023, 1024, 1025])
+    rng = np.random.default_rng(12)
+    indptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    indices = rng.integers(0, n_src, indptr[-1]).astype(np.int32)
+    indices[::7] = n_src - 1
+    indices[3::11] = 0
+    values = rng.integers(0, 19, indptr[-1]).astype(np.float32)
+    src = rng.normal(size=(n_src, kp)).astype(np.float32)
+    d_ip, d_ix, d_v = _csr_to_dev(indptr, indices, values, device)
+    d_src = torch.as_tensor(src, device=device)
+    a = torch.full((len(deg), kp), 3.0, device=device)
+    b = torch.full((len(deg), kp), 5.0, device=device)
+    h.als_half_sweep(d_ip, d_ix, d_v, d_src, k, 0.1, a)
+    s64 = h.f32_to_f64(d_src)
+    assert torch.equal(s64, d_src.double())
+    h.als_half_sweep(d_ip, d_ix, d_v, d_src, k, 0.1, b, src64=s64)
+    assert torch.equal(a, b)
+    np.testing.assert_allclose(b.cpu().numpy(), obuild.half_sweep(indptr, indices, values, src, k, 0.1),
+                               rtol=1e-5, atol=1e-6)
+
+
+def test_engine_uses_src64_for_cached_sources(device):
+    """DeviceALS gathers sources of at most SRC64_MAX_BYTES from an f64 copy
+    and larger ones in f32: the fit is the same either way."""
+    from src import als_engine, synthetic
+    from src.als_engine import DeviceALS
+
+    n_users, n_items, dens, k = 600, 300, 0.05, 64
+    fits = []
+    for limit in (1 << 40, 0):
+        old = als_engine.SRC64_MAX_BYTES
+        als_engine.SRC64_MAX_BYTES = limit
+        try:
+            csr = synthetic.generate(n_users, n_items, dens, False)
+            csc = synthetic.generate(n_users, n_items, dens, True)
+            eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc)
+            eng.init_user_factors(synthetic.SEED_INIT)
+            eng.fit(3)
+            assert (eng._s64 is not None) == (limit > 0)
+            fits.append((eng.user_factors.clone(), eng.item_factors.clone()))
+        finally:
+            als_engine.SRC64_MAX_BYTES = old
+    assert torch.equal(fits[0][0], fits[1][0]) and torch.equal(fits[0][1], fits[1][1])
+
+
 def test_half_sweep_spark_literal_small(device):
     h = _hrec()
     indptr, indices, values, src = _problem(7, 12, 20, 10, 20, 16)
