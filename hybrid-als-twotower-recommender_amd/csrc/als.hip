@@ -58,6 +58,9 @@
 #ifndef HREC_ALS_PF64
 #define HREC_ALS_PF64 4  // prefetch distance of f64-source gathers (steps)
 #endif
+#ifndef HREC_ALS_PAIR8
+#define HREC_ALS_PAIR8 1  // DIAG4 = 3: two diagonal tiles share one rotation-by-8 product
+#endif
 #ifndef HREC_ALS_PR
 #define HREC_ALS_PR 2  // DIAG4 = 3: prefetch distance of the rotated loads (steps)
 #endif
@@ -183,6 +186,13 @@ __device__ __forceinline__ double row_ror(double x) {
   const long long v = __double_as_longlong(x);
   const int lo = __builtin_amdgcn_mov_dpp((int)v, 0x120 + N, 0xf, 0xf, false);
   const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), 0x120 + N, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// c ? x : y on a double as two 32-bit selects (v_cndmask_b32).
+__device__ __forceinline__ double sel64(bool c, double x, double y) {
+  const long long a = __double_as_longlong(x), b = __double_as_longlong(y);
+  const int lo = c ? (int)a : (int)b, hi = c ? (int)(a >> 32) : (int)(b >> 32);
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
@@ -358,6 +368,15 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   double dg[NT][3];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dg[t][0] = dg[t][1] = dg[t][2] = 0.0;
+  // PAIR8 (DIAG4 = 3): the rotation-by-8 product of a diagonal tile has 2
+  // distinct sub-blocks in its 4 blocks, so tiles 2P and 2P + 1 share one
+  // v_mfma_f64_4x4x4_4b: blocks 0, 1 (lanes with col < 8) take tile 2P's
+  // operands, blocks 2, 3 tile 2P + 1's (one conversion instead of two)
+  constexpr bool kPair8 = kMemRot && HREC_ALS_PAIR8 && NT % 2 == 0;
+  const bool hi8 = (lane & 8) != 0;
+  double dc[NT / 2 > 0 ? NT / 2 : 1];
+#pragma unroll
+  for (int t = 0; t < (NT / 2 > 0 ? NT / 2 : 1); ++t) dc[t] = 0.0;
   const int ra1 = 4 * ((lane & 48) | ((lane + 4) & 15)), ra2 = 4 * ((lane & 48) | ((lane + 8) & 15));
   auto bperm64 = [](double x, int addr) {
     const long long v = __double_as_longlong(x);
@@ -387,7 +406,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         break;
       }
       const RingT cur = ring[s % PF];
-      double a[NT], ar1[NT], ar2[NT];
+      double a[NT], ar1[NT], ar2[NT], apair[NT / 2 > 0 ? NT / 2 : 1];
       if constexpr (kAhead) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -408,10 +427,18 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         for (int t = 0; t < NT; ++t) {
           if constexpr (S64) {
             ar1[t] = rot1[s % PR].x[t];
-            ar2[t] = rot2[s % PR].x[t];
+            if constexpr (!kPair8) ar2[t] = rot2[s % PR].x[t];
           } else {
             ar1[t] = gram_cvt(rot1[s % PR].x[t]);
-            ar2[t] = gram_cvt(rot2[s % PR].x[t]);
+            if constexpr (!kPair8) ar2[t] = gram_cvt(rot2[s % PR].x[t]);
+          }
+        }
+        if constexpr (kPair8) {
+#pragma unroll
+          for (int t = 0; t < NT / 2; ++t) {
+            if constexpr (S64) ar2[t] = sel64(hi8, rot2[s % PR].x[2 * t + 1], rot2[s % PR].x[2 * t]);
+            else ar2[t] = gram_cvt(hi8 ? rot2[s % PR].x[2 * t + 1] : rot2[s % PR].x[2 * t]);
+            apair[t] = sel64(hi8, a[2 * t + 1], a[2 * t]);
           }
         }
         const int vr = (s + PR < 16) ? bperm(iw0, s + PR) : bperm(iw1, s + PR - 16);
@@ -444,8 +471,13 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
               dg[I][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], a[I], dg[I][0], 0, 0, 0);
               dg[I][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], (kAhead || kMemRot) ? ar1[I] : row_ror<12>(a[I]),
                                                             dg[I][1], 0, 0, 0);
-              dg[I][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], (kAhead || kMemRot) ? ar2[I] : row_ror<8>(a[I]),
-                                                            dg[I][2], 0, 0, 0);
+              if constexpr (kPair8) {
+                if (I % 2 == 0)
+                  dc[I / 2] = __builtin_amdgcn_mfma_f64_4x4x4f64(apair[I / 2], ar2[I / 2], dc[I / 2], 0, 0, 0);
+              } else {
+                dg[I][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], (kAhead || kMemRot) ? ar2[I] : row_ror<8>(a[I]),
+                                                              dg[I][2], 0, 0, 0);
+              }
             } else {
               acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I], a[J], acc[p], 0, 0, 0);
             }
@@ -482,6 +514,13 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
 #pragma unroll
       for (int sh = 0; sh < 3; ++sh) {
         const int r = 4 * q4 + i4, c = 4 * ((q4 + sh) & 3) + j4;
+        if (kPair8 && sh == 2) {  // this tile's blocks of the shared product (with their mirrors: all 4)
+          // the other tile's lanes write the same values to the junk slots 256, 257
+          const bool mine = (q4 >= 2) == (I % 2 == 1);
+          stage[mine ? r * 16 + c : 256] = dc[I / 2];
+          stage[mine ? c * 16 + r : 257] = dc[I / 2];
+          continue;
+        }
         stage[r * 16 + c] = dg[I][sh];
         stage[c * 16 + r] = dg[I][sh];
       }

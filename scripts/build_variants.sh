@@ -5,7 +5,7 @@ D=hybrid-als-twotower-recommender_amd
 mkdir -p $D/lib/ab
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags $D/csrc/*.hip -o $D/lib/ab/libhrec_$name.so &
+  timeout -k 5 900 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags $D/csrc/*.hip -o $D/lib/ab/libhrec_$name.so &
 done
 wait
 ls -la $D/lib/ab
