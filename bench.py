@@ -740,6 +740,7 @@ def main():
     # source it profiled is the one this tree runs (sha256 stamped by
     # scripts/summarize_profile.py); otherwise null + the reason.
     traffic, traffic_src, tsw, pj, fresh = None, None, None, {}, {}
+    traffic_sides = None
     prof = args.traffic_json or latest_profile()
     if prof and os.path.exists(prof) and args.accum_mode == 0:
         with open(prof) as f:
@@ -749,6 +750,9 @@ def main():
         traffic_src = {"profile": os.path.relpath(prof, ROOT), "kernel_source_matches": fresh["als.hip"]}
         if fresh["als.hip"] and world == 1:
             traffic = pj["als_half_sweep"].get("hbm_bytes_avg_per_launch")
+            per = pj["als_half_sweep"].get("hbm_bytes_per_launch_corrected") or []
+            if len(per) >= 2:  # launches alternate item, user
+                traffic_sides = {"item": sum(per[0::2]) / len(per[0::2]), "user": sum(per[1::2]) / len(per[1::2])}
         if fresh["tt.hip"]:
             tsw = pj.get("tt_adam_sweep", {})
     if tt_iv is not None:
@@ -802,8 +806,12 @@ def main():
                 "frac": achieved_tf / F64_MFMA_PEAK_TFLOPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "traffic_note": ("HBM-side bytes per launch from rocprofv3 FETCH_SIZE(x2, gfx950) + WRITE_SIZE, "
-                                 "separate PMC passes of this command (scripts/gpu_profile.sh -> profiles/)"),
+                "traffic_note": ("memory-side bytes per launch from rocprofv3 FETCH_SIZE(x2, gfx950) + WRITE_SIZE, "
+                                 "separate PMC passes of this command (scripts/gpu_profile.sh -> profiles/); "
+                                 "FETCH_SIZE counts L2 fills from the Infinity Cache as well as HBM: the user "
+                                 "side gathers the f64 copy of the item factors (51 MB, Infinity-Cache resident, "
+                                 "512 B per rating), so most of its bytes are L3 -> L2 fills, not HBM"),
+                "traffic_per_side": traffic_sides,
                 "algorithmic_flops_per_launch": flops / 2,
                 "avg_launch_ms": (item_ms + user_ms) / 2,
                 "kernel_ms_per_epoch": {"item": item_ms, "user": user_ms},

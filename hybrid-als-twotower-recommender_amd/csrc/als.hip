@@ -61,6 +61,9 @@
 #ifndef HREC_ALS_PAIR8
 #define HREC_ALS_PAIR8 1  // DIAG4 = 3: two diagonal tiles share one rotation-by-8 product
 #endif
+#ifndef HREC_ALS_ROT1DPP
+#define HREC_ALS_ROT1DPP 0  // f32 sources: rotation by 4 by DPP moves of the converted operands
+#endif
 #ifndef HREC_ALS_PR
 #define HREC_ALS_PR 2  // DIAG4 = 3: prefetch distance of the rotated loads (steps)
 #endif
@@ -350,6 +353,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   constexpr bool kAhead = HREC_ALS_DIAG4 == 2 && MODE == 0;
   constexpr bool kMemRot = HREC_ALS_DIAG4 == 3 && MODE == 0;
   constexpr int PR = kMemRot ? HREC_ALS_PR : 1;  // rotated-load prefetch distance (steps)
+  constexpr bool kRot1Dpp = kMemRot && !S64 && HREC_ALS_ROT1DPP;
   static_assert(PR < PF, "rotated loads are issued from the current windows");
   const int voff1 = (S64 ? 8 : 4) * NT * ((col + 4) & 15), voff2 = (S64 ? 8 : 4) * NT * ((col + 8) & 15);
   auto rot_load = [&](int vi, int vo) -> RingT {
@@ -361,7 +365,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
 #pragma unroll
     for (int q = 0; q < PR; ++q) {
       const int vi = bperm(iw0, q);
-      rot1[q] = rot_load(vi, voff1);
+      if constexpr (!kRot1Dpp) rot1[q] = rot_load(vi, voff1);
       rot2[q] = rot_load(vi, voff2);
     }
   }
@@ -429,7 +433,9 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
             ar1[t] = rot1[s % PR].x[t];
             if constexpr (!kPair8) ar2[t] = rot2[s % PR].x[t];
           } else {
-            ar1[t] = gram_cvt(rot1[s % PR].x[t]);
+            // ROT1DPP: the rotation by 4 lanes of the converted operand (two
+            // 32-bit DPP moves) instead of a converted rotated load
+            ar1[t] = kRot1Dpp ? row_ror<12>(a[t]) : gram_cvt(rot1[s % PR].x[t]);
             if constexpr (!kPair8) ar2[t] = gram_cvt(rot2[s % PR].x[t]);
           }
         }
@@ -442,7 +448,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
           }
         }
         const int vr = (s + PR < 16) ? bperm(iw0, s + PR) : bperm(iw1, s + PR - 16);
-        rot1[s % PR] = rot_load(vr, voff1);
+        if constexpr (!kRot1Dpp) rot1[s % PR] = rot_load(vr, voff1);
         rot2[s % PR] = rot_load(vr, voff2);
       }
       if constexpr (kAhead) {
