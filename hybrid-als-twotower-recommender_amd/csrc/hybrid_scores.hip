@@ -60,7 +60,7 @@ struct HybScoresArgs {
 };
 
 #ifndef HREC_HS_ABLATE
-#define HREC_HS_ABLATE 0  // timing-only builds: 1 = no score stores, 2 = and no min/max, 3 = staging only
+#define HREC_HS_ABLATE 0  // timing-only builds: 1 = no score stores, 2 = and no min/max, 3 = staging only, 4 = MFMAs, no epilogue
 #endif
 
 #ifndef HREC_HS_NT
@@ -100,7 +100,10 @@ struct HsShape {
   static constexpr int NU = NI == 4 ? 2 : 4;    // user tiles per chunk (NI 4: each user fragment feeds 4 MFMAs)
 };
 
-template <int DK>
+// NCH: user chunks of CU = 16 NU users in the tile (compile-time, so the
+// per-lane running min / max of every chunk stays in registers and the last
+// chunk's item refills are unconditional).
+template <int DK, int NCH>
 __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a) {
   using S = HsShape<DK>;
   constexpr int KS = S::KS, NI = S::NI, NU = S::NU, CU = 16 * NU;
@@ -119,6 +122,36 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   const int b0 = ut * a.UB;
   const int ub = a.B - b0 < a.UB ? a.B - b0 : a.UB;
 
+  // the wave's first item slice is requested before the user staging, so its
+  // fragments arrive while the users are converted
+  const int xq = c ^ g;
+  const uint64_t vb = (uint64_t)a.items[model];
+  hs_rsrc rsrc;
+  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
+  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * 2) << 16));
+  rsrc.z = __builtin_amdgcn_readfirstlane((int)a.N);
+  rsrc.w = 0x00020000;
+  const int voff = 16 * g;
+  auto rows_of = [&](int64_t jb, int (&vi)[NI]) {
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int64_t j = jb + 16 * t + c;
+      vi[t] = j < i1 ? (int)j : 0x7fffffff;  // out of range: the buffer check reads zeros
+    }
+  };
+  constexpr int64_t kSlice = 16 * NI, kStride = 8 * kSlice;  // items per wave slice / per block round
+  int64_t jb = i0 + kSlice * w;
+  const bool work = HREC_HS_ABLATE < 3 && ub > 0 && jb < i1;
+  int vnext[NI];
+  rows_of(jb, vnext);
+  HsFrag it_f[KS][NI];
+  if (work) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+  }
+
   // users of the tile -> LDS as bf16 (zero rows / columns beyond the batch /
   // width). Batches of chunks (8 floats each) per thread: all loads are
   // issued before the first conversion (16-B loads when the row allows).
@@ -128,7 +161,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
     const int64_t* rws = a.rows[model];
     const int wd = a.width[model];
     const bool vec = (ld & 3) == 0 && ((uintptr_t)src & 15) == 0;
-    constexpr int kBatch = DK == 256 ? 16 : 8;  // one round of loads at UB = 256
+    constexpr int kBatch = 8;  // chunks in flight per thread (the first item slice is in flight too)
     const int n_chunks = a.UB * S::kChunks;
     for (int o0 = threadIdx.x; o0 < n_chunks; o0 += kBatch * kHsThreads) {
       float f[kBatch][8];
@@ -170,32 +203,14 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   }
   __syncthreads();
 
-  const int xq = c ^ g;
-  const uint64_t vb = (uint64_t)a.items[model];
-  hs_rsrc rsrc;
-  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
-  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * 2) << 16));
-  rsrc.z = __builtin_amdgcn_readfirstlane((int)a.N);
-  rsrc.w = 0x00020000;
-  const int voff = 16 * g;
-  auto rows_of = [&](int64_t jb, int (&vi)[NI]) {
+  // running min / max of this lane's scores per (chunk, user tile): the
+  // lane's user is CU ch + 16 u + c in every slice; folded across lanes once
+  float lo[NCH][NU], hi[NCH][NU];
 #pragma unroll
-    for (int t = 0; t < NI; ++t) {
-      const int64_t j = jb + 16 * t + c;
-      vi[t] = j < i1 ? (int)j : 0x7fffffff;  // out of range: the buffer check reads zeros
-    }
-  };
-  const int n_ch = (ub + CU - 1) / CU;
-  constexpr int64_t kSlice = 16 * NI, kStride = 8 * kSlice;  // items per wave slice / per block round
-  int64_t jb = i0 + kSlice * w;
-  if (HREC_HS_ABLATE < 3 && ub > 0 && jb < i1) {
-    int vnext[NI];
-    rows_of(jb, vnext);
-    HsFrag it_f[KS][NI];
+  for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+    for (int u = 0; u < NU; ++u) lo[ch][u] = __builtin_inff(), hi[ch][u] = -__builtin_inff();
+  if (work) {
     HsFrag ua[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
@@ -205,16 +220,17 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
     float* const out = a.out[model];
     for (; jb < i1; jb += kStride) {
       rows_of(jb + kStride, vnext);
+      const bool full = jb + kSlice <= i1;  // wave-uniform: every item of the slice is in range
       auto user_frag = [&](int ch, int u, int ks) {
         HsFrag f;
         const int off = S::kSwz ? 16 * ((4 * ks) ^ xq) : 64 * ks + 16 * g;
         f.i = *reinterpret_cast<const int4*>(us + (CU * ch + 16 * u + c) * kRowB + off);
         return f;
       };
-      // the last chunk is peeled: its item refills (the next slice) are unconditional
-      auto chunk = [&](int ch, auto last_t) {
-        constexpr bool last = decltype(last_t)::value;
-        const int ch_next = ch + 1 < n_ch ? ch + 1 : 0;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const bool last = ch == NCH - 1;
+        const int ch_next = last ? 0 : ch + 1;
         hs_f4 acc[NU][NI];
 #pragma unroll
         for (int u = 0; u < NU; ++u)
@@ -235,7 +251,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
               acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it_f[ks][t].i),
                                                                   __builtin_bit_cast(hs_bf8, f[u].i), acc[u][t], 0,
                                                                   0, 0);
-          if constexpr (last) {
+          if (last) {  // step ks of this slice is done: refill it with the next slice's
 #pragma unroll
             for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
           }
@@ -250,26 +266,27 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
           const int bl = CU * ch + 16 * u + c;
-          float lo = __builtin_inff(), hi = -__builtin_inff();
+          if (full) {
 #pragma unroll
-          for (int t = 0; t < NI; ++t) {
-            const int64_t j = jb + 16 * t + 4 * g;
-            if (j + 3 < i1) {
+            for (int t = 0; t < NI; ++t) {
+              lo[ch][u] = fminf(fminf(lo[ch][u], fminf(acc[u][t][0], acc[u][t][1])), fminf(acc[u][t][2], acc[u][t][3]));
+              hi[ch][u] = fmaxf(fmaxf(hi[ch][u], fmaxf(acc[u][t][0], acc[u][t][1])), fmaxf(acc[u][t][2], acc[u][t][3]));
+            }
+          } else {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                lo = fminf(lo, acc[u][t][r]);
-                hi = fmaxf(hi, acc[u][t][r]);
-              }
-            } else {
+            for (int t = 0; t < NI; ++t)
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                if (j + r < i1) {
-                  lo = fminf(lo, acc[u][t][r]);
-                  hi = fmaxf(hi, acc[u][t][r]);
+                if (jb + 16 * t + 4 * g + r < i1) {
+                  lo[ch][u] = fminf(lo[ch][u], acc[u][t][r]);
+                  hi[ch][u] = fmaxf(hi[ch][u], acc[u][t][r]);
                 }
-            }
-            if (HREC_HS_ABLATE == 0 && bl < ub) {
-              float* o = out + (int64_t)(b0 + bl) * a.ldo;
+          }
+          if (HREC_HS_ABLATE == 0 && bl < ub) {
+            float* o = out + (int64_t)(b0 + bl) * a.ldo;
+#pragma unroll
+            for (int t = 0; t < NI; ++t) {
+              const int64_t j = jb + 16 * t + 4 * g;
               if (j + 3 < i1 && (a.ldo & 3) == 0) {
                 if constexpr (HREC_HS_NT) {
                   __builtin_nontemporal_store(acc[u][t], reinterpret_cast<hs_f4*>(o + j));
@@ -284,19 +301,27 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
               }
             }
           }
-          lo = fminf(lo, __shfl_xor(lo, 16, kWave));
-          lo = fminf(lo, __shfl_xor(lo, 32, kWave));
-          hi = fmaxf(hi, __shfl_xor(hi, 16, kWave));
-          hi = fmaxf(hi, __shfl_xor(hi, 32, kWave));
-          if (HREC_HS_ABLATE < 2 && g == 0 && bl < ub) {
-            atomicMax(&mmk[2 * bl], ~hs_key(lo));
-            atomicMax(&mmk[2 * bl + 1], hs_key(hi));
-          }
         }
-      };
-      for (int ch = 0; ch + 1 < n_ch; ++ch) chunk(ch, std::false_type{});
-      chunk(n_ch - 1, std::true_type{});
+      }
     }
+  }
+  // fold the lanes' running min / max per user into the block's LDS slots
+  if (HREC_HS_ABLATE < 2 && ub > 0) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int bl = CU * ch + 16 * u + c;
+        float l = lo[ch][u], h = hi[ch][u];
+        l = fminf(l, __shfl_xor(l, 16, kWave));
+        l = fminf(l, __shfl_xor(l, 32, kWave));
+        h = fmaxf(h, __shfl_xor(h, 16, kWave));
+        h = fmaxf(h, __shfl_xor(h, 32, kWave));
+        if (g == 0 && bl < ub) {
+          atomicMax(&mmk[2 * bl], ~hs_key(l));
+          atomicMax(&mmk[2 * bl + 1], hs_key(h));
+        }
+      }
   }
   __syncthreads();
   for (int o = threadIdx.x; o < ub; o += kHsThreads) {
@@ -355,24 +380,37 @@ static int hs_groups(int64_t n_items) {
 
 template <int DK>
 static int hs_user_tile(int B) {
+  constexpr int CU = 16 * HsShape<DK>::NU;
   int ub_max = kHsMaxUserBytes / HsShape<DK>::kRowB;
-  ub_max = ub_max / 64 * 64;
-  if (ub_max > 256) ub_max = 256;
+  ub_max = ub_max / CU * CU;
+  if (ub_max > 4 * CU) ub_max = 4 * CU;  // <= 4 chunks (NCH instantiations)
   const int n_ut = (B + ub_max - 1) / ub_max;
   int UB = (B + n_ut - 1) / n_ut;
-  return (UB + 63) / 64 * 64;
+  return (UB + CU - 1) / CU * CU;
+}
+
+template <int DK, int NCH>
+static int hs_launch_n(HybScoresArgs& a, size_t lds, hipStream_t s) {
+  const auto kfn = hyb_scores_kernel<DK, NCH>;
+  if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return check_launch("hyb_scores_kernel: LDS attribute");
+  hipLaunchKernelGGL(kfn, dim3((unsigned)(2 * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
+  return check_launch("hyb_scores_kernel");
 }
 
 template <int DK>
 static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
+  constexpr int CU = 16 * HsShape<DK>::NU;
   a.UB = hs_user_tile<DK>(a.B);
   a.n_ut = (a.B + a.UB - 1) / a.UB;
   const size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * 8;
-  const auto kfn = hyb_scores_kernel<DK>;
-  if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return check_launch("hyb_scores_kernel: LDS attribute");
-  hipLaunchKernelGGL(kfn, dim3((unsigned)(2 * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
-  int rc = check_launch("hyb_scores_kernel");
+  int rc;
+  switch (a.UB / CU) {
+    case 1: rc = hs_launch_n<DK, 1>(a, lds, s); break;
+    case 2: rc = hs_launch_n<DK, 2>(a, lds, s); break;
+    case 3: rc = hs_launch_n<DK, 3>(a, lds, s); break;
+    default: rc = hs_launch_n<DK, 4>(a, lds, s); break;
+  }
   if (rc) return rc;
   hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((a.B + 63) / 64), 2), dim3(256), 0, s, a.part, a.B, a.G,
                      mm0, mm1);
