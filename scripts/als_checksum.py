@@ -1,0 +1,22 @@
+"""sha256 of the factors after 2 epochs of a mid-sized synthetic fit: compares
+ALS kernel variants for bit-identity (HREC_LIB selects the build)."""
+import hashlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "hybrid-als-twotower-recommender_amd"))
+from src import synthetic  # noqa: E402
+from src.als_engine import DeviceALS  # noqa: E402
+
+n_users, n_items = 200_000, 20_000
+csr = synthetic.generate(n_users, n_items, 0.005, False)
+csc = synthetic.generate(n_users, n_items, 0.005, True)
+eng = DeviceALS(n_users, n_items, 64, 0.1, csr, csc)
+eng.init_user_factors(7)
+eng.fit(2)
+torch.cuda.synchronize()
+h = hashlib.sha256(eng.U.cpu().numpy().tobytes() + eng.V.cpu().numpy().tobytes()).hexdigest()
+print(os.path.basename(os.environ.get("HREC_LIB", "default")), h[:16])

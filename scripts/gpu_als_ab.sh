@@ -1,7 +1,9 @@
-# ALS half-sweep parity tests on the default library, then the A/B variants.
+# ALS variants: half-sweep parity tests on the first ab/ build given, factor
+# checksums of every ab/ build (bit-identity), then the epoch A/B.
 set -e
-python -c "import __graft_entry__ as g; g.build()"
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests/test_gpu_core.py -q -x -k "half_sweep or engine" > gpurun_out/als_tests.log 2>&1 || { tail -30 gpurun_out/als_tests.log; exit 1; }
-tail -3 gpurun_out/als_tests.log
+V=hybrid-als-twotower-recommender_amd/lib/ab
+HREC_LIB=$V/libhrec_$1.so timeout -k 10 300 python -u -m pytest tests/test_gpu_core.py -q -x -k "half_sweep or engine" --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
+tail -1 gpurun_out/ab_tests.log
+for lib in $V/*.so; do HREC_LIB=$lib timeout -k 10 120 python scripts/als_checksum.py; done
 bash scripts/ab_variants.sh
