@@ -59,7 +59,7 @@
 #define HREC_ALS_PF64 4  // prefetch distance of f64-source gathers (steps)
 #endif
 #ifndef HREC_ALS_PAIR8
-#define HREC_ALS_PAIR8 1  // DIAG4 = 3: two diagonal tiles share one rotation-by-8 product
+#define HREC_ALS_PAIR8 2  // DIAG4 = 3: two diagonal tiles share one rotation-by-8 product (2: pairs (0,2), (1,3) by half-width loads)
 #endif
 #ifndef HREC_ALS_ROT1DPP
 #define HREC_ALS_ROT1DPP 0  // f32 sources: rotation by 4 by DPP moves of the converted operands
@@ -124,6 +124,18 @@ __device__ __forceinline__ VecD struct_load_d(i4v rsrc, int vindex, int voffset)
   v.x[1] = __hiloint2double(__float_as_int(lo.w), __float_as_int(lo.z));
   v.x[2] = __hiloint2double(__float_as_int(hi.y), __float_as_int(hi.x));
   v.x[3] = __hiloint2double(__float_as_int(hi.w), __float_as_int(hi.z));
+  return v;
+}
+
+// Two f64 source-factor columns (16 B).
+struct VecD2 {
+  double x[2];
+};
+__device__ __forceinline__ VecD2 struct_load_d2(i4v rsrc, int vindex, int voffset) {
+  const f4 t = sbuf_load_f4(rsrc, vindex, voffset, 0, 0);
+  VecD2 v;
+  v.x[0] = __hiloint2double(__float_as_int(t.y), __float_as_int(t.x));
+  v.x[1] = __hiloint2double(__float_as_int(t.w), __float_as_int(t.z));
   return v;
 }
 
@@ -360,13 +372,31 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
     if constexpr (S64) return struct_load_d(rsrc, vi, vo);
     else return struct_load<NT>(rsrc, vi, vo);
   };
+  // PAIR8 = 2: the shared rotation-by-8 product pairs tiles (0, 2) and
+  // (1, 3), whose operands are adjacent components: lanes col < 8 need
+  // components {0, 1}, lanes col >= 8 {2, 3} — of the own slice (A) and of
+  // the col + 8 slice (B). Two half-width loads at a per-lane offset deliver
+  // exactly those, so no lane selects are needed.
+  constexpr bool kPairL = kMemRot && HREC_ALS_PAIR8 == 2 && NT == 4;
+  using PairT = std::conditional_t<S64, VecD2, Vec<2>>;
+  const int hoff = (lane & 8) ? (S64 ? 16 : 8) : 0;
+  auto pair_load = [&](int vi, int vo) -> PairT {
+    if constexpr (S64) return struct_load_d2(rsrc, vi, vo);
+    else return struct_load<2>(rsrc, vi, vo);
+  };
   RingT rot1[PR], rot2[PR];
+  PairT rotA[PR], rotB[PR];
   if constexpr (kMemRot) {
 #pragma unroll
     for (int q = 0; q < PR; ++q) {
       const int vi = bperm(iw0, q);
       if constexpr (!kRot1Dpp) rot1[q] = rot_load(vi, voff1);
-      rot2[q] = rot_load(vi, voff2);
+      if constexpr (kPairL) {
+        rotA[q] = pair_load(vi, voff + hoff);
+        rotB[q] = pair_load(vi, voff2 + hoff);
+      } else {
+        rot2[q] = rot_load(vi, voff2);
+      }
     }
   }
   double dg[NT][3];
@@ -439,7 +469,18 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
             if constexpr (!kPair8) ar2[t] = gram_cvt(rot2[s % PR].x[t]);
           }
         }
-        if constexpr (kPair8) {
+        if constexpr (kPairL) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            if constexpr (S64) {
+              apair[t] = rotA[s % PR].x[t];
+              ar2[t] = rotB[s % PR].x[t];
+            } else {
+              apair[t] = gram_cvt(rotA[s % PR].x[t]);
+              ar2[t] = gram_cvt(rotB[s % PR].x[t]);
+            }
+          }
+        } else if constexpr (kPair8) {
 #pragma unroll
           for (int t = 0; t < NT / 2; ++t) {
             if constexpr (S64) ar2[t] = sel64(hi8, rot2[s % PR].x[2 * t + 1], rot2[s % PR].x[2 * t]);
@@ -449,7 +490,12 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         }
         const int vr = (s + PR < 16) ? bperm(iw0, s + PR) : bperm(iw1, s + PR - 16);
         if constexpr (!kRot1Dpp) rot1[s % PR] = rot_load(vr, voff1);
-        rot2[s % PR] = rot_load(vr, voff2);
+        if constexpr (kPairL) {
+          rotA[s % PR] = pair_load(vr, voff + hoff);
+          rotB[s % PR] = pair_load(vr, voff2 + hoff);
+        } else {
+          rot2[s % PR] = rot_load(vr, voff2);
+        }
       }
       if constexpr (kAhead) {
         const Vec<NT> nx = ring[(s + 1) % PF];
@@ -477,7 +523,9 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
               dg[I][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], a[I], dg[I][0], 0, 0, 0);
               dg[I][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[I], (kAhead || kMemRot) ? ar1[I] : row_ror<12>(a[I]),
                                                             dg[I][1], 0, 0, 0);
-              if constexpr (kPair8) {
+              if constexpr (kPairL) {  // tiles I and I + 2
+                if (I < 2) dc[I] = __builtin_amdgcn_mfma_f64_4x4x4f64(apair[I], ar2[I], dc[I], 0, 0, 0);
+              } else if constexpr (kPair8) {
                 if (I % 2 == 0)
                   dc[I / 2] = __builtin_amdgcn_mfma_f64_4x4x4f64(apair[I / 2], ar2[I / 2], dc[I / 2], 0, 0, 0);
               } else {
@@ -522,9 +570,10 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
         const int r = 4 * q4 + i4, c = 4 * ((q4 + sh) & 3) + j4;
         if (kPair8 && sh == 2) {  // this tile's blocks of the shared product (with their mirrors: all 4)
           // the other tile's lanes write the same values to the junk slots 256, 257
-          const bool mine = (q4 >= 2) == (I % 2 == 1);
-          stage[mine ? r * 16 + c : 256] = dc[I / 2];
-          stage[mine ? c * 16 + r : 257] = dc[I / 2];
+          const bool mine = kPairL ? (q4 >= 2) == (I >= 2) : (q4 >= 2) == (I % 2 == 1);
+          const double v = kPairL ? dc[I & 1] : dc[I / 2];
+          stage[mine ? r * 16 + c : 256] = v;
+          stage[mine ? c * 16 + r : 257] = v;
           continue;
         }
         stage[r * 16 + c] = dg[I][sh];
