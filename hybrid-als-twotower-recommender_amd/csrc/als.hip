@@ -62,7 +62,7 @@
 #define HREC_ALS_PAIR8 2  // DIAG4 = 3: two diagonal tiles share one rotation-by-8 product (2: pairs (0,2), (1,3) by half-width loads)
 #endif
 #ifndef HREC_ALS_ROT1DPP
-#define HREC_ALS_ROT1DPP 0  // f32 sources: rotation by 4 by DPP moves of the converted operands
+#define HREC_ALS_ROT1DPP 1  // f32 sources: rotation by 4 by DPP moves of the converted operands (0: rotated load + conversion)
 #endif
 #ifndef HREC_ALS_PR
 #define HREC_ALS_PR 2  // DIAG4 = 3: prefetch distance of the rotated loads (steps)
