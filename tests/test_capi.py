@@ -53,6 +53,24 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert f(None, 9, *args) == -1
     assert b"tables" in lib.hrec_last_error()
     assert f(None, 0, *args) == 0  # nothing to update
+    # f64-source half-sweep: kp 64 only
+    h = lib.hrec_als_half_sweep_src64
+    h.restype = ctypes.c_int
+    assert h(None, None, None, ctypes.c_int64(1), None, ctypes.c_int64(1), 8, 32, ctypes.c_double(0.1), None,
+             None) == -1
+    assert b"kp must be 64" in lib.hrec_last_error()
+    # bf16 hybrid scores: operand width and workspace are checked first
+    hs = lib.hrec_hybrid_scores
+    hs.restype = ctypes.c_int
+    hs.argtypes = ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
+                   + [ctypes.c_void_p] * 2 + [ctypes.c_int64] + [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_void_p])
+    assert hs(None, 96, None, 96, None, 96, 96, 4, None, None, 10, 96, None, None, 10, None, None, None, 0, None) == -1
+    assert b"dk must be 64, 128 or 256" in lib.hrec_last_error()
+    assert hs(None, 64, None, 64, None, 64, 64, 4, None, None, 10, 64, None, None, 10, None, None, None, 0, None) == -1
+    assert b"null min/max output or workspace" in lib.hrec_last_error()
+    assert hs(None, 64, None, 64, None, 64, 64, 0, None, None, 10, 64, None, None, 10, None, None, None, 0,
+              None) == 0  # no users: nothing to do
 
 
 def test_product_has_no_oracle_imports():
