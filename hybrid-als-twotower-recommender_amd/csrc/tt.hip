@@ -636,7 +636,27 @@ __global__ __launch_bounds__(64) void sparse_dedup_group_kernel(const SparseGrou
   if (lane == 0) T.mark[key] = s;
 }
 
-// blocks of kBlock threads x 4 elements (every dim % 4 == 0, 16-B aligned)
+// One element of the whole-table Adam step (has_g: the row is in the batch;
+// g its summed gradient). The two fma are spelled out so every kernel that
+// updates a row (the sweep, the touched-rows kernel of the phased form)
+// rounds it identically.
+__device__ __forceinline__ void adam_elem(float& m, float& v, float& x, float g, bool has_g, float lr, float b1,
+                                          float omb1, float b2, float omb2, float eps) {
+  float me = m * b1;
+  float ve = v * b2;
+  if (has_g) {
+    me = __builtin_fmaf(g, omb1, me);
+    ve = __builtin_fmaf(g * g, omb2, ve);
+  }
+  m = me;
+  v = ve;
+  x = x - (lr * me) / (sqrtf(ve) + eps);
+}
+
+// blocks of kBlock threads x 4 elements (every dim % 4 == 0, 16-B aligned).
+// SKIP_TOUCHED (phase 1 of the phased form): rows marked in this batch are
+// left alone (phase 2 updates them once the gradients exist).
+template <bool SKIP_TOUCHED>
 __global__ __launch_bounds__(kBlock) void adam_sparse_group4_kernel(const SparseGroup G, float lr, float b1,
                                                                      float omb1, float b2, float omb2, float eps) {
   const int i = group_of(G, blockIdx.x);
@@ -648,6 +668,7 @@ __global__ __launch_bounds__(kBlock) void adam_sparse_group4_kernel(const Sparse
   const int64_t r = o / dim;
   const int c = (int)(o - r * dim);
   const int32_t q = T.mark[r];
+  if (SKIP_TOUCHED && q >= 0) return;
   float4 mo = reinterpret_cast<const float4*>(T.m)[o4];
   float4 vo = reinterpret_cast<const float4*>(T.v)[o4];
   float4 xo = reinterpret_cast<const float4*>(T.var)[o4];
@@ -655,23 +676,64 @@ __global__ __launch_bounds__(kBlock) void adam_sparse_group4_kernel(const Sparse
   float* vp = &vo.x;
   float* xp = &xo.x;
   float4 gr = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (q >= 0) gr = *reinterpret_cast<const float4*>(T.gsum + (int64_t)q * dim + c);
+  if (!SKIP_TOUCHED && q >= 0) gr = *reinterpret_cast<const float4*>(T.gsum + (int64_t)q * dim + c);
   const float* gp = &gr.x;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float me = mp[e] * b1;
-    float ve = vp[e] * b2;
-    if (q >= 0) {
-      me = me + gp[e] * omb1;
-      ve = ve + (gp[e] * gp[e]) * omb2;
-    }
-    mp[e] = me;
-    vp[e] = ve;
-    xp[e] = xp[e] - (lr * me) / (sqrtf(ve) + eps);
-  }
+  for (int e = 0; e < 4; ++e) adam_elem(mp[e], vp[e], xp[e], gp[e], !SKIP_TOUCHED && q >= 0, lr, b1, omb1, b2, omb2, eps);
   reinterpret_cast<float4*>(T.m)[o4] = mo;
   reinterpret_cast<float4*>(T.v)[o4] = vo;
   reinterpret_cast<float4*>(T.var)[o4] = xo;
+}
+
+// Phase 0 of the phased form: mark[key] = first slot of key (no gradients).
+__global__ __launch_bounds__(64) void sparse_mark_group_kernel(const SparseGroup G) {
+  const int i = group_of(G, blockIdx.x);
+  const hrec_sparse_table& T = G.t[i];
+  const int s = (int)(blockIdx.x - G.start[i]), lane = threadIdx.x;
+  const int32_t* __restrict__ idx = T.indices;
+  const int32_t key = idx[s];
+  for (int t0 = 0; t0 < s; t0 += kWave) {
+    const int t = t0 + lane;
+    if (__ballot(t < s && idx[t] == key)) return;
+  }
+  if (lane == 0) T.mark[key] = s;
+}
+
+// Phase 2: one wave per first slot of a key — the slots' gradients summed in
+// slot order (as sparse_dedup_group_kernel) and the row's Adam step (as the
+// sweep's marked rows), straight into var / m / v.
+__global__ __launch_bounds__(64) void sparse_touched_group_kernel(const SparseGroup G, float lr, float b1, float omb1,
+                                                                  float b2, float omb2, float eps) {
+  const int i = group_of(G, blockIdx.x);
+  const hrec_sparse_table& T = G.t[i];
+  const int s = (int)(blockIdx.x - G.start[i]), lane = threadIdx.x;
+  const int32_t* __restrict__ idx = T.indices;
+  const float* __restrict__ g = T.grad_rows;
+  const int B = T.batch, dim = T.dim;
+  const int32_t key = idx[s];
+  if (T.mark[key] != s) return;  // a later slot of a key: summed by its first
+  for (int c0 = 0; c0 < dim; c0 += kWave) {
+    const int c = c0 + lane;
+    const bool on = c < dim;
+    float acc = on ? g[(int64_t)s * dim + c] : 0.f;
+    for (int t0 = s + 1; t0 < B; t0 += kWave) {
+      const int t = t0 + lane;
+      uint64_t msk = __ballot(t < B && idx[t] == key);
+      while (msk) {
+        const int u = t0 + __builtin_ctzll(msk);
+        msk &= msk - 1;
+        if (on) acc = acc + g[(int64_t)u * dim + c];
+      }
+    }
+    if (on) {
+      const int64_t o = (int64_t)key * dim + c;
+      float m = T.m[o], v = T.v[o], x = T.var[o];
+      adam_elem(m, v, x, acc, true, lr, b1, omb1, b2, omb2, eps);
+      T.m[o] = m;
+      T.v[o] = v;
+      T.var[o] = x;
+    }
+  }
 }
 
 __global__ void sparse_unmark_group_kernel(const SparseGroup G) {
@@ -947,7 +1009,7 @@ extern "C" int hrec_adam_sparse_tables(const hrec_sparse_table* tables, int n_ta
     acc += (H.t[i].n_rows * H.t[i].dim / 4 + kBlock - 1) / kBlock;
   }
   H.start[H.n] = acc;
-  hipLaunchKernelGGL(adam_sparse_group4_kernel, dim3((unsigned)acc), dim3(kBlock), 0, s, H, lr, beta1,
+  hipLaunchKernelGGL(adam_sparse_group4_kernel<false>, dim3((unsigned)acc), dim3(kBlock), 0, s, H, lr, beta1,
                      one_minus_beta1, beta2, one_minus_beta2, epsilon);
   int rc = check_launch("adam_sparse_group4_kernel");
   if (rc || n_slots == 0) return rc;
@@ -964,4 +1026,64 @@ extern "C" int hrec_tt_pair_score(const float* user_vec, const float* item_vec, 
   hipLaunchKernelGGL(tt_pair_score_kernel, dim3((unsigned)((n + 3) / 4)), dim3(kBlock), 0, as_stream(stream),
                      user_vec, item_vec, n, d, out);
   return check_launch("tt_pair_score_kernel");
+}
+
+// hrec_adam_sparse_tables split into phases (HREC_SPARSE_*), so that the
+// whole-table sweep of the rows the batch does not touch — nearly all of the
+// step's HBM traffic — can run on a second stream beside the batch's
+// forward / backward (which read only touched rows). Phases 0, 1, 2, 3 in
+// stream order give bit for bit the rows of hrec_adam_sparse_tables; phase 1
+// may overlap phase 2 (disjoint rows) but neither phase 0 nor phase 3 (they
+// write the marks phase 1 reads). Needs dim % 4 == 0 and 16-B aligned
+// var / m / v (hrec_adam_sparse_tables takes every shape); gsum is unused and
+// grad_rows is read by phase 2 only.
+extern "C" int hrec_adam_sparse_tables_phase(const hrec_sparse_table* tables, int n_tables, int phase, float lr,
+                                             float beta1, float one_minus_beta1, float beta2, float one_minus_beta2,
+                                             float epsilon, void* stream) {
+  HREC_REQUIRE(n_tables >= 0 && n_tables <= HREC_MAX_SPARSE_TABLES, "adam_sparse_tables_phase: 0..%d tables",
+               HREC_MAX_SPARSE_TABLES);
+  HREC_REQUIRE(phase >= HREC_SPARSE_MARK && phase <= HREC_SPARSE_UNMARK, "adam_sparse_tables_phase: phase %d not in 0..3",
+               phase);
+  if (n_tables == 0) return HREC_OK;
+  HREC_REQUIRE(tables, "adam_sparse_tables_phase: null table list");
+  for (int i = 0; i < n_tables; ++i) {
+    const hrec_sparse_table& T = tables[i];
+    HREC_REQUIRE(T.n_rows >= 0 && T.dim >= 1 && T.batch >= 0, "adam_sparse_tables_phase: table %d: bad shape", i);
+    HREC_REQUIRE(T.n_rows == 0 || (T.var && T.m && T.v && T.mark), "adam_sparse_tables_phase: table %d: null pointer",
+                 i);
+    HREC_REQUIRE(T.batch == 0 || (T.indices && (phase != HREC_SPARSE_TOUCHED || T.grad_rows)),
+                 "adam_sparse_tables_phase: table %d: null slices", i);
+    HREC_REQUIRE(T.dim % 4 == 0 && (((uintptr_t)T.var | (uintptr_t)T.m | (uintptr_t)T.v) & 15) == 0,
+                 "adam_sparse_tables_phase: table %d: needs dim %% 4 == 0 and 16-B aligned rows "
+                 "(use hrec_adam_sparse_tables)", i);
+  }
+  hipStream_t s = as_stream(stream);
+  SparseGroup G{};
+  int64_t acc = 0;
+  for (int i = 0; i < n_tables; ++i) {
+    if (tables[i].n_rows == 0) continue;
+    G.t[G.n] = tables[i];
+    G.start[G.n] = acc;
+    acc += phase == HREC_SPARSE_SWEEP_UNTOUCHED ? (tables[i].n_rows * tables[i].dim / 4 + kBlock - 1) / kBlock
+                                                : tables[i].batch;
+    ++G.n;
+  }
+  G.start[G.n] = acc;
+  if (G.n == 0 || acc == 0) return HREC_OK;
+  switch (phase) {
+    case HREC_SPARSE_MARK:
+      hipLaunchKernelGGL(sparse_mark_group_kernel, dim3((unsigned)acc), dim3(kWave), 0, s, G);
+      return check_launch("sparse_mark_group_kernel");
+    case HREC_SPARSE_SWEEP_UNTOUCHED:
+      hipLaunchKernelGGL(adam_sparse_group4_kernel<true>, dim3((unsigned)acc), dim3(kBlock), 0, s, G, lr, beta1,
+                         one_minus_beta1, beta2, one_minus_beta2, epsilon);
+      return check_launch("adam_sparse_group4_kernel (untouched rows)");
+    case HREC_SPARSE_TOUCHED:
+      hipLaunchKernelGGL(sparse_touched_group_kernel, dim3((unsigned)acc), dim3(kWave), 0, s, G, lr, beta1,
+                         one_minus_beta1, beta2, one_minus_beta2, epsilon);
+      return check_launch("sparse_touched_group_kernel");
+    default:
+      hipLaunchKernelGGL(sparse_unmark_group_kernel, dim3((unsigned)((acc + 255) / 256)), dim3(256), 0, s, G);
+      return check_launch("sparse_unmark_group_kernel");
+  }
 }

@@ -105,6 +105,8 @@ _SIGNATURES.update({
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
                          [ctypes.c_float] * 6 + [_vp]),
     "hrec_adam_sparse_tables": (_c_i32, [ctypes.POINTER(SparseTable), _c_i32] + [ctypes.c_float] * 6 + [_vp]),
+    "hrec_adam_sparse_tables_phase": (_c_i32, [ctypes.POINTER(SparseTable), _c_i32, _c_i32] + [ctypes.c_float] * 6
+                                      + [_vp]),
 })
 
 ABI_VERSION = 1
@@ -710,6 +712,34 @@ def adam_sparse_tables(tables, lr, beta1, omb1, beta2, omb2, eps):
                              _dev(mark, torch.int32, "mark"), _dev(gsum, torch.float32, "gsum"))
     _check("hrec_adam_sparse_tables", lib().hrec_adam_sparse_tables(
         arr, len(tables), float(lr), float(beta1), float(omb1), float(beta2), float(omb2), float(eps), _stream()))
+
+
+SPARSE_MARK, SPARSE_SWEEP_UNTOUCHED, SPARSE_TOUCHED, SPARSE_UNMARK = 0, 1, 2, 3
+
+
+def sparse_tables_arg(tables):
+    """ctypes array of hrec_sparse_table for the phased sparse Adam: tables is
+    a list of (var, m, v, indices, grad_rows, mark) (no gsum: phase 2 sums
+    the gradients in registers). Build once per step, pass to every phase."""
+    if len(tables) > MAX_SPARSE_TABLES:
+        raise HrecError(f"adam_sparse_tables_phase: at most {MAX_SPARSE_TABLES} tables")
+    arr = (SparseTable * max(1, len(tables)))()
+    for j, (var, m, v, indices, grad_rows, mark) in enumerate(tables):
+        n_rows, dim = var.shape
+        arr[j] = SparseTable(_dev(var, torch.float32, "var"), _dev(m, torch.float32, "m"),
+                             _dev(v, torch.float32, "v"), n_rows, dim, indices.numel(),
+                             _dev(indices, torch.int32, "indices"), _dev(grad_rows, torch.float32, "grad_rows"),
+                             _dev(mark, torch.int32, "mark"), None)
+    return arr, len(tables)
+
+
+def adam_sparse_tables_phase(arg, phase, lr=0.0, beta1=0.0, omb1=0.0, beta2=0.0, omb2=0.0, eps=0.0):
+    """One phase of hrec_adam_sparse_tables_phase on the current stream
+    (arg from sparse_tables_arg)."""
+    arr, n = arg
+    _check("hrec_adam_sparse_tables_phase", lib().hrec_adam_sparse_tables_phase(
+        arr, n, int(phase), float(lr), float(beta1), float(omb1), float(beta2), float(omb2), float(eps),
+        _stream()))
 
 
 # --------------------------------------------------------- batched fusion

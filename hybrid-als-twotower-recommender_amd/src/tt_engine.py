@@ -6,9 +6,12 @@ Dense parameters live in ONE flat f32 buffer laid out exactly like the
 gradient block of hrec_tt_forward_backward
     W2[(d+32)*d] | b2[d] | gamma_i[d] | beta_i[d] | gamma_u[d] | beta_u[d] | W1[32] | b1[16]
 so one hrec_adam_dense launch updates them all. Embedding tables get Keras'
-sparse Adam (whole-table slot decay), one hrec_adam_sparse launch each.
+sparse Adam (whole-table slot decay): all four tables in one grouped call,
+or (rows of whole 16-B vectors) its phased form with the sweep of the
+untouched rows on a side stream beside the forward / backward.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -116,6 +119,13 @@ class DeviceTwoTower:
         self.v_tab = {n: torch.zeros_like(self.tensors[n]) for n in TABLES}
         self.mark = {n: torch.full((self.tensors[n].shape[0],), -1, dtype=torch.int32, device=dev) for n in TABLES}
         self._ws = None
+        # two-stream sparse Adam (hrec_adam_sparse_tables_phase) when every
+        # table row is a whole number of 16-B vectors
+        self._phased = (os.environ.get("HREC_TT_PHASED", "1") != "0"
+                        and all(self.tensors[n].shape[1] % 4 == 0 for n in TABLES))
+        if self._phased:
+            self._side = torch.cuda.Stream(device=dev)
+            self._ev_mark, self._ev_sweep = torch.cuda.Event(), torch.cuda.Event()
         self._refresh_params()
 
     def _refresh_params(self):
@@ -142,17 +152,39 @@ class DeviceTwoTower:
         need = int(_hrec.lib().hrec_tt_train_workspace_bytes(self.d, B))
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        gd, gu, gi, gm, gc = _hrec.tt_forward_backward(self.params, user, item, man, cat, numeric, y, self._ws)
         c = self.opt.coefficients(self.iterations)
+        adam = (c["sparse_lr"], self.opt.b1, c["omb1"], self.opt.b2, c["omb2"], self.opt.eps)
+        idxs = (("user_emb", user), ("item_emb", item), ("man_emb", man), ("cat_emb", cat))
+        if self._phased:
+            # Two streams: the whole-table sweep of the rows this batch does
+            # not touch (nearly all of the step's HBM bytes) runs on the side
+            # stream while the forward / backward (which reads only touched
+            # rows) runs here; the touched rows are stepped once their
+            # gradients exist. Same bits as the one-stream grouped call.
+            main = torch.cuda.current_stream(self.device)
+            arg = _hrec.sparse_tables_arg([(self.tensors[n], self.m_tab[n], self.v_tab[n], idx, None, self.mark[n])
+                                           for n, idx in idxs])
+            _hrec.adam_sparse_tables_phase(arg, _hrec.SPARSE_MARK)
+            self._ev_mark.record(main)
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(self._ev_mark)
+                _hrec.adam_sparse_tables_phase(arg, _hrec.SPARSE_SWEEP_UNTOUCHED, *adam)
+                self._ev_sweep.record(self._side)
+        gd, gu, gi, gm, gc = _hrec.tt_forward_backward(self.params, user, item, man, cat, numeric, y, self._ws)
         _hrec.adam_dense(self.dense, self.m_dense, self.v_dense, gd[: self.n_dense], c["dense_alpha"],
                          self.opt.b1, self.opt.b2, self.opt.eps)
-        # the four embedding tables' IndexedSlices updates in one grouped call
-        tabs = [(self.tensors[name], self.m_tab[name], self.v_tab[name], idx, g, self.mark[name],
-                 torch.empty_like(g))
-                for name, idx, g in (("user_emb", user, gu), ("item_emb", item, gi), ("man_emb", man, gm),
-                                     ("cat_emb", cat, gc))]
-        _hrec.adam_sparse_tables(tabs, c["sparse_lr"], self.opt.b1, c["omb1"], self.opt.b2, c["omb2"],
-                                 self.opt.eps)
+        grads = (gu, gi, gm, gc)
+        if self._phased:
+            arg2 = _hrec.sparse_tables_arg([(self.tensors[n], self.m_tab[n], self.v_tab[n], idx, g, self.mark[n])
+                                            for (n, idx), g in zip(idxs, grads)])
+            _hrec.adam_sparse_tables_phase(arg2, _hrec.SPARSE_TOUCHED, *adam)
+            main.wait_event(self._ev_sweep)
+            _hrec.adam_sparse_tables_phase(arg, _hrec.SPARSE_UNMARK)
+        else:
+            # the four embedding tables' IndexedSlices updates in one grouped call
+            tabs = [(self.tensors[n], self.m_tab[n], self.v_tab[n], idx, g, self.mark[n], torch.empty_like(g))
+                    for (n, idx), g in zip(idxs, grads)]
+            _hrec.adam_sparse_tables(tabs, *adam)
         self.iterations += 1
         return gd[self.n_dense:]
 

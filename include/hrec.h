@@ -341,6 +341,23 @@ int hrec_adam_sparse_tables(const hrec_sparse_table* tables, int n_tables, float
                             float beta1, float one_minus_beta1, float beta2,
                             float one_minus_beta2, float epsilon, void* stream);
 
+/* hrec_adam_sparse_tables in phases, for a two-stream train step: the
+ * whole-table sweep of the rows the batch does NOT touch (phase 1, nearly all
+ * of the step's HBM bytes) runs on a second stream beside the batch's
+ * forward / backward, which read only touched rows; phase 2 then sums the
+ * batch's gradients and steps the touched rows. Phases 0..3 in order give
+ * bit for bit the rows of hrec_adam_sparse_tables (same Keras IndexedSlices
+ * Adam, src/two_tower_model.py:111 via model.fit). Phase 1 may overlap phase
+ * 2, never phase 0 or 3. Needs dim % 4 == 0 and 16-B aligned var/m/v; gsum
+ * is not used, grad_rows only by phase 2. */
+#define HREC_SPARSE_MARK 0
+#define HREC_SPARSE_SWEEP_UNTOUCHED 1
+#define HREC_SPARSE_TOUCHED 2
+#define HREC_SPARSE_UNMARK 3
+int hrec_adam_sparse_tables_phase(const hrec_sparse_table* tables, int n_tables, int phase,
+                                  float lr, float beta1, float one_minus_beta1, float beta2,
+                                  float one_minus_beta2, float epsilon, void* stream);
+
 /* ---------------------------------------------------------------------
  * Matrix-core dot-product scoring + fused top-k (csrc/dot_topk.hip).
  * Replaces Keras Dot(axes=1) over every candidate in model.predict

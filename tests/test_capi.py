@@ -53,6 +53,14 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert f(None, 9, *args) == -1
     assert b"tables" in lib.hrec_last_error()
     assert f(None, 0, *args) == 0  # nothing to update
+    # phased sparse Adam: phase range and table count before any device work
+    fp = lib.hrec_adam_sparse_tables_phase
+    fp.restype = ctypes.c_int
+    assert fp(None, 1, 4, *args) == -1
+    assert b"phase 4 not in 0..3" in lib.hrec_last_error()
+    assert fp(None, 9, 0, *args) == -1
+    assert b"tables" in lib.hrec_last_error()
+    assert fp(None, 0, 1, *args) == 0
     # f64-source half-sweep: kp 64 only
     h = lib.hrec_als_half_sweep_src64
     h.restype = ctypes.c_int

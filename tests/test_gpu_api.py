@@ -383,6 +383,91 @@ def test_sparse_adam_grouped_matches_per_table(device):
             assert torch.equal(a_[j], b_[j])
 
 
+def test_sparse_adam_phased_matches_grouped(device):
+    """hrec_adam_sparse_tables_phase 0..3 (the untouched-rows sweep on a side
+    stream, overlapping the touched-rows phase) == hrec_adam_sparse_tables,
+    bit for bit, incl. duplicate indices, an empty batch and a row-less table."""
+    from src import _hrec as h
+
+    rng = np.random.default_rng(22)
+    shapes = [(1000, 64, 256), (300, 64, 256), (40, 8, 256), (7, 8, 0), (0, 8, 0)]
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    runs = [[], []]
+    for n_rows, dim, B in shapes:
+        var = rng.normal(size=(n_rows, dim)).astype(np.float32)
+        m = rng.normal(size=(n_rows, dim)).astype(np.float32)
+        v = rng.uniform(0, 1, size=(n_rows, dim)).astype(np.float32)
+        idx = rng.integers(0, max(n_rows, 1), B).astype(np.int32)
+        g = rng.normal(size=(B, dim)).astype(np.float32)
+        for run in runs:
+            run.append((T(var), T(m), T(v), T(idx), T(g), T(np.full(n_rows, -1, np.int32)),
+                        torch.empty((B, dim), dtype=torch.float32, device=device)))
+    coef = (1e-3, 0.9, 0.1, 0.999, 1e-3, 1e-7)
+    h.adam_sparse_tables(runs[0], *coef)
+    arg = h.sparse_tables_arg([t[:4] + (None, t[5]) for t in runs[1]])
+    h.adam_sparse_tables_phase(arg, h.SPARSE_MARK)
+    side = torch.cuda.Stream(device=device)
+    ev = torch.cuda.Event()
+    ev.record()
+    with torch.cuda.stream(side):
+        side.wait_event(ev)
+        h.adam_sparse_tables_phase(arg, h.SPARSE_SWEEP_UNTOUCHED, *coef)
+        done = torch.cuda.Event()
+        done.record(side)
+    arg2 = h.sparse_tables_arg([t[:6] for t in runs[1]])
+    h.adam_sparse_tables_phase(arg2, h.SPARSE_TOUCHED, *coef)
+    torch.cuda.current_stream().wait_event(done)
+    h.adam_sparse_tables_phase(arg, h.SPARSE_UNMARK)
+    torch.cuda.synchronize()
+    for a_, b_ in zip(runs[0], runs[1]):
+        for j in (0, 1, 2, 5):  # var, m, v, mark
+            assert torch.equal(a_[j], b_[j])
+
+
+def test_sparse_adam_phase_argument_checks(device):
+    from src import _hrec as h
+
+    T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
+    tab = (T(np.zeros((10, 6), np.float32)), T(np.zeros((10, 6), np.float32)), T(np.zeros((10, 6), np.float32)),
+           T(np.zeros(4, np.int32)), None, T(np.full(10, -1, np.int32)))
+    with pytest.raises(h.HrecError, match="dim % 4"):
+        h.adam_sparse_tables_phase(h.sparse_tables_arg([tab]), h.SPARSE_MARK)
+    with pytest.raises(h.HrecError, match="phase"):
+        h.adam_sparse_tables_phase(h.sparse_tables_arg([]), 7)
+
+
+def test_tt_engine_two_stream_step_matches_one_stream(device, monkeypatch):
+    """TTEngine.train_step with the phased two-stream sparse Adam == the
+    grouped one-stream call: every parameter and slot bit-identical after
+    several steps with repeated ids in the batches."""
+    from src import tt_engine
+
+    rng = np.random.default_rng(23)
+    engines = []
+    for phased in ("1", "0"):
+        monkeypatch.setenv("HREC_TT_PHASED", phased)
+        e = tt_engine.DeviceTwoTower(500, 300, 20, 12, 64, 1e-3, seed=5, device=device)
+        assert e._phased == (phased == "1")
+        engines.append(e)
+    B = 128
+    for step in range(4):
+        u = torch.as_tensor(rng.integers(0, 60, B).astype(np.int32), device=device)
+        i = torch.as_tensor(rng.integers(0, 300, B).astype(np.int32), device=device)
+        mn = torch.as_tensor(rng.integers(0, 20, B).astype(np.int32), device=device)
+        ct = torch.as_tensor(rng.integers(0, 12, B).astype(np.int32), device=device)
+        x = torch.as_tensor(rng.uniform(0, 1, (B, 2)).astype(np.float32), device=device)
+        y = torch.as_tensor(rng.integers(0, 19, B).astype(np.float32), device=device)
+        for e in engines:
+            e.train_step(u, i, mn, ct, x, y)
+    torch.cuda.synchronize()
+    a, b = engines
+    assert torch.equal(a.dense, b.dense) and torch.equal(a.m_dense, b.m_dense)
+    for n in tt_engine.TABLES:
+        assert torch.equal(a.tensors[n], b.tensors[n]), n
+        assert torch.equal(a.m_tab[n], b.m_tab[n]) and torch.equal(a.v_tab[n], b.v_tab[n]), n
+        assert (a.mark[n] == -1).all()
+
+
 def _tt_frame(rng, n, nu, ni, nm, nc):
     return pd.DataFrame({
         "userId": rng.integers(0, nu, n), "itemId": rng.integers(0, ni, n),
