@@ -724,7 +724,9 @@ def main():
         tt_train = {"samples_per_s": Bt / tts, "ms_per_step": tts * 1e3, "batch": Bt, "d": dtt,
                     "tables": {"users": n_users, "items": n_items, "manufacturers": n_man, "categories": n_cat},
                     "steps": args.tt_steps,
-                    "step": "hrec_tt_forward_backward + hrec_adam_dense + hrec_adam_sparse_tables (4 tables, Keras-exact)",
+                    "step": ("hrec_tt_forward_backward + hrec_adam_dense + Keras-exact sparse Adam on 4 tables "
+                             + ("(hrec_adam_sparse_tables_phase: untouched-rows sweep on a side stream beside the "
+                                "forward / backward)" if tt._phased else "(hrec_adam_sparse_tables, one stream)")),
                     "roofline": {"bound": "hbm", "achieved": step_bytes / dev_s / 1e9, "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": step_bytes / dev_s / 1e9 / HBM_PEAK_GBS,
                                  "algorithmic_bytes_per_step": step_bytes}}
@@ -763,7 +765,7 @@ def main():
     if tt_train is not None:
         tt_train["roofline"]["traffic"] = tsw.get("hbm_bytes_avg_per_launch_corrected") if tsw else None
         tt_train["roofline"]["traffic_note"] = (
-            "HBM bytes per launch of the grouped whole-table Adam sweep (adam_sparse_group4_kernel, rocprofv3 "
+            "HBM bytes per launch of the whole-table Adam sweep (adam_sparse_group4_kernel, rocprofv3 "
             "FETCH_SIZE x2 + WRITE_SIZE, scripts/gpu_profile.sh; null when the profile predates csrc/tt.hip); "
             "achieved above is the whole step's")
 
