@@ -255,9 +255,25 @@ def api_line(eng, n_users, n_items, k, reps):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps * 1e3
 
+    class Candidates:
+        """all_items that both models score: iterates as item ids (ALS side),
+        indexes as the frame (two-tower side)."""
+
+        def __iter__(self):
+            return iter(ids)
+
+        def __len__(self):
+            return len(items)
+
+        def __getitem__(self, key):
+            return items[key]
+
+    both = Candidates()
     parts = {}
     with contextlib.redirect_stdout(sink):
         ref_ms = timed(lambda u: h.get_hybrid_recommendations(u, items, top_k=5))
+        both_ms = timed(lambda u: h.get_hybrid_recommendations(u, both, top_k=5))
+        top_api = h.get_hybrid_recommendations(uids[0], both, top_k=5)
         parts["als.predict_for_user (id list)"] = timed(lambda u: als.predict_for_user(u, ids))
         parts["twotower.predict_for_user (item frame)"] = timed(lambda u: tt.predict_for_user(u, items))
         a, t = als.predict_for_user(uids[0], ids), tt.predict_for_user(uids[0], items)
@@ -271,12 +287,17 @@ def api_line(eng, n_users, n_items, k, reps):
         parts["_union + fuse_device top-5"] = timed(fuse)
         top = fuse(0)
     work = sum(parts.values())
-    return {"users_per_s": 1e3 / work, "pairs_per_s": n_items * 1e3 / work, "working_call_ms": work,
-            "reference_call_ms": ref_ms, "parts_ms": parts, "items": n_items, "top_k": 5, "reps": reps,
-            "top5_nonempty": len(top) == 5,
-            "note": ("one user per call (the reference API); reference_call = get_hybrid_recommendations(uid, "
-                     "item_frame) as the reference wires it (ALS side -> [] by SURVEY D9); working_call = ALS "
-                     "on an id list + two-tower on the frame + the call's own fusion/top-5")}
+    return {"users_per_s": 1e3 / both_ms, "pairs_per_s": n_items * 1e3 / both_ms, "api_call_ms": both_ms,
+            "reference_call_ms": ref_ms, "list_path_ms": work, "list_parts_ms": parts, "items": n_items,
+            "top_k": 5, "reps": reps, "top5_nonempty": len(top_api) == 5,
+            "api_top5_equals_list_path": [i for i, _ in top_api] == [i for i, _ in top],
+            "note": ("one user per call (the reference API, src/hybrid_system.py:95-116); api_call = "
+                     "get_hybrid_recommendations(uid, candidates) with candidates both models score (ids for "
+                     "ALS, the frame for the two-tower side); reference_call = get_hybrid_recommendations(uid, "
+                     "item_frame) as the reference wires it (ALS side -> [] by SURVEY D9). Both run the array "
+                     "path (device scores -> device fusion + top-6 -> tie check), no per-item Python objects; "
+                     "list_path = the per-model predict_for_user lists + _union + fuse_device the call used "
+                     "before (still taken on ties / duplicate ids / cold-start rows)")}
 
 
 def WANT_CPU(args, rank, world):
@@ -565,10 +586,10 @@ def main():
     # tables). The reference hands the same `all_items` object to both models
     # (src/hybrid_system.py:100-101): with the item DataFrame the ALS side
     # fails as the reference's does -> "reference_call"; the
-    # "working_call" feeds ALS an id list and the two-tower side the frame,
-    # then _union + device fusion + stable top-5 — what the call does once
-    # both models answer. Host-side Python (dicts / sets over 100k items)
-    # dominates; the device kernels are in the lines above.
+    # "api_call" hands both models candidates they can score (ids for ALS,
+    # the frame for the two-tower side). Both take the array path (device
+    # scores -> device fusion + top-6 -> tie check); "list_path" times the
+    # per-model predict_for_user lists + _union + fuse_device it replaces.
     api = None
     if rank == 0 and world == 1 and args.api_reps > 0:
         api = api_line(eng, n_users, n_items, k, args.api_reps)

@@ -236,23 +236,51 @@ class ALSModel:
             if not ok(type(x)):
                 raise TypeError(f"field itemId: IntegerType() can not accept object {x!r} in type {type(x)}")
 
-    def predict_for_user(self, user_id, all_items):
+    def _score_device(self, user_id, all_items):
+        """predict_for_user up to the transform: (items, int64 keys, f32 device
+        scores [n] or None). Raises where the reference's createDataFrame /
+        transform would."""
+        items = list(all_items)
+        self._check_int_ids([user_id])
+        self._check_int_ids(items)
+        if not items:
+            return items, None, None
+        keys = np.fromiter(items, np.int64, len(items))
+        return items, keys, self.model.score([user_id], keys)[0]
+
+    def _predict_device(self, user_id, all_items):
+        """For HybridRecommendationSystem's array path: (items, keys, f32
+        device scores) when every score is a transform output (no cold-start
+        row), else the predict_for_user list itself (same prints, same [])."""
         try:
-            items = list(all_items)
-            self._check_int_ids([user_id])
-            self._check_int_ids(items)
-            scores = self.model.score([user_id], items)[0].cpu().numpy() if items else np.zeros(0, np.float32)
-            out = list(zip(items, scores.tolist()))  # (item, float(prediction)) as :84
-            missing = np.flatnonzero(np.isnan(scores)).tolist()
-            if missing:  # cold-start fallback (:78-86): mean rating of <= 3 similar items, else the global mean
-                sims = self._similar_batch([items[n] for n in missing])
-                for n, sim in zip(missing, sims):
-                    out[n] = (items[n], np.mean([self.item_features[s]["rating"] for s in sim]) if sim
-                              else self.global_mean)
-            return out
+            items, keys, scores = self._score_device(user_id, all_items)
+            if scores is not None and not bool(torch.isnan(scores).any()):
+                return items, keys, scores
+            return self._predictions(items, scores)
         except Exception as e:
             print(f"Prediction error: {str(e)}")
             return []
+
+    def predict_for_user(self, user_id, all_items):
+        try:
+            items, _, scores = self._score_device(user_id, all_items)
+            return self._predictions(items, scores)
+        except Exception as e:
+            print(f"Prediction error: {str(e)}")
+            return []
+
+    def _predictions(self, items, scores):
+        """The (item, prediction) list of :84 with the cold-start fallback
+        (:78-86) for rows the transform left NaN."""
+        scores = scores.cpu().numpy() if scores is not None else np.zeros(0, np.float32)
+        out = list(zip(items, scores.tolist()))  # (item, float(prediction)) as :84
+        missing = np.flatnonzero(np.isnan(scores)).tolist()
+        if missing:  # cold-start fallback (:78-86): mean rating of <= 3 similar items, else the global mean
+            sims = self._similar_batch([items[n] for n in missing])
+            for n, sim in zip(missing, sims):
+                out[n] = (items[n], np.mean([self.item_features[s]["rating"] for s in sim]) if sim
+                          else self.global_mean)
+        return out
 
     def _feature_matrix(self):
         if self._feat_cache is None:

@@ -78,6 +78,12 @@ def fuse_device(als_scores, tt_scores, als_wins, top_k, device=None, want_fused=
     return fused_np, idx.cpu().numpy(), sc.cpu().numpy()
 
 
+def _scored(model, cls, user_id, all_items):
+    if type(model).predict_for_user is cls.predict_for_user:
+        return model._predict_device(user_id, all_items)
+    return model.predict_for_user(user_id, all_items)
+
+
 class HybridRecommendationSystem:
     def __init__(self):
         self.als_model = None
@@ -155,10 +161,24 @@ class HybridRecommendationSystem:
         if not self.models_loaded:
             raise ValueError("Models not loaded. Call load_models() first.")
         try:
-            als_preds = self.als_model.predict_for_user(user_id, all_items)
-            tt_preds = self.twotower_model.predict_for_user(user_id, all_items)
+            # the drop-in models hand over device scores (the lists are built
+            # below only if the list path runs); other model objects are used
+            # through their predict_for_user as the reference does
+            als_preds = _scored(self.als_model, ALSModel, user_id, all_items)
+            tt_preds = _scored(self.twotower_model, TwoTowerModel, user_id, all_items)
             if actual_ratings:
                 self.evaluate_individual_models(user_id, actual_ratings, all_items)
+            if not save_predictions:
+                try:
+                    top = self._top_on_device(als_preds, tt_preds, top_k)
+                except Exception:  # the list path below meets the same error and reports it as the reference does
+                    top = None
+                if top is not None:
+                    return top
+            if isinstance(als_preds, tuple):  # the lists predict_for_user returns (:101-102)
+                als_preds = self.als_model._predictions(als_preds[0], als_preds[2])
+            if isinstance(tt_preds, tuple):
+                tt_preds = self.twotower_model._predictions(*tt_preds)
             try:
                 items, als_scores, tt_scores = self._union(als_preds, tt_preds)
                 fused, idx, sc = fuse_device(als_scores, tt_scores, self.als_f1_score > self.twotower_f1_score,
@@ -175,6 +195,50 @@ class HybridRecommendationSystem:
         except Exception as e:
             print(f"Error generating recommendations: {str(e)}")
             return []
+
+    def _top_on_device(self, als_side, tt_side, top_k):
+        """get_hybrid_recommendations without the Python lists: when both
+        sides cover the same unique candidate ids (or the ALS side is empty,
+        the reference's DataFrame wiring, SURVEY D9) the union is those ids;
+        the fusion runs on the device scores and the top_k + 1 fused scores
+        come back. If they are finite and strictly decreasing, the stable
+        top_k is the same whatever order the reference's set(...) union put
+        the items in, so it is returned; otherwise (ties, NaN/inf scores,
+        duplicate or mismatched ids) None sends the call down the list path,
+        which reproduces the set order exactly. The scalers are fitted as
+        fit_transform leaves them either way (min/max are order-free)."""
+        if not isinstance(tt_side, tuple) or not isinstance(top_k, (int, np.integer)) or top_k < 0:
+            return None
+        frame, t = tt_side
+        col = frame["itemId"]
+        vals = col.values
+        if not isinstance(vals, np.ndarray) or vals.dtype.kind not in "iu" or not col.is_unique:
+            return None
+        n = t.numel()
+        if isinstance(als_side, tuple):
+            items, keys, a = als_side
+            if keys.shape != vals.shape or not np.array_equal(keys, vals):
+                return None
+            a = a.double()
+            def item(i): return items[i]      # the union keeps the ALS side's key objects
+        elif not als_side:
+            a = torch.zeros(n, dtype=torch.float64, device=t.device)
+            def item(i): return vals.item(i)  # iterating the Series yields .item() scalars
+        else:
+            return None
+        k = min(int(top_k), n)
+        k1 = min(k + 1, n)
+        mm = torch.empty(4, dtype=torch.float64, device=t.device)
+        idx, sc, _ = _hrec.fuse_topk(a, t, self.als_f1_score > self.twotower_f1_score, k1, want_fused=False,
+                                     minmax=mm)
+        bad = (~torch.isfinite(a).all() | ~torch.isfinite(t).all()).double().view(1)
+        host = torch.cat([sc, idx.double(), mm, bad]).cpu().numpy()
+        sc_h, idx_h, m = host[:k1], host[k1:2 * k1].astype(np.int64), host[2 * k1: 2 * k1 + 4]
+        if host[-1] != 0 or not np.all(sc_h[:-1] > sc_h[1:]):
+            return None
+        _set_fitted(self.als_scaler, m[0], m[1], n, np.float64)
+        _set_fitted(self.twotower_scaler, m[2], m[3], n, np.float32)
+        return [(item(int(i)), np.float64(s)) for i, s in zip(idx_h[:k], sc_h[:k])]
 
     def cleanup(self):
         if self.als_model:

@@ -153,6 +153,26 @@ class TwoTowerModel:
     # ------------------------------------------------------------- predict
     def predict_for_user(self, user_id, item_features):
         """Generate predictions for one user over candidate rows (:136-146)."""
+        scored = self._predict_device(user_id, item_features)
+        return self._predictions(*scored) if scored else []
+
+    def _score_device(self, inputs):
+        """model.predict on the assembled inputs: f32 device scores [n]."""
+        dev_in = self._device_inputs(inputs)
+        u = dev_in[0][:1]
+        uvec = self.model.user_vectors(u)
+        ivec = self.model.item_vectors(*dev_in[1:])
+        return _hrec.tt_score(uvec, ivec).reshape(-1)
+
+    @staticmethod
+    def _predictions(item_features, scores):
+        predictions = scores.cpu().numpy().reshape(-1, 1)
+        return list(zip(item_features["itemId"], predictions.flatten()))
+
+    def _predict_device(self, user_id, item_features):
+        """For HybridRecommendationSystem's array path: predict_for_user up to
+        the device scores, (item_features, f32 device scores [n]); [] for an
+        empty frame. Raises where predict_for_user raises."""
         inputs = {
             "user_in": np.full(len(item_features), user_id),
             "item_id_in": item_features["itemId"].values,
@@ -162,12 +182,7 @@ class TwoTowerModel:
         }
         if len(item_features) == 0:
             return []
-        dev_in = self._device_inputs(inputs)
-        u = dev_in[0][:1]
-        uvec = self.model.user_vectors(u)
-        ivec = self.model.item_vectors(*dev_in[1:])
-        predictions = _hrec.tt_score(uvec, ivec).cpu().numpy().reshape(-1, 1)
-        return list(zip(item_features["itemId"], predictions.flatten()))
+        return item_features, self._score_device(inputs)
 
     # --------------------------------------------------------- persistence
     def save_model(self, model_path="models/twotower.keras"):

@@ -658,6 +658,101 @@ def test_hybrid_end_to_end(device, tmp_path):
                                             ofus.adaptive_fusion(a, t, h.als_f1_score, h.twotower_f1_score)]
 
 
+class _IdsFrame:
+    """Candidates that iterate as item ids (the ALS side scores them) and
+    index as a frame (the two-tower side), so one all_items object feeds
+    both models with scores."""
+
+    def __init__(self, df):
+        self.df = df
+
+    def __iter__(self):
+        return iter(self.df["itemId"].tolist())
+
+    def __len__(self):
+        return len(self.df)
+
+    def __getitem__(self, key):
+        return self.df[key]
+
+
+def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
+    """get_hybrid_recommendations' array path (_top_on_device: fusion on the
+    device scores, no Python lists) returns exactly what the list path
+    (predict_for_user lists + _union + fuse_device) returns, and leaves the
+    scalers fitted the same: frame wiring (ALS -> []), ids on both sides,
+    cold-start rows (NaN -> fallback), duplicate ids, ties, top_k >= n and
+    top_k = 0, both F1 orders."""
+    from src.als_model import ALSModel
+    from src.hybrid_system import HybridRecommendationSystem
+    from src.two_tower_model import TwoTowerModel
+
+    rng = np.random.default_rng(21)
+    df = _tt_frame(rng, 900, 60, 40, 5, 4)
+    als = ALSModel(rank=8, max_iter=3, seed=2)
+    assert als.train(df)
+    tt = TwoTowerModel(60, 40, 5, 4, embedding_size=16)
+    tt.train(df, batch_size=128, epochs=1)
+    items = df[["itemId", "manufacturer_id", "category_id", "price", "average_review_rating"]].drop_duplicates(
+        "itemId").reset_index(drop=True)
+    dup = pd.concat([items, items.head(7)], ignore_index=True)
+    # tied two-tower scores: identical feature rows under a zero item table
+    tie = items.copy()
+    tie[["manufacturer_id", "category_id", "price", "average_review_rating"]] = tie.iloc[0][
+        ["manufacturer_id", "category_id", "price", "average_review_rating"]].values
+    # cold-start rows: ids inside the two-tower table that ALS never saw
+    als_half = ALSModel(rank=8, max_iter=2, seed=3)
+    assert als_half.train(df.head(60))
+    assert len(set(items["itemId"]) - set(df["itemId"].head(60))) > 0
+    cases = [("frame", items), ("ids", _IdsFrame(items)), ("dup", _IdsFrame(dup)), ("frame_dup", dup)]
+    calls = {"fast": 0}
+    orig = HybridRecommendationSystem._top_on_device
+
+    def counting(self, *a):
+        r = orig(self, *a)
+        calls["fast"] += r is not None
+        return r
+
+    def run(cand, uid, k, f1, list_path):
+        h = HybridRecommendationSystem()
+        h.als_model, h.twotower_model, h.models_loaded = als, tt, True
+        h.als_f1_score, h.twotower_f1_score = f1
+        with monkeypatch.context() as m:
+            m.setattr(HybridRecommendationSystem, "_top_on_device",
+                      (lambda self, *a: None) if list_path else counting)
+            top = h.get_hybrid_recommendations(uid, cand, top_k=k)
+        return top, h
+
+    saved = tt.model.tensors["item_emb"].clone()
+    try:
+        for name, cand in cases + [("cold", _IdsFrame(items)), ("tie", tie)]:
+            if name == "cold":
+                als_model = als
+                als = als_half  # items holds ids this model never saw -> NaN -> fallback rows
+            if name == "tie":
+                als = als_model
+                tt.model.tensors["item_emb"].zero_()
+            for uid in (3, 17):
+                for k in (0, 5, 50, 1000):
+                    for f1 in ((0.5, 0.1), (0.1, 0.5)):
+                        a, ha = run(cand, uid, k, f1, False)
+                        b, hb = run(cand, uid, k, f1, True)
+                        assert a == b, (name, uid, k, f1)
+                        assert [type(i) for i, _ in a] == [type(i) for i, _ in b]
+                        assert all(type(s) is np.float64 for _, s in a)
+                        for x, y in ((ha.als_scaler, hb.als_scaler), (ha.twotower_scaler, hb.twotower_scaler)):
+                            assert hasattr(x, "scale_") == hasattr(y, "scale_") and hasattr(x, "scale_")
+                            for attr in ("data_min_", "data_max_", "data_range_", "scale_", "min_"):
+                                assert getattr(x, attr).dtype == getattr(y, attr).dtype
+                                assert np.array_equal(getattr(x, attr), getattr(y, attr)), (name, attr)
+                            assert x.n_samples_seen_ == y.n_samples_seen_
+    finally:
+        tt.model.tensors["item_emb"].copy_(saved)
+    # the array path served the unique-id cases; the tie case fell back
+    assert calls["fast"] > 0
+    capsys.readouterr()
+
+
 def test_batched_hybrid_matches_per_user_fusion(device):
     """ShardedRecommender (1 GPU) == the reference's per-user fusion + top-k
     over the same ALS (JVM-exact) and two-tower scores, bit for bit."""
