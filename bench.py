@@ -326,7 +326,7 @@ def main():
                     help="users of the scoring batch timed by the C JVM-exact scoring baseline")
     ap.add_argument("--rank256-epochs", type=int, default=1,
                     help="timed rank-256 ALS epochs on the same matrix (BASELINE c5's ALS half; 0 = skip)")
-    ap.add_argument("--api-reps", type=int, default=5,
+    ap.add_argument("--api-reps", type=int, default=20,
                     help="users timed through HybridRecommendationSystem.get_hybrid_recommendations (0 = skip)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="W > 1: user-side ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")

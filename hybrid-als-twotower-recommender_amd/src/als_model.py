@@ -54,6 +54,7 @@ class DeviceALSFactors:
         self.V = V                               # [n_items, kp] f32 device
         self.k = int(k)
         self.Vt = _hrec.transpose(V) if V.shape[0] else V.t().contiguous()
+        self._item_ids_dev = None
 
     @staticmethod
     def _lookup(ids, keys):
@@ -65,11 +66,27 @@ class DeviceALSFactors:
         ok = ids[pos] == keys
         return np.where(ok, pos, -1).astype(np.int64)
 
+    def _lookup_device(self, keys):
+        """_lookup for long candidate lists: the same binary search on the
+        device over a cached copy of the sorted item ids."""
+        dev = self.U.device
+        if self._item_ids_dev is None:
+            self._item_ids_dev = torch.as_tensor(np.asarray(self.item_ids, np.int64), device=dev)
+        ids = self._item_ids_dev
+        k = torch.as_tensor(keys, device=dev)
+        if ids.numel() == 0:
+            return torch.full_like(k, -1)
+        pos = torch.searchsorted(ids, k).clamp_(max=ids.numel() - 1)
+        return torch.where(ids[pos] == k, pos, torch.full_like(pos, -1))
+
     def score(self, user_ids, item_list):
         """f32 [len(user_ids), len(item_list)]; NaN where either id is unknown."""
         dev = self.U.device
         urows = torch.as_tensor(self._lookup(self.user_ids, user_ids), device=dev)
-        irows = torch.as_tensor(self._lookup(self.item_ids, item_list), device=dev)
+        if isinstance(item_list, np.ndarray) and item_list.dtype == np.int64 and item_list.size > 4096:
+            irows = self._lookup_device(item_list)
+        else:
+            irows = torch.as_tensor(self._lookup(self.item_ids, item_list), device=dev)
         return _hrec.als_score(self.U, urows, self.Vt, irows, irows.numel(), self.k)
 
     # Spark 3.5 ALSModel directory layout (MLWriter): metadata/part-00000 is

@@ -78,6 +78,17 @@ def fuse_device(als_scores, tt_scores, als_wins, top_k, device=None, want_fused=
     return fused_np, idx.cpu().numpy(), sc.cpu().numpy()
 
 
+def _unique(vals, col):
+    """No repeated id: a bincount when the ids are small non-negative ints
+    (catalogue ids), else pandas' hash check."""
+    if vals.size == 0:
+        return True
+    lo, hi = int(vals.min()), int(vals.max())
+    if lo >= 0 and hi < 4 * vals.size + 4096:
+        return int(np.bincount(vals.astype(np.int64, copy=False)).max()) <= 1
+    return bool(col.is_unique)
+
+
 def _scored(model, cls, user_id, all_items):
     if type(model).predict_for_user is cls.predict_for_user:
         return model._predict_device(user_id, all_items)
@@ -212,7 +223,7 @@ class HybridRecommendationSystem:
         frame, t = tt_side
         col = frame["itemId"]
         vals = col.values
-        if not isinstance(vals, np.ndarray) or vals.dtype.kind not in "iu" or not col.is_unique:
+        if not isinstance(vals, np.ndarray) or vals.dtype.kind not in "iu" or not _unique(vals, col):
             return None
         n = t.numel()
         if isinstance(als_side, tuple):

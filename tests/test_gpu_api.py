@@ -924,3 +924,22 @@ def test_fuse_rows_topk_filter_matches_reference(device, n, kk, pattern):
         ei, ev = _fuse_rows_reference(a[list(rows)], t[list(rows)], wins, kk)
         np.testing.assert_array_equal(gi.cpu().numpy()[list(rows)], ei + 11)
         np.testing.assert_array_equal(gv.cpu().numpy()[list(rows)], ev)
+
+
+def test_als_device_lookup_matches_host(device):
+    """DeviceALSFactors.score's device id lookup (long candidate lists) ==
+    the host binary search: same rows, -1 (-> NaN score) for unknown ids."""
+    from src.als_model import DeviceALSFactors
+
+    rng = np.random.default_rng(8)
+    ids = np.unique(rng.integers(-50, 30000, 9000))
+    U = torch.randn(4, 16, device=device)
+    V = torch.randn(len(ids), 16, device=device)
+    f = DeviceALSFactors(np.arange(4), ids, U, V, 10)
+    keys = np.concatenate([rng.choice(ids, 6000), rng.integers(-100, 31000, 3000), [ids[0], ids[-1]]])
+    host = DeviceALSFactors._lookup(f.item_ids, keys)
+    assert (host == -1).any() and (host >= 0).any()
+    assert np.array_equal(f._lookup_device(keys.astype(np.int64)).cpu().numpy(), host)
+    a = f.score([1], keys.astype(np.int64)).cpu().numpy()
+    b = f.score([1], keys.tolist()).cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)])
