@@ -20,6 +20,7 @@ import os
 import pickle
 
 import numpy as np
+import pandas as pd
 import torch
 from sklearn.model_selection import train_test_split  # noqa: F401  (reference import surface)
 from sklearn.preprocessing import MinMaxScaler
@@ -189,7 +190,11 @@ class TwoTowerModel:
     @staticmethod
     def _predictions(item_features, scores):
         predictions = scores.cpu().numpy().reshape(-1, 1)
-        return list(zip(item_features["itemId"], predictions.flatten()))
+        col = item_features["itemId"]
+        # iterating a numpy-backed Series yields values.item(i), which is
+        # what ndarray.tolist() builds in one call (same objects and types)
+        keys = col.to_numpy().tolist() if isinstance(col.array, pd.arrays.NumpyExtensionArray) else col
+        return list(zip(keys, predictions.flatten()))
 
     def _predict_device(self, user_id, item_features):
         """For HybridRecommendationSystem's array path: predict_for_user up to
