@@ -168,7 +168,7 @@ def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
     return dict(dom, stages=out)
 
 
-def cpu_baseline(eng, cfg, n_user_rows, n_item_rows):
+def cpu_baseline(eng, cfg, n_user_rows, n_item_rows, k=None):
     """C oracle on a bounded sample of the same matrix (rank 0, N=1)."""
     import numpy as np
 
@@ -177,7 +177,7 @@ def cpu_baseline(eng, cfg, n_user_rows, n_item_rows):
     from oracle.cpu_baseline import cpu_model
 
     obuild.build()
-    k = cfg["rank"]
+    k = cfg["rank"] if k is None else int(k)
 
     def sample(csr, rows):
         ip = csr.indptr[: rows + 1].cpu().numpy()
@@ -198,7 +198,7 @@ def cpu_baseline(eng, cfg, n_user_rows, n_item_rows):
         "value": 1.0 / epoch_s, "unit": "epochs/s", "cores": int(obuild.load().oracle_max_threads()),
         "kind": "port", "cpu_model": cpu_model(),
         "sample": (f"C oracle (Spark 3.5.1 ALS restated: f64 dspr Gramian + dpptrf/dpptrs, OpenMP) on "
-                   f"{n_item_rows} item rows + {n_user_rows} user rows of the same c2 matrix, "
+                   f"{n_item_rows} item rows + {n_user_rows} user rows of the same c2 matrix at rank {k}, "
                    f"{t_item + t_user:.1f} s measured, extrapolated to one full epoch"),
     }
 
@@ -577,6 +577,10 @@ def main():
                   "epochs": args.rank256_epochs, "kernel_ms_per_epoch": {"item": it_ms, "user": ut_ms},
                   "roofline": roofline("mfma", fl256 / 2, (it_ms + ut_ms) / 2, F64_MFMA_PEAK_TFLOPS, "TFLOP/s",
                                        "als_half_sweep_wide_kernel (item + user launches)")}
+        if WANT_CPU(args, rank, world):
+            # ~16x the per-rating Gramian work of rank 64: a 16x smaller row sample
+            als256["cpu_baseline"] = cpu_baseline(e256, cfg, max(args.cpu_user_rows // 16, 1),
+                                                  max(args.cpu_item_rows // 16, 1), k=k256)
         del e256
         torch.cuda.empty_cache()
 
@@ -621,7 +625,32 @@ def main():
         ingest = {"ratings_per_s": csr.nnz / gs, "ms": gs * 1e3, "ratings": csr.nnz,
                   "steps": ("encode user ids + encode item ids (radix sort on the id range + scan) + CSR + CSC "
                             "(stable radix sort)"),
-                  "csr_matches_generator": ok}
+                  "csr_matches_generator": ok,
+                  # algorithmic bytes per rating: read user id, item id (int64) + rating (f32) = 20 B; write
+                  # both id codes (2 x int32) + CSR and CSC column/value arrays (2 x (int32 + f32)) = 24 B
+                  "roofline": roofline("hbm", 44.0 * csr.nnz, gs * 1e3, HBM_PEAK_GBS, "GB/s",
+                                       "ingest (4 launches' sequence: encode_ids x2 + coo_to_csr x2, wall clock)",
+                                       note=("several radix-sort passes per step: the bytes moved are a multiple "
+                                             "of the algorithmic 44 B per rating"))}
+        if WANT_CPU(args, rank, world):
+            import numpy as np
+
+            from oracle.cpu_baseline import cpu_model
+
+            S = min(int(csr.nnz), 20_000_000)
+            hu, hi, hv = uid[:S].cpu().numpy(), iid[:S].cpu().numpy(), vals[:S].cpu().numpy()
+            c0 = time.perf_counter()
+            _, hur = np.unique(hu, return_inverse=True)
+            ius, hir = np.unique(hi, return_inverse=True)
+            o1 = np.argsort(hur, kind="stable")
+            o2 = np.argsort(hir, kind="stable")
+            _ = (hir[o1], hv[o1], hur[o2], hv[o2], np.bincount(hur), np.bincount(hir))
+            cs = time.perf_counter() - c0
+            ingest["cpu_baseline"] = {
+                "value": S / cs, "unit": "ratings/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+                "sample": (f"numpy (the reference's ALSModel.train path is a Spark DataFrame; restated as "
+                           f"np.unique(return_inverse) x2 + stable argsort CSR/CSC) on the first {S} of the "
+                           f"{csr.nnz} ratings, {cs:.1f} s")}
         del uid, iid, out
         torch.cuda.empty_cache()
 
