@@ -57,6 +57,38 @@ __global__ __launch_bounds__(256) void scatter_codes_kernel(const K* __restrict_
   }
 }
 
+// Dense id ranges (span <= n): np.unique(return_inverse) without a sort.
+// Mark the ids present in a span-long table, one inclusive scan gives every
+// present id its rank among the sorted distinct ids, and the codes are read
+// back from the table: two streaming passes over the ids instead of a radix
+// sort of (id, position) pairs. Same codes and uniq as the sort path.
+__global__ __launch_bounds__(256) void mark_present_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
+                                                           int64_t span, int32_t* __restrict__ present) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = ids[i] - lo;
+    if (v >= 0 && v < span) present[v] = 1;  // every writer stores the same value
+  }
+}
+
+__global__ __launch_bounds__(256) void codes_from_rank_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
+                                                              int64_t span, const int32_t* __restrict__ incl,
+                                                              int32_t* __restrict__ codes) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = ids[i] - lo;
+    codes[i] = (v >= 0 && v < span) ? incl[v] - 1 : -1;  // out-of-range ids (a caller error) -> -1
+  }
+}
+
+__global__ __launch_bounds__(256) void uniq_from_rank_kernel(const int32_t* __restrict__ present,
+                                                             const int32_t* __restrict__ incl, int64_t span,
+                                                             int64_t lo, int64_t* __restrict__ uniq,
+                                                             int64_t* __restrict__ n_uniq) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < span; v += (int64_t)gridDim.x * blockDim.x) {
+    if (present[v]) uniq[incl[v] - 1] = v + lo;
+    if (v == span - 1) *n_uniq = (int64_t)incl[v];
+  }
+}
+
 __global__ void minmax_store_kernel(const int64_t* __restrict__ mn, const int64_t* __restrict__ mx,
                                     int64_t* __restrict__ out) {
   out[0] = *mn;
@@ -164,9 +196,22 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
   void* temp = w + L.temp;
   size_t temp_bytes = L.total - L.temp;
   const unsigned g = grid_for(n);
-  hipLaunchKernelGGL(iota_i32_kernel, dim3(g), dim3(256), 0, s, pos, n);
   // A narrow id range sorts (id - lo) on only the bits it spans.
   const bool narrow = (uint64_t)id_hi - (uint64_t)id_lo < 0x7fffffffull;
+  const int64_t span = narrow ? (int64_t)((uint64_t)id_hi - (uint64_t)id_lo) + 1 : 0;
+  if (narrow && span <= n && span < 0x7fffffffll) {
+    // dense range: the span-long tables fit the flag / incl buffers (n entries each)
+    if (hipMemsetAsync(flag, 0, (size_t)span * sizeof(int32_t), s) != hipSuccess)
+      return check_launch("encode_ids: memset");
+    hipLaunchKernelGGL(mark_present_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, flag);
+    if (hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, flag, incl, (int)span, s) != hipSuccess)
+      return check_launch("encode_ids: scan");
+    hipLaunchKernelGGL(codes_from_rank_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, incl, codes);
+    hipLaunchKernelGGL(uniq_from_rank_kernel, dim3(grid_for(span)), dim3(256), 0, s, flag, incl, span, id_lo, uniq,
+                       n_uniq);
+    return check_launch("encode_ids: dense");
+  }
+  hipLaunchKernelGGL(iota_i32_kernel, dim3(g), dim3(256), 0, s, pos, n);
   if (narrow) {
     int32_t* k32 = reinterpret_cast<int32_t*>(w + L.keys);
     int32_t* k32s = k32 + n;

@@ -25,8 +25,11 @@ def _np_csr(rows, cols, vals, n_rows):
 
 
 @pytest.mark.parametrize("n,lo,hi", [(1, 5, 6), (17, -3, 4), (1000, 0, 50), (100000, -(2 ** 31), 2 ** 31),
-                                     (65537, 10 ** 12, 10 ** 12 + 7)])
+                                     (65537, 10 ** 12, 10 ** 12 + 7), (200000, 0, 150000), (4096, 0, 4096),
+                                     (3000, -5000, -1000)])
 def test_encode_ids_matches_numpy_unique(device, n, lo, hi):
+    """Both encode paths: dense id spans (span <= n: presence table + scan)
+    and the radix-sort ones (32-bit narrow, 64-bit)."""
     h = _hrec()
     rng = np.random.default_rng(n)
     ids = rng.integers(lo, hi, n, dtype=np.int64)
