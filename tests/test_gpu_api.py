@@ -617,7 +617,8 @@ def test_hybrid_not_loaded_raises(device):
         HybridRecommendationSystem().get_hybrid_recommendations(1, [1, 2])
 
 
-def test_hybrid_end_to_end(device, tmp_path):
+def test_hybrid_end_to_end(device, tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)  # save_predictions writes results/predictions/ under the cwd
     from src.als_model import ALSModel
     from src.hybrid_system import HybridRecommendationSystem
     from src.two_tower_model import TwoTowerModel
