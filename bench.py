@@ -137,6 +137,36 @@ def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
                dict(bound="valu", work=2.0 * rec.k * B * N, peak=F32_VALU_MULADD_TFLOPS, unit="TFLOP/s")),
               ("tt_score (f32 MFMA Dot)", lambda: o.tt_scores(uvec, rec.iv),
                dict(bound="mfma", work=2.0 * d * B * N, peak=F32_MFMA_PEAK_TFLOPS, unit="TFLOP/s"))]
+    elif getattr(rec, "pruned", False) and top_k <= _hrec.PRUNE_MAX_K:
+        # pruned bf16 path (csrc/hybrid_prune.hip): no score matrix; phase 1
+        # reads both models' item operands, phase 2 the heavier model's
+        hp = o.hybrid_prune(rec.U, hu, uvec, rec.V_op, rec.iv_op, top_k)
+        a_mm, t_mm = hp.minmax()
+        op_b = 2.0 * rec.dk * N  # one model's bf16 item operand
+        st = [("hybrid_prune_minmax (both bf16 GEMMs, dk %d, no score stores: row min/max + group max slices)"
+               % rec.dk, hp.minmax,
+               dict(bound="hbm", work=2 * op_b, peak=HBM_PEAK_GBS, unit="GB/s", mfma_flops=2 * 2.0 * rec.dk * B * N)),
+              ("hybrid_prune_topk (bound + heavier model's bf16 GEMM with survivor filter + survivors' fusion "
+               "+ stable top-k)", lambda: hp.topk(a_mm, t_mm, False, top_k, rec.offset),
+               dict(bound="hbm", work=op_b, peak=HBM_PEAK_GBS, unit="GB/s", mfma_flops=2.0 * rec.dk * B * N))]
+        out = []
+        for name, fn, rf in st:
+            fn()
+            ms = ev_time(fn, reps, stream)
+            r = roofline(rf["bound"], rf["work"], ms, rf["peak"], rf["unit"], name)
+            tf = rf["mfma_flops"] / (ms * 1e-3) / 1e12
+            r["mfma_view"] = {"achieved": tf, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": tf / BF16_MFMA_PEAK_TFLOPS}
+            out.append(r)
+        fell_back = hp.fallback_taken()
+        tot = sum(r["avg_launch_ms"] for r in out)
+        dom = max(out, key=lambda r: r["avg_launch_ms"])
+        return dict(dom, stages=out, fallback_taken=fell_back,
+                    batch_view={"ms": tot, "algorithmic_bytes": 2 * op_b,
+                                "note": "no-store bytes (both item operands once) / both phases' time",
+                                "achieved": 2 * op_b / (tot * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": 2 * op_b / (tot * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                "bytes_read_by_design": 3 * op_b})
     else:
         als, tt, a_mm, t_mm = o.hybrid_scores(rec.U, hu, uvec, rec.V_op, rec.iv_op)
         # one launch: user gather + bf16 conversion, both GEMMs, both rows'
@@ -217,7 +247,7 @@ def source_sha256(name):
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def api_line(eng, n_users, n_items, k, reps):
+def api_line(eng, n_users, n_items, k, reps, want_cpu):
     import contextlib
     import io
 
@@ -229,11 +259,12 @@ def api_line(eng, n_users, n_items, k, reps):
     from src.hybrid_system import HybridRecommendationSystem, fuse_device
     from src.two_tower_model import TwoTowerModel
 
+    d = 64
     als = ALSModel(rank=k)
     als.spark = DeviceSession()
     als.model = DeviceALSFactors(np.arange(n_users), np.arange(n_items), eng.U[:n_users], eng.V[:n_items], k)
     als.item_features = {}
-    tt = TwoTowerModel(n_users, n_items, 2651, 255, embedding_size=64, seed=4)
+    tt = TwoTowerModel(n_users, n_items, 2651, 255, embedding_size=d, seed=4)
     tt.build_model()
     rng = np.random.default_rng(9)
     items = pd.DataFrame({"itemId": np.arange(n_items), "manufacturer_id": rng.integers(0, 2651, n_items),
@@ -256,8 +287,8 @@ def api_line(eng, n_users, n_items, k, reps):
         return (time.perf_counter() - t0) / reps * 1e3
 
     class Candidates:
-        """all_items that both models score: iterates as item ids (ALS side),
-        indexes as the frame (two-tower side)."""
+        """all_items that both models score: iterates as a list of item ids
+        (ALS side), indexes as the frame (two-tower side)."""
 
         def __iter__(self):
             return iter(ids)
@@ -268,12 +299,26 @@ def api_line(eng, n_users, n_items, k, reps):
         def __getitem__(self, key):
             return items[key]
 
+    class IdArray(np.ndarray):
+        """The same candidates as an integer id array (what the ALS side
+        iterates, src/als_model.py:70, e.g. df["itemId"].unique() as the
+        reference's tuning loop passes it, :155) that answers the two-tower
+        side's column lookups (src/two_tower_model.py:138-143) from the frame."""
+
+        def __getitem__(self, key):
+            if isinstance(key, (str, list)):
+                return items[key]
+            return super().__getitem__(key)
+
     both = Candidates()
+    arr = items["itemId"].to_numpy().view(IdArray)
     parts = {}
     with contextlib.redirect_stdout(sink):
         ref_ms = timed(lambda u: h.get_hybrid_recommendations(u, items, top_k=5))
-        both_ms = timed(lambda u: h.get_hybrid_recommendations(u, both, top_k=5))
-        top_api = h.get_hybrid_recommendations(uids[0], both, top_k=5)
+        iter_ms = timed(lambda u: h.get_hybrid_recommendations(u, both, top_k=5))
+        arr_ms = timed(lambda u: h.get_hybrid_recommendations(u, arr, top_k=5))
+        top_api = h.get_hybrid_recommendations(uids[0], arr, top_k=5)
+        top_iter = h.get_hybrid_recommendations(uids[0], both, top_k=5)
         parts["als.predict_for_user (id list)"] = timed(lambda u: als.predict_for_user(u, ids))
         parts["twotower.predict_for_user (item frame)"] = timed(lambda u: tt.predict_for_user(u, items))
         a, t = als.predict_for_user(uids[0], ids), tt.predict_for_user(uids[0], items)
@@ -287,18 +332,117 @@ def api_line(eng, n_users, n_items, k, reps):
         parts["_union + fuse_device top-5"] = timed(fuse)
         top = fuse(0)
     work = sum(parts.values())
-    return {"users_per_s": 1e3 / both_ms, "pairs_per_s": n_items * 1e3 / both_ms, "api_call_ms": both_ms,
-            "reference_call_ms": ref_ms, "list_path_ms": work, "list_parts_ms": parts, "items": n_items,
-            "top_k": 5, "reps": reps, "top5_nonempty": len(top_api) == 5,
-            "api_top5_equals_list_path": [i for i, _ in top_api] == [i for i, _ in top],
-            "note": ("one user per call (the reference API, src/hybrid_system.py:95-116); api_call = "
-                     "get_hybrid_recommendations(uid, candidates) with candidates both models score (ids for "
-                     "ALS, the frame for the two-tower side); reference_call = get_hybrid_recommendations(uid, "
-                     "item_frame) as the reference wires it (ALS side -> [] by SURVEY D9). Both run the array "
-                     "path (device scores -> device fusion + top-6 -> tie check), no per-item Python objects; "
-                     "list_path = the per-model predict_for_user lists + _union + fuse_device the call used "
-                     "before (still taken on ties / duplicate ids / cold-start rows)")}
 
+    # device share of one call: the same kernels on device-resident inputs
+    # (ALS transform, item tower + user tower + Dot, fusion + top-6), HIP events
+    stream = torch.cuda.current_stream()
+    keys = np.arange(n_items, dtype=np.int64)
+    dev_in = tt._device_inputs({"user_in": np.full(n_items, uids[0]), "item_id_in": keys,
+                                "manufacturer_in": items["manufacturer_id"].values,
+                                "category_in": items["category_id"].values,
+                                "numeric_in": tt.scaler.transform(items[["price", "average_review_rating"]])})
+    irows = als.model._lookup_device(keys)
+    urow = torch.as_tensor(als.model._lookup(als.model.user_ids, [uids[0]]), device="cuda")
+
+    def device_call():
+        sa = _hrec.als_score(als.model.U, urow, als.model.Vt, irows, n_items, k)[0]
+        uv = tt.model.user_vectors(dev_in[0][:1])
+        iv = tt.model.item_vectors(*dev_in[1:])
+        st = _hrec.tt_score(uv, iv).reshape(-1)
+        return _hrec.fuse_topk(sa.double(), st, False, 6, want_fused=False)
+
+    device_call()
+    dev_ms = ev_time(device_call, reps, stream)
+    item_bytes = n_items * (4.0 * k + 4.0 * d)  # each candidate's ALS factor row + tower vector, read once
+    out = {"users_per_s": 1e3 / arr_ms, "pairs_per_s": n_items * 1e3 / arr_ms, "api_call_ms": arr_ms,
+           "api_call_iterable_ms": iter_ms, "reference_call_ms": ref_ms, "list_path_ms": work,
+           "list_parts_ms": parts, "items": n_items, "top_k": 5, "reps": reps,
+           "top5_nonempty": len(top_api) == 5,
+           "api_top5_equals_list_path": [i for i, _ in top_api] == [i for i, _ in top] == [i for i, _ in top_iter],
+           "roofline": {"kernel": "one call's device work (hrec_als_score + tt towers + hrec_tt_score + "
+                                  "hrec_fuse_topk), HIP events", "bound": "hbm",
+                        "achieved": item_bytes / (arr_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": item_bytes / (arr_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes": item_bytes,
+                        "device_ms": dev_ms, "device_frac": item_bytes / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                        "host_share": max(0.0, 1.0 - dev_ms / arr_ms),
+                        "note": ("algorithmic bytes = N (4k + 4d): every candidate's ALS item factor row and "
+                                 "two-tower item vector read once; achieved over the whole API call (host "
+                                 "work included: the share of the call that is not device time is host_share)")},
+           "note": ("one user per call (the reference API, src/hybrid_system.py:95-116). api_call = "
+                    "get_hybrid_recommendations(uid, candidates) with the candidates an integer id array that "
+                    "also answers the two-tower side's column lookups (ALS reads it without a per-item Python "
+                    "pass); api_call_iterable = the same candidates iterating as a Python list of ids; "
+                    "reference_call = get_hybrid_recommendations(uid, item_frame) as the reference wires it "
+                    "(ALS side -> [] by SURVEY D9). All run the array path (device scores -> device fusion + "
+                    "top-6 -> tie check); list_path = the per-model predict_for_user lists + _union + "
+                    "fuse_device (still taken on ties / duplicate ids / cold-start rows)")}
+    if want_cpu:
+        from oracle import cpu_baseline as cb
+
+        out["cpu_baseline"] = cb.api_call(n_items, k, d, 5)
+    return out
+
+
+
+def c4_tower_check(tt4, it4, mn4, ct4, nu4, V4, n_rows=500):
+    """BASELINE c4 at full size: 500 sampled rows of the 50M-item tower output
+    against the f64 Keras graph (oracle/two_tower.py forward, rtol 1e-5 /
+    atol 2e-5 as tests/test_gpu_api.py), on the host."""
+    import numpy as np
+
+    from oracle import two_tower as ott
+
+    n = V4.shape[0]
+    g = np.random.default_rng(77)
+    rows = np.unique(np.concatenate([g.integers(0, n, n_rows), [0, n - 1]]))
+    rt = torch.as_tensor(rows, device=V4.device)
+    p = {name: t.detach().cpu().numpy() for name, t in tt4.tensors.items() if name not in ("user_emb", "item_emb")}
+    p["item_emb"] = tt4.tensors["item_emb"].index_select(0, rt).cpu().numpy()
+    p["user_emb"] = np.zeros((1, tt4.d), np.float32)
+    ref = ott.forward(p, np.zeros(len(rows), np.int64), np.arange(len(rows)), mn4[rt].cpu().numpy(),
+                      ct4[rt].cpu().numpy(), nu4[rt].cpu().numpy())["ivec"]
+    got = V4.index_select(0, rt).cpu().numpy().astype(np.float64)
+    err = np.abs(got - ref) - (1e-5 * np.abs(ref) + 2e-5)
+    return {"rows_checked": int(len(rows)), "rows_match_oracle": bool(np.all(err <= 0)),
+            "max_abs_err": float(np.max(np.abs(got - ref))),
+            "tolerance": "|gpu - f64 graph| <= 1e-5 |ref| + 2e-5 (oracle/two_tower.py forward)"}
+
+
+def c4_ranking_check(Ud, Vd, sc, k=5, chunk=1 << 20):
+    """Top-k of 8 users over all items of the c4 catalogue vs the f64 ranking
+    of the same operands (bf16: the bf16-rounded values), computed here in
+    f64 chunks on the device; indices must agree wherever the f64 top-(k+1)
+    is separated by more than the f32 score tolerance."""
+    gi, gv = sc.topk(Ud, k)
+    U64 = Ud.double()
+    best_v, best_i = [], []
+    for j0 in range(0, Vd.shape[0], chunk):
+        s = U64 @ Vd[j0: j0 + chunk].double().T
+        v, i = torch.topk(s, k + 1, dim=1, sorted=True)
+        best_v.append(v)
+        best_i.append(i + j0)
+    v = torch.cat(best_v, 1)
+    i = torch.cat(best_i, 1)
+    # stable order: larger score first, ties -> smaller index
+    key = torch.argsort(i, dim=1)
+    v, i = v.gather(1, key), i.gather(1, key)
+    order = torch.argsort(-v, dim=1, stable=True)[:, : k + 1]
+    rv, ri = v.gather(1, order).cpu(), i.gather(1, order).cpu()
+    gi = gi.cpu()
+    checked, ok, tol = 0, True, 0.0
+    for b in range(Ud.shape[0]):
+        # f32 accumulation bound: 1e-6 x sum_c |u_c v_c| (tests/test_gpu_dot.py), x2 margin
+        rows = Vd.index_select(0, ri[b].to(Vd.device)).double().abs()
+        tol_b = 2e-6 * float((rows @ U64[b].abs()).max())
+        tol = max(tol, tol_b)
+        gaps = (rv[b, :-1] - rv[b, 1:]).tolist()
+        if all(x > 2 * tol_b for x in gaps):
+            checked += 1
+            ok = ok and gi[b].tolist() == ri[b, :k].tolist()
+    return {"users": int(Ud.shape[0]), "users_separated": checked, "top5_matches_f64_ranking": ok,
+            "score_tol_max": tol, "rule": ("indices equal for every user whose f64 top-6 gaps all exceed 2 x tol_b, "
+                                           "tol_b = 2e-6 x max sum_c |u_c v_c| over those items")}
 
 def WANT_CPU(args, rank, world):
     """CPU baselines run on rank 0 at N = 1 only (a bounded sample each)."""
@@ -533,7 +677,10 @@ def main():
                      "graph_ms_per_batch": hs_g * 1e3 if hs_eager else None, "launch": how,
                      "top_k": 5, "rank": k5, "d": d5, "dtype": "bf16 operands, f32 accumulation",
                      "items_sharded_over": world,
-                     "steps": "ALS + two-tower scores and their row min/max in one bf16 MFMA launch (hrec_hybrid_scores) + min-max fusion + stable top-5"}
+                     "steps": ("pruned bf16 hybrid (hrec_hybrid_prune_minmax: both GEMMs, row min/max, no score "
+                               "stores; hrec_hybrid_prune_topk: bound from the group maxima + the heavier model's "
+                               "GEMM with a survivor filter + the survivors' light scores and fusion + stable "
+                               "top-5; exact unfused fallback gated on the device)")}
         if world == 1:
             hybrid_c5["roofline"] = hybrid_stages(rec5, hu5, uv5, 5, 10, stream)
         if WANT_CPU(args, rank, world):
@@ -596,7 +743,7 @@ def main():
     # per-model predict_for_user lists + _union + fuse_device it replaces.
     api = None
     if rank == 0 and world == 1 and args.api_reps > 0:
-        api = api_line(eng, n_users, n_items, k, args.api_reps)
+        api = api_line(eng, n_users, n_items, k, args.api_reps, WANT_CPU(args, rank, world))
 
     # Ingest (§8(f) row 1, ALSModel.train's DataFrame -> CSR/CSC step): the
     # rank's user shard as COO columns (int64 ids, ratings) -> id codes +
@@ -696,6 +843,8 @@ def main():
 
             tt_iv["cpu_baseline"] = cb.item_vectors(args.c4_items // 100, args.c4_items, d4)
         U4 = tt4.user_vectors(torch.arange(args.c4_users, dtype=torch.int32, device="cuda"))
+        if world == 1:
+            tt_c4["tower_check"] = c4_tower_check(tt4, it4, mn4, ct4, nu4, V4)
         del tt4, it4, mn4, ct4, nu4
         torch.cuda.empty_cache()
         for name, dt, peak in (("f32", torch.float32, F32_MFMA_PEAK_TFLOPS),
@@ -703,27 +852,42 @@ def main():
             Vd = _hrec.dot_operand(V4, dt)
             Ud = _hrec.dot_operand(U4, dt)
             sc = ShardedScorer(Vd, c0, world=world, rank=rank, group=group)
-            sc.topk(Ud, 5)
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            reps = 3
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            q0 = time.perf_counter()
-            e0.record(stream)
-            for _ in range(reps):
-                sc.topk(Ud, 5)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            qt = torch.tensor([(time.perf_counter() - q0) / reps], dtype=torch.float64, device="cuda")
-            if world > 1:
-                dist.all_reduce(qt, op=dist.ReduceOp.MAX)
-            qs = float(qt.item())
-            local_s = e0.elapsed_time(e1) / reps / 1e3  # this rank's launches, HIP events on the launch stream
-            tf = 2.0 * args.c4_users * c_loc * d4 / local_s / 1e12
-            tt_c4[name] = {"pairs_per_s": args.c4_users * args.c4_items / qs, "ms_per_batch": qs * 1e3,
-                           "roofline": {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
-                                        "frac": tf / peak}}
+            for nb in (args.c4_users, 1):  # B in {1, 1024}
+                Ub = Ud[:nb].contiguous()
+                sc.topk(Ub, 5)
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                reps = 3 if nb > 1 else 10
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                q0 = time.perf_counter()
+                e0.record(stream)
+                for _ in range(reps):
+                    sc.topk(Ub, 5)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                qt = torch.tensor([(time.perf_counter() - q0) / reps], dtype=torch.float64, device="cuda")
+                if world > 1:
+                    dist.all_reduce(qt, op=dist.ReduceOp.MAX)
+                qs = float(qt.item())
+                local_s = e0.elapsed_time(e1) / reps / 1e3  # this rank's launches, HIP events on the launch stream
+                if nb > 1:
+                    tf = 2.0 * nb * c_loc * d4 / local_s / 1e12
+                    tt_c4[name] = {"pairs_per_s": nb * args.c4_items / qs, "ms_per_batch": qs * 1e3,
+                                   "roofline": {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
+                                                "frac": tf / peak}}
+                else:
+                    # one user: a GEMV, bound by reading every item operand once
+                    ib = float(c_loc) * Vd.shape[1] * Vd.element_size()
+                    gbs = ib / local_s / 1e9
+                    tt_c4[name + "_B1"] = {"pairs_per_s": args.c4_items / qs, "ms_per_batch": qs * 1e3, "users": 1,
+                                           "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                                                        "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                                        "algorithmic_bytes": ib,
+                                                        "note": "item operand bytes of this rank read once "
+                                                                "(N x dk x element size) / HIP-event time"}}
+            if world == 1:
+                tt_c4[name]["ranking_check"] = c4_ranking_check(Ud[:8].contiguous(), Vd, sc)
             del Vd, Ud
         if WANT_CPU(args, rank, world):
             from oracle import cpu_baseline as cb

@@ -637,6 +637,19 @@ static int64_t dot_sample(int64_t n, int kk) {
   return s < n ? s : n;
 }
 
+// The survivor filter alone (the pruned hybrid's pass 2, csrc/hybrid_prune.hip):
+// append (score, j) of every item j with score >= thr[b] to user b's list
+// (cap entries; cn[b] counts every survivor, so cn[b] > cap = overflow).
+int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr, int cap,
+                   float* cv, int64_t* ci, int* cn, hipStream_t s) {
+  return dot_launch<true>(U, B, V, n_items, n_items, 1, dk, bf16, nullptr, 0, thr, 1, cap, cv, ci, cn, 0, s);
+}
+
+int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s) {
+  hipLaunchKernelGGL(dot_overflow_kernel, dim3(64), dim3(256), 0, s, cn, n_users, cap, flag);
+  return check_launch("dot_overflow_kernel");
+}
+
 int offset_ids(int64_t* idx, int64_t n, int64_t off, hipStream_t s) {
   if (n <= 0 || off == 0) return HREC_OK;
   hipLaunchKernelGGL(dot_offset_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx, n, off);

@@ -47,6 +47,7 @@ struct HybScoresArgs {
   const float* users[2];   // f32 user rows: ALS factors, two-tower user vectors
   int64_t ld[2];           // their row strides (elements)
   const int64_t* rows[2];  // row of batch user b (nullptr: row b)
+  int64_t n_rows[2];       // rows of users[m]: a row outside [0, n_rows) reads as NaN
   int width[2];            // valid columns (<= DK; the operand is zero beyond)
   int B;
   const char* items[2];    // bf16 item operands [N, DK]
@@ -54,6 +55,8 @@ struct HybScoresArgs {
   float* out[2];           // score matrices [B, ldo]
   int64_t ldo;
   float* part;             // [2][G][2][B]: per-block min / max
+  int* argpos;             // HS_PRUNE: [2][G][B] slice of each block's max ((jb / 16) * 4 + g), -1 = none
+  const int* gate;         // HS_GATED: skip the launch while *gate == 0
   int G;                   // item groups per (model, user tile)
   int UB;                  // users per tile (multiple of 64)
   int n_ut;
@@ -100,17 +103,26 @@ struct HsShape {
   static constexpr int NU = NI == 4 ? 2 : 4;    // user tiles per chunk (NI 4: each user fragment feeds 4 MFMAs)
 };
 
+// Modes: HS_FULL = score stores + per-block min / max (hrec_hybrid_scores);
+// HS_PRUNE = no stores, min / max + the item slice holding each block's max
+// (pass 1 of the pruned hybrid top-k, csrc/hybrid_prune.hip); HS_GATED =
+// score stores only, skipped unless *gate (that path's exact fallback).
+enum { HS_FULL = 0, HS_PRUNE = 1, HS_GATED = 2 };
+
 // NCH: user chunks of CU = 16 NU users in the tile (compile-time, so the
 // per-lane running min / max of every chunk stays in registers and the last
 // chunk's item refills are unconditional).
-template <int DK, int NCH>
+template <int DK, int NCH, int MODE>
 __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a) {
+  if (MODE == HS_GATED && *a.gate == 0) return;  // block-uniform
   using S = HsShape<DK>;
   constexpr int KS = S::KS, NI = S::NI, NU = S::NU, CU = 16 * NU;
   constexpr int kRowB = S::kRowB;
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   char* us = dsm;
   uint32_t* mmk = reinterpret_cast<uint32_t*>(dsm + (size_t)a.UB * kRowB);  // [UB][2]: ~key(min), key(max)
+  // HS_PRUNE: [UB] key(max) << 32 | ~slice (ds_max_u64: the larger max, then the earlier slice)
+  unsigned long long* amk = reinterpret_cast<unsigned long long*>(dsm + (size_t)a.UB * kRowB + (size_t)a.UB * 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int model = blockIdx.x & 1;
@@ -174,7 +186,10 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         if (o < n_chunks && r < ub && 8 * q < wd) {
           const int64_t row = rws ? rws[b0 + r] : (int64_t)(b0 + r);
           const float* p = src + row * ld + 8 * q;
-          if (vec && 8 * q + 8 <= wd) {
+          if (row < 0 || row >= a.n_rows[model]) {  // unknown / stale row: NaN scores (as hrec_als_score's -1)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[j][e] = __builtin_nanf("");
+          } else if (vec && 8 * q + 8 <= wd) {
             const float4 x0 = *reinterpret_cast<const float4*>(p);
             const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
             f[j][0] = x0.x, f[j][1] = x0.y, f[j][2] = x0.z, f[j][3] = x0.w;
@@ -200,16 +215,22 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       }
     }
     for (int o = threadIdx.x; o < 2 * a.UB; o += kHsThreads) mmk[o] = 0u;
+    if (MODE == HS_PRUNE)
+      for (int o = threadIdx.x; o < a.UB; o += kHsThreads) amk[o] = 0ull;
   }
   __syncthreads();
 
   // running min / max of this lane's scores per (chunk, user tile): the
   // lane's user is CU ch + 16 u + c in every slice; folded across lanes once
   float lo[NCH][NU], hi[NCH][NU];
+  int hp[NCH][MODE == HS_PRUNE ? NU : 1];  // HS_PRUNE: slice (jb / 16) of the lane's max
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-    for (int u = 0; u < NU; ++u) lo[ch][u] = __builtin_inff(), hi[ch][u] = -__builtin_inff();
+    for (int u = 0; u < NU; ++u) {
+      lo[ch][u] = __builtin_inff(), hi[ch][u] = -__builtin_inff();
+      if constexpr (MODE == HS_PRUNE) hp[ch][u] = -1;
+    }
   if (work) {
     HsFrag ua[NU];
 #pragma unroll
@@ -266,23 +287,47 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
           const int bl = CU * ch + 16 * u + c;
-          if (full) {
+          if constexpr (MODE == HS_PRUNE) {
+            // slice max first, then one compare: the lane's max and its slice
+            float mx = -__builtin_inff();
+            if (full) {
 #pragma unroll
-            for (int t = 0; t < NI; ++t) {
-              lo[ch][u] = fminf(fminf(lo[ch][u], fminf(acc[u][t][0], acc[u][t][1])), fminf(acc[u][t][2], acc[u][t][3]));
-              hi[ch][u] = fmaxf(fmaxf(hi[ch][u], fmaxf(acc[u][t][0], acc[u][t][1])), fmaxf(acc[u][t][2], acc[u][t][3]));
+              for (int t = 0; t < NI; ++t) {
+                lo[ch][u] = fminf(fminf(lo[ch][u], fminf(acc[u][t][0], acc[u][t][1])), fminf(acc[u][t][2], acc[u][t][3]));
+                mx = fmaxf(fmaxf(mx, fmaxf(acc[u][t][0], acc[u][t][1])), fmaxf(acc[u][t][2], acc[u][t][3]));
+              }
+            } else {
+#pragma unroll
+              for (int t = 0; t < NI; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (jb + 16 * t + 4 * g + r < i1) {
+                    lo[ch][u] = fminf(lo[ch][u], acc[u][t][r]);
+                    mx = fmaxf(mx, acc[u][t][r]);
+                  }
             }
-          } else {
+            const bool gt = mx > hi[ch][u];
+            hi[ch][u] = gt ? mx : hi[ch][u];
+            hp[ch][u] = gt ? (int)(jb >> 4) : hp[ch][u];
+          } else if constexpr (MODE == HS_FULL) {
+            if (full) {
 #pragma unroll
-            for (int t = 0; t < NI; ++t)
+              for (int t = 0; t < NI; ++t) {
+                lo[ch][u] = fminf(fminf(lo[ch][u], fminf(acc[u][t][0], acc[u][t][1])), fminf(acc[u][t][2], acc[u][t][3]));
+                hi[ch][u] = fmaxf(fmaxf(hi[ch][u], fmaxf(acc[u][t][0], acc[u][t][1])), fmaxf(acc[u][t][2], acc[u][t][3]));
+              }
+            } else {
 #pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (jb + 16 * t + 4 * g + r < i1) {
-                  lo[ch][u] = fminf(lo[ch][u], acc[u][t][r]);
-                  hi[ch][u] = fmaxf(hi[ch][u], acc[u][t][r]);
-                }
+              for (int t = 0; t < NI; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (jb + 16 * t + 4 * g + r < i1) {
+                    lo[ch][u] = fminf(lo[ch][u], acc[u][t][r]);
+                    hi[ch][u] = fmaxf(hi[ch][u], acc[u][t][r]);
+                  }
+            }
           }
-          if (HREC_HS_ABLATE == 0 && bl < ub) {
+          if (MODE != HS_PRUNE && HREC_HS_ABLATE == 0 && bl < ub) {
             float* o = out + (int64_t)(b0 + bl) * a.ldo;
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
@@ -305,6 +350,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       }
     }
   }
+  if constexpr (MODE == HS_GATED) return;  // scores only (the mm are known)
   // fold the lanes' running min / max per user into the block's LDS slots
   if (HREC_HS_ABLATE < 2 && ub > 0) {
 #pragma unroll
@@ -315,8 +361,23 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         float l = lo[ch][u], h = hi[ch][u];
         l = fminf(l, __shfl_xor(l, 16, kWave));
         l = fminf(l, __shfl_xor(l, 32, kWave));
-        h = fmaxf(h, __shfl_xor(h, 16, kWave));
-        h = fmaxf(h, __shfl_xor(h, 32, kWave));
+        if constexpr (MODE == HS_PRUNE) {
+          // (max, slice * 4 + g) of the 4 lane groups: larger max, then the smaller position
+          int p = hp[ch][u] < 0 ? 0x7fffffff : hp[ch][u] * 4 + g;
+#pragma unroll
+          for (int off = 16; off < 64; off <<= 1) {
+            const float oh = __shfl_xor(h, off, kWave);
+            const int op = __shfl_xor(p, off, kWave);
+            const bool take = oh > h || (oh == h && op < p);
+            h = take ? oh : h;
+            p = take ? op : p;
+          }
+          if (g == 0 && bl < ub && p != 0x7fffffff)
+            atomicMax(&amk[bl], ((unsigned long long)hs_key(h) << 32) | (uint32_t)~p);
+        } else {
+          h = fmaxf(h, __shfl_xor(h, 16, kWave));
+          h = fmaxf(h, __shfl_xor(h, 32, kWave));
+        }
         if (g == 0 && bl < ub) {
           atomicMax(&mmk[2 * bl], ~hs_key(l));
           atomicMax(&mmk[2 * bl + 1], hs_key(h));
@@ -329,6 +390,10 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
     float* pp = a.part + ((int64_t)(model * a.G + grp) * 2) * a.B + b0 + o;
     pp[0] = kmin ? hs_unkey(~kmin) : __builtin_inff();
     pp[a.B] = kmax ? hs_unkey(kmax) : -__builtin_inff();
+    if constexpr (MODE == HS_PRUNE) {
+      const unsigned long long k = amk[o];
+      a.argpos[(int64_t)(model * a.G + grp) * a.B + b0 + o] = k ? (int)~(uint32_t)k : -1;
+    }
   }
 }
 
@@ -373,7 +438,9 @@ __global__ __launch_bounds__(256) void hyb_mm_reduce_kernel(const float* __restr
   }
 }
 
-static int hs_groups(int64_t n_items) {
+int hs_slice_tiles(int dk) { return dk == 64 ? HsShape<64>::NI : (dk == 128 ? HsShape<128>::NI : HsShape<256>::NI); }
+
+int hs_groups(int64_t n_items) {
   const int64_t g = (n_items + 255) / 256;
   return (int)(g < 128 ? (g < 1 ? 1 : g) : 128);
 }
@@ -389,32 +456,77 @@ static int hs_user_tile(int B) {
   return (UB + CU - 1) / CU * CU;
 }
 
-template <int DK, int NCH>
+template <int DK, int NCH, int MODE>
 static int hs_launch_n(HybScoresArgs& a, size_t lds, hipStream_t s) {
-  const auto kfn = hyb_scores_kernel<DK, NCH>;
+  const auto kfn = hyb_scores_kernel<DK, NCH, MODE>;
   if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return check_launch("hyb_scores_kernel: LDS attribute");
   hipLaunchKernelGGL(kfn, dim3((unsigned)(2 * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
   return check_launch("hyb_scores_kernel");
 }
 
-template <int DK>
+template <int DK, int MODE>
 static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
   constexpr int CU = 16 * HsShape<DK>::NU;
   a.UB = hs_user_tile<DK>(a.B);
   a.n_ut = (a.B + a.UB - 1) / a.UB;
-  const size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * 8;
+  const size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * (MODE == HS_PRUNE ? 16 : 8);
   int rc;
   switch (a.UB / CU) {
-    case 1: rc = hs_launch_n<DK, 1>(a, lds, s); break;
-    case 2: rc = hs_launch_n<DK, 2>(a, lds, s); break;
-    case 3: rc = hs_launch_n<DK, 3>(a, lds, s); break;
-    default: rc = hs_launch_n<DK, 4>(a, lds, s); break;
+    case 1: rc = hs_launch_n<DK, 1, MODE>(a, lds, s); break;
+    case 2: rc = hs_launch_n<DK, 2, MODE>(a, lds, s); break;
+    case 3: rc = hs_launch_n<DK, 3, MODE>(a, lds, s); break;
+    default: rc = hs_launch_n<DK, 4, MODE>(a, lds, s); break;
   }
-  if (rc) return rc;
+  if (rc || MODE == HS_GATED) return rc;
   hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((a.B + 63) / 64), 2), dim3(256), 0, s, a.part, a.B, a.G,
                      mm0, mm1);
   return check_launch("hyb_mm_reduce_kernel");
+}
+
+template <int MODE>
+static int hs_dispatch(HybScoresArgs& a, int dk, float* mm0, float* mm1, hipStream_t s) {
+  switch (dk) {
+    case 64: return hs_launch<64, MODE>(a, mm0, mm1, s);
+    case 128: return hs_launch<128, MODE>(a, mm0, mm1, s);
+    default: return hs_launch<256, MODE>(a, mm0, mm1, s);
+  }
+}
+
+// The launch behind hrec_hybrid_scores and the pruned hybrid top-k
+// (csrc/hybrid_prune.hip; arguments validated by the caller, n_items > 0).
+int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const int64_t* als_rows, int64_t n_als_rows,
+                      int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
+                      const void* als_items, const void* tt_items, int64_t n_items, int dk, float* als_out,
+                      float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm, float* part, int* argpos,
+                      const int* gate, hipStream_t s) {
+  HybScoresArgs a{};
+  a.users[0] = als_users;
+  a.users[1] = tt_users;
+  a.ld[0] = als_ld;
+  a.ld[1] = tt_ld;
+  a.rows[0] = als_rows;
+  a.rows[1] = nullptr;
+  a.n_rows[0] = als_rows ? n_als_rows : (int64_t)n_users;
+  a.n_rows[1] = n_users;
+  a.width[0] = als_width;
+  a.width[1] = tt_width;
+  a.B = n_users;
+  a.items[0] = static_cast<const char*>(als_items);
+  a.items[1] = static_cast<const char*>(tt_items);
+  a.N = n_items;
+  a.out[0] = als_out;
+  a.out[1] = tt_out;
+  a.ldo = ld_out;
+  a.part = part;
+  a.argpos = argpos;
+  a.gate = gate;
+  a.G = hs_groups(n_items);
+  switch (mode) {
+    case HS_PRUNE: return hs_dispatch<HS_PRUNE>(a, dk, als_mm, tt_mm, s);
+    case HS_GATED: return hs_dispatch<HS_GATED>(a, dk, als_mm, tt_mm, s);
+    default: return hs_dispatch<HS_FULL>(a, dk, als_mm, tt_mm, s);
+  }
 }
 
 }  // namespace hrec
@@ -426,7 +538,8 @@ extern "C" size_t hrec_hybrid_scores_workspace_bytes(int n_users, int64_t n_item
   return (size_t)2 * hs_groups(n_items) * 2 * B * sizeof(float) + 256;
 }
 
-extern "C" int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* als_rows, int als_width,
+extern "C" int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* als_rows,
+                                  int64_t n_als_rows, int als_width,
                                   const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                                   const void* als_items, const void* tt_items, int64_t n_items, int dk,
                                   float* als_out, float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm,
@@ -438,6 +551,7 @@ extern "C" int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const 
   HREC_REQUIRE(als_width >= 0 && als_width <= dk && tt_width >= 0 && tt_width <= dk,
                "hybrid_scores: user widths must be in [0, dk]");
   HREC_REQUIRE(als_ld >= als_width && tt_ld >= tt_width, "hybrid_scores: row stride below the width");
+  HREC_REQUIRE(n_als_rows >= 0, "hybrid_scores: negative n_als_rows");
   HREC_REQUIRE(ld_out >= n_items, "hybrid_scores: ld_out < n_items");
   if (n_users == 0) return HREC_OK;
   HREC_REQUIRE(als_mm && tt_mm && workspace, "hybrid_scores: null min/max output or workspace");
@@ -453,27 +567,7 @@ extern "C" int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const 
                        static_cast<const float*>(workspace), n_users, 0, als_mm, tt_mm);
     return check_launch("hyb_mm_reduce_kernel");
   }
-  HybScoresArgs a{};
-  a.users[0] = als_users;
-  a.users[1] = tt_users;
-  a.ld[0] = als_ld;
-  a.ld[1] = tt_ld;
-  a.rows[0] = als_rows;
-  a.rows[1] = nullptr;
-  a.width[0] = als_width;
-  a.width[1] = tt_width;
-  a.B = n_users;
-  a.items[0] = static_cast<const char*>(als_items);
-  a.items[1] = static_cast<const char*>(tt_items);
-  a.N = n_items;
-  a.out[0] = als_out;
-  a.out[1] = tt_out;
-  a.ldo = ld_out;
-  a.part = static_cast<float*>(workspace);
-  a.G = hs_groups(n_items);
-  switch (dk) {
-    case 64: return hs_launch<64>(a, als_mm, tt_mm, s);
-    case 128: return hs_launch<128>(a, als_mm, tt_mm, s);
-    default: return hs_launch<256>(a, als_mm, tt_mm, s);
-  }
+  return hybrid_scores_run(HS_FULL, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld, tt_width,
+                           n_users, als_items, tt_items, n_items, dk, als_out, tt_out, ld_out, als_mm, tt_mm,
+                           static_cast<float*>(workspace), nullptr, nullptr, s);
 }

@@ -1419,6 +1419,46 @@ extern "C" int hrec_fuse_rows_topk(const float* als, const float* tt, int64_t n_
   return check_launch("add_offset_kernel");
 }
 
+namespace hrec {
+// The exact segment path of hrec_fuse_rows_topk (kk <= kFuseK), gated on a
+// device flag (launches do nothing while *gate == 0): the pruned hybrid
+// top-k's fallback (csrc/hybrid_prune.hip). One block per row walks every
+// segment; then the keyed top-kk of the segments' candidates.
+size_t fuse_rows_exact_ws_bytes(int64_t n_rows, int64_t n, int kk) {
+  const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg;
+  return 2 * al256((size_t)n_rows * segs * kk * 8) + topk_ws_bytes(n_rows, segs * kk, kk, 8) + 256;
+}
+
+int fuse_rows_exact(const float* als, const float* tt, int64_t n_rows, int64_t n, int64_t ld, const float* als_mm,
+                    const float* tt_mm, double w0, double w1, int kk, int64_t* out_idx, double* out_val, void* ws,
+                    hipStream_t s, const int* gate) {
+  if (kk < 1 || kk > kFuseK) {
+    set_error("fuse_rows_exact: kk must be in [1, %d]", kFuseK);
+    return HREC_E_INVALID;
+  }
+  const int64_t segs = (n + kFuseSeg - 1) / kFuseSeg;
+  char* p = (char*)ws;
+  double* gv = (double*)p;
+  p += al256((size_t)n_rows * segs * kk * 8);
+  int64_t* gi = (int64_t*)p;
+  p += al256((size_t)n_rows * segs * kk * 8);
+  const dim3 grid(1, (unsigned)n_rows);
+  switch (kk) {
+#define HREC_FX(K)                                                                                                  \
+  case K:                                                                                                           \
+    hipLaunchKernelGGL(fuse_segment_topk_kernel<K>, grid, dim3(256), 0, s, als, tt, n, ld, segs, als_mm, tt_mm, w0, \
+                       w1, gv, gi, gate, nullptr);                                                                  \
+    break;
+    HREC_FX(1) HREC_FX(2) HREC_FX(3) HREC_FX(4) HREC_FX(5) HREC_FX(6) HREC_FX(7) default : HREC_FX(8)
+#undef HREC_FX
+  }
+  const int rc = check_launch("fuse_segment_topk_kernel (exact, gated)");
+  if (rc) return rc;
+  return topk_rows<double>(gv, n_rows, segs * kk, segs * kk, kk, out_idx, out_val, p, (size_t)1 << 62, s, gi, nullptr,
+                           gate);
+}
+}  // namespace hrec
+
 extern "C" int hrec_topk_f64_keyed(const double* vals, const int64_t* keys, int64_t n_rows, int64_t n, int top_k,
                                    int64_t* out_idx, double* out_val, void* workspace, size_t workspace_bytes,
                                    void* stream) {

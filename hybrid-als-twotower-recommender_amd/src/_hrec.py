@@ -95,13 +95,19 @@ _SIGNATURES.update({
     "hrec_dot_topk": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp,
                                _c_sz, _vp]),
     "hrec_hybrid_scores_workspace_bytes": (_c_sz, [_c_i32, _c_i64]),
-    "hrec_hybrid_scores": (_c_i32, [_vp, _c_i64, _vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32,
+    "hrec_hybrid_scores": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32,
                                     _vp, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_minmax_workspace_bytes": (_c_sz, [_c_i32]),
     "hrec_hybrid_minmax": (_c_i32, [_vp, _vp, _c_i32, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
     "hrec_hybrid_topk": (_c_i32, [_vp, _vp, _c_i32, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _c_i32, _vp, _c_i64,
                                   _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_prune_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32, _c_i32]),
+    "hrec_hybrid_prune_minmax": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp,
+                                          _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_prune_topk": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp,
+                                        _c_i64, _c_i32, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_prune_fallback_taken": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
                          [ctypes.c_float] * 6 + [_vp]),
     "hrec_adam_sparse_tables": (_c_i32, [ctypes.POINTER(SparseTable), _c_i32] + [ctypes.c_float] * 6 + [_vp]),
@@ -109,7 +115,7 @@ _SIGNATURES.update({
                                       + [_vp]),
 })
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _LIB = None
 
 
@@ -572,7 +578,9 @@ def hybrid_scores(als_users, als_rows, tt_users, als_item, tt_item):
     (rows als_rows [B] int64 are used), tt_users [B, kt] f32 two-tower user
     vectors, als_item / tt_item bf16 [N, dk] item operands (dot_operand).
     Returns (als [B, N] f32, tt [B, N] f32, als_mm [2, B], tt_mm [2, B]) —
-    dot_scores of the bf16 user operands and rows_minmax of each."""
+    dot_scores of the bf16 user operands and rows_minmax of each. A row of
+    als_rows outside [0, als_users.shape[0]) gives a NaN ALS score row (as
+    als_score does for an unknown user)."""
     dk = _hyb_args(als_item, tt_item)
     B, N = int(als_rows.shape[0]), int(als_item.shape[0])
     if tt_item.shape[0] != N or tt_users.shape[0] != B:
@@ -591,11 +599,73 @@ def hybrid_scores(als_users, als_rows, tt_users, als_item, tt_item):
     need = int(lib().hrec_hybrid_scores_workspace_bytes(B, N))
     ws = torch.empty(need, dtype=torch.uint8, device=dev)
     _check("hrec_hybrid_scores", lib().hrec_hybrid_scores(
-        _vp(als_users.data_ptr()), als_users.stride(0), _vp(rows.data_ptr()), als_users.shape[1],
+        _vp(als_users.data_ptr()), als_users.stride(0), _vp(rows.data_ptr()), als_users.shape[0], als_users.shape[1],
         _vp(tt_users.data_ptr()), tt_users.stride(0), tt_users.shape[1], B, _vp(als_item.data_ptr()),
         _vp(tt_item.data_ptr()), N, dk, _vp(als.data_ptr()), _vp(tt.data_ptr()), N, _vp(a_mm.data_ptr()),
         _vp(t_mm.data_ptr()), _vp(ws.data_ptr()), need, _stream()))
     return als, tt, a_mm, t_mm
+
+
+PRUNE_MAX_K = 8
+
+
+class HybridPrune:
+    """The pruned bf16 hybrid top-k (hrec_hybrid_prune_*) for one batch
+    shape: minmax() -> (als_mm, tt_mm) [2, B] (all-reduce them across item
+    shards), then topk(als_mm, tt_mm, als_wins, top_k, idx_offset) -> (ids
+    [B, kk] int64, fused f64 [B, kk]). Same user / item arguments as
+    hybrid_scores; the workspace carries phase 1 into phase 2."""
+
+    def __init__(self, als_users, als_rows, tt_users, als_item, tt_item, top_k):
+        self.dk = _hyb_args(als_item, tt_item)
+        self.B, self.N = int(als_rows.shape[0]), int(als_item.shape[0])
+        if tt_item.shape[0] != self.N or tt_users.shape[0] != self.B:
+            raise HrecError("hybrid_prune: item counts / batch sizes differ")
+        for t, name in ((als_users, "als_users"), (tt_users, "tt_users")):
+            if t.dtype != torch.float32 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+                raise HrecError(f"hybrid_prune: {name} must be a row-major float32 device matrix")
+            if t.shape[1] > self.dk:
+                raise HrecError(f"hybrid_prune: {name} width {t.shape[1]} > operand width {self.dk}")
+        if not 1 <= int(top_k) <= PRUNE_MAX_K:
+            raise HrecError(f"hybrid_prune: top_k must be in [1, {PRUNE_MAX_K}]")
+        self.top_k = int(top_k)
+        self.kk = min(self.top_k, self.N)
+        self.U, self.rows, self.T = als_users, als_rows.to(torch.int64).contiguous(), tt_users
+        self.Va, self.Vt = als_item, tt_item
+        dev = als_item.device
+        self.need = int(lib().hrec_hybrid_prune_workspace_bytes(self.B, self.N, self.dk, self.top_k))
+        self.ws = torch.empty(self.need, dtype=torch.uint8, device=dev)
+
+    def _users(self):
+        return (_vp(self.U.data_ptr()), self.U.stride(0), _vp(self.rows.data_ptr()), self.U.shape[0], self.U.shape[1],
+                _vp(self.T.data_ptr()), self.T.stride(0), self.T.shape[1], self.B, _vp(self.Va.data_ptr()),
+                _vp(self.Vt.data_ptr()), self.N, self.dk)
+
+    def minmax(self):
+        dev = self.Va.device
+        a_mm = torch.empty((2, self.B), dtype=torch.float32, device=dev)
+        t_mm = torch.empty((2, self.B), dtype=torch.float32, device=dev)
+        _check("hrec_hybrid_prune_minmax", lib().hrec_hybrid_prune_minmax(
+            *self._users(), _vp(a_mm.data_ptr()), _vp(t_mm.data_ptr()), _vp(self.ws.data_ptr()), self.need,
+            _stream()))
+        return a_mm, t_mm
+
+    def topk(self, als_mm, tt_mm, als_wins, idx_offset=0):
+        dev = self.Va.device
+        out_i = torch.empty((self.B, self.kk), dtype=torch.int64, device=dev)
+        out_v = torch.empty((self.B, self.kk), dtype=torch.float64, device=dev)
+        _check("hrec_hybrid_prune_topk", lib().hrec_hybrid_prune_topk(
+            *self._users(), _dev(als_mm, torch.float32, "als_mm"), _dev(tt_mm, torch.float32, "tt_mm"),
+            int(bool(als_wins)), self.top_k, int(idx_offset), _vp(out_i.data_ptr()), _vp(out_v.data_ptr()),
+            _vp(self.ws.data_ptr()), self.need, _stream()))
+        return out_i, out_v
+
+    def fallback_taken(self):
+        """Whether the last topk() took the exact unfused path (device flag)."""
+        out = torch.empty(1, dtype=torch.int32, device=self.Va.device)
+        _check("hrec_hybrid_prune_fallback_taken", lib().hrec_hybrid_prune_fallback_taken(
+            _vp(self.ws.data_ptr()), self.B, self.N, self.dk, self.top_k, _vp(out.data_ptr()), _stream()))
+        return bool(int(out.item()))
 
 
 def _hyb_args(*ops):

@@ -144,6 +144,24 @@ class DeviceALSFactors:
         return cls(user_ids, item_ids, U, V, k)
 
 
+class _PyInts:
+    """Candidate ids from a pandas Index / Series: element i is the Python int
+    the Series iteration yields (vals.item(i)); the list is built only if
+    someone iterates (the per-item list path)."""
+
+    def __init__(self, vals):
+        self.vals = vals
+
+    def __len__(self):
+        return len(self.vals)
+
+    def __getitem__(self, i):
+        return self.vals.item(i)
+
+    def __iter__(self):
+        return iter(self.vals.tolist())
+
+
 def _int_ids(col, name):
     a = np.asarray(col)
     if a.dtype.kind == "f":
@@ -253,16 +271,38 @@ class ALSModel:
             if not ok(type(x)):
                 raise TypeError(f"field itemId: IntegerType() can not accept object {x!r} in type {type(x)}")
 
+    @staticmethod
+    def _id_array(all_items):
+        """(items, int64 keys) for an integer numpy array / pandas Index /
+        Series of candidate ids without a per-element Python pass, else None.
+        `items` is indexable and iterates like `all_items` does in the
+        reference's loop (:70): a numpy array yields numpy scalars, an Index or
+        Series Python ints."""
+        if isinstance(all_items, np.ndarray):
+            if all_items.ndim == 1 and all_items.dtype.kind in "iu":
+                return all_items, np.asarray(all_items).astype(np.int64, copy=False)
+            return None
+        import pandas as pd
+
+        if isinstance(all_items, (pd.Index, pd.Series)) and all_items.dtype.kind in "iu":
+            vals = all_items.to_numpy()
+            return _PyInts(vals), vals.astype(np.int64, copy=False)
+        return None
+
     def _score_device(self, user_id, all_items):
         """predict_for_user up to the transform: (items, int64 keys, f32 device
         scores [n] or None). Raises where the reference's createDataFrame /
         transform would."""
-        items = list(all_items)
         self._check_int_ids([user_id])
-        self._check_int_ids(items)
-        if not items:
+        fast = self._id_array(all_items)
+        if fast is not None:
+            items, keys = fast
+        else:
+            items = list(all_items)
+            self._check_int_ids(items)
+            keys = np.fromiter(items, np.int64, len(items)) if items else None
+        if len(items) == 0:
             return items, None, None
-        keys = np.fromiter(items, np.int64, len(items))
         return items, keys, self.model.score([user_id], keys)[0]
 
     def _predict_device(self, user_id, all_items):

@@ -56,6 +56,7 @@ class DeviceOps:
 
     dot_scores = staticmethod(_hrec.dot_scores)
     hybrid_scores = staticmethod(_hrec.hybrid_scores)
+    hybrid_prune = staticmethod(_hrec.HybridPrune)
     rows_minmax = staticmethod(_hrec.rows_minmax)
     fuse_rows_topk = staticmethod(_hrec.fuse_rows_topk)
     topk_keyed = staticmethod(_hrec.topk_keyed)
@@ -65,12 +66,16 @@ class ShardedRecommender:
     """precision "exact": JVM-exact ALS scores (Spark's f32 mul/add chain) and
     f32 two-tower Dot — the reference's numerics. precision "bf16" (BASELINE
     config c5: rank-256 factors and d = 256 towers stored in bf16): both
-    score matrices on the bf16 matrix cores (hrec_dot_scores, f32
-    accumulation) from bf16 copies of the factors / item vectors made once
-    here; pass V_local (the shard's ALS item factor rows) instead of Vt_local."""
+    models' scores on the bf16 matrix cores (f32 accumulation) from bf16
+    copies of the factors / item vectors made once here; pass V_local (the
+    shard's ALS item factor rows) instead of Vt_local. For top_k <= 8 the bf16
+    path is the pruned one (hrec_hybrid_prune_*: no score matrix in HBM,
+    exact fallback gated on the device); pruned=False keeps the score
+    matrices (hrec_hybrid_scores + hrec_fuse_rows_topk); all three bf16
+    paths return the same bits."""
 
     def __init__(self, U, Vt_local, item_vecs_local, item_offset, k, world=1, rank=0, group=None, ops=None,
-                 precision="exact", V_local=None, fused=False):
+                 precision="exact", V_local=None, fused=False, pruned=True):
         self.U = U                          # [n_users, kp] ALS user factors (replicated)
         self.Vt = Vt_local                  # [kp, ld] transposed ALS item factors of this shard
         self.iv = item_vecs_local           # [n_local, d] two-tower item vectors of this shard
@@ -92,6 +97,7 @@ class ShardedRecommender:
             # are cheap and the fused path's per-batch overflow check (a host
             # sync) costs more than it saves
             self.fused = bool(fused) and hasattr(self.ops, "hybrid_topk")
+            self.pruned = bool(pruned) and hasattr(self.ops, "hybrid_prune")
             self.V_op = self.ops.operand(V_local, torch.bfloat16, self.dk)
             self.iv_op = self.ops.operand(item_vecs_local, torch.bfloat16, self.dk)
 
@@ -139,11 +145,41 @@ class ShardedRecommender:
             return idx, val
         return merge_candidates(idx, val, top_k, self.world, self.group, o)
 
+    def _recommend_pruned(self, user_rows, user_vecs, als_wins, top_k):
+        """bf16 path without score matrices (hrec_hybrid_prune_*): phase 1 gives
+        each user's min / max of both rows (C2 makes them global), phase 2 the
+        local top-k from the heavier model's survivors."""
+        o = self.ops
+        B = int(user_rows.shape[0])
+        dev = user_vecs.device
+        if self.n_local > 0:
+            hp = o.hybrid_prune(self.U, user_rows, user_vecs, self.V_op, self.iv_op, top_k)
+            a_mm, t_mm = hp.minmax()
+        else:
+            inf = float("inf")
+            a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
+            t_mm = a_mm.clone()
+        if self.world > 1:
+            for mm in (a_mm, t_mm):
+                dist.all_reduce(mm[0], op=dist.ReduceOp.MIN, group=self.group)
+                dist.all_reduce(mm[1], op=dist.ReduceOp.MAX, group=self.group)
+        if self.n_local > 0:
+            idx, val = hp.topk(a_mm, t_mm, als_wins, self.offset)
+            self.last_prune = hp
+        else:
+            idx = torch.empty((B, 0), dtype=torch.int64, device=dev)
+            val = torch.empty((B, 0), dtype=torch.float64, device=dev)
+        if self.world == 1:
+            return idx, val
+        return merge_candidates(idx, val, top_k, self.world, self.group, o)
+
     def recommend(self, user_rows, user_vecs, als_wins, top_k):
         """user_rows: [B] int64 ALS rows; user_vecs: [B, d] two-tower user
         vectors. Returns (global item ids [B, k], fused scores f64 [B, k])."""
         if self.precision == "bf16" and self.fused:
             return self._recommend_fused(user_rows, user_vecs, als_wins, top_k)
+        if self.precision == "bf16" and self.pruned and 1 <= int(top_k) <= _hrec.PRUNE_MAX_K:
+            return self._recommend_pruned(user_rows, user_vecs, als_wins, top_k)
         o = self.ops
         B = int(user_rows.shape[0])
         dev = user_vecs.device
@@ -231,6 +267,10 @@ class CapturedRecommend:
 
         cap = CapturedRecommend(rec, user_rows, user_vecs, als_wins, top_k)
         idx, val = cap(new_user_rows, new_user_vecs)   # same shapes
+
+    Each call returns fresh tensors (copies of the graph's static outputs, B x k
+    elements), so results kept or queued by a serving loop are not overwritten
+    by the next replay.
     """
 
     def __init__(self, rec, user_rows, user_vecs, als_wins, top_k, warmup=2):
@@ -254,4 +294,4 @@ class CapturedRecommend:
         if user_vecs is not None:
             self.vecs.copy_(user_vecs)
         self.graph.replay()
-        return self.out
+        return self.out[0].clone(), self.out[1].clone()

@@ -37,7 +37,8 @@
 extern "C" {
 #endif
 
-#define HREC_ABI_VERSION 1
+/* 2: hrec_fuse_topk gained out_minmax; hrec_hybrid_scores gained n_als_rows. */
+#define HREC_ABI_VERSION 2
 
 #define HREC_OK 0
 #define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
@@ -417,18 +418,57 @@ int hrec_hybrid_topk(const void* als_user, const void* tt_user, int n_users, con
  * (ALS transform + Keras Dot over every candidate, src/hybrid_system.py:95-116)
  * and the per-model MinMaxScaler extremes it fits (src/hybrid_system.py:57-75).
  * User rows are f32 (ALS: als_users[als_rows[b] * als_ld + c], als_rows may
- * be NULL for row b; two-tower: tt_users[b * tt_ld + c]), converted to bf16
+ * be NULL for row b; a row outside [0, n_als_rows) — an unknown user — gives
+ * a NaN score row, as hrec_als_score does for row -1, whose min / max are
+ * +inf / -inf; two-tower: tt_users[b * tt_ld + c]), converted to bf16
  * (round to nearest even) for columns c < width and zero up to dk; item
  * operands are bf16 [n_items, dk], dk in {64, 128, 256}. Writes
  * als_out / tt_out [n_users, ld_out] f32 (bit-identical to hrec_dot_scores on
  * hrec_f32_to_bf16 operands) and als_mm / tt_mm [2, n_users] f32 =
  * hrec_rows_minmax_f32 of those rows. */
 size_t hrec_hybrid_scores_workspace_bytes(int n_users, int64_t n_items);
-int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* als_rows, int als_width,
+int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* als_rows,
+                       int64_t n_als_rows, int als_width,
                        const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                        const void* als_items, const void* tt_items, int64_t n_items, int dk,
                        float* als_out, float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm,
                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------
+ * Pruned bf16 hybrid top-k (csrc/hybrid_prune.hip, BASELINE config c5):
+ * get_hybrid_recommendations for a batch of users over an item shard
+ * (src/hybrid_system.py:57-75, :108) without writing either score matrix.
+ * Same arguments as hrec_hybrid_scores for the users / items; results bit for
+ * bit those of hrec_hybrid_scores + hrec_fuse_rows_topk.
+ * Phase 1 (hrec_hybrid_prune_minmax): per-user [min | max] of both score rows
+ *   into als_mm / tt_mm ([2, n_users] f32, the hrec_rows_minmax_f32 layout)
+ *   and, in the workspace, each item group's maximum slice. With the items
+ *   sharded, all-reduce the mins (MIN) and maxes (MAX) across shards before
+ *   phase 2.
+ * Phase 2 (hrec_hybrid_prune_topk): with the (global) min / max: a lower
+ *   bound of each user's k-th best fused score from the group maxima, the
+ *   heavier-weighted model's scores filtered against it, the survivors' other
+ *   score and fused score, the stable top-k (ties -> smaller item; ids +
+ *   idx_offset). Lists that overflow, users with non-finite scores or fewer
+ *   survivors than k take the exact unfused path, gated on the device (no host
+ *   round trip; hrec_hybrid_prune_fallback_taken copies that flag).
+ * top_k in [1, 8]; the workspace (hrec_hybrid_prune_workspace_bytes, the same
+ * dk and top_k) carries phase 1's state into phase 2 and holds the fallback's
+ * two score matrices (2 n_users n_items floats). n_users < 65536. */
+size_t hrec_hybrid_prune_workspace_bytes(int n_users, int64_t n_items, int dk, int top_k);
+int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, const int64_t* als_rows,
+                             int64_t n_als_rows, int als_width, const float* tt_users, int64_t tt_ld,
+                             int tt_width, int n_users, const void* als_items, const void* tt_items,
+                             int64_t n_items, int dk, float* als_mm, float* tt_mm, void* workspace,
+                             size_t workspace_bytes, void* stream);
+int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, const int64_t* als_rows,
+                           int64_t n_als_rows, int als_width, const float* tt_users, int64_t tt_ld,
+                           int tt_width, int n_users, const void* als_items, const void* tt_items,
+                           int64_t n_items, int dk, const float* als_mm, const float* tt_mm, int als_wins,
+                           int top_k, int64_t idx_offset, int64_t* out_idx, double* out_val,
+                           void* workspace, size_t workspace_bytes, void* stream);
+int hrec_hybrid_prune_fallback_taken(const void* workspace, int n_users, int64_t n_items, int dk,
+                                     int top_k, int* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -242,3 +242,50 @@ def item_vectors(n_slice, n_total, d, n_man=2651, n_cat=255, chunk=1 << 18, seed
     return _line(n_slice / dt, "items/s", "port", (
         f"torch-CPU f32 Keras item tower (Dense(16, relu) + concat + Dense({d}) + LayerNorm) over {n_slice} of the "
         f"{n_total} catalogue items, {dt:.2f} s"), cores)
+
+
+# ------------------------------------------------------------- API call
+def api_call(n_items, k, d, top_k, users=8, seed=0):
+    """One get_hybrid_recommendations call per user on the CPU, restated:
+    Spark's JVM-exact f32 transform over every candidate (the per-rank
+    sequential mul/add of oracle/als.py, vectorised over items), the Keras
+    item tower + user tower + Dot (torch-CPU f32) over the same candidates,
+    the per-model MinMaxScaler fusion in f64 (src/hybrid_system.py:57-75) and
+    the stable sorted()[:top_k] (:108)."""
+    from . import als as oals
+
+    cores = _setup()
+    g = torch.Generator().manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    U = rng.normal(size=(users + 1, k)).astype(np.float32)
+    V = rng.normal(size=(n_items, k)).astype(np.float32)
+    p = _init((users + 1, n_items, 2651, 255), d, g)
+    item = torch.arange(n_items)
+    man = torch.randint(0, 2651, (n_items,), generator=g)
+    cat = torch.randint(0, 255, (n_items,), generator=g)
+    num = torch.rand((n_items, 2), generator=g)
+
+    def call(u):
+        a = oals.score_matrix(U[u: u + 1], V)[0].astype(np.float64)
+        iv = item_tower(p, item, man, cat, num)[0]
+        uv = _ln(p["user_emb"][u: u + 1], p["gu"], p["bu"])[0]
+        t = (iv @ uv[0]).numpy()
+
+        def mm(x):
+            lo, hi = x.min(), x.max()
+            r = hi - lo
+            r = 1.0 if r < 10 * np.finfo(x.dtype).eps else r
+            return (x - lo) / r
+
+        fused = 0.2 * mm(a) + 0.8 * mm(t).astype(np.float64)
+        return np.argsort(-fused, kind="stable")[:top_k]
+
+    call(users)
+    t0 = time.perf_counter()
+    for u in range(users):
+        call(u)
+    dt = (time.perf_counter() - t0) / users
+    return _line(1.0 / dt, "users/s", "port", (
+        f"one user per call over {n_items} candidates: JVM-exact f32 ALS transform (rank {k}, numpy, "
+        f"oracle/als.py score_matrix) + Keras item/user towers and Dot (d = {d}, torch-CPU f32) + f64 min-max "
+        f"fusion + stable top-{top_k}; {users} users, {dt * 1e3:.1f} ms each"), cores)

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared if not hasattr(lib, n)]
     assert not missing, missing
     lib.hrec_abi_version.restype = ctypes.c_int
-    assert lib.hrec_abi_version() == 1
+    assert lib.hrec_abi_version() == 2
 
 
 def test_python_binding_covers_the_header():
@@ -70,14 +70,18 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     # bf16 hybrid scores: operand width and workspace are checked first
     hs = lib.hrec_hybrid_scores
     hs.restype = ctypes.c_int
-    hs.argtypes = ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+    hs.argtypes = ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                    ctypes.c_int64,
                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
                    + [ctypes.c_void_p] * 2 + [ctypes.c_int64] + [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_void_p])
-    assert hs(None, 96, None, 96, None, 96, 96, 4, None, None, 10, 96, None, None, 10, None, None, None, 0, None) == -1
+    assert hs(None, 96, None, 0, 96, None, 96, 96, 4, None, None, 10, 96, None, None, 10, None, None, None, 0, None) == -1
     assert b"dk must be 64, 128 or 256" in lib.hrec_last_error()
-    assert hs(None, 64, None, 64, None, 64, 64, 4, None, None, 10, 64, None, None, 10, None, None, None, 0, None) == -1
+    assert hs(None, 64, None, 0, 64, None, 64, 64, 4, None, None, 10, 64, None, None, 10, None, None, None, 0, None) == -1
     assert b"null min/max output or workspace" in lib.hrec_last_error()
-    assert hs(None, 64, None, 64, None, 64, 64, 0, None, None, 10, 64, None, None, 10, None, None, None, 0,
+    assert hs(None, 64, None, -1, 64, None, 64, 64, 4, None, None, 10, 64, None, None, 10, None, None, None, 0,
+              None) == -1
+    assert b"negative n_als_rows" in lib.hrec_last_error()
+    assert hs(None, 64, None, 0, 64, None, 64, 64, 0, None, None, 10, 64, None, None, 10, None, None, None, 0,
               None) == 0  # no users: nothing to do
 
 

@@ -944,3 +944,40 @@ def test_als_device_lookup_matches_host(device):
     a = f.score([1], keys.astype(np.int64)).cpu().numpy()
     b = f.score([1], keys.tolist()).cpu().numpy()
     assert np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)])
+
+
+@pytest.mark.parametrize("als_wins", [True, False])
+def test_top_on_device_matches_numpy_fusion(device, als_wins):
+    """get_hybrid_recommendations' array path (_top_on_device) on
+    f64 ALS + f32 two-tower device scores against the reference arithmetic
+    written in numpy + sklearn (tests/test_oracle.py::_numpy_fusion). The
+    device fusion follows numpy 1.21.5's promotion (requirements.txt:5: the
+    Python-float weight times an np.float32 element widens to float64): top-k
+    ids and scores bit-exact against it. Against numpy 2's float32 product
+    (NEP 50, the container's numpy) the ids agree wherever the top-k is
+    separated by more than the f32 product's rounding (2^-24 relative)."""
+    from src.hybrid_system import HybridRecommendationSystem
+    from test_oracle import _numpy_fusion
+
+    rng = np.random.default_rng(31 + als_wins)
+    n, k = 50_000, 10
+    als = rng.normal(size=n) * 2
+    tt = (rng.normal(size=n) * 3).astype(np.float32)
+    frame = pd.DataFrame({"itemId": np.arange(n)})
+    h = HybridRecommendationSystem()
+    h.als_f1_score, h.twotower_f1_score = (0.5, 0.1) if als_wins else (0.1, 0.5)
+    keys = np.arange(n, dtype=np.int64)
+    top = h._top_on_device((keys.tolist(), keys, torch.as_tensor(als, device=device).float().double()),
+                           (frame, torch.as_tensor(tt, device=device)), k)
+    als_used = als.astype(np.float32).astype(np.float64)  # the ALS side hands over f32 transform scores
+    ref = _numpy_fusion(als_used, tt, als_wins, "1.21")
+    order = sorted(range(n), key=lambda j: ref[j], reverse=True)[:k]
+    assert top is not None
+    assert [i for i, _ in top] == order
+    assert [float(s) for _, s in top] == [float(ref[j]) for j in order]
+    np2 = _numpy_fusion(als_used, tt, als_wins, "2")
+    o2 = sorted(range(n), key=lambda j: np2[j], reverse=True)
+    gaps = np.abs(np.diff(np2[o2[: k + 1]]))
+    for j in range(k):
+        if gaps[j] > 1e-7 and (j == 0 or gaps[j - 1] > 1e-7):
+            assert top[j][0] == o2[j]

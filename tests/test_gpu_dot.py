@@ -246,6 +246,24 @@ def test_hybrid_scores_equals_dot_scores_and_minmax(device, dk, B, N, ka, kt):
     assert torch.equal(a_mm, h.rows_minmax(ref_a)) and torch.equal(t_mm, h.rows_minmax(ref_t))
 
 
+def test_hybrid_scores_unknown_rows_are_nan(device):
+    """an ALS row outside [0, n) (the -1 of an unknown user, or a
+    stale row) is never read: its score row is NaN (as hrec_als_score gives
+    for -1) and its min / max +inf / -inf; the other rows are unchanged."""
+    h = _h()
+    rng = np.random.default_rng(3)
+    U = torch.as_tensor(rng.normal(size=(10, 64)).astype(np.float32), device=device)
+    uv = torch.as_tensor(rng.normal(size=(4, 64)).astype(np.float32), device=device)
+    v = h.dot_operand(torch.as_tensor(rng.normal(size=(300, 64)).astype(np.float32), device=device), torch.bfloat16)
+    rows = torch.tensor([2, -1, 10, 1 << 40], dtype=torch.int64, device=device)
+    als, tt, a_mm, _ = h.hybrid_scores(U, rows, uv, v, v)
+    assert torch.isnan(als[1:]).all() and not torch.isnan(als[0]).any()
+    ref = h.dot_scores(h.dot_operand(U[2:3], torch.bfloat16), v)
+    assert torch.equal(als[0:1], ref)
+    assert torch.all(a_mm[0, 1:] == float("inf")) and torch.all(a_mm[1, 1:] == -float("inf"))
+    assert not torch.isnan(tt).any()
+
+
 def test_hybrid_scores_empty_catalogue(device):
     h = _h()
     U = torch.ones((4, 64), device=device)
@@ -301,6 +319,86 @@ def test_captured_recommend_matches_eager(device, precision):
     for wins in (True, False):
         cap = CapturedRecommend(rec, rows[0], vecs[0], wins, 5)
         for r, v in zip(rows, vecs):
-            gi, gv = (t.clone() for t in cap(r, v))
+            gi, gv = cap(r, v)
             ei, ev = rec.recommend(r, v, wins, 5)
             assert torch.equal(gi, ei) and torch.equal(gv, ev)
+
+
+def _unfused_bf16(h, U, rows, uv, va, vt, als_wins, k, offset=0):
+    als, tt, a_mm, t_mm = h.hybrid_scores(U, rows, uv, va, vt)
+    return h.fuse_rows_topk(als, tt, a_mm, t_mm, als_wins, k, offset), (a_mm, t_mm)
+
+
+@pytest.mark.parametrize("dk,B,N,ka,kt,k", [(256, 256, 100_003, 256, 256, 5), (256, 70, 20_000, 200, 250, 8),
+                                            (128, 130, 40_001, 100, 64, 1), (64, 33, 5_000, 48, 64, 3),
+                                            (64, 300, 777, 64, 33, 5), (256, 5, 9, 256, 7, 8), (128, 2, 1, 128, 128, 5)])
+def test_hybrid_prune_equals_unfused(device, dk, B, N, ka, kt, k):
+    """K9p (csrc/hybrid_prune.hip: no score matrix; bound from the group
+    maxima, heavy-model survivor filter, light scores of the survivors) ==
+    hrec_hybrid_scores + hrec_fuse_rows_topk bit for bit — ids, fused scores
+    and both min / max rows — for both weight orders, and on random data the
+    pruned path itself answered (no fallback)."""
+    h = _h()
+    rng = np.random.default_rng(B * 3 + N)
+    n_users = B + 7
+    U = torch.as_tensor(rng.normal(size=(n_users, ka)).astype(np.float32), device=device)
+    uv = torch.as_tensor(rng.normal(size=(B, kt)).astype(np.float32) / 4, device=device)
+    va = h.dot_operand(torch.as_tensor(rng.normal(size=(N, ka)).astype(np.float32), device=device), torch.bfloat16, dk)
+    vt = h.dot_operand(torch.as_tensor(rng.normal(size=(N, kt)).astype(np.float32), device=device), torch.bfloat16, dk)
+    rows = torch.as_tensor(rng.integers(0, n_users, B), dtype=torch.int64, device=device)
+    for wins in (True, False):
+        (ei, ev), (ea, et) = _unfused_bf16(h, U, rows, uv, va, vt, wins, k, 11)
+        hp = h.HybridPrune(U, rows, uv, va, vt, k)
+        a_mm, t_mm = hp.minmax()
+        assert torch.equal(a_mm, ea) and torch.equal(t_mm, et)
+        gi, gv = hp.topk(a_mm, t_mm, wins, 11)
+        assert torch.equal(gi, ei), (wins, (gi != ei).nonzero()[:5])
+        assert torch.equal(gv, ev)
+        if N >= 1000:
+            assert not hp.fallback_taken()
+
+
+def test_hybrid_prune_fallback_cases(device):
+    """The gated exact path answers (same bits as the unfused path) when the
+    pruned one cannot: every item identical (all fused scores tie: the
+    survivor list overflows), an unknown ALS row (NaN scores) and a catalogue
+    with tied maxima."""
+    h = _h()
+    rng = np.random.default_rng(12)
+    B, N, dk = 40, 30_000, 128
+    U = torch.as_tensor(rng.normal(size=(60, 128)).astype(np.float32), device=device)
+    uv = torch.as_tensor(rng.normal(size=(B, 128)).astype(np.float32), device=device)
+    same = np.tile(rng.normal(size=(1, 128)).astype(np.float32), (N, 1))
+    va = h.dot_operand(torch.as_tensor(same, device=device), torch.bfloat16, dk)
+    vt = h.dot_operand(torch.as_tensor(rng.normal(size=(N, 128)).astype(np.float32), device=device), torch.bfloat16, dk)
+    rows = torch.as_tensor(rng.integers(0, 60, B), dtype=torch.int64, device=device)
+    rows_bad = rows.clone()
+    rows_bad[3] = -1
+    for r, a_items, wins in ((rows, va, True), (rows_bad, vt, True), (rows_bad, vt, False)):
+        (ei, ev), _ = _unfused_bf16(h, U, r, uv, a_items, vt, wins, 5)
+        hp = h.HybridPrune(U, r, uv, a_items, vt, 5)
+        gi, gv = hp.topk(*hp.minmax(), wins)
+        assert hp.fallback_taken()
+        assert torch.equal(gi, ei)
+        np.testing.assert_array_equal(gv.cpu().numpy(), ev.cpu().numpy())  # NaN == NaN position-wise
+
+
+def test_recommender_bf16_paths_agree(device):
+    """ShardedRecommender precision "bf16": pruned (default), unfused
+    (pruned=False) and K9f (fused=True) return the same ids and scores."""
+    from src.recommend import ShardedRecommender
+
+    rng = np.random.default_rng(44)
+    n_users, n_items, k, d, B = 400, 50_000, 200, 256, 64
+    U = torch.as_tensor(rng.normal(size=(n_users, 256)).astype(np.float32), device=device)
+    V = torch.as_tensor(rng.normal(size=(n_items, k)).astype(np.float32), device=device)
+    iv = torch.as_tensor(rng.normal(size=(n_items, d)).astype(np.float32), device=device)
+    uv = torch.as_tensor(rng.normal(size=(B, d)).astype(np.float32), device=device)
+    rows = torch.as_tensor(rng.choice(n_users, B, replace=False), device=device)
+    recs = [ShardedRecommender(U, None, iv, 0, k, precision="bf16", V_local=V, **kw)
+            for kw in ({}, {"pruned": False}, {"fused": True})]
+    for wins in (True, False):
+        outs = [r.recommend(rows, uv, wins, 5) for r in recs]
+        for i, v in outs[1:]:
+            assert torch.equal(outs[0][0], i) and torch.equal(outs[0][1], v)
+    assert not recs[0].last_prune.fallback_taken()

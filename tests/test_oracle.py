@@ -265,3 +265,61 @@ def test_cpu_baseline_keras_step_matches_oracle():
         ott.train_step(po, so, u, i, m, c, x, y, it)
     for n, t in p.items():
         np.testing.assert_allclose(t.numpy(), po[names.get(n, n)], rtol=1e-4, atol=1e-6, err_msg=n)
+
+
+def _numpy_fusion(als, tt, als_wins, promotion):
+    """The reference's adaptive_fusion arithmetic (src/hybrid_system.py:62-72)
+    written with numpy + sklearn directly on arrays in candidate order: als
+    float64 (Python floats), tt float32 (np.float32 Keras scores), one
+    MinMaxScaler.fit_transform per model, then w0 * als_norm[i] + w1 *
+    tt_norm[i] per item. promotion "1.21": w1 * np.float32 -> float64 (numpy
+    1.21.5, requirements.txt:5, value-based casting of the Python float);
+    "2": NEP 50, the float32 product numpy >= 2 computes."""
+    from sklearn.preprocessing import MinMaxScaler
+
+    a = MinMaxScaler().fit_transform(np.asarray(als, np.float64).reshape(-1, 1)).flatten()
+    t = MinMaxScaler().fit_transform(np.asarray(tt, np.float32).reshape(-1, 1)).flatten()
+    w = (0.8, 0.2) if als_wins else (0.2, 0.8)
+    if promotion == "1.21":
+        return w[0] * a + w[1] * t.astype(np.float64)
+    return w[0] * a + (np.float32(w[1]) * t).astype(np.float64)
+
+
+@pytest.mark.parametrize("als_wins", [True, False])
+def test_fusion_oracle_matches_numpy_sklearn(als_wins):
+    """oracle.fusion.adaptive_fusion (the restatement the device fusion is
+    checked against) == the numpy/sklearn arithmetic above: legacy=True is
+    numpy 1.21's promotion bit for bit, legacy=False numpy 2's (the container
+    runs numpy 2, so the latter is also exactly what the reference's own
+    Python computes here)."""
+    rng = np.random.default_rng(3 + als_wins)
+    n = 3000
+    ids = list(range(n))
+    als = rng.normal(size=n) * 2
+    tt = (rng.normal(size=n) * 3).astype(np.float32)
+    tt[::50] = tt[0]   # ties
+    for legacy, promo in ((True, "1.21"), (False, "2")):
+        got = ofus.adaptive_fusion(list(zip(ids, als.tolist())), list(zip(ids, tt)), *((0.5, 0.1) if als_wins
+                                   else (0.1, 0.5)), legacy=legacy)
+        assert [i for i, _ in got] == ids   # dense ids: the set union iterates ascending
+        np.testing.assert_array_equal(np.array([s for _, s in got], np.float64),
+                                      _numpy_fusion(als, tt, als_wins, promo))
+
+
+def test_parity_rule_decided_positions():
+    """tests/parity_rules.py (the served-ranking rule of the trained-model GPU
+    tests): a position is decided iff its item cannot trade places with any
+    other under the tolerances; a swap at a decided position fails, one
+    inside an undecided tie passes."""
+    from parity_rules import check_served, decided_positions
+
+    o = np.array([5.0, 9.0, 7.0, 7.00001, 1.0, 3.0])
+    t = np.full(6, 1e-3)
+    order, dec = decided_positions(o, t, 4)
+    assert order.tolist() == [1, 3, 2, 0, 5, 4]
+    assert dec.tolist() == [True, False, False, True]
+    ids = list("abcdef")
+    assert check_served(["b", "c", "d", "a"], ids, o, t, 4) is False   # the 7 / 7.00001 tie may swap
+    with pytest.raises(AssertionError):
+        check_served(["c", "b", "d", "a"], ids, o, t, 4)                # position 0 is decided
+    assert check_served(["b", "d", "c", "a"], ids, o, np.full(6, 1e-9), 4) is True
