@@ -147,7 +147,7 @@ def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
                % rec.dk, hp.minmax,
                dict(bound="hbm", work=2 * op_b, peak=HBM_PEAK_GBS, unit="GB/s", mfma_flops=2 * 2.0 * rec.dk * B * N)),
               ("hybrid_prune_topk (bound + heavier model's bf16 GEMM with survivor filter + survivors' fusion "
-               "+ stable top-k)", lambda: hp.topk(a_mm, t_mm, False, top_k, rec.offset),
+               "+ stable top-k)", lambda: hp.topk(a_mm, t_mm, False, rec.offset),
                dict(bound="hbm", work=op_b, peak=HBM_PEAK_GBS, unit="GB/s", mfma_flops=2.0 * rec.dk * B * N))]
         out = []
         for name, fn, rf in st:
@@ -159,9 +159,11 @@ def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
                               "frac": tf / BF16_MFMA_PEAK_TFLOPS}
             out.append(r)
         fell_back = hp.fallback_taken()
+        surv = hp.survivors().double()
         tot = sum(r["avg_launch_ms"] for r in out)
         dom = max(out, key=lambda r: r["avg_launch_ms"])
         return dict(dom, stages=out, fallback_taken=fell_back,
+                    survivors_per_user={"mean": float(surv.mean()), "max": float(surv.max())},
                     batch_view={"ms": tot, "algorithmic_bytes": 2 * op_b,
                                 "note": "no-store bytes (both item operands once) / both phases' time",
                                 "achieved": 2 * op_b / (tot * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

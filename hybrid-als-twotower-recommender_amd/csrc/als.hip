@@ -1337,6 +1337,11 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
   HREC_REQUIRE(n_src > 0 && src_factors && indices && values,
                "als_half_sweep: null source factors / CSR arrays");
   HREC_REQUIRE(n_src < 0x7fffffffll, "als_half_sweep: too many source rows for one launch");
+  // the kp-64 gather addresses source rows through one buffer resource, whose
+  // 32-bit byte offsets span 4 GiB (16.7M f32 rows of 64)
+  HREC_REQUIRE(kp != 64 || n_src * (int64_t)kp * 4 <= (int64_t)0xffffffffll,
+               "als_half_sweep: %lld source rows of %d floats exceed the 4 GiB a gather resource spans; shard the "
+               "source side", (long long)n_src, kp);
   if (kp > 64) {
     HREC_REQUIRE(accum_mode == 0, "als_half_sweep: kp > 64 supports accum_mode 0 (f64) only");
     return hrec_als_half_sweep_wide(indptr, indices, values, n_rows, src_factors, n_src, k, kp, reg_param,
@@ -1396,6 +1401,8 @@ extern "C" int hrec_als_half_sweep_src64(const int64_t* indptr, const int32_t* i
   HREC_REQUIRE(k >= 1 && k <= kp, "als_half_sweep_src64: need 1 <= k <= kp (k=%d kp=%d)", k, kp);
   HREC_REQUIRE(n_rows >= 0 && n_src >= 0, "als_half_sweep_src64: negative size");
   HREC_REQUIRE(n_rows < 0x7fffffffll && n_src < 0x7fffffffll, "als_half_sweep_src64: too many rows for one launch");
+  HREC_REQUIRE(n_src * (int64_t)kp * 8 <= (int64_t)0xffffffffll,
+               "als_half_sweep_src64: %lld f64 source rows exceed the 4 GiB a gather resource spans", (long long)n_src);
   HREC_REQUIRE(reg_param >= 0.0, "als_half_sweep_src64: reg_param must be >= 0");
   if (n_rows == 0) return HREC_OK;
   HREC_REQUIRE(indptr && dst_factors, "als_half_sweep_src64: null pointer");

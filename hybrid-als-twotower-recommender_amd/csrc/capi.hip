@@ -1,6 +1,9 @@
 // Error plumbing and version of the C-ABI (include/hrec.h).
 #include <stdarg.h>
 
+#include <mutex>
+#include <unordered_set>
+
 #include "common.h"
 
 namespace hrec {
@@ -21,6 +24,18 @@ int check_launch(const char* what) {
     return HREC_E_LAUNCH;
   }
   return HREC_OK;
+}
+
+// Kernels that take more than 64 KiB of dynamic LDS need the attribute raised
+// once (per process: the attribute belongs to the kernel, not the launch).
+bool allow_max_lds_ptr(const void* kfn) {
+  static std::mutex mu;
+  static std::unordered_set<const void*> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count(kfn)) return true;
+  if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
+  done.insert(kfn);
+  return true;
 }
 
 }  // namespace hrec

@@ -47,6 +47,34 @@ template <typename T>
 int sort_topk_rows(const T* vals, int64_t n_rows, int64_t n, int64_t row_stride, int kk, int64_t* out_idx,
                    T* out_val, void* ws, size_t ws_bytes, hipStream_t s);
 
+// Buffer resource over rows [row0, n_rows) of a row-major matrix of
+// row_bytes (< 2^14) per row, for structured loads (vindex = row - row0).
+// The hardware forms vindex * stride + voffset as a 32-bit offset, which
+// wraps at 4 GiB, so a resource never spans more than that: streaming
+// kernels re-base it per tile (rows past the span read as zeros, like rows
+// past the end of the matrix).
+typedef int hrec_rsrc_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ hrec_rsrc_t rows_rsrc(const void* base, int64_t row0, int row_bytes, int64_t n_rows) {
+  const uint64_t a = (uint64_t)base + (uint64_t)row0 * (uint64_t)row_bytes;
+  const int64_t span = (int64_t)(0xffffffffull / (uint64_t)row_bytes);
+  int64_t rem = n_rows - row0;
+  rem = rem < 0 ? 0 : (rem > span ? span : rem);
+  hrec_rsrc_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) | (row_bytes << 16));
+  r.z = __builtin_amdgcn_readfirstlane((int)(uint32_t)rem);
+  r.w = 0x00020000;
+  return r;
+}
+
+// Allow a kernel the CU's whole LDS (160 KiB) as dynamic shared memory, once
+// per kernel (hipFuncSetAttribute costs a runtime call per launch otherwise).
+bool allow_max_lds_ptr(const void* kfn);  // csrc/capi.hip: a set of the kernels already raised
+template <typename K>
+inline bool allow_max_lds(K kfn) {
+  return allow_max_lds_ptr((const void*)kfn);
+}
+
 // splitmix64 finaliser; host and device identical (integer only).
 __host__ __device__ inline uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;

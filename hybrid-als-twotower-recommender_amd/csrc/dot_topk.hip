@@ -146,34 +146,33 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
   constexpr int PB = FILTER ? 4 : 2;
   constexpr int P = BF16 ? (S::kSteps < PB ? S::kSteps : PB) : (S::kSteps < 2 ? S::kSteps : 2);
   static_assert(S::kSteps % P == 0, "ring depth must divide the k steps");
-  const uint64_t vb = (uint64_t)V;
-  dot_rsrc rsrc;
-  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
-  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * S::kElem) << 16));
-  rsrc.z = __builtin_amdgcn_readfirstlane((int)n_rows);
-  rsrc.w = 0x00020000;
+  // one resource per item tile, based at the tile's first row (row indices
+  // relative to it: a resource spans at most 4 GiB, see rows_rsrc)
   const int voff = 16 * g;
+  auto rsrc_of = [&](int64_t tile) { return rows_rsrc(V, tile * TL::kItems * item_step, DK * S::kElem, n_rows); };
   auto rows_of = [&](int64_t tile, int (&vi)[NI]) {
     const int64_t jb = tile * TL::kItems + 16 * NI * wi;
 #pragma unroll
     for (int t = 0; t < NI; ++t) {
       const int64_t j = jb + 16 * t + c;
-      vi[t] = j < n_items ? (int)(j * item_step) : 0x7fffffff;
+      vi[t] = j < n_items ? (int)((j - tile * TL::kItems) * item_step) : 0x7fffffff;
     }
   };
   int vcur[NI], vnext[NI];
   rows_of(ig, vcur);
+  dot_rsrc rs_cur = rsrc_of(ig), rs_next = rs_cur;
   DotFrag ring[P][NI];
 #pragma unroll
   for (int q = 0; q < P; ++q)
 #pragma unroll
-    for (int t = 0; t < NI; ++t) ring[q][t].f = dot_sbuf_load(rsrc, vcur[t], voff + 64 * q, 0, 0);
+    for (int t = 0; t < NI; ++t) ring[q][t].f = dot_sbuf_load(rs_cur, vcur[t], voff + 64 * q, 0, 0);
   DotFrag ua[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) ua[u] = user_frag(u, 0);
   for (int64_t it = ig; it < n_it; it += n_ig) {
     const int64_t j0 = it * TL::kItems + 16 * NI * wi;
     rows_of(it + n_ig, vnext);
+    rs_next = rsrc_of(it + n_ig);
     dot_f4 acc[NU][NI];
 #pragma unroll
     for (int u = 0; u < NU; ++u)
@@ -190,7 +189,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
 #pragma unroll
         for (int t = 0; t < NI; ++t) {
           b[t] = ring[q][t];
-          ring[q][t].f = dot_sbuf_load(rsrc, same ? vcur[t] : vnext[t], off, 0, 0);
+          ring[q][t].f = dot_sbuf_load(same ? rs_cur : rs_next, same ? vcur[t] : vnext[t], off, 0, 0);
         }
         const int kn = ks + 1 < S::kSteps ? ks + 1 : 0;
 #pragma unroll
@@ -207,6 +206,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_tile_kernel(
     }
 #pragma unroll
     for (int t = 0; t < NI; ++t) vcur[t] = vnext[t];
+    rs_cur = rs_next;
     if constexpr (!FILTER) {
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
@@ -353,23 +353,20 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   }
   __syncthreads();
   const int xq = c ^ g;
-  const uint64_t vb = (uint64_t)V;
-  dot_rsrc rsrc;
-  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
-  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * S::kElem) << 16));
-  rsrc.z = __builtin_amdgcn_readfirstlane((int)n_rows);
-  rsrc.w = 0x00020000;
+  // one resource per item tile, based at the tile's first row (rows_rsrc)
   const int voff = 16 * g;
+  auto rsrc_of = [&](int64_t tile) { return rows_rsrc(V, tile * kItems * item_step, DK * S::kElem, n_rows); };
   auto rows_of = [&](int64_t tile, int (&vi)[NI]) {
     const int64_t jb = tile * kItems + 16 * NI * w;
 #pragma unroll
     for (int t = 0; t < NI; ++t) {
       const int64_t j = jb + 16 * t + c;
-      vi[t] = (tile < n_it && j < n_items) ? (int)(j * item_step) : 0x7fffffff;
+      vi[t] = (tile < n_it && j < n_items) ? (int)((j - tile * kItems) * item_step) : 0x7fffffff;
     }
   };
   int vnext[NI];
   rows_of(ig, vnext);
+  dot_rsrc rsrc = rsrc_of(ig);
   DotFrag it_f[KS][NI];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
@@ -385,6 +382,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   for (int64_t it = ig; it < n_it; it += n_ig) {
     const int64_t j0 = it * kItems + 16 * NI * w;
     rows_of(it + n_ig, vnext);
+    rsrc = rsrc_of(it + n_ig);  // the last chunk refills the fragments with the next tile's
     auto user_frag = [&](int ch, int u, int ks) {
       DotFrag a;
       const int off = kSwz ? 16 * ((4 * ks) ^ xq) : 64 * ks + 16 * g;
@@ -581,7 +579,7 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
 #define HREC_DOTR(BF, DK)                                                                                      \
   do {                                                                                                         \
     auto kfn = dot_res_pick<BF, DK, FILTER>(ni);                                                               \
-    if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+    if (!allow_max_lds(kfn))                                                                                   \
       return check_launch("dot_res_kernel: LDS attribute");                                                   \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, u, B, UB, v, n_rows, n_items, step, n_ut, out, ldo, thr,         \
                        thr_stride, cap, cv, ci, cn, off);                                                      \

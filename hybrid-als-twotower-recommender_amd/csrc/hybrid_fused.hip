@@ -158,42 +158,40 @@ __global__ __launch_bounds__(kHyThreads) void hybrid_tile_kernel(
       a.i = *reinterpret_cast<const int4*>((m ? ubase_t : ubase_a) + 16 * u * S::kRowB + off);
       return a;
     };
-    hy_rsrc ra, rt;
-    {
-      const uint64_t va = (uint64_t)Va, vt = (uint64_t)Vt;
-      ra.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)va);
-      ra.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(va >> 32) | ((DK * 2) << 16));
-      rt.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vt);
-      rt.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vt >> 32) | ((DK * 2) << 16));
-      ra.z = rt.z = __builtin_amdgcn_readfirstlane((int)n_rows);
-      ra.w = rt.w = 0x00020000;
-    }
+    // resources per item tile, based at the tile's first row (rows_rsrc: a
+    // resource spans at most 4 GiB)
+    auto rsrc_of = [&](const char* V, int64_t tile) {
+      return rows_rsrc(V, tile * kHyItems * item_step, DK * 2, n_rows);
+    };
+    hy_rsrc ra = rsrc_of(Va, ig), rt = rsrc_of(Vt, ig), ra_n = ra, rt_n = rt;
     const int voff = 16 * g;
     auto rows_of = [&](int64_t tile, int (&vi)[NI]) {
       const int64_t jb = tile * kHyItems + 16 * NI * wi;
 #pragma unroll
       for (int t = 0; t < NI; ++t) {
         const int64_t j = jb + 16 * t + c;
-        vi[t] = (tile < n_it && j < n_items) ? (int)(j * item_step) : 0x7fffffff;  // range check -> 0
+        vi[t] = (tile < n_it && j < n_items) ? (int)((j - tile * kHyItems) * item_step) : 0x7fffffff;  // range check -> 0
       }
     };
     // step s of a tile: s < KS from the ALS matrix, s >= KS from the two-tower one
-    auto item_load = [&](int s, const int (&vi)[NI], HyFrag (&f)[NI]) {
+    auto item_load = [&](int s, const int (&vi)[NI], HyFrag (&f)[NI], const hy_rsrc& a_, const hy_rsrc& t_) {
 #pragma unroll
       for (int t = 0; t < NI; ++t)
-        f[t].f = hy_sbuf_load(s < KS ? ra : rt, vi[t], voff + 64 * (s < KS ? s : s - KS), 0, 0);
+        f[t].f = hy_sbuf_load(s < KS ? a_ : t_, vi[t], voff + 64 * (s < KS ? s : s - KS), 0, 0);
     };
     int vcur[NI], vnext[NI];
     rows_of(ig, vcur);
     HyFrag ring[P][NI];
 #pragma unroll
-    for (int q = 0; q < P; ++q) item_load(q, vcur, ring[q]);
+    for (int q = 0; q < P; ++q) item_load(q, vcur, ring[q], ra, rt);
     HyFrag ua[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) ua[u] = user_frag(0, u, 0);
     for (int64_t it = ig; it < n_it; it += n_ig) {
       const int64_t j0 = it * kHyItems + 16 * NI * wi;
       rows_of(it + n_ig, vnext);
+      ra_n = rsrc_of(Va, it + n_ig);
+      rt_n = rsrc_of(Vt, it + n_ig);
       hy_f4 acc[2][NU][NI];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
@@ -207,8 +205,8 @@ __global__ __launch_bounds__(kHyThreads) void hybrid_tile_kernel(
         HyFrag b[NI], a[NU];
 #pragma unroll
         for (int t = 0; t < NI; ++t) b[t] = ring[s % P][t];
-        if (s + P < 2 * KS) item_load(s + P, vcur, ring[s % P]);
-        else item_load(s + P - 2 * KS, vnext, ring[s % P]);
+        if (s + P < 2 * KS) item_load(s + P, vcur, ring[s % P], ra, rt);
+        else item_load(s + P - 2 * KS, vnext, ring[s % P], ra_n, rt_n);
         // user fragments one step ahead (after the last step: step 0 of the
         // next tile — the users do not change)
         const int sn = s + 1 < 2 * KS ? s + 1 : 0;
@@ -231,6 +229,8 @@ __global__ __launch_bounds__(kHyThreads) void hybrid_tile_kernel(
       }
 #pragma unroll
       for (int t = 0; t < NI; ++t) vcur[t] = vnext[t];
+      ra = ra_n;
+      rt = rt_n;
       // C/D: lane holds user ub + 16 u, items j0 + 16 t + 4 g + r
       if constexpr (MODE == kHyMinMax) {
 #pragma unroll

@@ -43,9 +43,6 @@ namespace hrec {
 
 typedef float hp_f4 __attribute__((ext_vector_type(4)));
 typedef __bf16 hp_bf8 __attribute__((ext_vector_type(8)));
-typedef int hp_rsrc __attribute__((ext_vector_type(4)));
-__device__ hp_f4 hp_sbuf_load(hp_rsrc rsrc, int vindex, int voffset, int soffset, int aux) __asm(
-    "llvm.amdgcn.struct.buffer.load.v4f32");
 
 union HpFrag {
   int4 i;
@@ -292,19 +289,16 @@ __global__ __launch_bounds__(256) void hp_cand_kernel(const int* __restrict__ cn
   HpFrag uf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) uf[ks].i = *reinterpret_cast<const int4*>(ur + 16 * g + 64 * ks);
-  const uint64_t vb = (uint64_t)light_items;
-  hp_rsrc rsrc;
-  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
-  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * 2) << 16));
-  rsrc.z = __builtin_amdgcn_readfirstlane((int)N);
-  rsrc.w = 0x00020000;
+  const char* vbase = static_cast<const char*>(light_items);
   for (int q = blockIdx.x * 4 + wv; 16 * q < nb; q += gridDim.x * 4) {
     const int pos = 16 * q + c;
     const int64_t item = pos < nb ? ci[(int64_t)b * cap + pos] : -1;
-    const int vi = item >= 0 ? (int)item : 0x7fffffff;  // out of range: the buffer check reads zeros
+    // survivors are arbitrary rows: 64-bit addresses (a buffer resource spans
+    // at most 4 GiB); a padding slot reads row 0 and its result is dropped
+    const char* row = vbase + (item >= 0 && item < N ? item : 0) * (int64_t)(DK * 2);
     HpFrag it[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) it[ks].f = hp_sbuf_load(rsrc, vi, 16 * g + 64 * ks, 0, 0);
+    for (int ks = 0; ks < KS; ++ks) it[ks].i = *reinterpret_cast<const int4*>(row + 16 * g + 64 * ks);
     hp_f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)  // A = items, B = users: the k order of hyb_scores_kernel / dot_res_kernel
@@ -489,6 +483,18 @@ extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, co
                        out_idx, out_val, w.fws, s, w.flag);
   if (rc) return rc;
   return offset_ids(out_idx, (int64_t)n_users * kk, idx_offset, s);
+}
+
+extern "C" int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,
+                                           int32_t* out, void* stream) {
+  HREC_REQUIRE(workspace && out && n_users >= 0 && n_items >= 0, "hybrid_prune_survivors: bad argument");
+  int kk = (int)(top_k < n_items ? top_k : n_items);
+  kk = kk < 1 ? 1 : (kk > kHpMaxK ? kHpMaxK : kk);
+  const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, kk);
+  if (n_users > 0 &&
+      hipMemcpyAsync(out, w.cn, (size_t)n_users * 4, hipMemcpyDeviceToDevice, as_stream(stream)) != hipSuccess)
+    return check_launch("hybrid_prune_survivors: copy");
+  return HREC_OK;
 }
 
 extern "C" int hrec_hybrid_prune_fallback_taken(const void* workspace, int n_users, int64_t n_items, int dk,

@@ -137,18 +137,15 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   // the wave's first item slice is requested before the user staging, so its
   // fragments arrive while the users are converted
   const int xq = c ^ g;
-  const uint64_t vb = (uint64_t)a.items[model];
-  hs_rsrc rsrc;
-  rsrc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
-  rsrc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32) | ((DK * 2) << 16));
-  rsrc.z = __builtin_amdgcn_readfirstlane((int)a.N);
-  rsrc.w = 0x00020000;
+  // resource based at the block's first item (rows relative to i0: a
+  // resource spans at most 4 GiB, rows_rsrc)
+  const hs_rsrc rsrc = rows_rsrc(a.items[model], i0, DK * 2, a.N);
   const int voff = 16 * g;
   auto rows_of = [&](int64_t jb, int (&vi)[NI]) {
 #pragma unroll
     for (int t = 0; t < NI; ++t) {
       const int64_t j = jb + 16 * t + c;
-      vi[t] = j < i1 ? (int)j : 0x7fffffff;  // out of range: the buffer check reads zeros
+      vi[t] = j < i1 ? (int)(j - i0) : 0x7fffffff;  // out of range: the buffer check reads zeros
     }
   };
   constexpr int64_t kSlice = 16 * NI, kStride = 8 * kSlice;  // items per wave slice / per block round
@@ -459,7 +456,7 @@ static int hs_user_tile(int B) {
 template <int DK, int NCH, int MODE>
 static int hs_launch_n(HybScoresArgs& a, size_t lds, hipStream_t s) {
   const auto kfn = hyb_scores_kernel<DK, NCH, MODE>;
-  if (hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  if (!allow_max_lds(kfn))
     return check_launch("hyb_scores_kernel: LDS attribute");
   hipLaunchKernelGGL(kfn, dim3((unsigned)(2 * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
   return check_launch("hyb_scores_kernel");

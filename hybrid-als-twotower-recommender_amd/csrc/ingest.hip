@@ -106,14 +106,40 @@ __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* 
   }
 }
 
-__global__ __launch_bounds__(256) void gather_entries_kernel(const int32_t* __restrict__ pos,
-                                                             const int32_t* __restrict__ cols,
-                                                             const float* __restrict__ vals, int64_t nnz,
-                                                             int32_t* __restrict__ indices, float* __restrict__ values) {
+// (col, rating bits) packed in one 64-bit radix-sort value: the sort then
+// carries the entries along (no random gather after it)
+__global__ __launch_bounds__(256) void pack_entries_kernel(const int32_t* __restrict__ cols,
+                                                           const float* __restrict__ vals, int64_t nnz,
+                                                           uint64_t* __restrict__ packed) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x)
+    packed[i] = (uint64_t)(uint32_t)cols[i] | ((uint64_t)__float_as_uint(vals[i]) << 32);
+}
+
+__global__ __launch_bounds__(256) void unpack_entries_kernel(const uint64_t* __restrict__ packed, int64_t nnz,
+                                                             int32_t* __restrict__ indices,
+                                                             float* __restrict__ values) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t p = pos[i];
-    indices[i] = cols[p];
-    values[i] = vals[p];
+    const uint64_t v = packed[i];
+    indices[i] = (int32_t)(uint32_t)v;
+    values[i] = __uint_as_float((uint32_t)(v >> 32));
+  }
+}
+
+// *flag = 1 if some x[i] > x[i + 1] (the caller zeroes it first)
+__global__ __launch_bounds__(256) void descent_kernel(const int32_t* __restrict__ x, int64_t n, int32_t* __restrict__ flag) {
+  bool d = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x)
+    d |= x[i] > x[i + 1];
+  if (__any(d) && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
+// rows already non-decreasing: the CSR is the input order (the stable sort is the identity)
+__global__ __launch_bounds__(256) void copy_entries_kernel(const int32_t* __restrict__ cols, const float* __restrict__ vals,
+                                                           int64_t nnz, int32_t* __restrict__ indices,
+                                                           float* __restrict__ values) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
+    indices[i] = cols[i];
+    values[i] = vals[i];
   }
 }
 
@@ -152,16 +178,18 @@ struct EncodeWs {
   }
 };
 
+// keys: sorted row codes; pk / pk2: packed (col, rating) entries before /
+// after the sort (8 B each)
 struct CsrWs {
-  size_t keys, pos, pos2, temp, total;
+  size_t keys, pk, pk2, temp, total;
   CsrWs(int64_t nnz, int bits) {
     size_t sort_tmp = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)nnz, 0, bits);
+                                             (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)nnz, 0, bits);
     keys = 0;
-    pos = keys + align256(4 * (size_t)nnz);
-    pos2 = pos + align256(4 * (size_t)nnz);
-    temp = pos2 + align256(4 * (size_t)nnz);
+    pk = keys + align256(4 * (size_t)nnz);
+    pk2 = pk + align256(8 * (size_t)nnz);
+    temp = pk2 + align256(8 * (size_t)nnz);
     total = temp + align256(sort_tmp);
   }
 };
@@ -289,18 +317,45 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   HREC_REQUIRE(ws_bytes >= L.total, "coo_to_csr: workspace %zu < %zu bytes", ws_bytes, L.total);
   char* w = static_cast<char*>(ws);
   int32_t* keys = reinterpret_cast<int32_t*>(w + L.keys);
-  int32_t* pos = reinterpret_cast<int32_t*>(w + L.pos);
-  int32_t* pos2 = reinterpret_cast<int32_t*>(w + L.pos2);
+  uint64_t* pk = reinterpret_cast<uint64_t*>(w + L.pk);
+  uint64_t* pk2 = reinterpret_cast<uint64_t*>(w + L.pk2);
   size_t temp_bytes = L.total - L.temp;
-  hipLaunchKernelGGL(iota_i32_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, pos, nnz);
-  if (hipcub::DeviceRadixSort::SortPairs(w + L.temp, temp_bytes, rows, keys, pos, pos2, (int)nnz, 0, bits, s) !=
+  hipLaunchKernelGGL(pack_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, cols, vals, nnz, pk);
+  if (hipcub::DeviceRadixSort::SortPairs(w + L.temp, temp_bytes, rows, keys, pk, pk2, (int)nnz, 0, bits, s) !=
       hipSuccess)
     return check_launch("coo_to_csr: radix sort");
-  hipLaunchKernelGGL(gather_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, pos2, cols, vals, nnz, indices,
-                     values);
+  hipLaunchKernelGGL(unpack_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, pk2, nnz, indices, values);
   hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz + 1)), dim3(256), 0, s, keys, nnz, n_rows,
                      indptr);
   return check_launch("coo_to_csr");
+}
+
+extern "C" int hrec_rows_descending_pairs(const int32_t* rows, int64_t n, int32_t* out, void* stream) {
+  HREC_REQUIRE(n >= 0 && out, "rows_descending_pairs: bad argument");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(out, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("rows_descending_pairs: memset");
+  if (n < 2) return HREC_OK;
+  HREC_REQUIRE(rows, "rows_descending_pairs: null rows");
+  hipLaunchKernelGGL(descent_kernel, dim3(grid_for(n)), dim3(256), 0, s, rows, n, out);
+  return check_launch("descent_kernel");
+}
+
+extern "C" int hrec_coo_to_csr_sorted(const int32_t* rows, const int32_t* cols, const float* vals, int64_t nnz,
+                                      int64_t n_rows, int64_t* indptr, int32_t* indices, float* values,
+                                      void* stream) {
+  HREC_REQUIRE(nnz >= 0 && nnz < 0x7fffffffll && n_rows >= 0 && n_rows < 0x7fffffffll,
+               "coo_to_csr_sorted: bad shape");
+  HREC_REQUIRE(indptr, "coo_to_csr_sorted: null indptr");
+  hipStream_t s = as_stream(stream);
+  if (nnz == 0) {
+    if (hipMemsetAsync(indptr, 0, sizeof(int64_t) * (size_t)(n_rows + 1), s) != hipSuccess)
+      return check_launch("coo_to_csr_sorted: memset");
+    return HREC_OK;
+  }
+  HREC_REQUIRE(n_rows > 0 && rows && cols && vals && indices && values, "coo_to_csr_sorted: null pointer");
+  hipLaunchKernelGGL(copy_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, cols, vals, nnz, indices, values);
+  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz + 1)), dim3(256), 0, s, rows, nnz, n_rows, indptr);
+  return check_launch("coo_to_csr_sorted");
 }
 
 // ------------------------------------------------------- shard layouts

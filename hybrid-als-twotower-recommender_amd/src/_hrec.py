@@ -36,6 +36,8 @@ _SIGNATURES = {
     "hrec_coo_to_csr_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
     "hrec_coo_to_csr": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_remap_i32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp]),
+    "hrec_rows_descending_pairs": (_c_i32, [_vp, _c_i64, _vp, _vp]),
+    "hrec_coo_to_csr_sorted": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "hrec_als_init_factors": (_c_i32, [_c_u64, _c_i64, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_als_half_sweep_src64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _c_dbl, _vp, _vp]),
     "hrec_f32_to_f64": (_c_i32, [_vp, _c_i64, _vp, _vp]),
@@ -108,6 +110,7 @@ _SIGNATURES.update({
     "hrec_hybrid_prune_topk": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp,
                                         _c_i64, _c_i32, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_prune_fallback_taken": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
+    "hrec_hybrid_prune_survivors": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
                          [ctypes.c_float] * 6 + [_vp]),
     "hrec_adam_sparse_tables": (_c_i32, [ctypes.POINTER(SparseTable), _c_i32] + [ctypes.c_float] * 6 + [_vp]),
@@ -244,6 +247,16 @@ def coo_to_csr(rows, cols, vals, n_rows):
     indptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
     indices = torch.empty(nnz, dtype=torch.int32, device=dev)
     values = torch.empty(nnz, dtype=torch.float32, device=dev)
+    # rows already in order (e.g. ratings grouped by user): no sort needed
+    flag = torch.empty(1, dtype=torch.int32, device=dev)
+    _check("hrec_rows_descending_pairs", lib().hrec_rows_descending_pairs(
+        _dev(rows, torch.int32, "rows"), nnz, _dev(flag, torch.int32, "out"), _stream()))
+    if int(flag.item()) == 0:
+        _check("hrec_coo_to_csr_sorted", lib().hrec_coo_to_csr_sorted(
+            _dev(rows, torch.int32, "rows"), _dev(cols, torch.int32, "cols"), _dev(vals, torch.float32, "vals"),
+            nnz, n_rows, _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),
+            _dev(values, torch.float32, "values"), _stream()))
+        return indptr, indices, values
     ws = torch.empty(max(int(lib().hrec_coo_to_csr_workspace_bytes(nnz, n_rows)), 16), dtype=torch.uint8,
                      device=dev)
     _check("hrec_coo_to_csr", lib().hrec_coo_to_csr(
@@ -636,6 +649,16 @@ class HybridPrune:
         self.need = int(lib().hrec_hybrid_prune_workspace_bytes(self.B, self.N, self.dk, self.top_k))
         self.ws = torch.empty(self.need, dtype=torch.uint8, device=dev)
 
+    def rebind(self, als_rows, tt_users):
+        """The same batch shape with other users (the workspace is reused)."""
+        if int(als_rows.shape[0]) != self.B or tuple(tt_users.shape) != tuple(self.T.shape) or \
+                tt_users.dtype != torch.float32 or tt_users.stride(1) != 1 or not tt_users.is_cuda:
+            raise HrecError("hybrid_prune.rebind: batch shape differs from the one the workspace was sized for")
+        self.rows = als_rows if als_rows.dtype == torch.int64 and als_rows.is_contiguous() else \
+            als_rows.to(torch.int64).contiguous()
+        self.T = tt_users
+        return self
+
     def _users(self):
         return (_vp(self.U.data_ptr()), self.U.stride(0), _vp(self.rows.data_ptr()), self.U.shape[0], self.U.shape[1],
                 _vp(self.T.data_ptr()), self.T.stride(0), self.T.shape[1], self.B, _vp(self.Va.data_ptr()),
@@ -659,6 +682,13 @@ class HybridPrune:
             int(bool(als_wins)), self.top_k, int(idx_offset), _vp(out_i.data_ptr()), _vp(out_v.data_ptr()),
             _vp(self.ws.data_ptr()), self.need, _stream()))
         return out_i, out_v
+
+    def survivors(self):
+        """Survivors of the last topk()'s heavy-model filter per user (int32 [B])."""
+        out = torch.empty(self.B, dtype=torch.int32, device=self.Va.device)
+        _check("hrec_hybrid_prune_survivors", lib().hrec_hybrid_prune_survivors(
+            _vp(self.ws.data_ptr()), self.B, self.N, self.dk, self.top_k, _vp(out.data_ptr()), _stream()))
+        return out
 
     def fallback_taken(self):
         """Whether the last topk() took the exact unfused path (device flag)."""

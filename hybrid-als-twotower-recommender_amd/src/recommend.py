@@ -153,7 +153,14 @@ class ShardedRecommender:
         B = int(user_rows.shape[0])
         dev = user_vecs.device
         if self.n_local > 0:
-            hp = o.hybrid_prune(self.U, user_rows, user_vecs, self.V_op, self.iv_op, top_k)
+            # one workspace per batch shape, reused across batches
+            cache = self.__dict__.setdefault("_prune", {})
+            hp = cache.get((B, int(top_k), tuple(user_vecs.shape)))
+            if hp is None:
+                hp = cache[(B, int(top_k), tuple(user_vecs.shape))] = o.hybrid_prune(
+                    self.U, user_rows, user_vecs, self.V_op, self.iv_op, top_k)
+            else:
+                hp.rebind(user_rows, user_vecs)
             a_mm, t_mm = hp.minmax()
         else:
             inf = float("inf")

@@ -97,13 +97,22 @@ int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi,
 /* hrec_coo_to_csr: (rows[nnz], cols[nnz], vals[nnz]) with 0 <= rows < n_rows
  * -> indptr[n_rows+1], indices[nnz], values[nnz]; rows ascending, the entries
  * of a row in input order (numpy.argsort(rows, kind="stable")). The CSC is
- * the same call with rows and cols swapped. nnz, n_rows < 2^31.
+ * the same call with rows and cols swapped. nnz, n_rows < 2^31. The entries
+ * ride the radix sort as 64-bit (col, rating) values (no gather after it).
  * Workspace: hrec_coo_to_csr_workspace_bytes(nnz, n_rows). */
 size_t hrec_coo_to_csr_workspace_bytes(int64_t nnz, int64_t n_rows);
 int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const float* vals,
                     int64_t nnz, int64_t n_rows, int64_t* indptr, int32_t* indices,
                     float* values, void* workspace, size_t workspace_bytes,
                     void* stream);
+/* The same CSR when rows[] is already non-decreasing (then input order is the
+ * stable order): entries copied, indptr from the rows, no sort or workspace.
+ * hrec_rows_descending_pairs writes *out (device int32) = 1 if some
+ * rows[i] > rows[i+1], else 0 — the caller's choice between the two. */
+int hrec_rows_descending_pairs(const int32_t* rows, int64_t n, int32_t* out, void* stream);
+int hrec_coo_to_csr_sorted(const int32_t* rows, const int32_t* cols, const float* vals,
+                           int64_t nnz, int64_t n_rows, int64_t* indptr, int32_t* indices,
+                           float* values, void* stream);
 
 /* hrec_remap_i32: x[i] = table[x[i]] in place (ids outside [0, table_n)
  * -> -1). Maps an ALS shard's column ids (global user / item rows) to rows
@@ -469,6 +478,10 @@ int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, const int64_t
                            void* workspace, size_t workspace_bytes, void* stream);
 int hrec_hybrid_prune_fallback_taken(const void* workspace, int n_users, int64_t n_items, int dk,
                                      int top_k, int* out, void* stream);
+/* Diagnostics of the last phase 2: the survivors of the heavy-model filter per
+ * user (out: n_users int32, device). */
+int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,
+                                int32_t* out, void* stream);
 
 #ifdef __cplusplus
 }

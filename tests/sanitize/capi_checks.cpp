@@ -1,8 +1,9 @@
 // Host-side argument checks of the C-ABI (include/hrec.h) under
 // AddressSanitizer + UndefinedBehaviorSanitizer ("host ASan/UBSan
 // on C-ABI glue"). Built by tests/test_sanitizers.py from the library
-// sources compiled host-only (hipcc --offload-host-only, -fsanitize= after
-// -Xarch_host), so it needs no GPU: every call below must be rejected by its
+// sources with the sanitizers on the host side only (each -fsanitize= after
+// -Xarch_host; the gfx950 code is built as usual and never launched), so it
+// needs no GPU: every call below must be rejected by its
 // HREC_REQUIRE checks (HREC_E_INVALID + a message) before any HIP call, and
 // the workspace-size queries must stay free of overflow / UB over a sweep of
 // shapes. The thread-local hrec_last_error is exercised from two threads.
@@ -39,6 +40,8 @@ int main() {
   INVALID(hrec_encode_ids(nullptr, -1, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_coo_to_csr(nullptr, nullptr, nullptr, -1, 4, nullptr, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_remap_i32(nullptr, -1, nullptr, 0, nullptr));
+  INVALID(hrec_rows_descending_pairs(nullptr, 4, nullptr, nullptr));
+  INVALID(hrec_coo_to_csr_sorted(nullptr, nullptr, nullptr, -1, 4, nullptr, nullptr, nullptr, nullptr));
   // ALS
   INVALID(hrec_als_init_factors(1, 0, 4, 65, 64, nullptr, nullptr));
   INVALID(hrec_als_half_sweep(nullptr, nullptr, nullptr, 4, nullptr, 4, 8, 48, 0.1, 0, nullptr, nullptr));
@@ -88,6 +91,7 @@ int main() {
   INVALID(hrec_hybrid_prune_topk(nullptr, 64, nullptr, 4, 64, nullptr, 64, 64, 4, nullptr, nullptr, 10, 64, nullptr,
                                  nullptr, 1, 9, 0, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_prune_fallback_taken(nullptr, 1, 1, 64, 5, nullptr, nullptr));
+  INVALID(hrec_hybrid_prune_survivors(nullptr, 1, 1, 64, 5, nullptr, nullptr));
 
   // workspace-size queries over a sweep of shapes (UBSan: no signed overflow)
   size_t acc = 0;

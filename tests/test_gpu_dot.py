@@ -402,3 +402,61 @@ def test_recommender_bf16_paths_agree(device):
         for i, v in outs[1:]:
             assert torch.equal(outs[0][0], i) and torch.equal(outs[0][1], v)
     assert not recs[0].last_prune.fallback_taken()
+
+
+def _f64_topk_chunked(U, V, k, chunk=1 << 20):
+    vs, is_ = [], []
+    for j0 in range(0, V.shape[0], chunk):
+        s = U.double() @ V[j0: j0 + chunk].double().T
+        v, i = torch.topk(s, k + 1, dim=1)
+        vs.append(v)
+        is_.append(i + j0)
+    v, i = torch.cat(vs, 1), torch.cat(is_, 1)
+    o = torch.argsort(-v, dim=1, stable=True)[:, : k + 1]
+    return v.gather(1, o), i.gather(1, o)
+
+
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 128), (torch.bfloat16, 256)])
+def test_dot_topk_beyond_4gib_operands(device, dtype, d):
+    """Item operands larger than the 4 GiB a buffer resource spans (20M x 128
+    f32 = 10 GB; 10M x 256 bf16 = 5 GB): the per-tile re-based resources read
+    every row (round 2's single resource wrapped at row 2^32 / row bytes and
+    ranked the first rows again). Top-5 of 8 users vs the f64 ranking."""
+    h = _h()
+    n = 20_000_000 if dtype == torch.float32 else 10_000_000
+    g = torch.Generator(device=device).manual_seed(3)
+    V = torch.randn((n, d), device=device, generator=g) * 0.1
+    U = torch.randn((8, d), device=device, generator=g)
+    Vd, Ud = h.dot_operand(V, dtype), h.dot_operand(U, dtype)
+    del V
+    gi, gv = h.dot_topk(Ud, Vd, 5)
+    rv, ri = _f64_topk_chunked(Ud, Vd, 5)
+    assert int(gi.max()) > (1 << 32) // (d * Vd.element_size())  # winners past the old wrap point exist
+    for b in range(8):
+        gaps = (rv[b, :-1] - rv[b, 1:]).min().item()
+        if gaps > 1e-3:
+            assert gi[b].tolist() == ri[b, :5].tolist(), b
+        np.testing.assert_allclose(gv[b].double().cpu().numpy(), rv[b, :5].cpu().numpy(), rtol=1e-5, atol=1e-4)
+
+
+def test_hybrid_paths_beyond_4gib_operands(device):
+    """The c5 kernels on item operands past 4 GiB (9M items x dk 256 bf16 =
+    4.6 GB per model): pruned == unfused bit for bit, and the unfused scores
+    of the last items equal a direct dot of those rows."""
+    h = _h()
+    n, B = 9_000_000, 8
+    g = torch.Generator(device=device).manual_seed(4)
+    va = h.dot_operand(torch.randn((n, 256), device=device, generator=g) * 0.1, torch.bfloat16)
+    vt = h.dot_operand(torch.randn((n, 256), device=device, generator=g) * 0.1, torch.bfloat16)
+    U = torch.randn((16, 256), device=device, generator=g)
+    uv = torch.randn((B, 256), device=device, generator=g)
+    rows = torch.arange(B, dtype=torch.int64, device=device) * 2
+    als, tt, a_mm, t_mm = h.hybrid_scores(U, rows, uv, va, vt)
+    tail = slice(n - 1000, n)
+    ua = h.dot_operand(U.index_select(0, rows), torch.bfloat16)
+    assert torch.equal(als[:, tail], h.dot_scores(ua, va[tail].contiguous()))
+    for wins in (True, False):
+        ei, ev = h.fuse_rows_topk(als, tt, a_mm, t_mm, wins, 5)
+        hp = h.HybridPrune(U, rows, uv, va, vt, 5)
+        gi, gv = hp.topk(*hp.minmax(), wins)
+        assert torch.equal(gi, ei) and torch.equal(gv, ev)

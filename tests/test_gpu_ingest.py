@@ -50,22 +50,30 @@ def test_encode_ids_empty(device):
     assert uniq.numel() == 0 and codes.numel() == 0
 
 
+@pytest.mark.parametrize("presorted", [False, True])
 @pytest.mark.parametrize("nnz,n_rows,n_cols", [(1, 1, 1), (50, 7, 9), (10000, 3, 500), (200000, 4097, 1000),
                                                (300000, 70000, 50)])
-def test_coo_to_csr_matches_stable_argsort(device, nnz, n_rows, n_cols):
+def test_coo_to_csr_matches_stable_argsort(device, nnz, n_rows, n_cols, presorted):
+    """Both paths: the radix sort with (col, rating) riding as 64-bit values,
+    and rows already in order (e.g. ratings grouped by user), taken without
+    a sort; rating bit patterns (-0.0, NaN payloads) pass unchanged."""
     h = _hrec()
     rng = np.random.default_rng(nnz + n_rows)
     rows = rng.integers(0, n_rows, nnz).astype(np.int32)
     rows[: min(nnz, 5)] = n_rows - 1          # the last row is populated
+    if presorted:
+        rows = np.sort(rows)
     cols = rng.integers(0, n_cols, nnz).astype(np.int32)
     vals = rng.integers(0, 19, nnz).astype(np.float32)
     vals[::3] += 0.25
+    vals[1::7] = -0.0
+    vals.view(np.uint32)[2::11] = 0x7fc01234  # a NaN with a payload
     ip, ix, v = h.coo_to_csr(torch.as_tensor(rows, device=device), torch.as_tensor(cols, device=device),
                              torch.as_tensor(vals, device=device), n_rows)
     e_ip, e_ix, e_v = _np_csr(rows, cols, vals, n_rows)
     np.testing.assert_array_equal(ip.cpu().numpy(), e_ip)
     np.testing.assert_array_equal(ix.cpu().numpy(), e_ix)
-    np.testing.assert_array_equal(v.cpu().numpy(), e_v)
+    np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), e_v.view(np.uint32))
 
 
 def test_coo_to_csr_empty_rows_and_duplicates(device):
