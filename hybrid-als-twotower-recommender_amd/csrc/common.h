@@ -120,13 +120,13 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
                       int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                       const void* als_items, const void* tt_items, int64_t n_items, int dk, float* als_out,
                       float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm, float* part, int* argpos,
-                      const int* gate, hipStream_t s);
+                      const int* gate, hipStream_t s, const uint16_t* uop = nullptr);
 int hs_groups(int64_t n_items);
 int hs_slice_tiles(int dk);  // item tiles of 16 per wave slice (a slice = 16 * tiles items)
 // csrc/dot_topk.hip: the matrix-core survivor filter (score >= thr[b]) and
 // the list-overflow flag (cn[b] > cap -> *flag = 1).
-int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr, int cap,
-                   float* cv, int64_t* ci, int* cn, hipStream_t s);
+int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr,
+                   int thr_stride, int64_t thr_per, int cap, float* cv, int64_t* ci, int* cn, hipStream_t s);
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s);
 // csrc/score.hip: hrec_fuse_rows_topk's exact segment path, gated on *gate.
 size_t fuse_rows_exact_ws_bytes(int64_t n_rows, int64_t n, int kk);

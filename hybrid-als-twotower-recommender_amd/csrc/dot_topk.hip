@@ -292,6 +292,7 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ in, int64_t n, uint
 #define HREC_RES_NU 4
 #endif
 constexpr int kResUserBytes = 128 * 1024;
+constexpr size_t kMaxLds = 160 * 1024;  // per workgroup (allow_max_lds raises the default)
 constexpr int kResNU = HREC_RES_NU;  // user tiles per chunk (64 users): leaves VGPRs for the prefetches
 #ifndef HREC_RES_NI_BF16
 #define HREC_RES_NI_BF16 4
@@ -302,7 +303,8 @@ template <bool BF16, int DK, bool FILTER, int NI_>
 __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
     const char* __restrict__ U, int B, int UB, const char* __restrict__ V, int64_t n_rows, int64_t n_items,
     int64_t item_step, int n_ut, float* __restrict__ out, int64_t ldo, const float* __restrict__ thr, int thr_stride,
-    int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n, int64_t idx_offset) {
+    int64_t thr_per, int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n,
+    int64_t idx_offset, int sbuf) {
   using S = DotShape<BF16, DK>;
   // NI = 4: 32-user chunks (8 MFMAs per 2 user-fragment reads, as 4 x 4
   // would be, at the register budget of two waves per SIMD)
@@ -314,6 +316,13 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   char* us = dsm;                                      // UB user rows
   float* ths = reinterpret_cast<float*>(dsm + (size_t)UB * kRowB);  // UB thresholds
+  // FILTER: survivors are staged in LDS and appended once per tile (below)
+  int* cnt_l = reinterpret_cast<int*>(ths + UB);                  // [UB] per-user counts, then list bases
+  int* ovf_l = cnt_l + UB;                                          // [UB] survivors dropped (buffer full)
+  int* buf_n = ovf_l + UB;                                          // entries staged this tile
+  // [sbuf] survivor meta (user << 22 | item in tile << 12 | list offset), then [sbuf] scores
+  uint32_t* buf = reinterpret_cast<uint32_t*>(dsm + (((size_t)UB * kRowB + (size_t)UB * 12 + 4 + 15) & ~(size_t)15));
+  float* buf_s = reinterpret_cast<float*>(buf + sbuf);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int per_xcd = gridDim.x >> 3;
@@ -343,13 +352,18 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   }
   if (FILTER) {
     for (int o = threadIdx.x; o < UB; o += kDotThreads) {
-      float t = __builtin_nanf("");  // absent user: never passes
-      if (b0 + o < B) {
-        t = thr[(int64_t)(b0 + o) * thr_stride];
-        t = t == t ? t : -INFINITY;  // NaN bound admits every score
+      if (thr_per == 0) {
+        float t = __builtin_nanf("");  // absent user: never passes
+        if (b0 + o < B) {
+          t = thr[(int64_t)(b0 + o) * thr_stride];
+          t = t == t ? (t == INFINITY ? __builtin_nanf("") : t) : -INFINITY;  // NaN admits all, +inf none
+        }
+        ths[o] = t;
       }
-      ths[o] = t;
+      cnt_l[o] = 0;
+      ovf_l[o] = 0;
     }
+    if (threadIdx.x == 0) *buf_n = 0;
   }
   __syncthreads();
   const int xq = c ^ g;
@@ -381,6 +395,28 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   }
   for (int64_t it = ig; it < n_it; it += n_ig) {
     const int64_t j0 = it * kItems + 16 * NI * w;
+    // the wave's valid items (positions relative to its first item, 32-bit)
+    const int w_n = (int)(n_items - j0 < 16 * NI ? (n_items - j0 > 0 ? n_items - j0 : 0) : 16 * NI);
+    if (FILTER && thr_per > 0) {
+      // per-group bounds: each user's loosest bound over the tile's groups
+      // gates the ballot (the survivor pass compares each item exactly)
+      const int64_t q0 = it * kItems / thr_per;
+      const int64_t q1 = ((it + 1) * kItems < n_items ? (it + 1) * kItems : n_items) - 1;
+      for (int o = threadIdx.x; o < UB; o += kDotThreads) {
+        float t = __builtin_nanf("");
+        if (b0 + o < B) {
+          const float* tr = thr + (int64_t)(b0 + o) * thr_stride;
+          t = INFINITY;
+          for (int64_t gq = q0; gq <= q1 / thr_per; ++gq) {
+            const float x = tr[gq];
+            t = fminf(t, x == x ? x : -INFINITY);
+          }
+          if (t == INFINITY) t = __builtin_nanf("");  // +inf admits none: the chunks skip this user
+        }
+        ths[o] = t;
+      }
+      __syncthreads();
+    }
     rows_of(it + n_ig, vnext);
     rsrc = rsrc_of(it + n_ig);  // the last chunk refills the fragments with the next tile's
     auto user_frag = [&](int ch, int u, int ks) {
@@ -401,11 +437,31 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
       for (int u = 0; u < NU; ++u)
 #pragma unroll
         for (int t = 0; t < NI; ++t) acc[u][t] = dot_f4{0.f, 0.f, 0.f, 0.f};
-      float th[NU];  // this chunk's bounds, read before the MFMAs (latency hidden)
+      // this chunk's bounds (LDS), read before the MFMAs: per user, or
+      // (thr_per > 0) the user's loosest bound over the tile's groups — the
+      // flush then checks each staged item against its own group's bound
+      float th[NU];
       if constexpr (FILTER) {
+        bool live = false;
 #pragma unroll
-        for (int u = 0; u < NU; ++u)
+        for (int u = 0; u < NU; ++u) {
           th[u] = CU * ch + 16 * u + c < UB ? ths[CU * ch + 16 * u + c] : __builtin_nanf("");
+          live = live || th[u] == th[u];
+        }
+        if (__ballot(live) == 0) {
+          // no user of the chunk can have a survivor in the tile (NaN bounds:
+          // absent users, +inf bounds): skip its MFMAs, keep the pipelines
+          // (the next chunk's first user fragments; the next tile's items)
+#pragma unroll
+          for (int u = 0; u < NU; ++u) ua[u] = user_frag(ch_next, u, 0);
+          if constexpr (last) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+              for (int t = 0; t < NI; ++t) it_f[ks][t].f = dot_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
+          }
+          return;
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -466,29 +522,103 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
           any |= __ballot(mx >= th[u]);
         }
         if (any) {
+          // Survivors -> the block's LDS staging buffer (one LDS reservation
+          // per lane); no global atomic waits in the MFMA loop. Entry: user
+          // << 22 | item in tile << 12 (| the user-list offset, set at the
+          // flush) + the score.
+          uint32_t msk[NU];
+          int cnt = 0;
 #pragma unroll
           for (int u = 0; u < NU; ++u) {
-            const int b = b0 + CU * ch + 16 * u + c;
+            uint32_t m = 0;
 #pragma unroll
             for (int t = 0; t < NI; ++t)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int64_t j = j0 + 16 * t + 4 * g + r;
-                const float sc = acc[u][t][r];
-                if (j < n_items && sc >= th[u]) {
-                  const int pos = atomicAdd(&cand_n[b], 1);
-                  if (pos < cap) {
-                    cand_v[(int64_t)b * cap + pos] = sc;
-                    cand_i[(int64_t)b * cap + pos] = j + idx_offset;
+              for (int r = 0; r < 4; ++r)
+                if (16 * t + 4 * g + r < w_n && acc[u][t][r] >= th[u]) m |= 1u << (4 * t + r);
+            msk[u] = m;
+            cnt += __popc(m);
+          }
+          int pos = cnt ? atomicAdd(buf_n, cnt) : 0;  // LDS: the lanes' reservations serialise in the LDS unit only
+          const int jt = 16 * NI * w;  // the wave's first item in the tile
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            if (msk[u] == 0) continue;
+            const int ul = CU * ch + 16 * u + c;
+#pragma unroll
+            for (int t = 0; t < NI; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if ((msk[u] >> (4 * t + r)) & 1u) {
+                  const float sc = acc[u][t][r];
+                  if (pos < sbuf) {
+                    buf[pos] = ((uint32_t)ul << 22) | ((uint32_t)(jt + 16 * t + 4 * g + r) << 12);
+                    buf_s[pos] = sc;
+                  } else {
+                    ovf_l[ul] = 1;  // buffer full: handled at the flush
                   }
+                  ++pos;
                 }
-              }
           }
         }
       }
     };
     for (int ch = 0; ch + 1 < n_ch; ++ch) chunk(ch, std::false_type{});
     chunk(n_ch - 1, std::true_type{});
+    if constexpr (FILTER) {
+      // flush the tile's staged survivors: per-user offsets (LDS atomics),
+      // one list reservation per user (global atomics, all in flight), then
+      // the appends
+      __syncthreads();
+      const int nb = *buf_n < sbuf ? *buf_n : sbuf;
+      for (int e = threadIdx.x; e < nb; e += kDotThreads) {
+        const uint32_t x = buf[e];
+        if (thr_per > 0) {  // the item's own group bound (the ballot used the tile's loosest)
+          const int64_t j = it * kItems + (int64_t)((x >> 12) & 1023u);
+          float t = thr[(int64_t)(b0 + (int)(x >> 22)) * thr_stride + j / thr_per];
+          t = t == t ? t : -INFINITY;
+          if (!(buf_s[e] >= t)) {
+            buf[e] = 0xffffffffu;  // dropped (no user 1023: UB <= 1023)
+            continue;
+          }
+        }
+        buf[e] = x | (uint32_t)atomicAdd(&cnt_l[x >> 22], 1);
+      }
+      __syncthreads();
+      for (int o = threadIdx.x; o < UB; o += kDotThreads) {
+        const int k = cnt_l[o];
+        if (k > 0) cnt_l[o] = atomicAdd(&cand_n[b0 + o], k);
+        if (ovf_l[o]) {
+          // the staging buffer dropped survivors of this user: its list is
+          // marked overflowing (cand_n > cap) and its free slots filled with
+          // (-inf, INT64_MAX - 1), so every slot < cap holds an entry and the
+          // list's k-th best stays a valid lower bound (hrec_dot_topk's
+          // second round)
+          const int64_t b = b0 + o;
+          for (int p = atomicAdd(&cand_n[b], cap + 1); p < cap; ++p) {
+            cand_v[b * cap + p] = -INFINITY;
+            cand_i[b * cap + p] = INT64_MAX - 1;
+          }
+          ovf_l[o] = 0;
+        }
+      }
+      __syncthreads();
+      for (int e = threadIdx.x; e < nb; e += kDotThreads) {
+        const uint32_t x = buf[e];
+        if (x == 0xffffffffu) continue;
+        const int ul = (int)(x >> 22);
+        const int p = cnt_l[ul] + (int)(x & 4095u);
+        if (p < cap) {
+          const int64_t b = b0 + ul;
+          cand_v[b * cap + p] = buf_s[e];
+          cand_i[b * cap + p] = it * kItems + (int64_t)((x >> 12) & 1023u) + idx_offset;
+        }
+      }
+      __syncthreads();
+      for (int o = threadIdx.x; o < UB; o += kDotThreads) cnt_l[o] = 0;
+      if (threadIdx.x == 0) *buf_n = 0;
+      __syncthreads();
+    }
   }
 }
 
@@ -560,7 +690,7 @@ static auto dot_res_pick(int ni) {
 template <bool FILTER>
 static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
                           int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
-                          int64_t* ci, int* cn, int64_t off, hipStream_t s) {
+                          int64_t* ci, int* cn, int64_t off, hipStream_t s, int64_t thr_per = 0) {
   const int row_b = dk * (bf16 ? 2 : 4);
   const int row_lds = row_b >= 256 ? row_b : row_b + 16;
   int ub_max = kResUserBytes / row_lds;
@@ -568,7 +698,16 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
   const int n_ut = (B + ub_max - 1) / ub_max;
   int UB = (B + n_ut - 1) / n_ut;
   UB = (UB + 16 * kResNU - 1) / (16 * kResNU) * (16 * kResNU);
-  const size_t lds = (size_t)UB * row_lds + (size_t)UB * 4;
+  // FILTER: + per-user counts, the staging counter and a survivor buffer in
+  // the rest of the 160 KiB (at most 4096 entries: 12-bit offsets)
+  size_t lds = (size_t)UB * row_lds + (size_t)UB * 4;
+  int sbuf = 0;
+  if (FILTER) {
+    const size_t head = ((size_t)UB * row_lds + (size_t)UB * 12 + 4 + 15) & ~(size_t)15;
+    const size_t room = head < kMaxLds ? (kMaxLds - head) / 8 : 0;
+    sbuf = (int)(room < 4096 ? room : 4096);
+    lds = head + (size_t)sbuf * 8;
+  }
   // bf16 at d <= 128: 64 items per wave (4 item tiles), so each user fragment
   // read from LDS feeds 4 MFMAs instead of 2 (the LDS read chain, not the
   // matrix cores, was what the waves waited on); f32 and d = 256 keep 32
@@ -582,7 +721,7 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
     if (!allow_max_lds(kfn))                                                                                   \
       return check_launch("dot_res_kernel: LDS attribute");                                                   \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, u, B, UB, v, n_rows, n_items, step, n_ut, out, ldo, thr,         \
-                       thr_stride, cap, cv, ci, cn, off);                                                      \
+                       thr_stride, thr_per, cap, cv, ci, cn, off, sbuf);                                       \
   } while (0)
   if (bf16) {
     switch (dk) {
@@ -636,11 +775,18 @@ static int64_t dot_sample(int64_t n, int kk) {
 }
 
 // The survivor filter alone (the pruned hybrid's pass 2, csrc/hybrid_prune.hip):
-// append (score, j) of every item j with score >= thr[b] to user b's list
-// (cap entries; cn[b] counts every survivor, so cn[b] > cap = overflow).
-int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr, int cap,
-                   float* cv, int64_t* ci, int* cn, hipStream_t s) {
-  return dot_launch<true>(U, B, V, n_items, n_items, 1, dk, bf16, nullptr, 0, thr, 1, cap, cv, ci, cn, 0, s);
+// append (score, j) of every item j with score >= thr[b * thr_stride + j /
+// thr_per] to user b's list (cap entries; cn[b] counts every survivor, so
+// cn[b] > cap = overflow). Always the resident-user kernel (the only one with
+// per-group bounds).
+int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr,
+                   int thr_stride, int64_t thr_per, int cap, float* cv, int64_t* ci, int* cn, hipStream_t s) {
+  if (!bf16 && dk > 128) {
+    set_error("dot_filter_run: f32 operands need dk <= 128");
+    return HREC_E_INVALID;
+  }
+  return dot_launch_res<true>(U, B, V, n_items, n_items, 1, dk, bf16, nullptr, 0, thr, thr_stride, cap, cv, ci, cn, 0,
+                              s, thr_per);
 }
 
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s) {
@@ -694,6 +840,21 @@ extern "C" int hrec_dot_scores(const void* user_vec, int n_users, const void* it
   HREC_REQUIRE(out, "dot_scores: null output");
   return dot_launch<false>(user_vec, n_users, item_vec, n_items, n_items, 1, dk, dtype, out, ld_out, nullptr, 0, 0, nullptr,
                            nullptr, nullptr, 0, as_stream(stream));
+}
+
+extern "C" int hrec_dot_filter(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
+                               int dtype, const float* thr, int thr_stride, int64_t thr_per, int cap, float* cand_val,
+                               int64_t* cand_idx, int* cand_n, void* stream) {
+  int rc = dot_check(user_vec, n_users, item_vec, n_items, dk, dtype, "dot_filter");
+  if (rc) return rc;
+  HREC_REQUIRE(dtype == 1 || dk <= 128, "dot_filter: f32 operands need dk <= 128");
+  HREC_REQUIRE(cap >= 0 && thr_per >= 0 && thr_stride >= 0, "dot_filter: bad cap / bound layout");
+  HREC_REQUIRE(thr_per == 0 || thr_stride >= (n_items + thr_per - 1) / thr_per,
+               "dot_filter: thr_stride < the number of item groups");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(thr && cand_n && (cap == 0 || (cand_val && cand_idx)), "dot_filter: null pointer");
+  return dot_filter_run(user_vec, n_users, item_vec, n_items, dk, dtype, thr, thr_stride, thr_per, cap, cand_val,
+                        cand_idx, cand_n, as_stream(stream));
 }
 
 extern "C" size_t hrec_dot_topk_workspace_bytes(int n_users, int64_t n_items, int top_k) {

@@ -50,6 +50,7 @@ union HpFrag {
 };
 
 constexpr int kHpCap = 8192;      // survivors per user (expected: a few hundred)
+static_assert(kHpCap >= 256, "hp_cand_topk_kernel reads the first 256 slots unconditionally");
 constexpr int kHpMaxK = 8;        // top_k handled here (kFuseK of the exact path)
 constexpr int kHpMaxGroups = 16;  // heavy-model groups whose max slices seed the bound
 
@@ -119,7 +120,48 @@ __global__ __launch_bounds__(256) void hp_user_ops_kernel(const float* __restric
   }
 }
 
-// 2a. The bound: one wave per user (no block barriers).
+// Order of the fused top-k (score.hip's better()): larger first, equal ->
+// smaller item id, NaN last.
+__device__ __forceinline__ bool hp_better(double va, int64_t ia, double vb, int64_t ib) {
+  const bool na = va != va, nb = vb != vb;
+  if (na || nb) return !na && nb ? true : (na && nb ? ia < ib : false);
+  return va > vb || (va == vb && ia < ib);
+}
+
+// 16 gathered item rows (A, row c = item c) against one user row (B, every
+// column the same user): acc[r] of lane (g, c) = the score of item 4 g + r,
+// the k order of hyb_scores_kernel / dot_res_kernel (bit-identical scores).
+// A padding slot (item < 0) reads row 0; its result is dropped.
+template <int DK>
+__device__ __forceinline__ hp_f4 hp_gather_dot(const char* __restrict__ vbase, int64_t item, int64_t N, int g,
+                                               const HpFrag (&uf)[DK / 32]) {
+  constexpr int KS = DK / 32;
+  // survivors are arbitrary rows: 64-bit addresses (a buffer resource spans at most 4 GiB)
+  const char* row = vbase + (item >= 0 && item < N ? item : 0) * (int64_t)(DK * 2);
+  HpFrag it[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) it[ks].i = *reinterpret_cast<const int4*>(row + 16 * g + 64 * ks);
+  hp_f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hp_bf8, it[ks].i),
+                                                  __builtin_bit_cast(hp_bf8, uf[ks].i), acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ float hp_pick(const hp_f4& a, int r) {
+  return r == 0 ? a[0] : (r == 1 ? a[1] : (r == 2 ? a[2] : a[3]));
+}
+
+// 2a. The bound: one 256-thread block per user. Seeds = the item slices of
+// the kHpMaxGroups groups with the largest heavy-model maxima (4 NI items
+// each); both scores of every seed by the same MFMA chain as the exact path,
+// so their fused scores are exact and tau = the kk-th best of them is a lower
+// bound of the shard's kk-th best. Then per item group gi a bound on the heavy
+// raw score: an item of gi in the top kk has w_h h_n >= tau - w_l l_n and l_n
+// <= the light model's group maximum scaled (pass 1's partials), so theta_gi
+// = the raw score of that h_n, lowered by a relative margin. Also resets the
+// user's survivor count, and block 0 the fallback flag.
 template <int DK>
 __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__ part, const int* __restrict__ argpos,
                                                        int G, int64_t N, int B, int hm, const float* __restrict__ als_mm,
@@ -127,207 +169,289 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
                                                        int slice_ni, const uint16_t* __restrict__ uop,
                                                        const uint16_t* __restrict__ als_items,
                                                        const uint16_t* __restrict__ tt_items,
-                                                       float* __restrict__ theta, int* __restrict__ flag) {
+                                                       float* __restrict__ theta, int* __restrict__ cn,
+                                                       int* __restrict__ uflag, int* __restrict__ flag) {
 #pragma clang fp contract(off)
+  constexpr int KS = DK / 32;
   constexpr int kSlots = kHpMaxGroups * 16;  // <= 16 groups x (4 NI <= 16) items
-  __shared__ float smax[4][128];
-  __shared__ int sitem[4][kSlots];
-  __shared__ double sfl[4][kSlots];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + wv;
-  if (b >= B) return;  // wave-uniform
+  __shared__ float smax[128];
+  __shared__ int sitem[kSlots];
+  __shared__ double sfl[kSlots];
+  __shared__ double s_tau;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int b = blockIdx.x;
+  if (b == 0 && tid == 0) *flag = 0;
+  if (tid == 0) cn[b] = 0;
+  float* th_row = theta + (int64_t)b * G;
   const float amin = als_mm[b], amax = als_mm[B + b], tmin = tt_mm[b], tmax = tt_mm[B + b];
   if (!(isfinite(amin) && isfinite(amax) && isfinite(tmin) && isfinite(tmax))) {
     // NaN / infinite scores (an unknown user row, non-finite vectors): the
-    // exact path ranks them
-    if (lane == 0) {
-      theta[b] = __builtin_nanf("");
-      *flag = 1;
-    }
-    return;
+    // exact path ranks them; nothing survives the filter
+    for (int gi = tid; gi < G; gi += 256) th_row[gi] = INFINITY;
+    if (tid == 0) uflag[b] = 1;
+    return;  // block-uniform
   }
   const HpScale sc = hp_scale(amin, amax, tmin, tmax);
   const int64_t per = ((N + G - 1) / G + 15) / 16 * 16;  // hyb_scores_kernel's group range
-  // group maxima of the heavy model and their rank (value desc, group asc)
-  for (int gi = lane; gi < 128; gi += 64) {
+  // every load the bound needs besides the seeds' rows, issued together: the
+  // heavy group maxima (+ their slices) and the light ones (for theta)
+  const int lm = 1 - hm;
+  float lmx = -INFINITY;
+  if (tid < 128) {
     float v = -INFINITY;
-    if (gi < G && argpos[((int64_t)hm * G + gi) * B + b] >= 0) v = part[(((int64_t)hm * G + gi) * 2 + 1) * B + b];
-    smax[wv][gi] = v;
+    if (tid < G) {
+      const int ap = argpos[((int64_t)hm * G + tid) * B + b];
+      const float pv = part[(((int64_t)hm * G + tid) * 2 + 1) * B + b];
+      lmx = part[(((int64_t)lm * G + tid) * 2 + 1) * B + b];
+      v = ap >= 0 ? pv : -INFINITY;
+    }
+    smax[tid] = v;
   }
-  wave_sync_lds();
-  const int M = 2 * kk < kHpMaxGroups ? 2 * kk : kHpMaxGroups;
+  for (int q = tid; q < kSlots; q += 256) sitem[q] = -1;
+  if (tid == 0) s_tau = -INFINITY;
+  __syncthreads();
+  // the kHpMaxGroups largest group maxima (value desc, group asc) -> seed slots
   const int per_g = 4 * slice_ni;
-  for (int s = lane; s < kSlots; s += 64) sitem[wv][s] = -1;
-  wave_sync_lds();
-  for (int gi = lane; gi < G; gi += 64) {
-    const float v = smax[wv][gi];
-    if (v == -INFINITY) continue;
-    int rank = 0;
-    for (int q = 0; q < G; ++q) {
-      const float o = smax[wv][q];
-      rank += (o > v || (o == v && q < gi)) ? 1 : 0;
-    }
-    if (rank < M) {
-      const int pos = argpos[((int64_t)hm * G + gi) * B + b];
-      const int64_t jb = (int64_t)(pos >> 2) * 16;
-      const int g = pos & 3;
-      const int64_t i1 = (int64_t)gi * per + per < N ? (int64_t)gi * per + per : N;
-      for (int t = 0; t < slice_ni; ++t)
-        for (int r = 0; r < 4; ++r) {
-          const int64_t j = jb + 16 * t + 4 * g + r;
-          sitem[wv][rank * per_g + 4 * t + r] = j < i1 ? (int)j : -1;
-        }
-    }
-  }
-  wave_sync_lds();
-  // both dot products of every seed item in f32 (products exact), lowered by
-  // the rounding bound to a valid lower bound of its fused score
-  const uint16_t* uh = uop + ((int64_t)hm * B + b) * DK;
-  const uint16_t* ul = uop + ((int64_t)(1 - hm) * B + b) * DK;
-  const uint16_t* vh_base = hm ? tt_items : als_items;
-  const uint16_t* vl_base = hm ? als_items : tt_items;
-  const int n_slots = M * per_g;
-  for (int s = lane; s < n_slots; s += 64) {
-    const int j = sitem[wv][s];
-    double fl = -INFINITY;
-    if (j >= 0) {
-      const uint16_t* vh = vh_base + (int64_t)j * DK;
-      const uint16_t* vl = vl_base + (int64_t)j * DK;
-      float ah = 0.f, al = 0.f, sh = 0.f, sl = 0.f;
-      for (int c0 = 0; c0 < DK; c0 += 8) {
-        const uint4 xh = *reinterpret_cast<const uint4*>(vh + c0);
-        const uint4 xl = *reinterpret_cast<const uint4*>(vl + c0);
-        const uint4 yh = *reinterpret_cast<const uint4*>(uh + c0);
-        const uint4 yl = *reinterpret_cast<const uint4*>(ul + c0);
-        const uint32_t ph[4] = {xh.x, xh.y, xh.z, xh.w}, pl[4] = {xl.x, xl.y, xl.z, xl.w};
-        const uint32_t qh[4] = {yh.x, yh.y, yh.z, yh.w}, ql[4] = {yl.x, yl.y, yl.z, yl.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float h0 = hp_f(ph[e] & 0xffffu) * hp_f(qh[e] & 0xffffu), h1 = hp_f(ph[e] >> 16) * hp_f(qh[e] >> 16);
-          const float l0 = hp_f(pl[e] & 0xffffu) * hp_f(ql[e] & 0xffffu), l1 = hp_f(pl[e] >> 16) * hp_f(ql[e] >> 16);
-          ah += h0;
-          ah += h1;
-          al += l0;
-          al += l1;
-          sh += fabsf(h0) + fabsf(h1);
-          sl += fabsf(l0) + fabsf(l1);
-        }
+  if (tid < G) {
+    const float v = smax[tid];
+    if (v != -INFINITY) {
+      int rank = 0;
+      for (int q = 0; q < G; ++q) {
+        const float o = smax[q];
+        rank += (o > v || (o == v && q < tid)) ? 1 : 0;
       }
-      // |f32 sum - exact| and |MFMA - exact| are each <= 2^-16 sum|p| (n <= 256)
-      const double mh = 0x1p-15 * (double)sh * 1.001, ml = 0x1p-15 * (double)sl * 1.001;
-      const float a = hm ? al : ah, t = hm ? ah : al;
-      const double ma = hm ? ml : mh, mt = hm ? mh : ml;
-      const double f = hp_fuse(sc, a, t, w0, w1);
-      // the fused score moves by at most w0 ascale ma + w1 (tscale mt + the f32 rounding of tn)
-      const double err = w0 * sc.ascale * ma + w1 * ((double)sc.tscale * mt * 1.001 + 1e-6) + 1e-12;
-      if (f == f) fl = f - err;
+      if (rank < kHpMaxGroups) {
+        const int pos = argpos[((int64_t)hm * G + tid) * B + b];
+        const int64_t jb = (int64_t)(pos >> 2) * 16;
+        const int gq = pos & 3;
+        const int64_t i1 = (int64_t)tid * per + per < N ? (int64_t)tid * per + per : N;
+        for (int t = 0; t < slice_ni; ++t)
+          for (int r = 0; r < 4; ++r) {
+            const int64_t j = jb + 16 * t + 4 * gq + r;
+            sitem[rank * per_g + 4 * t + r] = j < i1 ? (int)j : -1;
+          }
+      }
     }
-    sfl[wv][s] = fl;
   }
-  wave_sync_lds();
-  // tau = the kk-th largest lower bound (the seed items are distinct)
-  double tau = -INFINITY;
-  for (int s = lane; s < n_slots; s += 64) {
-    const double v = sfl[wv][s];
+  __syncthreads();
+  // exact fused scores of the seeds: 16 per MFMA group, both models
+  const char* uh = reinterpret_cast<const char*>(uop + ((int64_t)hm * B + b) * DK);
+  const char* ul = reinterpret_cast<const char*>(uop + ((int64_t)(1 - hm) * B + b) * DK);
+  HpFrag fh[KS], fl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    fh[ks].i = *reinterpret_cast<const int4*>(uh + 16 * g + 64 * ks);
+    fl[ks].i = *reinterpret_cast<const int4*>(ul + 16 * g + 64 * ks);
+  }
+  const char* vh = reinterpret_cast<const char*>(hm ? tt_items : als_items);
+  const char* vl = reinterpret_cast<const char*>(hm ? als_items : tt_items);
+  const int n_slots = kHpMaxGroups * per_g;
+  for (int q = wv; 16 * q < n_slots; q += 4) {
+    const int item = sitem[16 * q + c];
+    const hp_f4 ah = hp_gather_dot<DK>(vh, item, N, g, fh);
+    const hp_f4 al = hp_gather_dot<DK>(vl, item, N, g, fl);
+    const int slot = 16 * q + 4 * g + (c & 3);
+    const int it_s = __shfl(item, 4 * g + (c & 3), kWave);
+    if (c < 4) {
+      const float h = hp_pick(ah, c), l = hp_pick(al, c);
+      const double f = hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1);
+      sfl[slot] = (it_s >= 0 && f == f) ? f : -INFINITY;
+    }
+  }
+  __syncthreads();
+  // tau = the kk-th largest (the seed items are distinct)
+  for (int q = tid; q < n_slots; q += 256) {
+    const double v = sfl[q];
     if (v == -INFINITY) continue;
     int rank = 0;
-    for (int q = 0; q < n_slots; ++q) {
-      const double o = sfl[wv][q];
-      rank += (o > v || (o == v && q < s)) ? 1 : 0;
+    for (int o = 0; o < n_slots; ++o) {
+      const double x = sfl[o];
+      rank += (x > v || (x == v && o < q)) ? 1 : 0;
     }
-    if (rank == kk - 1) tau = v;
+    if (rank == kk - 1) s_tau = v;
   }
-  // the lane that found it: broadcast by a max over the wave (-inf elsewhere)
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) tau = fmax(tau, __shfl_xor(tau, off, kWave));
-  if (lane != 0) return;
-  float th = -INFINITY;
-  if (tau > -INFINITY) {
-    if (hm == 0) {  // heavy = ALS (w0): a_n >= (tau - w1 * max t_n) / w0
-      const float tn_max = tmax * sc.tscale + sc.tmin_;
-      const double hn = (tau - w1 * (double)tn_max) / w0 - 1e-9;
-      double x = (hn - sc.amin_) / sc.ascale;
-      x -= 1e-6 * (fabs(x) + ((double)amax - (double)amin));
-      th = (float)x;
-      if ((double)th > x) th = nextafterf(th, -INFINITY);
-    } else {        // heavy = two-tower (w1): t_n >= (tau - w0 * max a_n) / w1
-      const double an_max = (double)amax * sc.ascale + sc.amin_;
-      const double hn = (tau - w0 * an_max) / w1 - 1e-9;
-      double x = (hn - (double)sc.tmin_) / (double)sc.tscale;
-      x -= 1e-6 * (fabs(x) + ((double)tmax - (double)tmin));
-      th = (float)x;
-      if ((double)th > x) th = nextafterf(th, -INFINITY);
+  __syncthreads();
+  const double tau = s_tau;
+  if (tau == -INFINITY) {  // fewer than kk numeric seeds: the exact path
+    for (int gi = tid; gi < G; gi += 256) th_row[gi] = INFINITY;
+    if (tid == 0) uflag[b] = 1;
+    return;
+  }
+  if (tid == 0) uflag[b] = 0;
+  for (int gi = tid; gi < G; gi += 256) {  // G <= 128: gi == tid, lmx loaded above
+    float th = INFINITY;  // no numeric light score in the group: fused NaN, below the kk seeds
+    if (lmx > -INFINITY) {
+      if (hm == 0) {  // heavy = ALS (w0): a_n >= (tau - w1 t_n) / w0, t_n <= the group's max scaled
+        const float tn_max = lmx * sc.tscale + sc.tmin_;
+        const double hn = (tau - w1 * (double)tn_max) / w0 - 1e-9;
+        double x = (hn - sc.amin_) / sc.ascale;
+        x -= 1e-6 * (fabs(x) + ((double)amax - (double)amin));
+        th = (float)x;
+        if ((double)th > x) th = nextafterf(th, -INFINITY);
+      } else {  // heavy = two-tower (w1): t_n >= (tau - w0 a_n) / w1
+        const double an_max = (double)lmx * sc.ascale + sc.amin_;
+        const double hn = (tau - w0 * an_max) / w1 - 1e-9;
+        double x = (hn - (double)sc.tmin_) / (double)sc.tscale;
+        x -= 1e-6 * (fabs(x) + ((double)tmax - (double)tmin));
+        th = (float)x;
+        if ((double)th > x) th = nextafterf(th, -INFINITY);
+      }
     }
+    // the group's heavy maximum is below its bound: nothing of it survives
+    // (+inf: the filter skips the group's tiles for this user)
+    if (gi < 128 && (double)th > (double)smax[gi]) th = INFINITY;
+    th_row[gi] = th;
   }
-  theta[b] = th;
 }
 
-// 2b'. list checks: overflow (cn > cap) or fewer survivors than the top-k
-// needs (only with NaN scores) -> the exact fallback.
-__global__ void hp_check_kernel(const int* __restrict__ cn, int B, int cap, int need, int* __restrict__ flag) {
-  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
-    if (cn[b] > cap || cn[b] < need) *flag = 1;
-}
-
-// 2c. Survivors: light scores (MFMA over 16 gathered items against the
-// user row), fused scores. One wave per 16 survivors of user blockIdx.y.
+// 2c. Survivors of user blockIdx.x (8 waves, 16 survivors per MFMA group):
+// light scores, fused scores, each lane's sorted best kk, then kk rounds of
+// block arg-best -> the user's top kk. Raises the fallback flag for a flagged
+// user, an overflowing / short list, or a NaN among the kk (the exact path
+// then orders the NaN items of the whole shard).
 template <int DK>
-__global__ __launch_bounds__(256) void hp_cand_kernel(const int* __restrict__ cn, int cap, const float* __restrict__ cv,
-                                                      const int64_t* __restrict__ ci, const uint16_t* __restrict__ ul_base,
-                                                      const void* __restrict__ light_items, int64_t N, int B, int hm,
-                                                      const float* __restrict__ als_mm, const float* __restrict__ tt_mm,
-                                                      double w0, double w1, double* __restrict__ fv) {
-  constexpr int KS = DK / 32;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+__global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict__ cn, int cap,
+                                                           const float* __restrict__ cv, const int64_t* __restrict__ ci,
+                                                           const int* __restrict__ uflag,
+                                                           const uint16_t* __restrict__ ul_base,
+                                                           const void* __restrict__ light_items, int64_t N, int B,
+                                                           int hm, const float* __restrict__ als_mm,
+                                                           const float* __restrict__ tt_mm, double w0, double w1,
+                                                           int kk, int64_t* __restrict__ out_idx,
+                                                           double* __restrict__ out_val, int* __restrict__ flag) {
+  constexpr int KS = DK / 32, KK = kHpMaxK;
+  __shared__ double rv[8];
+  __shared__ int64_t ri[8];
+  __shared__ int64_t s_win;
+  __shared__ int s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int b = blockIdx.y;
-  int nb = cn[b];
-  nb = nb < cap ? nb : cap;
-  if (16 * (blockIdx.x * 4 + wv) >= nb) return;  // wave-uniform
-  const HpScale sc = hp_scale(als_mm[b], als_mm[B + b], tt_mm[b], tt_mm[B + b]);
+  const int b = blockIdx.x;
+  const float* cvb = cv + (int64_t)b * cap;
+  const int64_t* cib = ci + (int64_t)b * cap;
+  // the wave's first two survivor groups (ids of rows c, heavy scores of
+  // slots 4 g + (c & 3)) load with the count: slots < cap always exist
+  const int hs = 4 * g + (c & 3);
+  int q0 = wv;
+  int64_t n_it0 = cib[16 * q0 + c], n_it1 = cib[16 * (q0 + 8) + c];
+  float n_h0 = cvb[16 * q0 + hs], n_h1 = cvb[16 * (q0 + 8) + hs];
   const char* ur = reinterpret_cast<const char*>(ul_base + (int64_t)b * DK);
   HpFrag uf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) uf[ks].i = *reinterpret_cast<const int4*>(ur + 16 * g + 64 * ks);
+  const int nb = cn[b];
+  if (uflag[b] || nb > cap || nb < kk) {
+    if (tid == 0) *flag = 1;
+    return;  // block-uniform
+  }
+  if (tid == 0) s_bad = 0;
+  const HpScale sc = hp_scale(als_mm[b], als_mm[B + b], tt_mm[b], tt_mm[B + b]);
   const char* vbase = static_cast<const char*>(light_items);
-  for (int q = blockIdx.x * 4 + wv; 16 * q < nb; q += gridDim.x * 4) {
-    const int pos = 16 * q + c;
-    const int64_t item = pos < nb ? ci[(int64_t)b * cap + pos] : -1;
-    // survivors are arbitrary rows: 64-bit addresses (a buffer resource spans
-    // at most 4 GiB); a padding slot reads row 0 and its result is dropped
-    const char* row = vbase + (item >= 0 && item < N ? item : 0) * (int64_t)(DK * 2);
-    HpFrag it[KS];
+  double lv[KK];
+  int64_t li[KK];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) it[ks].i = *reinterpret_cast<const int4*>(row + 16 * g + 64 * ks);
-    hp_f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < KK; ++j) {
+    lv[j] = 0.0;
+    li[j] = INT64_MAX;  // empty slot
+  }
+  auto take = [&](const hp_f4& acc, int q, int64_t item, float h) {
+    const int p = 16 * q + hs;
+    const int64_t pid = __shfl(item, hs, kWave);
+    if (c < 4 && p < nb) {
+      const float l = hp_pick(acc, c);
+      double xv = hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1);
+      int64_t xi = pid;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)  // A = items, B = users: the k order of hyb_scores_kernel / dot_res_kernel
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hp_bf8, it[ks].i),
-                                                    __builtin_bit_cast(hp_bf8, uf[ks].i), acc, 0, 0, 0);
-    if (c == 0) {  // C/D: lane (g, c) holds rows 4 g + r (the survivors) of column c (every column is the user)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = 16 * q + 4 * g + r;
-        if (p < nb) {
-          const float h = cv[(int64_t)b * cap + p], l = acc[r];
-          fv[(int64_t)b * cap + p] = hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1);
-        }
+      for (int j = 0; j < KK; ++j) {  // compare-exchange chain (sorted list)
+        const bool sw = li[j] == INT64_MAX || hp_better(xv, xi, lv[j], li[j]);
+        const double tv = lv[j];
+        const int64_t ti = li[j];
+        lv[j] = sw ? xv : tv;
+        li[j] = sw ? xi : ti;
+        xv = sw ? tv : xv;
+        xi = sw ? ti : xi;
       }
     }
+  };
+  // two groups per wave in flight (q0, q0 + 8); the next pair's ids and
+  // heavy scores load while this pair's rows are gathered
+  for (; 16 * q0 < nb; q0 += 16) {
+    const int q1 = q0 + 8;
+    const int64_t it0 = 16 * q0 + c < nb ? n_it0 : -1;
+    const int64_t it1 = 16 * q1 + c < nb ? n_it1 : -1;
+    const float h0 = n_h0, h1 = n_h1;
+    const int qn = q0 + 16;
+    if (16 * qn < nb) {
+      n_it0 = cib[16 * qn + c];
+      n_h0 = cvb[16 * qn + hs];
+      if (16 * (qn + 8) < cap) {
+        n_it1 = cib[16 * (qn + 8) + c];
+        n_h1 = cvb[16 * (qn + 8) + hs];
+      }
+    }
+    const hp_f4 a0 = hp_gather_dot<DK>(vbase, it0, N, g, uf);
+    if (16 * q1 < nb) {  // wave-uniform
+      const hp_f4 a1 = hp_gather_dot<DK>(vbase, it1, N, g, uf);
+      take(a0, q0, it0, h0);
+      take(a1, q1, it1, h1);
+    } else {
+      take(a0, q0, it0, h0);
+    }
   }
+  for (int r = 0; r < kk; ++r) {
+    double bv = lv[0];
+    int64_t bi = li[0];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double yv = __shfl_xor(bv, off, kWave);
+      const int64_t yi = __shfl_xor(bi, off, kWave);
+      const bool tk = bi == INT64_MAX ? yi != INT64_MAX : (yi != INT64_MAX && hp_better(yv, yi, bv, bi));
+      bv = tk ? yv : bv;
+      bi = tk ? yi : bi;
+    }
+    if (lane == 0) {
+      rv[wv] = bv;
+      ri[wv] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double wvv = rv[0];
+      int64_t wi = ri[0];
+      for (int q = 1; q < 8; ++q)
+        if (ri[q] != INT64_MAX && (wi == INT64_MAX || hp_better(rv[q], ri[q], wvv, wi))) {
+          wvv = rv[q];
+          wi = ri[q];
+        }
+      if (wi == INT64_MAX || wvv != wvv) s_bad = 1;
+      out_idx[(int64_t)b * kk + r] = wi == INT64_MAX ? -1 : wi;
+      out_val[(int64_t)b * kk + r] = wi == INT64_MAX ? 0.0 : wvv;
+      s_win = wi;
+    }
+    __syncthreads();
+    const int64_t win = s_win;
+    if (win != INT64_MAX && li[0] == win) {  // the (unique) owner pops its head
+#pragma unroll
+      for (int j = 0; j + 1 < KK; ++j) {
+        lv[j] = lv[j + 1];
+        li[j] = li[j + 1];
+      }
+      li[KK - 1] = INT64_MAX;
+    }
+  }
+  if (tid == 0 && s_bad) *flag = 1;
 }
 
 struct HpWs {
   float* part;
   int* argpos;
   uint16_t* uop;
-  float* theta;
+  float* theta;  // [B][G] heavy raw-score bound per item group
+  int* uflag;    // [B] the bound's per-user fallback reason
   float* cv;
   int64_t* ci;
   int* cn;
   int* flag;
-  double* fv;
-  char* tws;
   float* fb;
   char* fws;
   size_t total;
@@ -347,13 +471,12 @@ static HpWs hp_layout(char* base, int B, int64_t N, int dk, int kk) {
   w.argpos = (int*)take((size_t)2 * G * B * 4);
   w.uop = (uint16_t*)take((size_t)2 * B * dk * 2);
   // phase 2
-  w.theta = (float*)take((size_t)B * 4);
+  w.theta = (float*)take((size_t)B * G * 4);
+  w.uflag = (int*)take((size_t)B * 4);
   w.cv = (float*)take((size_t)B * kHpCap * 4);
   w.ci = (int64_t*)take((size_t)B * kHpCap * 8);
   w.cn = (int*)take((size_t)B * 4);
   w.flag = (int*)take(4);
-  w.fv = (double*)take((size_t)B * kHpCap * 8);
-  w.tws = take(topk_ws_bytes(B, kHpCap, kk, 8));
   w.fb = (float*)take((size_t)2 * B * N * 4);  // exact fallback: both score matrices
   w.fws = take(fuse_rows_exact_ws_bytes(B, N, kk));
   w.total = off + 256;
@@ -410,7 +533,7 @@ extern "C" int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, 
                               (size_t)2 * 2 * n_users * 4 + 256, stream);
   return hybrid_scores_run(1 /* HS_PRUNE */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
                            tt_width, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, 0, als_mm, tt_mm,
-                           w.part, w.argpos, nullptr, s);
+                           w.part, w.argpos, nullptr, s, w.uop);
 }
 
 extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, const int64_t* als_rows,
@@ -435,14 +558,12 @@ extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, co
   const double w0 = als_wins ? 0.8 : 0.2, w1 = als_wins ? 0.2 : 0.8;
   const int hm = als_wins ? 0 : 1;
   const int G = hs_groups(n_items);
-  if (hipMemsetAsync(w.flag, 0, 4, s) != hipSuccess || hipMemsetAsync(w.cn, 0, (size_t)n_users * 4, s) != hipSuccess)
-    return check_launch("hybrid_prune_topk: memset");
-  const dim3 gb((unsigned)((n_users + 3) / 4));
   const uint16_t* ai = static_cast<const uint16_t*>(als_items);
   const uint16_t* ti = static_cast<const uint16_t*>(tt_items);
-#define HREC_HP_BOUND(DK)                                                                                        \
-  hipLaunchKernelGGL(hp_bound_kernel<DK>, gb, dim3(256), 0, s, w.part, w.argpos, G, n_items, n_users, hm, als_mm, \
-                     tt_mm, w0, w1, kk, hs_slice_tiles(DK), w.uop, ai, ti, w.theta, w.flag)
+#define HREC_HP_BOUND(DK)                                                                                          \
+  hipLaunchKernelGGL(hp_bound_kernel<DK>, dim3((unsigned)n_users), dim3(256), 0, s, w.part, w.argpos, G, n_items,   \
+                     n_users, hm, als_mm, tt_mm, w0, w1, kk, hs_slice_tiles(DK), w.uop, ai, ti, w.theta, w.cn,     \
+                     w.uflag, w.flag)
   switch (dk) {
     case 64: HREC_HP_BOUND(64); break;
     case 128: HREC_HP_BOUND(128); break;
@@ -451,33 +572,30 @@ extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, co
 #undef HREC_HP_BOUND
   rc = check_launch("hp_bound_kernel");
   if (rc) return rc;
-  // b. the heavy model's scores, survivors of theta
+  // b. the heavy model's scores, survivors of the per-group bounds
   const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
   const uint16_t* ul = w.uop + (size_t)(1 - hm) * n_users * dk;
-  rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, kHpCap, w.cv, w.ci, w.cn, s);
+  const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
+  rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
+                      w.cn, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(hp_check_kernel, dim3(64), dim3(256), 0, s, w.cn, n_users, kHpCap, kk, w.flag);
-  rc = check_launch("hp_check_kernel");
-  if (rc) return rc;
-  // c. light scores + fusion of the survivors, exact top-k
-  const dim3 gc(8, (unsigned)n_users);
-#define HREC_HP_CAND(DK)                                                                                          \
-  hipLaunchKernelGGL(hp_cand_kernel<DK>, gc, dim3(256), 0, s, w.cn, kHpCap, w.cv, w.ci, ul, hm ? als_items : tt_items, \
-                     n_items, n_users, hm, als_mm, tt_mm, w0, w1, w.fv)
+  // c. light scores + fusion of the survivors, exact top-k, fallback flag
+#define HREC_HP_CAND(DK)                                                                                           \
+  hipLaunchKernelGGL(hp_cand_topk_kernel<DK>, dim3((unsigned)n_users), dim3(512), 0, s, w.cn, kHpCap, w.cv, w.ci,   \
+                     w.uflag, ul, hm ? als_items : tt_items, n_items, n_users, hm, als_mm, tt_mm, w0, w1, kk,      \
+                     out_idx, out_val, w.flag)
   switch (dk) {
     case 64: HREC_HP_CAND(64); break;
     case 128: HREC_HP_CAND(128); break;
     default: HREC_HP_CAND(256); break;
   }
 #undef HREC_HP_CAND
-  rc = check_launch("hp_cand_kernel");
-  if (rc) return rc;
-  rc = topk_rows<double>(w.fv, n_users, kHpCap, kHpCap, kk, out_idx, out_val, w.tws, (size_t)1 << 62, s, w.ci, w.cn);
+  rc = check_launch("hp_cand_topk_kernel");
   if (rc) return rc;
   // d. exact fallback, gated on the flag (no host round trip)
   rc = hybrid_scores_run(2 /* HS_GATED */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
                          tt_width, n_users, als_items, tt_items, n_items, dk, w.fb, w.fb + (size_t)n_users * n_items,
-                         n_items, nullptr, nullptr, nullptr, nullptr, w.flag, s);
+                         n_items, nullptr, nullptr, nullptr, nullptr, w.flag, s, w.uop);
   if (rc) return rc;
   rc = fuse_rows_exact(w.fb, w.fb + (size_t)n_users * n_items, n_users, n_items, n_items, als_mm, tt_mm, w0, w1, kk,
                        out_idx, out_val, w.fws, s, w.flag);

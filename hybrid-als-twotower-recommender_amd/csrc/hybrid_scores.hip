@@ -57,6 +57,7 @@ struct HybScoresArgs {
   float* part;             // [2][G][2][B]: per-block min / max
   int* argpos;             // HS_PRUNE: [2][G][B] slice of each block's max ((jb / 16) * 4 + g), -1 = none
   const int* gate;         // HS_GATED: skip the launch while *gate == 0
+  const uint16_t* uop;     // optional: the batch's bf16 user operands [2][B][DK] (staged as is)
   int G;                   // item groups per (model, user tile)
   int UB;                  // users per tile (multiple of 64)
   int n_ut;
@@ -164,7 +165,31 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   // users of the tile -> LDS as bf16 (zero rows / columns beyond the batch /
   // width). Batches of chunks (8 floats each) per thread: all loads are
   // issued before the first conversion (16-B loads when the row allows).
-  {
+  if (a.uop) {  // pre-converted rows (hp_user_ops_kernel): 16-B copies
+    const char* src = reinterpret_cast<const char*>(a.uop) + ((int64_t)model * a.B + b0) * (DK * 2);
+    constexpr int kBatch = 8;
+    const int n_chunks = a.UB * S::kChunks;
+    for (int o0 = threadIdx.x; o0 < n_chunks; o0 += kBatch * kHsThreads) {
+      int4 v[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int o = o0 + j * kHsThreads;
+        const int r = o / S::kChunks, q = o % S::kChunks;
+        v[j] = int4{0, 0, 0, 0};
+        if (o < n_chunks && r < ub) v[j] = *reinterpret_cast<const int4*>(src + (int64_t)r * (DK * 2) + 16 * q);
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int o = o0 + j * kHsThreads;
+        if (o >= n_chunks) break;
+        const int r = o / S::kChunks, q = o % S::kChunks;
+        *reinterpret_cast<int4*>(us + r * kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v[j];
+      }
+    }
+    for (int o = threadIdx.x; o < 2 * a.UB; o += kHsThreads) mmk[o] = 0u;
+    if (MODE == HS_PRUNE)
+      for (int o = threadIdx.x; o < a.UB; o += kHsThreads) amk[o] = 0ull;
+  } else {
     const float* src = a.users[model];
     const int64_t ld = a.ld[model];
     const int64_t* rws = a.rows[model];
@@ -496,8 +521,9 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
                       int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                       const void* als_items, const void* tt_items, int64_t n_items, int dk, float* als_out,
                       float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm, float* part, int* argpos,
-                      const int* gate, hipStream_t s) {
+                      const int* gate, hipStream_t s, const uint16_t* uop) {
   HybScoresArgs a{};
+  a.uop = uop;
   a.users[0] = als_users;
   a.users[1] = tt_users;
   a.ld[0] = als_ld;

@@ -96,6 +96,8 @@ _SIGNATURES.update({
     "hrec_dot_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
     "hrec_dot_topk": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp,
                                _c_sz, _vp]),
+    "hrec_dot_filter": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp,
+                                 _vp, _vp]),
     "hrec_hybrid_scores_workspace_bytes": (_c_sz, [_c_i32, _c_i64]),
     "hrec_hybrid_scores": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32,
                                     _vp, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
@@ -566,6 +568,25 @@ def dot_topk(U, V, top_k, idx_offset=0, max_rounds=2):
             oi.copy_(ci)
             ov.copy_(cv)
     return out_i, out_v
+
+
+def dot_filter(U, V, thr, thr_per=0, cap=8192):
+    """Survivors of <U[b], V[j]> >= thr[b, j // thr_per] (thr [B] or [B, G]
+    f32; thr_per = 0: one bound per user) — hrec_dot_filter. Returns (val f32
+    [B, cap], idx int64 [B, cap], count int32 [B]); count > cap = overflow,
+    list order unspecified."""
+    dk, bf = _dot_args(U, V)
+    B, N = U.shape[0], V.shape[0]
+    dev = U.device
+    thr = thr.to(device=dev, dtype=torch.float32)
+    thr = thr.reshape(B, -1).contiguous()
+    cv = torch.empty((B, cap), dtype=torch.float32, device=dev)
+    ci = torch.empty((B, cap), dtype=torch.int64, device=dev)
+    cn = torch.zeros(B, dtype=torch.int32, device=dev)
+    _check("hrec_dot_filter", lib().hrec_dot_filter(
+        _vp(U.data_ptr()), B, _vp(V.data_ptr()), N, dk, bf, _dev(thr, torch.float32, "thr"), thr.shape[1],
+        int(thr_per), int(cap), _vp(cv.data_ptr()), _vp(ci.data_ptr()), _vp(cn.data_ptr()), _stream()))
+    return cv, ci, cn
 
 
 def hybrid_minmax(als_user, tt_user, als_item, tt_item):

@@ -395,6 +395,16 @@ int hrec_dot_topk(const void* user_vec, int n_users, const void* item_vec, int64
                   int dtype, int top_k, const float* thr_in, int64_t idx_offset, int64_t* out_idx,
                   float* out_val, int* overflow, void* workspace, size_t workspace_bytes,
                   void* stream);
+/* The survivor filter of hrec_dot_topk / the pruned hybrid alone: append
+ * (score, j) of every item j with <U[b], V[j]> >= thr[b * thr_stride + (thr_per
+ * ? j / thr_per : 0)] to user b's list (cand_val / cand_idx [n_users, cap]; a
+ * NaN bound admits every score, a +inf bound none; list order unspecified). cand_n[b], zeroed by
+ * the caller, ends as the user's survivor count, or > cap when the list
+ * overflowed (the list then holds an arbitrary subset). bf16 operands, or f32
+ * at dk <= 128. */
+int hrec_dot_filter(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
+                    int dtype, const float* thr, int thr_stride, int64_t thr_per, int cap, float* cand_val,
+                    int64_t* cand_idx, int* cand_n, void* stream);
 
 /* ---------------------------------------------------------------------
  * Fused hybrid recommendation on bf16 operands (csrc/hybrid_fused.hip,

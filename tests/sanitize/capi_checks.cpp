@@ -81,6 +81,8 @@ int main() {
   INVALID(hrec_f32_to_bf16(nullptr, -1, nullptr, nullptr));
   INVALID(hrec_dot_scores(nullptr, 1, nullptr, 4, 48, 0, nullptr, 4, nullptr));
   INVALID(hrec_dot_topk(nullptr, 1, nullptr, 4, 64, 2, 5, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr));
+  INVALID(hrec_dot_filter(nullptr, 1, nullptr, 4, 256, 0, nullptr, 1, 0, 8, nullptr, nullptr, nullptr, nullptr));
+  INVALID(hrec_dot_filter(nullptr, 1, nullptr, 100, 64, 1, nullptr, 2, 32, -8, nullptr, nullptr, nullptr, nullptr));
   INVALID(hrec_hybrid_minmax(nullptr, nullptr, 1, nullptr, nullptr, 4, 32, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_topk(nullptr, nullptr, 1, nullptr, nullptr, 4, 64, nullptr, nullptr, 1, 0, nullptr, 0, nullptr,
                            nullptr, nullptr, nullptr, 0, nullptr));

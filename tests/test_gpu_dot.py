@@ -80,6 +80,68 @@ def test_dot_topk_bit_exact_vs_full_scores(device, dtype, B, N, d, k):
     np.testing.assert_array_equal(gv.cpu().numpy(), ev)
 
 
+@pytest.mark.parametrize("dtype,d,B,N,per", [(torch.bfloat16, 256, 256, 100_003, 784), (torch.bfloat16, 64, 70, 5000, 0),
+                                             (torch.float32, 128, 33, 20_000, 300), (torch.bfloat16, 128, 300, 777, 16)])
+def test_dot_filter_per_group_bounds(device, dtype, d, B, N, per):
+    """hrec_dot_filter: exactly the items with score >= the bound of their
+    (user, item group) survive (a NaN bound admits the group), each with its
+    hrec_dot_scores value (bit-exact); the count of an overflowing list is
+    still exact. Survivors cluster on the same items for every user (as the
+    pruned hybrid's do): one shared direction dominates the user vectors."""
+    h = _h()
+    rng = np.random.default_rng(7)
+    common = rng.standard_normal(d).astype(np.float32)
+    U = (_vecs(B, d, 8, 0.3) + common).astype(np.float32)
+    Ud = h.dot_operand(torch.from_numpy(U).to(device), dtype)
+    Vd = h.dot_operand(torch.from_numpy(_vecs(N, d, 9)).to(device), dtype)
+    S = h.dot_scores(Ud, Vd).cpu().numpy()
+    G = (N + per - 1) // per if per else 1
+    grp = (np.arange(N) // per) if per else np.zeros(N, dtype=np.int64)
+    hi = S.max(1, keepdims=True)
+    lo = np.quantile(S, 0.99, axis=1, keepdims=True)
+    thr = (lo + (hi - lo) * rng.random((B, G))).astype(np.float32)
+    thr[5] = np.inf  # admits nothing (the kernel skips such users' chunks)
+    if per:
+        thr[3, G // 2] = np.nan  # admits the whole group
+        thr[7:, 1::2] = np.inf  # dead groups
+    cap = 512
+    cv, ci, cn = h.dot_filter(Ud, Vd, torch.from_numpy(thr), per, cap)
+    cv, ci, cn = cv.cpu().numpy(), ci.cpu().numpy(), cn.cpu().numpy()
+    tf = thr[:, grp]
+    want = np.where(np.isnan(tf), True, S >= tf)
+    np.testing.assert_array_equal(cn, want.sum(1))  # no list here overflows a block's staging buffer
+    for b in range(B):
+        if cn[b] > cap:
+            continue
+        order = np.argsort(ci[b, : cn[b]])
+        ids = ci[b, : cn[b]][order]
+        np.testing.assert_array_equal(ids, np.nonzero(want[b])[0])
+        np.testing.assert_array_equal(cv[b, : cn[b]][order], S[b, ids])
+
+
+def test_dot_filter_staging_overflow_keeps_lists_valid(device):
+    """More survivors in one tile than a block's LDS staging buffer holds
+    (every score admitted): every such user is marked overflowing (count >
+    cap) and every list slot still holds an entry — a real survivor with its
+    exact score, or the (-inf, INT64_MAX - 1) filler — so the list's k-th best
+    stays a valid lower bound."""
+    h = _h()
+    B, N, d, cap = 256, 5000, 256, 512
+    Ud = h.dot_operand(torch.from_numpy(_vecs(B, d, 10)).to(device), torch.bfloat16)
+    Vd = h.dot_operand(torch.from_numpy(_vecs(N, d, 11)).to(device), torch.bfloat16)
+    S = h.dot_scores(Ud, Vd).cpu().numpy()
+    thr = torch.full((B,), float("nan"))
+    cv, ci, cn = h.dot_filter(Ud, Vd, thr, 0, cap)
+    cv, ci, cn = cv.cpu().numpy(), ci.cpu().numpy(), cn.cpu().numpy()
+    assert np.all(cn > cap)
+    filler = ci == np.iinfo(np.int64).max - 1
+    assert np.all(cv[filler] == -np.inf)
+    for b in range(B):
+        ids = ci[b][~filler[b]]
+        assert np.all((ids >= 0) & (ids < N)) and len(np.unique(ids)) == len(ids)
+        np.testing.assert_array_equal(cv[b][~filler[b]], S[b, ids])
+
+
 def test_dot_topk_ties_keep_candidate_order(device):
     """Duplicated item vectors score identically: the reference's stable sort
     keeps candidate (index) order among them."""
