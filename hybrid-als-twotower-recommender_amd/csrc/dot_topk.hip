@@ -632,9 +632,17 @@ typedef DotTiling<8, 2, 1> DotTileB;   // 128 users x 256 items, wave 128 x 32
 // Grid of the tile kernel: 8 * n_ut * m blocks (a multiple of 8 so the XCD map
 // is a bijection), about two 512-thread blocks per CU, no more item groups
 // than item tiles.
-static unsigned dot_grid(int n_ut, int64_t n_items, int tile_items) {
+// blocks_per_cu: what the block's LDS allows (the resident-user kernel with
+// > 80 KB: one, so a second round of blocks would re-stage every user row).
+static unsigned dot_grid(int n_ut, int64_t n_items, int tile_items, int blocks_per_cu = 2) {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
   const int64_t n_it = (n_items + tile_items - 1) / tile_items;
-  int64_t m = (512 + 8 * n_ut - 1) / (8 * n_ut);
+  const int64_t target = (int64_t)cus * blocks_per_cu;
+  int64_t m = (target + 8 * n_ut - 1) / (8 * n_ut);
   const int64_t m_max = (n_it + 7) / 8;
   if (m > m_max) m = m_max;
   if (m < 1) m = 1;
@@ -712,7 +720,7 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
   // read from LDS feeds 4 MFMAs instead of 2 (the LDS read chain, not the
   // matrix cores, was what the waves waited on); f32 and d = 256 keep 32
   const int ni = (bf16 && dk <= 128) ? kResNIbf16 : 2;
-  const dim3 grid(dot_grid(n_ut, n_items, 128 * ni)), block(kDotThreads);
+  const dim3 grid(dot_grid(n_ut, n_items, 128 * ni, lds > kMaxLds / 2 ? 1 : 2)), block(kDotThreads);
   const char* u = (const char*)U;
   const char* v = (const char*)V;
 #define HREC_DOTR(BF, DK)                                                                                      \

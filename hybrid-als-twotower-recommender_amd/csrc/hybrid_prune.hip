@@ -8,30 +8,30 @@
 // score exists, so the scores are computed twice, the second time for one
 // model only:
 //   phase 1 (hrec_hybrid_prune_minmax): the user rows gathered + converted to
-//     bf16 operands; both GEMMs (hyb_scores_kernel, mode HS_PRUNE: no stores)
-//     -> per-user min / max of both rows, and per item group (block) the 16-NI
-//     item slice holding the group's maximum;
+//     bf16 operands once; both GEMMs (hyb_scores_kernel, mode HS_PRUNE: no
+//     stores) -> per-user min / max of both rows, and per item group (block)
+//     both models' group maxima + the 16-NI item slice holding the heavy one;
 //   [the caller all-reduces the min / max across item shards (C2)]
-//   phase 2 (hrec_hybrid_prune_topk):
-//     a. bound: per user, the slices of the 2k groups with the largest maxima
-//        of the HEAVY model (weight 0.8) — 8 or 16 distinct items each; their
-//        fused scores, from both dot products recomputed in f32 and lowered by
-//        the rounding bound (|sum - mfma| <= 2^-15 sum|p| at dk <= 256), give
-//        tau <= the k-th best fused score of the shard. Any item of the top k
-//        has w_h h_n + w_l l_n >= tau with l_n <= the light row's max scaled,
-//        hence its heavy raw score >= theta (computed in f64, lowered by a
-//        relative margin);
-//     b. the heavy model's GEMM alone with the survivor filter score >= theta
-//        (dot_res_kernel FILTER, K8): the few survivors (item ids + exact
-//        heavy scores) per user;
+//   phase 2 (hrec_hybrid_prune_topk), three launches:
+//     a. bound: per user, the slices of the 16 groups with the largest maxima
+//        of the HEAVY model (weight 0.8); both scores of these seeds by the
+//        exact path's MFMA chains -> exact fused scores, tau = their k-th
+//        best <= the shard's k-th best. An item of group g in the top k has
+//        w_h h_n >= tau - w_l l_n with l_n <= the light model's group maximum
+//        scaled, hence a raw heavy score >= theta_g (f64, lowered by a
+//        relative margin); +inf where the group's heavy maximum is below it;
+//     b. the heavy model's GEMM alone with the per-group survivor filter
+//        (dot_res_kernel FILTER, K8, survivors staged in LDS per tile): item
+//        ids + exact heavy scores per user;
 //     c. each survivor's light score with the same bf16 MFMA k order (A =
 //        the gathered item rows, B = the user row), the fused score with
 //        fuse_rows_kernel's arithmetic (ALS branch f64, two-tower f32, numpy
-//        1.21 promotion), then the exact stable top-k (ties -> smaller item);
-//     d. (gated on the device flag: list overflow, fewer than k survivors or
-//        non-finite extremes) the exact unfused path — both score matrices
-//        into the workspace + hrec_fuse_rows_topk's segment path — so no host
-//        round trip is needed and a batch can be captured as one HIP graph.
+//        1.21 promotion), the exact stable top-k (ties -> smaller item) —
+//        and, in the same block, the exact path over every item of the shard
+//        for a user without a bound (non-finite extremes), with an
+//        overflowing or short list, or with a NaN among its k: no fallback
+//        launch and no host round trip, so a batch can be captured as one
+//        HIP graph.
 // Bit-identical to hrec_hybrid_scores + hrec_fuse_rows_topk: every score is
 // the same MFMA chain and every fused score the same arithmetic.
 #include <float.h>
@@ -194,6 +194,15 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   }
   const HpScale sc = hp_scale(amin, amax, tmin, tmax);
   const int64_t per = ((N + G - 1) / G + 15) / 16 * 16;  // hyb_scores_kernel's group range
+  // the user's bf16 rows (B operands of the seed MFMAs)
+  const char* uh = reinterpret_cast<const char*>(uop + ((int64_t)hm * B + b) * DK);
+  const char* ul = reinterpret_cast<const char*>(uop + ((int64_t)(1 - hm) * B + b) * DK);
+  HpFrag fh[KS], fl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    fh[ks].i = *reinterpret_cast<const int4*>(uh + 16 * g + 64 * ks);
+    fl[ks].i = *reinterpret_cast<const int4*>(ul + 16 * g + 64 * ks);
+  }
   // every load the bound needs besides the seeds' rows, issued together: the
   // heavy group maxima (+ their slices) and the light ones (for theta)
   const int lm = 1 - hm;
@@ -235,28 +244,33 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     }
   }
   __syncthreads();
-  // exact fused scores of the seeds: 16 per MFMA group, both models
-  const char* uh = reinterpret_cast<const char*>(uop + ((int64_t)hm * B + b) * DK);
-  const char* ul = reinterpret_cast<const char*>(uop + ((int64_t)(1 - hm) * B + b) * DK);
-  HpFrag fh[KS], fl[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    fh[ks].i = *reinterpret_cast<const int4*>(uh + 16 * g + 64 * ks);
-    fl[ks].i = *reinterpret_cast<const int4*>(ul + 16 * g + 64 * ks);
-  }
+  // exact fused scores of the seeds: 16 per MFMA group, both models, two
+  // groups' rows in flight per wave
   const char* vh = reinterpret_cast<const char*>(hm ? tt_items : als_items);
   const char* vl = reinterpret_cast<const char*>(hm ? als_items : tt_items);
   const int n_slots = kHpMaxGroups * per_g;
-  for (int q = wv; 16 * q < n_slots; q += 4) {
-    const int item = sitem[16 * q + c];
-    const hp_f4 ah = hp_gather_dot<DK>(vh, item, N, g, fh);
-    const hp_f4 al = hp_gather_dot<DK>(vl, item, N, g, fl);
+  auto seed = [&](int q, const hp_f4& ah, const hp_f4& al, int item) {
     const int slot = 16 * q + 4 * g + (c & 3);
     const int it_s = __shfl(item, 4 * g + (c & 3), kWave);
     if (c < 4) {
       const float h = hp_pick(ah, c), l = hp_pick(al, c);
       const double f = hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1);
       sfl[slot] = (it_s >= 0 && f == f) ? f : -INFINITY;
+    }
+  };
+  for (int q = wv; 16 * q < n_slots; q += 8) {
+    const int q2 = q + 4;
+    const int item = sitem[16 * q + c];
+    const int item2 = 16 * q2 < n_slots ? sitem[16 * q2 + c] : -1;
+    const hp_f4 ah = hp_gather_dot<DK>(vh, item, N, g, fh);
+    const hp_f4 al = hp_gather_dot<DK>(vl, item, N, g, fl);
+    if (16 * q2 < n_slots) {  // wave-uniform
+      const hp_f4 ah2 = hp_gather_dot<DK>(vh, item2, N, g, fh);
+      const hp_f4 al2 = hp_gather_dot<DK>(vl, item2, N, g, fl);
+      seed(q, ah, al, item);
+      seed(q2, ah2, al2, item2);
+    } else {
+      seed(q, ah, al, item);
     }
   }
   __syncthreads();
@@ -306,102 +320,75 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
 }
 
 // 2c. Survivors of user blockIdx.x (8 waves, 16 survivors per MFMA group):
-// light scores, fused scores, each lane's sorted best kk, then kk rounds of
-// block arg-best -> the user's top kk. Raises the fallback flag for a flagged
-// user, an overflowing / short list, or a NaN among the kk (the exact path
-// then orders the NaN items of the whole shard).
+// light scores, fused scores, each lane's sorted best kk, each wave's best
+// kk, wave 0 merges -> the user's top kk (+ idx_offset). A flagged user (no
+// bound, non-finite extremes), an overflowing / short list, or a NaN among the
+// kk (the exact order then depends on the NaN items of the whole shard) takes
+// the exact path IN THE SAME BLOCK: both scores of every item of the shard
+// by the same MFMA chains, the same fusion and the same order — so no
+// fallback launch exists, and only the users that need it pay for it. (All
+// of one model's scores NaN, e.g. an unknown user: every fused score is NaN
+// and the top kk are the shard's first kk items.) Sets *flag when any user
+// took the exact path.
 template <int DK>
 __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict__ cn, int cap,
                                                            const float* __restrict__ cv, const int64_t* __restrict__ ci,
                                                            const int* __restrict__ uflag,
-                                                           const uint16_t* __restrict__ ul_base,
-                                                           const void* __restrict__ light_items, int64_t N, int B,
-                                                           int hm, const float* __restrict__ als_mm,
+                                                           const uint16_t* __restrict__ uop, int hm,
+                                                           const void* __restrict__ als_items,
+                                                           const void* __restrict__ tt_items, int64_t N, int B,
+                                                           const float* __restrict__ als_mm,
                                                            const float* __restrict__ tt_mm, double w0, double w1,
-                                                           int kk, int64_t* __restrict__ out_idx,
+                                                           int kk, int64_t idx_offset, int64_t* __restrict__ out_idx,
                                                            double* __restrict__ out_val, int* __restrict__ flag) {
   constexpr int KS = DK / 32, KK = kHpMaxK;
-  __shared__ double rv[8];
-  __shared__ int64_t ri[8];
-  __shared__ int64_t s_win;
-  __shared__ int s_bad;
+  __shared__ double rv[8 * KK];
+  __shared__ int64_t ri[8 * KK];
+  __shared__ int s_full;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int b = blockIdx.x;
   const float* cvb = cv + (int64_t)b * cap;
   const int64_t* cib = ci + (int64_t)b * cap;
+  const char* vh = static_cast<const char*>(hm ? tt_items : als_items);
+  const char* vl = static_cast<const char*>(hm ? als_items : tt_items);
   // the wave's first two survivor groups (ids of rows c, heavy scores of
   // slots 4 g + (c & 3)) load with the count: slots < cap always exist
   const int hs = 4 * g + (c & 3);
   int q0 = wv;
   int64_t n_it0 = cib[16 * q0 + c], n_it1 = cib[16 * (q0 + 8) + c];
   float n_h0 = cvb[16 * q0 + hs], n_h1 = cvb[16 * (q0 + 8) + hs];
-  const char* ur = reinterpret_cast<const char*>(ul_base + (int64_t)b * DK);
+  const char* ur = reinterpret_cast<const char*>(uop + ((int64_t)(1 - hm) * B + b) * DK);
   HpFrag uf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) uf[ks].i = *reinterpret_cast<const int4*>(ur + 16 * g + 64 * ks);
   const int nb = cn[b];
-  if (uflag[b] || nb > cap || nb < kk) {
-    if (tid == 0) *flag = 1;
-    return;  // block-uniform
-  }
-  if (tid == 0) s_bad = 0;
-  const HpScale sc = hp_scale(als_mm[b], als_mm[B + b], tt_mm[b], tt_mm[B + b]);
-  const char* vbase = static_cast<const char*>(light_items);
+  const bool flagged = uflag[b] || nb > cap || nb < kk;  // block-uniform
+  const float amin = als_mm[b], amax = als_mm[B + b], tmin = tt_mm[b], tmax = tt_mm[B + b];
+  const HpScale sc = hp_scale(amin, amax, tmin, tmax);
   double lv[KK];
   int64_t li[KK];
+  auto reset = [&]() {
 #pragma unroll
-  for (int j = 0; j < KK; ++j) {
-    lv[j] = 0.0;
-    li[j] = INT64_MAX;  // empty slot
-  }
-  auto take = [&](const hp_f4& acc, int q, int64_t item, float h) {
-    const int p = 16 * q + hs;
-    const int64_t pid = __shfl(item, hs, kWave);
-    if (c < 4 && p < nb) {
-      const float l = hp_pick(acc, c);
-      double xv = hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1);
-      int64_t xi = pid;
-#pragma unroll
-      for (int j = 0; j < KK; ++j) {  // compare-exchange chain (sorted list)
-        const bool sw = li[j] == INT64_MAX || hp_better(xv, xi, lv[j], li[j]);
-        const double tv = lv[j];
-        const int64_t ti = li[j];
-        lv[j] = sw ? xv : tv;
-        li[j] = sw ? xi : ti;
-        xv = sw ? tv : xv;
-        xi = sw ? ti : xi;
-      }
+    for (int j = 0; j < KK; ++j) {
+      lv[j] = 0.0;
+      li[j] = INT64_MAX;  // empty slot
     }
   };
-  // two groups per wave in flight (q0, q0 + 8); the next pair's ids and
-  // heavy scores load while this pair's rows are gathered
-  for (; 16 * q0 < nb; q0 += 16) {
-    const int q1 = q0 + 8;
-    const int64_t it0 = 16 * q0 + c < nb ? n_it0 : -1;
-    const int64_t it1 = 16 * q1 + c < nb ? n_it1 : -1;
-    const float h0 = n_h0, h1 = n_h1;
-    const int qn = q0 + 16;
-    if (16 * qn < nb) {
-      n_it0 = cib[16 * qn + c];
-      n_h0 = cvb[16 * qn + hs];
-      if (16 * (qn + 8) < cap) {
-        n_it1 = cib[16 * (qn + 8) + c];
-        n_h1 = cvb[16 * (qn + 8) + hs];
-      }
+  auto insert = [&](double xv, int64_t xi) {
+#pragma unroll
+    for (int j = 0; j < KK; ++j) {  // compare-exchange chain (sorted list)
+      const bool sw = li[j] == INT64_MAX || hp_better(xv, xi, lv[j], li[j]);
+      const double tv = lv[j];
+      const int64_t ti = li[j];
+      lv[j] = sw ? xv : tv;
+      li[j] = sw ? xi : ti;
+      xv = sw ? tv : xv;
+      xi = sw ? ti : xi;
     }
-    const hp_f4 a0 = hp_gather_dot<DK>(vbase, it0, N, g, uf);
-    if (16 * q1 < nb) {  // wave-uniform
-      const hp_f4 a1 = hp_gather_dot<DK>(vbase, it1, N, g, uf);
-      take(a0, q0, it0, h0);
-      take(a1, q1, it1, h1);
-    } else {
-      take(a0, q0, it0, h0);
-    }
-  }
-  for (int r = 0; r < kk; ++r) {
-    double bv = lv[0];
-    int64_t bi = li[0];
+  };
+  auto fused = [&](float h, float l) { return hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1); };
+  auto wave_best = [&](double& bv, int64_t& bi) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const double yv = __shfl_xor(bv, off, kWave);
@@ -410,36 +397,128 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
       bv = tk ? yv : bv;
       bi = tk ? yi : bi;
     }
-    if (lane == 0) {
-      rv[wv] = bv;
-      ri[wv] = bi;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double wvv = rv[0];
-      int64_t wi = ri[0];
-      for (int q = 1; q < 8; ++q)
-        if (ri[q] != INT64_MAX && (wi == INT64_MAX || hp_better(rv[q], ri[q], wvv, wi))) {
-          wvv = rv[q];
-          wi = ri[q];
-        }
-      if (wi == INT64_MAX || wvv != wvv) s_bad = 1;
-      out_idx[(int64_t)b * kk + r] = wi == INT64_MAX ? -1 : wi;
-      out_val[(int64_t)b * kk + r] = wi == INT64_MAX ? 0.0 : wvv;
-      s_win = wi;
-    }
-    __syncthreads();
-    const int64_t win = s_win;
-    if (win != INT64_MAX && li[0] == win) {  // the (unique) owner pops its head
-#pragma unroll
-      for (int j = 0; j + 1 < KK; ++j) {
-        lv[j] = lv[j + 1];
-        li[j] = li[j + 1];
+  };
+  // the lanes' lists -> each wave's best kk (LDS) -> wave 0's merge; writes
+  // the outputs when `write`; returns (in s_full) whether a NaN or a missing
+  // entry is among the kk. Called block-uniformly.
+  auto merge = [&](bool write) {
+    for (int r = 0; r < kk; ++r) {
+      double bv = lv[0];
+      int64_t bi = li[0];
+      wave_best(bv, bi);
+      if (lane == 0) {
+        rv[wv * KK + r] = bv;
+        ri[wv * KK + r] = bi;
       }
-      li[KK - 1] = INT64_MAX;
+      if (bi != INT64_MAX && li[0] == bi) {  // the (unique) owner pops its head
+#pragma unroll
+        for (int j = 0; j + 1 < KK; ++j) {
+          lv[j] = lv[j + 1];
+          li[j] = li[j + 1];
+        }
+        li[KK - 1] = INT64_MAX;
+      }
+    }
+    __syncthreads();
+    if (wv == 0) {
+      // lane l holds candidates l (and l + 64 when 8 kk > 64), better one first
+      double v0 = 0.0, v1 = 0.0;
+      int64_t i0 = INT64_MAX, i1 = INT64_MAX;
+      if (lane < 8 * KK && (lane % KK) < kk) {
+        v0 = rv[lane];
+        i0 = ri[lane];
+      }
+      if (lane + 64 < 8 * KK && ((lane + 64) % KK) < kk) {
+        v1 = rv[lane + 64];
+        i1 = ri[lane + 64];
+      }
+      if (i1 != INT64_MAX && (i0 == INT64_MAX || hp_better(v1, i1, v0, i0))) {
+        const double tv = v0;
+        const int64_t ti = i0;
+        v0 = v1;
+        i0 = i1;
+        v1 = tv;
+        i1 = ti;
+      }
+      bool bad = false;
+      for (int r = 0; r < kk; ++r) {
+        double bv = v0;
+        int64_t bi = i0;
+        wave_best(bv, bi);
+        if (bi == INT64_MAX || bv != bv) bad = true;
+        if (write && lane == 0) {
+          out_idx[(int64_t)b * kk + r] = bi == INT64_MAX ? -1 : bi + idx_offset;
+          out_val[(int64_t)b * kk + r] = bi == INT64_MAX ? 0.0 : bv;
+        }
+        if (bi != INT64_MAX && i0 == bi) {
+          v0 = v1;
+          i0 = i1;
+          i1 = INT64_MAX;
+        }
+      }
+      if (lane == 0) s_full = bad ? 1 : 0;
+    }
+    __syncthreads();
+  };
+  reset();
+  if (!flagged) {
+    // two survivor groups per wave in flight (q0, q0 + 8); the next pair's
+    // ids and heavy scores load while this pair's rows are gathered
+    auto take = [&](const hp_f4& acc, int q, int64_t item, float h) {
+      const int p = 16 * q + hs;
+      const int64_t pid = __shfl(item, hs, kWave);
+      if (c < 4 && p < nb) insert(fused(h, hp_pick(acc, c)), pid);
+    };
+    for (; 16 * q0 < nb; q0 += 16) {
+      const int q1 = q0 + 8;
+      const int64_t it0 = 16 * q0 + c < nb ? n_it0 : -1;
+      const int64_t it1 = 16 * q1 + c < nb ? n_it1 : -1;
+      const float h0 = n_h0, h1 = n_h1;
+      const int qn = q0 + 16;
+      if (16 * qn < nb) {
+        n_it0 = cib[16 * qn + c];
+        n_h0 = cvb[16 * qn + hs];
+        if (16 * (qn + 8) < cap) {
+          n_it1 = cib[16 * (qn + 8) + c];
+          n_h1 = cvb[16 * (qn + 8) + hs];
+        }
+      }
+      const hp_f4 a0 = hp_gather_dot<DK>(vl, it0, N, g, uf);
+      if (16 * q1 < nb) {  // wave-uniform
+        const hp_f4 a1 = hp_gather_dot<DK>(vl, it1, N, g, uf);
+        take(a0, q0, it0, h0);
+        take(a1, q1, it1, h1);
+      } else {
+        take(a0, q0, it0, h0);
+      }
     }
   }
-  if (tid == 0 && s_bad) *flag = 1;
+  merge(!flagged);
+  if (!flagged && s_full == 0) return;  // block-uniform
+  // the exact path for this user
+  if (tid == 0) *flag = 1;
+  if (!(amin <= amax) || !(tmin <= tmax)) {
+    // one model has no number at all: every fused score is NaN, and NaN
+    // orders by item id
+    if (tid < kk) {
+      out_idx[(int64_t)b * kk + tid] = tid < N ? tid + idx_offset : -1;
+      out_val[(int64_t)b * kk + tid] = tid < N ? __builtin_nan("") : 0.0;
+    }
+    return;
+  }
+  const char* uhr = reinterpret_cast<const char*>(uop + ((int64_t)hm * B + b) * DK);
+  HpFrag uh[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) uh[ks].i = *reinterpret_cast<const int4*>(uhr + 16 * g + 64 * ks);
+  reset();
+  for (int64_t q = wv; 16 * q < N; q += 8) {
+    const int64_t item = 16 * q + c < N ? 16 * q + c : -1;
+    const hp_f4 ah = hp_gather_dot<DK>(vh, item, N, g, uh);
+    const hp_f4 al = hp_gather_dot<DK>(vl, item, N, g, uf);
+    const int64_t p = 16 * q + hs;
+    if (c < 4 && p < N) insert(fused(hp_pick(ah, c), hp_pick(al, c)), p);
+  }
+  merge(true);
 }
 
 struct HpWs {
@@ -452,8 +531,6 @@ struct HpWs {
   int64_t* ci;
   int* cn;
   int* flag;
-  float* fb;
-  char* fws;
   size_t total;
 };
 
@@ -477,8 +554,6 @@ static HpWs hp_layout(char* base, int B, int64_t N, int dk, int kk) {
   w.ci = (int64_t*)take((size_t)B * kHpCap * 8);
   w.cn = (int*)take((size_t)B * 4);
   w.flag = (int*)take(4);
-  w.fb = (float*)take((size_t)2 * B * N * 4);  // exact fallback: both score matrices
-  w.fws = take(fuse_rows_exact_ws_bytes(B, N, kk));
   w.total = off + 256;
   return w;
 }
@@ -574,33 +649,23 @@ extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, co
   if (rc) return rc;
   // b. the heavy model's scores, survivors of the per-group bounds
   const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
-  const uint16_t* ul = w.uop + (size_t)(1 - hm) * n_users * dk;
   const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
   rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
                       w.cn, s);
   if (rc) return rc;
-  // c. light scores + fusion of the survivors, exact top-k, fallback flag
+  // c. light scores + fusion of the survivors, exact top-k; the exact path in
+  //    the same block for the users that need it
 #define HREC_HP_CAND(DK)                                                                                           \
   hipLaunchKernelGGL(hp_cand_topk_kernel<DK>, dim3((unsigned)n_users), dim3(512), 0, s, w.cn, kHpCap, w.cv, w.ci,   \
-                     w.uflag, ul, hm ? als_items : tt_items, n_items, n_users, hm, als_mm, tt_mm, w0, w1, kk,      \
-                     out_idx, out_val, w.flag)
+                     w.uflag, w.uop, hm, als_items, tt_items, n_items, n_users, als_mm, tt_mm, w0, w1, kk,         \
+                     idx_offset, out_idx, out_val, w.flag)
   switch (dk) {
     case 64: HREC_HP_CAND(64); break;
     case 128: HREC_HP_CAND(128); break;
     default: HREC_HP_CAND(256); break;
   }
 #undef HREC_HP_CAND
-  rc = check_launch("hp_cand_topk_kernel");
-  if (rc) return rc;
-  // d. exact fallback, gated on the flag (no host round trip)
-  rc = hybrid_scores_run(2 /* HS_GATED */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
-                         tt_width, n_users, als_items, tt_items, n_items, dk, w.fb, w.fb + (size_t)n_users * n_items,
-                         n_items, nullptr, nullptr, nullptr, nullptr, w.flag, s, w.uop);
-  if (rc) return rc;
-  rc = fuse_rows_exact(w.fb, w.fb + (size_t)n_users * n_items, n_users, n_items, n_items, als_mm, tt_mm, w0, w1, kk,
-                       out_idx, out_val, w.fws, s, w.flag);
-  if (rc) return rc;
-  return offset_ids(out_idx, (int64_t)n_users * kk, idx_offset, s);
+  return check_launch("hp_cand_topk_kernel");
 }
 
 extern "C" int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,

@@ -12,7 +12,9 @@
 //   hrec_coo_to_csr  : (row code, col code, rating) -> indptr / indices / values,
 //                      rows ascending, entries of a row in input order
 //                      (numpy.argsort(rows, kind="stable")).
-// Both are radix sorts (hipCUB, stable LSD) plus O(n) integer passes; HBM-bound.
+// encode_ids: a marked table + scan for dense id ranges (hipCUB radix sort of
+// (id, position) otherwise); coo_to_csr: a hand-written stable LSD radix sort
+// of the dense row codes (below); plus O(n) integer passes. HBM-bound.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -62,20 +64,71 @@ __global__ __launch_bounds__(256) void scatter_codes_kernel(const K* __restrict_
 // present id its rank among the sorted distinct ids, and the codes are read
 // back from the table: two streaming passes over the ids instead of a radix
 // sort of (id, position) pairs. Same codes and uniq as the sort path.
+// Streaming passes take 4 independent elements per thread per iteration
+// (loads in flight), grid-stride.
+constexpr int kStreamUnroll = 4;
+
+__device__ __forceinline__ void load_id_pair(const int64_t* __restrict__ ids, int64_t n, int64_t p, int64_t lo,
+                                             bool vec, int64_t& a, int64_t& b) {
+  // ids 2p, 2p + 1 (one 16-B load when both exist and ids is 16-B aligned),
+  // shifted by lo; -1 past the end
+  if (vec && 2 * p + 1 < n) {
+    const longlong2 v = *reinterpret_cast<const longlong2*>(ids + 2 * p);
+    a = v.x - lo;
+    b = v.y - lo;
+  } else {
+    a = 2 * p < n ? ids[2 * p] - lo : -1;
+    b = 2 * p + 1 < n ? ids[2 * p + 1] - lo : -1;
+  }
+}
+
 __global__ __launch_bounds__(256) void mark_present_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
                                                            int64_t span, int32_t* __restrict__ present) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t v = ids[i] - lo;
-    if (v >= 0 && v < span) present[v] = 1;  // every writer stores the same value
+  const bool vec = ((uintptr_t)ids & 15) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
+    int64_t v[4];
+    load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
+    if (p0 + stride < np) {
+      load_id_pair(ids, n, p0 + stride, lo, vec, v[2], v[3]);
+    } else {
+      v[2] = v[3] = -1;
+    }
+    // every writer stores the same value; a read first keeps the repeats of
+    // a hot id (an item rated ~5000 times) from hammering its line with stores
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (v[u] >= 0 && v[u] < span && present[v[u]] == 0) present[v[u]] = 1;
   }
 }
 
 __global__ __launch_bounds__(256) void codes_from_rank_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
                                                               int64_t span, const int32_t* __restrict__ incl,
                                                               int32_t* __restrict__ codes) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t v = ids[i] - lo;
-    codes[i] = (v >= 0 && v < span) ? incl[v] - 1 : -1;  // out-of-range ids (a caller error) -> -1
+  const bool vec = ((uintptr_t)ids & 15) == 0, vst = ((uintptr_t)codes & 7) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
+    int64_t v[4];
+    load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
+    if (p0 + stride < np) {
+      load_id_pair(ids, n, p0 + stride, lo, vec, v[2], v[3]);
+    } else {
+      v[2] = v[3] = -1;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t p = p0 + h * stride;
+      if (p >= np) break;
+      // out-of-range ids (a caller error) -> -1
+      const int32_t c0 = (v[2 * h] >= 0 && v[2 * h] < span) ? incl[v[2 * h]] - 1 : -1;
+      const int32_t c1 = (v[2 * h + 1] >= 0 && v[2 * h + 1] < span) ? incl[v[2 * h + 1]] - 1 : -1;
+      if (vst && 2 * p + 1 < n) {
+        *reinterpret_cast<int2*>(codes + 2 * p) = make_int2(c0, c1);
+      } else {
+        codes[2 * p] = c0;
+        if (2 * p + 1 < n) codes[2 * p + 1] = c1;
+      }
+    }
   }
 }
 
@@ -106,30 +159,249 @@ __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* 
   }
 }
 
-// (col, rating bits) packed in one 64-bit radix-sort value: the sort then
-// carries the entries along (no random gather after it)
-__global__ __launch_bounds__(256) void pack_entries_kernel(const int32_t* __restrict__ cols,
-                                                           const float* __restrict__ vals, int64_t nnz,
-                                                           uint64_t* __restrict__ packed) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x)
-    packed[i] = (uint64_t)(uint32_t)cols[i] | ((uint64_t)__float_as_uint(vals[i]) << 32);
+// ---------------------------------------------------------------- CSR build
+// Stable LSD radix sort of the row codes carrying (col, rating), written for
+// this shape: dense codes < n_rows, so ceil(bits / 10) passes of <= 10-bit
+// digits (c2's CSC: 100k item codes = 17 bits = 2 passes of 9 + 8 bits).
+// Per pass:
+//   1. upsweep: per tile of kSortTile entries, the digit histogram (LDS
+//      atomics) -> counts[tile][digit];
+//   2. a column scan of the tile-major counts (sort_colsum / colscan_*): the
+//      output offset of every (tile, digit) — digits ascending, tiles in
+//      input order;
+//   3. downsweep: each wave takes a contiguous 1/8 of the block's tile into
+//      registers and ranks its entries among its own same-digit entries in
+//      input order (per 64-entry round: the lanes below with the same digit,
+//      from `bits` ballots, plus the wave's running per-digit count in LDS —
+//      no block barriers); one scan over (digit, wave) turns the per-wave
+//      counts into offsets in the tile's digit-sorted order; the tile is
+//      sorted in LDS and written out, so each digit's entries leave as one
+//      coalesced run at the (digit, tile) offset: a stable scatter with
+//      per-block ranks. The last pass writes indices / values unpacked; the
+//      first reads cols / values unpacked.
+constexpr int kSortThreads = 512, kSortIPT = 16, kSortTile = kSortThreads * kSortIPT;  // 8192 entries
+constexpr int kSortMaxBits = 10;
+
+__global__ __launch_bounds__(kSortThreads) void sort_upsweep_kernel(const int32_t* __restrict__ keys, int64_t n,
+                                                                    int shift, int bits, int64_t n_tiles,
+                                                                    uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[1 << kSortMaxBits];
+  const int R = 1 << bits;
+  for (int d = threadIdx.x; d < R; d += kSortThreads) h[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll 8
+  for (int e = 0; e < kSortIPT; ++e) {
+    const int64_t i = base + (int64_t)e * kSortThreads + threadIdx.x;
+    if (i < n) atomicAdd(&h[((uint32_t)keys[i] >> shift) & (uint32_t)(R - 1)], 1u);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < R; d += kSortThreads) counts[(int64_t)blockIdx.x * R + d] = h[d];
 }
 
-__global__ __launch_bounds__(256) void unpack_entries_kernel(const uint64_t* __restrict__ packed, int64_t nnz,
-                                                             int32_t* __restrict__ indices,
-                                                             float* __restrict__ values) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t v = packed[i];
-    indices[i] = (int32_t)(uint32_t)v;
-    values[i] = __uint_as_float((uint32_t)(v >> 32));
+// counts [tile][digit] (tile-major: every access below reads or writes whole
+// rows) -> in place, the output offset of (tile, digit) = the entries of all
+// smaller digits + the entries of this digit in earlier tiles. Column sums
+// per chunk of kScanTiles tiles, one block scans them (per digit over the
+// chunks, then the digit totals), chunks add their running prefix.
+constexpr int kScanTiles = 256;
+
+__global__ __launch_bounds__(512) void sort_colsum_kernel(const uint32_t* __restrict__ cnt, int64_t n_tiles, int R,
+                                                          uint32_t* __restrict__ csum) {
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTiles;
+  const int64_t t1 = t0 + kScanTiles < n_tiles ? t0 + kScanTiles : n_tiles;
+  for (int d = threadIdx.x; d < R; d += 512) {
+    uint32_t a = 0;
+#pragma unroll 8
+    for (int64_t t = t0; t < t1; ++t) a += cnt[t * R + d];
+    csum[(int64_t)blockIdx.x * R + d] = a;
+  }
+}
+
+__global__ __launch_bounds__(1024) void sort_colscan_top_kernel(uint32_t* __restrict__ csum, int64_t n_chunks, int R) {
+  __shared__ uint32_t tot[1 << kSortMaxBits];
+  __shared__ uint32_t wsum[16];
+  const int d = threadIdx.x;  // R <= 1024 = blockDim
+  uint32_t run = 0;
+  if (d < R)
+    for (int64_t c = 0; c < n_chunks; ++c) {
+      const uint32_t v = csum[c * R + d];
+      csum[c * R + d] = run;
+      run += v;
+    }
+  // exclusive scan of the digit totals
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = d < R ? run : 0;
+  const uint32_t mine = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t base = x - mine;
+  for (int q = 0; q < w; ++q) base += wsum[q];
+  tot[d] = base;
+  __syncthreads();
+  if (d < R)
+    for (int64_t c = 0; c < n_chunks; ++c) csum[c * R + d] += tot[d];
+}
+
+__global__ __launch_bounds__(512) void sort_colscan_apply_kernel(uint32_t* __restrict__ cnt, int64_t n_tiles, int R,
+                                                                 const uint32_t* __restrict__ csum) {
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTiles;
+  const int64_t t1 = t0 + kScanTiles < n_tiles ? t0 + kScanTiles : n_tiles;
+  for (int d = threadIdx.x; d < R; d += 512) {
+    uint32_t run = csum[(int64_t)blockIdx.x * R + d];
+#pragma unroll 8
+    for (int64_t t = t0; t < t1; ++t) {
+      const uint32_t v = cnt[t * R + d];
+      cnt[t * R + d] = run;
+      run += v;
+    }
+  }
+}
+
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
+    const int32_t* __restrict__ keys_in, const int32_t* __restrict__ cols_in, const float* __restrict__ vals_in,
+    const uint64_t* __restrict__ pay_in, int64_t n, int shift, int bits, int64_t n_tiles,
+    const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out, uint64_t* __restrict__ pay_out,
+    int32_t* __restrict__ idx_out, float* __restrict__ val_out) {
+  constexpr int R_MAX = 1 << kSortMaxBits, NW = kSortThreads / 64, PW = kSortTile / NW;  // entries per wave
+  __shared__ int32_t sk[kSortTile];                 // the tile, sorted by digit (stable)
+  __shared__ uint64_t sp[kSortTile];
+  __shared__ uint16_t wh[NW][R_MAX];                // per wave and digit: count, then the wave's tile offset
+  __shared__ uint32_t goff[R_MAX];                  // per digit: the tile's first output position
+  __shared__ uint32_t scan_sh[NW];
+  const int R = 1 << bits;
+  const uint32_t dmask = (uint32_t)(R - 1);
+  for (int d = threadIdx.x; d < R; d += kSortThreads) {
+    goff[d] = offs[(int64_t)blockIdx.x * R + d];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) wh[q][d] = 0;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int tn = (int)(n - base < kSortTile ? n - base : kSortTile);  // entries of this tile
+  // 1. wave w takes tile entries [w PW, (w + 1) PW) into registers, 64 per
+  //    round (coalesced)
+  int32_t key[kSortIPT];
+  uint64_t pay[kSortIPT];
+#pragma unroll
+  for (int r = 0; r < kSortIPT; ++r) {
+    const int e = w * PW + r * 64 + lane;
+    key[r] = 0;
+    pay[r] = 0;
+    if (e < tn) {
+      key[r] = keys_in[base + e];
+      if constexpr (FIRST) {
+        pay[r] = (uint64_t)(uint32_t)cols_in[base + e] | ((uint64_t)__float_as_uint(vals_in[base + e]) << 32);
+      } else {
+        pay[r] = pay_in[base + e];
+      }
+    }
+  }
+  __syncthreads();
+  // 2. each wave ranks its own entries in order (no block barriers): within a
+  //    round the lanes below with the same digit (peer mask from `bits`
+  //    ballots), before it the wave's running per-digit count (LDS)
+  uint32_t rk[kSortIPT];
+#pragma unroll
+  for (int r = 0; r < kSortIPT; ++r) {
+    const bool active = w * PW + r * 64 + lane < tn;
+    const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
+    uint64_t peers = __ballot(active);
+    for (int b = 0; b < bits; ++b) {
+      const uint64_t m = __ballot((dg >> b) & 1u);
+      peers &= ((dg >> b) & 1u) ? m : ~m;
+    }
+    const int rank = __popcll(peers & lt);
+    const uint32_t before = active ? wh[w][dg] : 0;
+    rk[r] = before + (uint32_t)rank;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (active && rank == 0) wh[w][dg] = (uint16_t)(before + __popcll(peers));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();
+  // 3. offsets in the tile's digit-sorted order: digits ascending, waves in
+  //    order within a digit (exclusive scan over (digit, wave); thread t owns
+  //    digits 2t, 2t + 1, R <= 1024)
+  {
+    const int d0 = 2 * threadIdx.x;
+    uint32_t c[2][NW], tot = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        c[h][q] = d0 + h < R ? wh[q][d0 + h] : 0;
+        tot += c[h][q];
+      }
+    uint32_t x = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) scan_sh[w] = x;
+    __syncthreads();
+    uint32_t run = x - tot;
+    for (int q = 0; q < w; ++q) run += scan_sh[q];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        if (d0 + h < R) wh[q][d0 + h] = (uint16_t)run;
+        run += c[h][q];
+      }
+  }
+  __syncthreads();
+  // 4. the tile sorted into LDS
+#pragma unroll
+  for (int r = 0; r < kSortIPT; ++r) {
+    if (w * PW + r * 64 + lane < tn) {
+      const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
+      const uint32_t q = wh[w][dg] + rk[r];
+      sk[q] = key[r];
+      sp[q] = pay[r];
+    }
+  }
+  __syncthreads();
+  // 5. write out: consecutive LDS entries of one digit go to consecutive
+  //    output positions (coalesced runs); the digit's first LDS slot is its
+  //    wave-0 offset
+  for (int q = threadIdx.x; q < tn; q += kSortThreads) {
+    const int32_t k = sk[q];
+    const uint32_t dg = ((uint32_t)k >> shift) & dmask;
+    const uint32_t pos = goff[dg] + ((uint32_t)q - wh[0][dg]);
+    const uint64_t pv = sp[q];
+    keys_out[pos] = k;
+    if constexpr (LAST) {
+      idx_out[pos] = (int32_t)(uint32_t)pv;
+      val_out[pos] = __uint_as_float((uint32_t)(pv >> 32));
+    } else {
+      pay_out[pos] = pv;
+    }
   }
 }
 
 // *flag = 1 if some x[i] > x[i + 1] (the caller zeroes it first)
 __global__ __launch_bounds__(256) void descent_kernel(const int32_t* __restrict__ x, int64_t n, int32_t* __restrict__ flag) {
   bool d = false;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x)
-    d |= x[i] > x[i + 1];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 + 1 < n; i0 += kStreamUnroll * stride) {
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i + 1 < n) d |= x[i] > x[i + 1];
+    }
+  }
   if (__any(d) && (threadIdx.x & 63) == 0) *flag = 1;
 }
 
@@ -137,9 +409,22 @@ __global__ __launch_bounds__(256) void descent_kernel(const int32_t* __restrict_
 __global__ __launch_bounds__(256) void copy_entries_kernel(const int32_t* __restrict__ cols, const float* __restrict__ vals,
                                                            int64_t nnz, int32_t* __restrict__ indices,
                                                            float* __restrict__ values) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
-    indices[i] = cols[i];
-    values[i] = vals[i];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nnz; i0 += kStreamUnroll * stride) {
+    int32_t c[kStreamUnroll];
+    float v[kStreamUnroll];
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; ++u)
+      if (i0 + u * stride < nnz) {
+        c[u] = cols[i0 + u * stride];
+        v[u] = vals[i0 + u * stride];
+      }
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; ++u)
+      if (i0 + u * stride < nnz) {
+        indices[i0 + u * stride] = c[u];
+        values[i0 + u * stride] = v[u];
+      }
   }
 }
 
@@ -178,19 +463,28 @@ struct EncodeWs {
   }
 };
 
-// keys: sorted row codes; pk / pk2: packed (col, rating) entries before /
-// after the sort (8 B each)
+// CSR build workspace: ping-pong keys / packed (col, rating) entries of the
+// intermediate passes, the (digit, tile) counts and the scan's chunk sums.
 struct CsrWs {
-  size_t keys, pk, pk2, temp, total;
+  size_t ka, kb, pa, pb, cnt, sums, total;
+  int passes, digit[4];
+  int64_t n_tiles, n_cnt, n_chunks;
   CsrWs(int64_t nnz, int bits) {
-    size_t sort_tmp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                             (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)nnz, 0, bits);
-    keys = 0;
-    pk = keys + align256(4 * (size_t)nnz);
-    pk2 = pk + align256(8 * (size_t)nnz);
-    temp = pk2 + align256(8 * (size_t)nnz);
-    total = temp + align256(sort_tmp);
+    passes = (bits + kSortMaxBits - 1) / kSortMaxBits;
+    if (passes < 1) passes = 1;
+    for (int p = 0; p < passes; ++p) digit[p] = bits / passes + (p < bits % passes ? 1 : 0);
+    n_tiles = (nnz + kSortTile - 1) / kSortTile;
+    int maxd = 0;
+    for (int p = 0; p < passes; ++p) maxd = digit[p] > maxd ? digit[p] : maxd;
+    n_cnt = ((int64_t)1 << maxd) * n_tiles;
+    n_chunks = ((n_tiles + kScanTiles - 1) / kScanTiles) << maxd;  // column sums
+    ka = 0;
+    kb = ka + align256(4 * (size_t)nnz);
+    pa = kb + align256(4 * (size_t)nnz);
+    pb = pa + align256(8 * (size_t)nnz);
+    cnt = pb + align256(8 * (size_t)nnz);
+    sums = cnt + align256(4 * (size_t)n_cnt);
+    total = sums + align256(4 * (size_t)n_chunks);
   }
 };
 
@@ -316,16 +610,40 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   const CsrWs L(nnz, bits);
   HREC_REQUIRE(ws_bytes >= L.total, "coo_to_csr: workspace %zu < %zu bytes", ws_bytes, L.total);
   char* w = static_cast<char*>(ws);
-  int32_t* keys = reinterpret_cast<int32_t*>(w + L.keys);
-  uint64_t* pk = reinterpret_cast<uint64_t*>(w + L.pk);
-  uint64_t* pk2 = reinterpret_cast<uint64_t*>(w + L.pk2);
-  size_t temp_bytes = L.total - L.temp;
-  hipLaunchKernelGGL(pack_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, cols, vals, nnz, pk);
-  if (hipcub::DeviceRadixSort::SortPairs(w + L.temp, temp_bytes, rows, keys, pk, pk2, (int)nnz, 0, bits, s) !=
-      hipSuccess)
-    return check_launch("coo_to_csr: radix sort");
-  hipLaunchKernelGGL(unpack_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, pk2, nnz, indices, values);
-  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz + 1)), dim3(256), 0, s, keys, nnz, n_rows,
+  int32_t* kbuf[2] = {reinterpret_cast<int32_t*>(w + L.ka), reinterpret_cast<int32_t*>(w + L.kb)};
+  uint64_t* pbuf[2] = {reinterpret_cast<uint64_t*>(w + L.pa), reinterpret_cast<uint64_t*>(w + L.pb)};
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
+  uint32_t* sums = reinterpret_cast<uint32_t*>(w + L.sums);
+  const unsigned nt = (unsigned)L.n_tiles;
+  const int32_t* kin = rows;
+  const uint64_t* pin = nullptr;
+  int shift = 0;
+  for (int p = 0; p < L.passes; ++p) {
+    const int db = L.digit[p];
+    const int R = 1 << db;
+    const int64_t n_chunks = (L.n_tiles + kScanTiles - 1) / kScanTiles;
+    hipLaunchKernelGGL(sort_upsweep_kernel, dim3(nt), dim3(kSortThreads), 0, s, kin, nnz, shift, db, L.n_tiles, cnt);
+    hipLaunchKernelGGL(sort_colsum_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
+    hipLaunchKernelGGL(sort_colscan_top_kernel, dim3(1), dim3(1024), 0, s, sums, n_chunks, R);
+    hipLaunchKernelGGL(sort_colscan_apply_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
+    const bool first = p == 0, last = p == L.passes - 1;
+    int32_t* kout = kbuf[p & 1];
+    uint64_t* pout = pbuf[p & 1];
+#define HREC_DOWN(F, LST)                                                                                        \
+  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nt), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
+                     shift, db, L.n_tiles, cnt, kout, pout, indices, values)
+    if (first && last) HREC_DOWN(true, true);
+    else if (first) HREC_DOWN(true, false);
+    else if (last) HREC_DOWN(false, true);
+    else HREC_DOWN(false, false);
+#undef HREC_DOWN
+    const int rc = check_launch("coo_to_csr: radix pass");
+    if (rc) return rc;
+    kin = kout;
+    pin = pout;
+    shift += db;
+  }
+  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz + 1)), dim3(256), 0, s, kin, nnz, n_rows,
                      indptr);
   return check_launch("coo_to_csr");
 }

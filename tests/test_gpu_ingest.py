@@ -44,6 +44,19 @@ def test_encode_ids_matches_numpy_unique(device, n, lo, hi):
         np.testing.assert_array_equal(codes.cpu().numpy(), exp_c.astype(np.int32))
 
 
+def test_encode_ids_dense_path_unaligned_views(device):
+    """The dense path's 16-B id loads: a view starting one element in (8-B
+    aligned only) and an odd length take the scalar loads."""
+    h = _hrec()
+    rng = np.random.default_rng(5)
+    ids = rng.integers(0, 3000, 20001, dtype=np.int64)
+    d_ids = torch.as_tensor(ids, device=device)[1:]
+    exp_u, exp_c = np.unique(ids[1:], return_inverse=True)
+    uniq, codes = h.encode_ids(d_ids, (0, 2999))
+    np.testing.assert_array_equal(uniq.cpu().numpy(), exp_u)
+    np.testing.assert_array_equal(codes.cpu().numpy(), exp_c.astype(np.int32))
+
+
 def test_encode_ids_empty(device):
     h = _hrec()
     uniq, codes = h.encode_ids(torch.zeros(0, dtype=torch.int64, device=device))
@@ -52,11 +65,14 @@ def test_encode_ids_empty(device):
 
 @pytest.mark.parametrize("presorted", [False, True])
 @pytest.mark.parametrize("nnz,n_rows,n_cols", [(1, 1, 1), (50, 7, 9), (10000, 3, 500), (200000, 4097, 1000),
-                                               (300000, 70000, 50)])
+                                               (300000, 70000, 50), (1_000_000, 1024, 10), (500_000, 1025, 7),
+                                               (3_000_000, 1_500_000, 100)])
 def test_coo_to_csr_matches_stable_argsort(device, nnz, n_rows, n_cols, presorted):
-    """Both paths: the radix sort with (col, rating) riding as 64-bit values,
-    and rows already in order (e.g. ratings grouped by user), taken without
-    a sort; rating bit patterns (-0.0, NaN payloads) pass unchanged."""
+    """Both paths: the hand-written stable LSD radix sort (1 pass at <= 10
+    bits of row code, 2 at 11-20, 3 at 21; (col, rating) ride as 64-bit
+    values between passes), and rows already in order (e.g. ratings grouped
+    by user), taken without a sort; rating bit patterns (-0.0, NaN payloads)
+    pass unchanged."""
     h = _hrec()
     rng = np.random.default_rng(nnz + n_rows)
     rows = rng.integers(0, n_rows, nnz).astype(np.int32)
