@@ -142,6 +142,117 @@ __global__ __launch_bounds__(256) void uniq_from_rank_kernel(const int32_t* __re
   }
 }
 
+// Small dense spans (<= kBitsSpan ids, e.g. c2's 100k items): presence as a
+// bitmap that every block keeps in LDS, ranks from per-word prefix counts —
+// the random per-entry table accesses stay in LDS instead of L2 lines.
+constexpr int64_t kBitsSpan = (int64_t)1 << 19;  // bitmap 64 KB + prefixes 64 KB
+constexpr unsigned kBitsBlocks = 1024;
+
+__global__ __launch_bounds__(256) void mark_bits_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
+                                                        int64_t span, uint32_t* __restrict__ bits) {
+  extern __shared__ uint32_t lb[];
+  const int nw = (int)((span + 31) >> 5);
+  for (int q = threadIdx.x; q < nw; q += 256) lb[q] = 0u;
+  __syncthreads();
+  const bool vec = ((uintptr_t)ids & 15) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
+    int64_t v[4];
+    load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
+    if (p0 + stride < np) {
+      load_id_pair(ids, n, p0 + stride, lo, vec, v[2], v[3]);
+    } else {
+      v[2] = v[3] = -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (v[u] >= 0 && v[u] < span) atomicOr(&lb[v[u] >> 5], 1u << (v[u] & 31));
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < nw; q += 256)
+    if (lb[q]) atomicOr(&bits[q], lb[q]);
+}
+
+// pre[q] = ids present below word q (one block: words <= 16384); total -> *n_uniq
+__global__ __launch_bounds__(1024) void bits_prefix_kernel(const uint32_t* __restrict__ bits, int nw,
+                                                           uint32_t* __restrict__ pre, int64_t* __restrict__ n_uniq) {
+  __shared__ uint32_t wsum[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (int q0 = 0; q0 < nw; q0 += 1024) {
+    const int q = q0 + threadIdx.x;
+    const uint32_t c = q < nw ? (uint32_t)__popc(bits[q]) : 0u;
+    uint32_t x = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t base = carry, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) base += wsum[k];
+      tot += wsum[k];
+    }
+    if (q < nw) pre[q] = base + x - c;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *n_uniq = (int64_t)carry;
+}
+
+__global__ __launch_bounds__(256) void codes_bits_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
+                                                         int64_t span, const uint32_t* __restrict__ bits,
+                                                         const uint32_t* __restrict__ pre,
+                                                         int32_t* __restrict__ codes) {
+  extern __shared__ uint32_t lb[];
+  const int nw = (int)((span + 31) >> 5);
+  uint32_t* lp = lb + nw;
+  for (int q = threadIdx.x; q < nw; q += 256) {
+    lb[q] = bits[q];
+    lp[q] = pre[q];
+  }
+  __syncthreads();
+  const bool vec = ((uintptr_t)ids & 15) == 0, vst = ((uintptr_t)codes & 7) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  auto code = [&](int64_t v) -> int32_t {
+    if (v < 0 || v >= span) return -1;  // out of range (a caller error)
+    const uint32_t wd = lb[v >> 5];
+    return (int32_t)(lp[v >> 5] + (uint32_t)__popc(wd & ((1u << (v & 31)) - 1u)));
+  };
+  for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
+    int64_t v[4];
+    load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
+    if (p0 + stride < np) {
+      load_id_pair(ids, n, p0 + stride, lo, vec, v[2], v[3]);
+    } else {
+      v[2] = v[3] = -1;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t p = p0 + h * stride;
+      if (p >= np) break;
+      const int32_t c0 = code(v[2 * h]), c1 = code(v[2 * h + 1]);
+      if (vst && 2 * p + 1 < n) {
+        *reinterpret_cast<int2*>(codes + 2 * p) = make_int2(c0, c1);
+      } else {
+        codes[2 * p] = c0;
+        if (2 * p + 1 < n) codes[2 * p + 1] = c1;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void uniq_bits_kernel(const uint32_t* __restrict__ bits,
+                                                        const uint32_t* __restrict__ pre, int64_t span, int64_t lo,
+                                                        int64_t* __restrict__ uniq) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < span; v += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t wd = bits[v >> 5];
+    if ((wd >> (v & 31)) & 1u) uniq[pre[v >> 5] + (uint32_t)__popc(wd & ((1u << (v & 31)) - 1u))] = v + lo;
+  }
+}
+
 __global__ void minmax_store_kernel(const int64_t* __restrict__ mn, const int64_t* __restrict__ mx,
                                     int64_t* __restrict__ out) {
   out[0] = *mn;
@@ -152,10 +263,28 @@ __global__ void minmax_store_kernel(const int64_t* __restrict__ mn, const int64_
 // Each boundary between distinct keys fills the empty rows in between.
 __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* __restrict__ keys, int64_t nnz,
                                                                  int64_t n_rows, int64_t* __restrict__ indptr) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= nnz; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t lo = (i == 0) ? -1 : (int64_t)keys[i - 1];
-    const int64_t hi = (i == nnz) ? n_rows : (int64_t)keys[i];
-    for (int64_t r = lo + 1; r <= hi && r <= n_rows; ++r) indptr[r] = i;
+  // thread j: positions 4j .. 4j + 3 (one 16-B load when aligned and in range)
+  const bool vec = ((uintptr_t)keys & 15) == 0;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * j <= nnz;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = 4 * j;
+    int64_t k[4];
+    if (vec && i0 + 3 < nnz) {
+      const int4 v = *reinterpret_cast<const int4*>(keys + i0);
+      k[0] = v.x, k[1] = v.y, k[2] = v.z, k[3] = v.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) k[e] = i0 + e < nnz ? (int64_t)keys[i0 + e] : n_rows;
+    }
+    int64_t lo = i0 == 0 ? -1 : (int64_t)keys[i0 - 1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t i = i0 + e;
+      if (i > nnz) break;
+      const int64_t hi = i == nnz ? n_rows : k[e];
+      for (int64_t r = lo + 1; r <= hi && r <= n_rows; ++r) indptr[r] = i;
+      lo = hi;
+    }
   }
 }
 
@@ -169,7 +298,9 @@ __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* 
 //   2. a column scan of the tile-major counts (sort_colsum / colscan_*): the
 //      output offset of every (tile, digit) — digits ascending, tiles in
 //      input order;
-//   3. downsweep: each wave takes a contiguous 1/8 of the block's tile into
+//   3. downsweep (persistent, one block per CU; the next tile's entries load
+//      while a tile is written out): each wave takes a contiguous 1/8 of the
+//      block's tile into
 //      registers and ranks its entries among its own same-digit entries in
 //      input order (per 64-entry round: the lanes below with the same digit,
 //      from `bits` ballots, plus the wave's running per-digit count in LDS —
@@ -277,117 +408,127 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
   __shared__ uint32_t scan_sh[NW];
   const int R = 1 << bits;
   const uint32_t dmask = (uint32_t)(R - 1);
-  for (int d = threadIdx.x; d < R; d += kSortThreads) {
-    goff[d] = offs[(int64_t)blockIdx.x * R + d];
-#pragma unroll
-    for (int q = 0; q < NW; ++q) wh[q][d] = 0;
-  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int tn = (int)(n - base < kSortTile ? n - base : kSortTile);  // entries of this tile
-  // 1. wave w takes tile entries [w PW, (w + 1) PW) into registers, 64 per
-  //    round (coalesced)
+  // wave w takes tile entries [w PW, (w + 1) PW), 64 per round (coalesced)
   int32_t key[kSortIPT];
   uint64_t pay[kSortIPT];
+  auto load = [&](int64_t tile) {
+    const int64_t base = tile * kSortTile;
 #pragma unroll
-  for (int r = 0; r < kSortIPT; ++r) {
-    const int e = w * PW + r * 64 + lane;
-    key[r] = 0;
-    pay[r] = 0;
-    if (e < tn) {
-      key[r] = keys_in[base + e];
-      if constexpr (FIRST) {
-        pay[r] = (uint64_t)(uint32_t)cols_in[base + e] | ((uint64_t)__float_as_uint(vals_in[base + e]) << 32);
-      } else {
-        pay[r] = pay_in[base + e];
+    for (int r = 0; r < kSortIPT; ++r) {
+      const int64_t i = base + w * PW + r * 64 + lane;
+      key[r] = 0;
+      pay[r] = 0;
+      if (tile < n_tiles && i < n) {
+        key[r] = keys_in[i];
+        if constexpr (FIRST) {
+          pay[r] = (uint64_t)(uint32_t)cols_in[i] | ((uint64_t)__float_as_uint(vals_in[i]) << 32);
+        } else {
+          pay[r] = pay_in[i];
+        }
       }
     }
-  }
-  __syncthreads();
-  // 2. each wave ranks its own entries in order (no block barriers): within a
-  //    round the lanes below with the same digit (peer mask from `bits`
-  //    ballots), before it the wave's running per-digit count (LDS)
-  uint32_t rk[kSortIPT];
+  };
+  // persistent blocks (one per CU: the tile takes 118 KB of LDS); the next
+  // tile's entries load while this tile is written out
+  int64_t tile = blockIdx.x;
+  load(tile);
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const int64_t base = tile * kSortTile;
+    const int tn = (int)(n - base < kSortTile ? n - base : kSortTile);  // entries of this tile
+    for (int d = threadIdx.x; d < R; d += kSortThreads) {
+      goff[d] = offs[tile * R + d];
 #pragma unroll
-  for (int r = 0; r < kSortIPT; ++r) {
-    const bool active = w * PW + r * 64 + lane < tn;
-    const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
-    uint64_t peers = __ballot(active);
-    for (int b = 0; b < bits; ++b) {
-      const uint64_t m = __ballot((dg >> b) & 1u);
-      peers &= ((dg >> b) & 1u) ? m : ~m;
+      for (int q = 0; q < NW; ++q) wh[q][d] = 0;
     }
-    const int rank = __popcll(peers & lt);
-    const uint32_t before = active ? wh[w][dg] : 0;
-    rk[r] = before + (uint32_t)rank;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (active && rank == 0) wh[w][dg] = (uint16_t)(before + __popcll(peers));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  __syncthreads();
-  // 3. offsets in the tile's digit-sorted order: digits ascending, waves in
-  //    order within a digit (exclusive scan over (digit, wave); thread t owns
-  //    digits 2t, 2t + 1, R <= 1024)
-  {
-    const int d0 = 2 * threadIdx.x;
-    uint32_t c[2][NW], tot = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        c[h][q] = d0 + h < R ? wh[q][d0 + h] : 0;
-        tot += c[h][q];
-      }
-    uint32_t x = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63) scan_sh[w] = x;
     __syncthreads();
-    uint32_t run = x - tot;
-    for (int q = 0; q < w; ++q) run += scan_sh[q];
+    // 1. each wave ranks its own entries in order (no block barriers): within
+    //    a round the lanes below with the same digit (peer mask from `bits`
+    //    ballots), before it the wave's running per-digit count (LDS)
+    uint32_t rk[kSortIPT];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        if (d0 + h < R) wh[q][d0 + h] = (uint16_t)run;
-        run += c[h][q];
-      }
-  }
-  __syncthreads();
-  // 4. the tile sorted into LDS
-#pragma unroll
-  for (int r = 0; r < kSortIPT; ++r) {
-    if (w * PW + r * 64 + lane < tn) {
+    for (int r = 0; r < kSortIPT; ++r) {
+      const bool active = w * PW + r * 64 + lane < tn;
       const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
-      const uint32_t q = wh[w][dg] + rk[r];
-      sk[q] = key[r];
-      sp[q] = pay[r];
+      uint64_t peers = __ballot(active);
+      for (int b = 0; b < bits; ++b) {
+        const uint64_t m = __ballot((dg >> b) & 1u);
+        peers &= ((dg >> b) & 1u) ? m : ~m;
+      }
+      const int rank = __popcll(peers & lt);
+      const uint32_t before = active ? wh[w][dg] : 0;
+      rk[r] = before + (uint32_t)rank;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (active && rank == 0) wh[w][dg] = (uint16_t)(before + __popcll(peers));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-  }
-  __syncthreads();
-  // 5. write out: consecutive LDS entries of one digit go to consecutive
-  //    output positions (coalesced runs); the digit's first LDS slot is its
-  //    wave-0 offset
-  for (int q = threadIdx.x; q < tn; q += kSortThreads) {
-    const int32_t k = sk[q];
-    const uint32_t dg = ((uint32_t)k >> shift) & dmask;
-    const uint32_t pos = goff[dg] + ((uint32_t)q - wh[0][dg]);
-    const uint64_t pv = sp[q];
-    keys_out[pos] = k;
-    if constexpr (LAST) {
-      idx_out[pos] = (int32_t)(uint32_t)pv;
-      val_out[pos] = __uint_as_float((uint32_t)(pv >> 32));
-    } else {
-      pay_out[pos] = pv;
+    __syncthreads();
+    // 2. offsets in the tile's digit-sorted order: digits ascending, waves in
+    //    order within a digit (exclusive scan over (digit, wave); thread t
+    //    owns digits 2t, 2t + 1, R <= 1024)
+    {
+      const int d0 = 2 * threadIdx.x;
+      uint32_t c[2][NW], tot = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          c[h][q] = d0 + h < R ? wh[q][d0 + h] : 0;
+          tot += c[h][q];
+        }
+      uint32_t x = tot;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      if (lane == 63) scan_sh[w] = x;
+      __syncthreads();
+      uint32_t run = x - tot;
+      for (int q = 0; q < w; ++q) run += scan_sh[q];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          if (d0 + h < R) wh[q][d0 + h] = (uint16_t)run;
+          run += c[h][q];
+        }
     }
+    __syncthreads();
+    // 3. the tile sorted into LDS; then the next tile's loads are issued
+#pragma unroll
+    for (int r = 0; r < kSortIPT; ++r) {
+      if (w * PW + r * 64 + lane < tn) {
+        const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
+        const uint32_t q = wh[w][dg] + rk[r];
+        sk[q] = key[r];
+        sp[q] = pay[r];
+      }
+    }
+    __syncthreads();
+    load(tile + gridDim.x);
+    // 4. write out: consecutive LDS entries of one digit go to consecutive
+    //    output positions (coalesced runs); a digit's first LDS slot is its
+    //    wave-0 offset
+    for (int q = threadIdx.x; q < tn; q += kSortThreads) {
+      const int32_t k = sk[q];
+      const uint32_t dg = ((uint32_t)k >> shift) & dmask;
+      const uint32_t pos = goff[dg] + ((uint32_t)q - wh[0][dg]);
+      const uint64_t pv = sp[q];
+      keys_out[pos] = k;
+      if constexpr (LAST) {
+        idx_out[pos] = (int32_t)(uint32_t)pv;
+        val_out[pos] = __uint_as_float((uint32_t)(pv >> 32));
+      } else {
+        pay_out[pos] = pv;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -401,8 +542,14 @@ __global__ __launch_bounds__(256) void descent_kernel(const int32_t* __restrict_
       const int64_t i = i0 + u * stride;
       if (i + 1 < n) d |= x[i] > x[i + 1];
     }
+    // stop once any wave has found a descent (unsorted input: the common
+    // case for the CSC rows ends after the grid's first pass)
+    if (__any(d)) {
+      if ((threadIdx.x & 63) == 0) *flag = 1;
+      return;
+    }
+    if (*reinterpret_cast<volatile const int32_t*>(flag)) return;
   }
-  if (__any(d) && (threadIdx.x & 63) == 0) *flag = 1;
 }
 
 // rows already non-decreasing: the CSR is the input order (the stable sort is the identity)
@@ -521,6 +668,22 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
   // A narrow id range sorts (id - lo) on only the bits it spans.
   const bool narrow = (uint64_t)id_hi - (uint64_t)id_lo < 0x7fffffffull;
   const int64_t span = narrow ? (int64_t)((uint64_t)id_hi - (uint64_t)id_lo) + 1 : 0;
+  if (narrow && span <= n && span <= kBitsSpan) {
+    // small dense range: LDS bitmaps (flag holds the bits, incl the word prefixes)
+    const int nw = (int)((span + 31) >> 5);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(flag);
+    uint32_t* pre = reinterpret_cast<uint32_t*>(incl);
+    if (hipMemsetAsync(bits, 0, (size_t)nw * sizeof(uint32_t), s) != hipSuccess)
+      return check_launch("encode_ids: memset");
+    const unsigned gb = g < kBitsBlocks ? g : kBitsBlocks;
+    hipLaunchKernelGGL(mark_bits_kernel, dim3(gb), dim3(256), (size_t)nw * 4, s, ids, n, id_lo, span, bits);
+    hipLaunchKernelGGL(bits_prefix_kernel, dim3(1), dim3(1024), 0, s, bits, nw, pre, n_uniq);
+    const auto kfn = codes_bits_kernel;
+    if (!allow_max_lds(kfn)) return check_launch("encode_ids: LDS attribute");
+    hipLaunchKernelGGL(kfn, dim3(gb), dim3(256), (size_t)nw * 8, s, ids, n, id_lo, span, bits, pre, codes);
+    hipLaunchKernelGGL(uniq_bits_kernel, dim3(grid_for(span)), dim3(256), 0, s, bits, pre, span, id_lo, uniq);
+    return check_launch("encode_ids: dense bitmap");
+  }
   if (narrow && span <= n && span < 0x7fffffffll) {
     // dense range: the span-long tables fit the flag / incl buffers (n entries each)
     if (hipMemsetAsync(flag, 0, (size_t)span * sizeof(int32_t), s) != hipSuccess)
@@ -615,6 +778,10 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
   uint32_t* sums = reinterpret_cast<uint32_t*>(w + L.sums);
   const unsigned nt = (unsigned)L.n_tiles;
+  // downsweep: persistent, one block per CU (its tile takes 118 KB of LDS)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const unsigned nd = (unsigned)(L.n_tiles < cus ? L.n_tiles : cus);
   const int32_t* kin = rows;
   const uint64_t* pin = nullptr;
   int shift = 0;
@@ -630,7 +797,7 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
     int32_t* kout = kbuf[p & 1];
     uint64_t* pout = pbuf[p & 1];
 #define HREC_DOWN(F, LST)                                                                                        \
-  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nt), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
+  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nd), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
                      shift, db, L.n_tiles, cnt, kout, pout, indices, values)
     if (first && last) HREC_DOWN(true, true);
     else if (first) HREC_DOWN(true, false);
@@ -643,7 +810,7 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
     pin = pout;
     shift += db;
   }
-  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz + 1)), dim3(256), 0, s, kin, nnz, n_rows,
+  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz / 4 + 1)), dim3(256), 0, s, kin, nnz, n_rows,
                      indptr);
   return check_launch("coo_to_csr");
 }
@@ -672,7 +839,8 @@ extern "C" int hrec_coo_to_csr_sorted(const int32_t* rows, const int32_t* cols, 
   }
   HREC_REQUIRE(n_rows > 0 && rows && cols && vals && indices && values, "coo_to_csr_sorted: null pointer");
   hipLaunchKernelGGL(copy_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, cols, vals, nnz, indices, values);
-  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz + 1)), dim3(256), 0, s, rows, nnz, n_rows, indptr);
+  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz / 4 + 1)), dim3(256), 0, s, rows, nnz, n_rows,
+                     indptr);
   return check_launch("coo_to_csr_sorted");
 }
 
