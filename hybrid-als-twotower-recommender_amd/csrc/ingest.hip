@@ -431,16 +431,29 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
     }
   };
   // persistent blocks (one per CU: the tile takes 118 KB of LDS); the next
-  // tile's entries load while this tile is written out
+  // tile's entries and digit offsets load while this tile is written out
+  uint32_t go[2];  // offsets of digits t, t + 512 (R <= 1024)
+  auto load_offs = [&](int64_t tile) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int d = threadIdx.x + h * kSortThreads;
+      go[h] = (tile < n_tiles && d < R) ? offs[tile * R + d] : 0u;
+    }
+  };
   int64_t tile = blockIdx.x;
   load(tile);
+  load_offs(tile);
   for (; tile < n_tiles; tile += gridDim.x) {
     const int64_t base = tile * kSortTile;
     const int tn = (int)(n - base < kSortTile ? n - base : kSortTile);  // entries of this tile
-    for (int d = threadIdx.x; d < R; d += kSortThreads) {
-      goff[d] = offs[tile * R + d];
 #pragma unroll
-      for (int q = 0; q < NW; ++q) wh[q][d] = 0;
+    for (int h = 0; h < 2; ++h) {
+      const int d = threadIdx.x + h * kSortThreads;
+      if (d < R) {
+        goff[d] = go[h];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) wh[q][d] = 0;
+      }
     }
     __syncthreads();
     // 1. each wave ranks its own entries in order (no block barriers): within
@@ -512,10 +525,14 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
     }
     __syncthreads();
     load(tile + gridDim.x);
+    load_offs(tile + gridDim.x);
     // 4. write out: consecutive LDS entries of one digit go to consecutive
     //    output positions (coalesced runs); a digit's first LDS slot is its
     //    wave-0 offset
-    for (int q = threadIdx.x; q < tn; q += kSortThreads) {
+#pragma unroll
+    for (int e = 0; e < kSortIPT; ++e) {
+      const int q = e * kSortThreads + threadIdx.x;
+      if (q >= tn) break;
       const int32_t k = sk[q];
       const uint32_t dg = ((uint32_t)k >> shift) & dmask;
       const uint32_t pos = goff[dg] + ((uint32_t)q - wh[0][dg]);

@@ -1,17 +1,13 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_ing_f -o f -- python scripts/ingest_probe.py > gpurun_out/pmc_ing_f.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_ing_w -o w -- python scripts/ingest_probe.py > gpurun_out/pmc_ing_w.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ingest.py > gpurun_out/ing_tests.log 2>&1 || { tail -30 gpurun_out/ing_tests.log; exit 1; }
+tail -1 gpurun_out/ing_tests.log
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ing -o ing -- python scripts/ingest_probe.py > gpurun_out/ing_probe.log 2>&1
+grep -E "ms" gpurun_out/ing_probe.log
 python - <<'P'
-import csv, glob, collections
-for tag in ('f', 'w'):
-    f = glob.glob('gpurun_out/pmc_ing_%s/**/*counter_collection.csv' % tag, recursive=True)[0]
-    acc = collections.defaultdict(float); n = collections.Counter()
-    for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'][:60]
-        acc[(k, r['Counter_Name'])] += float(r['Counter_Value']); n[(k, r['Counter_Name'])] += 1
-    for (k, c), v in sorted(acc.items()):
-        if any(s in k for s in ('sort_', 'mark', 'codes', 'indptr', 'copy_entries', 'descent')):
-            print(tag, "%-60s %-11s per-call %.3f GB" % (k, c, v / n[(k, c)] / 1e9))
+import csv
+for r in csv.DictReader(open('gpurun_out/prof_ing/ing_kernel_stats.csv')):
+    if 'sort_down' in r['Name'] or 'sort_up' in r['Name']:
+        print("%-70s calls %4s avg %9.1f us" % (r['Name'][:70], r['Calls'], float(r['AverageNs'])/1e3))
 P

@@ -20,6 +20,13 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/p
 TT_ONLY="--no-ingest --score-users 0 --hybrid-users 0 --c4-items 0 --c5-users 0 --api-reps 0 --rank256-epochs 0 --steps 1 --warmup 0 --no-cpu-baseline"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_tt -o fetchtt -- python bench.py $TT_ONLY > /dev/null 2> gpurun_out/prof_fetch_tt.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_tt -o writett -- python bench.py $TT_ONLY > /dev/null 2> gpurun_out/prof_write_tt.err
+# c5 pruned hybrid (hyb_scores_kernel HS_PRUNE, dot_res_kernel FILTER, hp_*): FETCH and WRITE passes
+C5_ONLY="--no-ingest --score-users 0 --hybrid-users 0 --c4-items 0 --tt-steps 0 --api-reps 0 --rank256-epochs 0 --steps 1 --warmup 0 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_c5 -o fetchc5 -- python bench.py $C5_ONLY > /dev/null 2> gpurun_out/prof_fetch_c5.err
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_c5 -o writec5 -- python bench.py $C5_ONLY > /dev/null 2> gpurun_out/prof_write_c5.err
+# ingest (encode + CSR/CSC radix build): FETCH and WRITE passes of the probe
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_ing -o fetching -- python scripts/ingest_probe.py > /dev/null 2> gpurun_out/prof_fetch_ing.err
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_ing -o writeing -- python scripts/ingest_probe.py > /dev/null 2> gpurun_out/prof_write_ing.err
 # rank-256 ALS half-sweeps (als_half_sweep_wide_kernel): kernel trace of the probe
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_wide -o wide -- python scripts/wide_quick.py 256 300000 100000 > gpurun_out/prof_wide.log 2>&1
 python scripts/summarize_profile.py gpurun_out > gpurun_out/prof_summary.json

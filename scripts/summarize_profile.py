@@ -126,6 +126,38 @@ def main(base):
         tf["hbm_bytes_avg_per_launch_corrected"] = 1024 * (2 * tf["FETCH_SIZE_KiB_avg_per_launch"] +
                                                            tf["WRITE_SIZE_KiB_avg_per_launch"])
     res["tt_item_forward_c4"] = tf
+
+    # c5 pruned hybrid and ingest: per kernel, trace average + PMC bytes per
+    # launch (FETCH x 2: 16-B lane loads)
+    def per_kernel(keys, fetch_sub, write_sub):
+        out = {}
+        for k in keys:
+            d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace if k in r["Kernel_Name"]]
+            e = {"launches": len(d), "avg_ms": sum(d) / max(len(d), 1)}
+            for name, sub in (("FETCH_SIZE", fetch_sub), ("WRITE_SIZE", write_sub)):
+                vals = [float(r["Counter_Value"]) for r in rows(os.path.join(base, sub, "**", "*counter_collection.csv"))
+                        if k in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+                if vals:
+                    e[name + "_KiB_avg_per_launch"] = sum(vals) / len(vals)
+            if "FETCH_SIZE_KiB_avg_per_launch" in e and "WRITE_SIZE_KiB_avg_per_launch" in e:
+                e["hbm_bytes_avg_per_launch_corrected"] = 1024 * (2 * e["FETCH_SIZE_KiB_avg_per_launch"] +
+                                                                  e["WRITE_SIZE_KiB_avg_per_launch"])
+            out[k] = e
+        return out
+
+    c5 = per_kernel(["hp_user_ops_kernel", "hyb_scores_kernel<256, 4, 1>", "hyb_mm_reduce_kernel",
+                     "hp_bound_kernel<256>", "dot_res_kernel<true, 256, true, 2>", "hp_cand_topk_kernel<256>"],
+                    "prof_fetch_c5", "prof_write_c5")
+    tot = sum(e.get("hbm_bytes_avg_per_launch_corrected", 0.0) for e in c5.values())
+    c5["batch_hbm_bytes_corrected"] = tot
+    c5["no_store_bytes"] = 102.4e6
+    c5["traffic_over_no_store"] = tot / 102.4e6
+    res["c5_pruned_hybrid"] = c5
+    res["ingest"] = per_kernel(["mark_present_kernel", "codes_from_rank_kernel", "mark_bits_kernel",
+                                "codes_bits_kernel", "descent_kernel", "copy_entries_kernel",
+                                "indptr_from_sorted_kernel", "sort_upsweep_kernel",
+                                "sort_downsweep_kernel<true, false>", "sort_downsweep_kernel<false, true>"],
+                               "prof_fetch_ing", "prof_write_ing")
     res["sources_sha256"] = source_hashes()
     print(json.dumps(res, indent=1))
 
