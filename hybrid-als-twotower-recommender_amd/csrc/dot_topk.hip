@@ -319,9 +319,12 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   // FILTER: survivors are staged in LDS and appended once per tile (below)
   int* cnt_l = reinterpret_cast<int*>(ths + UB);                  // [UB] per-user counts, then list bases
   int* ovf_l = cnt_l + UB;                                          // [UB] survivors dropped (buffer full)
-  int* buf_n = ovf_l + UB;                                          // entries staged this tile
+  // entries staged per tile: three counters in rotation (tile i uses i % 3;
+  // its flush resets the one of tile i + 2), so a tile without survivors
+  // needs a single barrier
+  int* bn = ovf_l + UB;
   // [sbuf] survivor meta (user << 22 | item in tile << 12 | list offset), then [sbuf] scores
-  uint32_t* buf = reinterpret_cast<uint32_t*>(dsm + (((size_t)UB * kRowB + (size_t)UB * 12 + 4 + 15) & ~(size_t)15));
+  uint32_t* buf = reinterpret_cast<uint32_t*>(dsm + (((size_t)UB * kRowB + (size_t)UB * 12 + 12 + 15) & ~(size_t)15));
   float* buf_s = reinterpret_cast<float*>(buf + sbuf);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
       cnt_l[o] = 0;
       ovf_l[o] = 0;
     }
-    if (threadIdx.x == 0) *buf_n = 0;
+    if (threadIdx.x < 3) bn[threadIdx.x] = 0;
   }
   __syncthreads();
   const int xq = c ^ g;
@@ -393,7 +396,8 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
     const int off = kSwz ? 16 * xq : 16 * g;
     ua[u].i = *reinterpret_cast<const int4*>(us + (16 * u + c) * kRowB + off);
   }
-  for (int64_t it = ig; it < n_it; it += n_ig) {
+  int cur = 0;  // FILTER: this tile's staging counter
+  for (int64_t it = ig; it < n_it; it += n_ig, cur = cur == 2 ? 0 : cur + 1) {
     const int64_t j0 = it * kItems + 16 * NI * w;
     // the wave's valid items (positions relative to its first item, 32-bit)
     const int w_n = (int)(n_items - j0 < 16 * NI ? (n_items - j0 > 0 ? n_items - j0 : 0) : 16 * NI);
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
             msk[u] = m;
             cnt += __popc(m);
           }
-          int pos = cnt ? atomicAdd(buf_n, cnt) : 0;  // LDS: the lanes' reservations serialise in the LDS unit only
+          int pos = cnt ? atomicAdd(&bn[cur], cnt) : 0;  // LDS: the lanes' reservations serialise in the LDS unit only
           const int jt = 16 * NI * w;  // the wave's first item in the tile
 #pragma unroll
           for (int u = 0; u < NU; ++u) {
@@ -570,7 +574,9 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
       // one list reservation per user (global atomics, all in flight), then
       // the appends
       __syncthreads();
-      const int nb = *buf_n < sbuf ? *buf_n : sbuf;
+      const int nb = bn[cur] < sbuf ? bn[cur] : sbuf;  // block-uniform: bn[cur] changes no more this tile
+      if (threadIdx.x == 0) bn[cur == 0 ? 2 : cur - 1] = 0;  // the counter of tile i + 2 (read by all at tile i - 1)
+      if (nb == 0) continue;  // nothing staged: no list to extend
       for (int e = threadIdx.x; e < nb; e += kDotThreads) {
         const uint32_t x = buf[e];
         if (thr_per > 0) {  // the item's own group bound (the ballot used the tile's loosest)
@@ -616,7 +622,6 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
       }
       __syncthreads();
       for (int o = threadIdx.x; o < UB; o += kDotThreads) cnt_l[o] = 0;
-      if (threadIdx.x == 0) *buf_n = 0;
       __syncthreads();
     }
   }
@@ -711,7 +716,7 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
   size_t lds = (size_t)UB * row_lds + (size_t)UB * 4;
   int sbuf = 0;
   if (FILTER) {
-    const size_t head = ((size_t)UB * row_lds + (size_t)UB * 12 + 4 + 15) & ~(size_t)15;
+    const size_t head = ((size_t)UB * row_lds + (size_t)UB * 12 + 12 + 15) & ~(size_t)15;
     const size_t room = head < kMaxLds ? (kMaxLds - head) / 8 : 0;
     sbuf = (int)(room < 4096 ? room : 4096);
     lds = head + (size_t)sbuf * 8;

@@ -2,7 +2,7 @@
 set -e
 mkdir -p gpurun_out
 python -c "import __graft_entry__ as g; g.build()"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests.log 2>&1 || { tail -40 gpurun_out/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/tests.log 2>&1 || { tail -40 gpurun_out/tests.log; exit 1; }
 tail -2 gpurun_out/tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | grep -v amdgpu.ids | tail -2
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
