@@ -160,9 +160,12 @@ def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
             out.append(r)
         fell_back = hp.fallback_taken()
         surv = hp.survivors().double()
+        # the single-shard call the recommender makes at W = 1 (both phases,
+        # the extremes folded into the bound launch)
+        local_ms = ev_time(lambda: hp.local(False, rec.offset), reps, stream)
         tot = sum(r["avg_launch_ms"] for r in out)
         dom = max(out, key=lambda r: r["avg_launch_ms"])
-        return dict(dom, stages=out, fallback_taken=fell_back,
+        return dict(dom, stages=out, fallback_taken=fell_back, one_shard_call_ms=local_ms,
                     survivors_per_user={"mean": float(surv.mean()), "max": float(surv.max())},
                     batch_view={"ms": tot, "algorithmic_bytes": 2 * op_b,
                                 "note": "no-store bytes (both item operands once) / both phases' time",

@@ -162,10 +162,14 @@ __device__ __forceinline__ float hp_pick(const hp_f4& a, int r) {
 // <= the light model's group maximum scaled (pass 1's partials), so theta_gi
 // = the raw score of that h_n, lowered by a relative margin. Also resets the
 // user's survivor count, and block 0 the fallback flag.
-template <int DK>
+// LOCAL (hrec_hybrid_prune_local, one shard): the user's row extremes are
+// first reduced here from phase 1's group partials (and written out), in
+// place of hyb_mm_reduce_kernel + a separate bound launch.
+template <int DK, bool LOCAL>
 __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__ part, const int* __restrict__ argpos,
                                                        int G, int64_t N, int B, int hm, const float* __restrict__ als_mm,
-                                                       const float* __restrict__ tt_mm, double w0, double w1, int kk,
+                                                       const float* __restrict__ tt_mm, float* __restrict__ als_mm_out,
+                                                       float* __restrict__ tt_mm_out, double w0, double w1, int kk,
                                                        int slice_ni, const uint16_t* __restrict__ uop,
                                                        const uint16_t* __restrict__ als_items,
                                                        const uint16_t* __restrict__ tt_items,
@@ -184,7 +188,40 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   if (b == 0 && tid == 0) *flag = 0;
   if (tid == 0) cn[b] = 0;
   float* th_row = theta + (int64_t)b * G;
-  const float amin = als_mm[b], amax = als_mm[B + b], tmin = tt_mm[b], tmax = tt_mm[B + b];
+  float amin, amax, tmin, tmax;
+  if constexpr (LOCAL) {
+    // thread t: model t >> 7, group t & 127 (G <= 128); fminf / fmaxf as
+    // hyb_mm_reduce_kernel (exact: the same extremes)
+    __shared__ float red[4][2];
+    const int m = tid >> 7, gi = tid & 127;
+    float lo = INFINITY, hi = -INFINITY;
+    if (gi < G) {
+      lo = part[(((int64_t)m * G + gi) * 2) * B + b];
+      hi = part[(((int64_t)m * G + gi) * 2 + 1) * B + b];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      lo = fminf(lo, __shfl_xor(lo, off, kWave));
+      hi = fmaxf(hi, __shfl_xor(hi, off, kWave));
+    }
+    if (lane == 0) {
+      red[wv][0] = lo;
+      red[wv][1] = hi;
+    }
+    __syncthreads();
+    amin = fminf(red[0][0], red[1][0]);
+    amax = fmaxf(red[0][1], red[1][1]);
+    tmin = fminf(red[2][0], red[3][0]);
+    tmax = fmaxf(red[2][1], red[3][1]);
+    if (tid == 0) {
+      als_mm_out[b] = amin;
+      als_mm_out[B + b] = amax;
+      tt_mm_out[b] = tmin;
+      tt_mm_out[B + b] = tmax;
+    }
+  } else {
+    amin = als_mm[b], amax = als_mm[B + b], tmin = tt_mm[b], tmax = tt_mm[B + b];
+  }
   if (!(isfinite(amin) && isfinite(amax) && isfinite(tmin) && isfinite(tmax))) {
     // NaN / infinite scores (an unknown user row, non-finite vectors): the
     // exact path ranks them; nothing survives the filter
@@ -611,6 +648,62 @@ extern "C" int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, 
                            w.part, w.argpos, nullptr, s, w.uop);
 }
 
+// Phase 2 launches (a - c). local: the bound kernel reduces the extremes
+// from phase 1's partials (written to als_mm_out / tt_mm_out) instead of
+// reading them.
+static int hp_phase2(bool local, int n_users, const void* als_items, const void* tt_items, int64_t n_items, int dk,
+                     const float* als_mm, const float* tt_mm, float* als_mm_out, float* tt_mm_out, int als_wins,
+                     int top_k, int64_t idx_offset, int64_t* out_idx, double* out_val, void* workspace,
+                     hipStream_t s) {
+  const int kk = (int)(top_k < n_items ? top_k : n_items);
+  const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, kk);
+  // src/hybrid_system.py:69 — strict '>' picks (0.8, 0.2), else (0.2, 0.8); the heavier model filters
+  const double w0 = als_wins ? 0.8 : 0.2, w1 = als_wins ? 0.2 : 0.8;
+  const int hm = als_wins ? 0 : 1;
+  const int G = hs_groups(n_items);
+  const uint16_t* ai = static_cast<const uint16_t*>(als_items);
+  const uint16_t* ti = static_cast<const uint16_t*>(tt_items);
+#define HREC_HP_BOUND(DK, L)                                                                                       \
+  hipLaunchKernelGGL((hp_bound_kernel<DK, L>), dim3((unsigned)n_users), dim3(256), 0, s, w.part, w.argpos, G,        \
+                     n_items, n_users, hm, als_mm, tt_mm, als_mm_out, tt_mm_out, w0, w1, kk, hs_slice_tiles(DK),   \
+                     w.uop, ai, ti, w.theta, w.cn, w.uflag, w.flag)
+  switch (dk) {
+    case 64:
+      if (local) HREC_HP_BOUND(64, true); else HREC_HP_BOUND(64, false);
+      break;
+    case 128:
+      if (local) HREC_HP_BOUND(128, true); else HREC_HP_BOUND(128, false);
+      break;
+    default:
+      if (local) HREC_HP_BOUND(256, true); else HREC_HP_BOUND(256, false);
+      break;
+  }
+#undef HREC_HP_BOUND
+  int rc = check_launch("hp_bound_kernel");
+  if (rc) return rc;
+  // b. the heavy model's scores, survivors of the per-group bounds
+  const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
+  const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
+  rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
+                      w.cn, s);
+  if (rc) return rc;
+  // c. light scores + fusion of the survivors, exact top-k; the exact path in
+  //    the same block for the users that need it
+  const float* amm = local ? als_mm_out : als_mm;
+  const float* tmm = local ? tt_mm_out : tt_mm;
+#define HREC_HP_CAND(DK)                                                                                           \
+  hipLaunchKernelGGL(hp_cand_topk_kernel<DK>, dim3((unsigned)n_users), dim3(512), 0, s, w.cn, kHpCap, w.cv, w.ci,   \
+                     w.uflag, w.uop, hm, als_items, tt_items, n_items, n_users, amm, tmm, w0, w1, kk,              \
+                     idx_offset, out_idx, out_val, w.flag)
+  switch (dk) {
+    case 64: HREC_HP_CAND(64); break;
+    case 128: HREC_HP_CAND(128); break;
+    default: HREC_HP_CAND(256); break;
+  }
+#undef HREC_HP_CAND
+  return check_launch("hp_cand_topk_kernel");
+}
+
 extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, const int64_t* als_rows,
                                       int64_t n_als_rows, int als_width, const float* tt_users, int64_t tt_ld,
                                       int tt_width, int n_users, const void* als_items, const void* tt_items,
@@ -626,46 +719,43 @@ extern "C" int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, co
   HREC_REQUIRE(als_mm && tt_mm && out_idx && out_val && workspace, "hybrid_prune_topk: null pointer");
   const size_t need = hrec_hybrid_prune_workspace_bytes(n_users, n_items, dk, top_k);
   HREC_REQUIRE(workspace_bytes >= need, "hybrid_prune_topk: workspace %zu < %zu", workspace_bytes, need);
+  return hp_phase2(false, n_users, als_items, tt_items, n_items, dk, als_mm, tt_mm, nullptr, nullptr, als_wins, top_k,
+                   idx_offset, out_idx, out_val, workspace, as_stream(stream));
+}
+
+extern "C" int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, const int64_t* als_rows,
+                                       int64_t n_als_rows, int als_width, const float* tt_users, int64_t tt_ld,
+                                       int tt_width, int n_users, const void* als_items, const void* tt_items,
+                                       int64_t n_items, int dk, int als_wins, int top_k, int64_t idx_offset,
+                                       float* als_mm, float* tt_mm, int64_t* out_idx, double* out_val,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = hp_check_args(als_users, als_ld, n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, als_items,
+                         tt_items, n_items, dk, "hybrid_prune_local");
+  if (rc) return rc;
+  HREC_REQUIRE(top_k >= 1 && top_k <= kHpMaxK, "hybrid_prune_local: top_k must be in [1, %d] (larger: the unfused path)",
+               kHpMaxK);
+  if (n_users == 0) return HREC_OK;
+  HREC_REQUIRE(als_mm && tt_mm && workspace, "hybrid_prune_local: null pointer");
+  if (n_items == 0)  // extremes of an empty shard; no top-k entries
+    return hrec_hybrid_prune_minmax(als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld, tt_width,
+                                    n_users, als_items, tt_items, 0, dk, als_mm, tt_mm, workspace, workspace_bytes,
+                                    stream);
+  HREC_REQUIRE(out_idx && out_val, "hybrid_prune_local: null output");
+  const size_t need = hrec_hybrid_prune_workspace_bytes(n_users, n_items, dk, top_k);
+  HREC_REQUIRE(workspace_bytes >= need, "hybrid_prune_local: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t s = as_stream(stream);
-  const int kk = (int)(top_k < n_items ? top_k : n_items);
-  const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, kk);
-  // src/hybrid_system.py:69 — strict '>' picks (0.8, 0.2), else (0.2, 0.8); the heavier model filters
-  const double w0 = als_wins ? 0.8 : 0.2, w1 = als_wins ? 0.2 : 0.8;
-  const int hm = als_wins ? 0 : 1;
-  const int G = hs_groups(n_items);
-  const uint16_t* ai = static_cast<const uint16_t*>(als_items);
-  const uint16_t* ti = static_cast<const uint16_t*>(tt_items);
-#define HREC_HP_BOUND(DK)                                                                                          \
-  hipLaunchKernelGGL(hp_bound_kernel<DK>, dim3((unsigned)n_users), dim3(256), 0, s, w.part, w.argpos, G, n_items,   \
-                     n_users, hm, als_mm, tt_mm, w0, w1, kk, hs_slice_tiles(DK), w.uop, ai, ti, w.theta, w.cn,     \
-                     w.uflag, w.flag)
-  switch (dk) {
-    case 64: HREC_HP_BOUND(64); break;
-    case 128: HREC_HP_BOUND(128); break;
-    default: HREC_HP_BOUND(256); break;
-  }
-#undef HREC_HP_BOUND
-  rc = check_launch("hp_bound_kernel");
+  const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, 1);
+  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
+                     n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
+  rc = check_launch("hp_user_ops_kernel");
   if (rc) return rc;
-  // b. the heavy model's scores, survivors of the per-group bounds
-  const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
-  const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
-  rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
-                      w.cn, s);
+  // phase 1 without its min / max reduce launch (the bound kernel folds it)
+  rc = hybrid_scores_run(1 /* HS_PRUNE */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
+                         tt_width, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, 0, nullptr, nullptr,
+                         w.part, w.argpos, nullptr, s, w.uop);
   if (rc) return rc;
-  // c. light scores + fusion of the survivors, exact top-k; the exact path in
-  //    the same block for the users that need it
-#define HREC_HP_CAND(DK)                                                                                           \
-  hipLaunchKernelGGL(hp_cand_topk_kernel<DK>, dim3((unsigned)n_users), dim3(512), 0, s, w.cn, kHpCap, w.cv, w.ci,   \
-                     w.uflag, w.uop, hm, als_items, tt_items, n_items, n_users, als_mm, tt_mm, w0, w1, kk,         \
-                     idx_offset, out_idx, out_val, w.flag)
-  switch (dk) {
-    case 64: HREC_HP_CAND(64); break;
-    case 128: HREC_HP_CAND(128); break;
-    default: HREC_HP_CAND(256); break;
-  }
-#undef HREC_HP_CAND
-  return check_launch("hp_cand_topk_kernel");
+  return hp_phase2(true, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, als_mm, tt_mm, als_wins, top_k,
+                   idx_offset, out_idx, out_val, workspace, s);
 }
 
 extern "C" int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,

@@ -500,7 +500,7 @@ static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
     case 3: rc = hs_launch_n<DK, 3, MODE>(a, lds, s); break;
     default: rc = hs_launch_n<DK, 4, MODE>(a, lds, s); break;
   }
-  if (rc || MODE == HS_GATED) return rc;
+  if (rc || MODE == HS_GATED || mm0 == nullptr) return rc;  // no extremes wanted: the caller folds the partials
   hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((a.B + 63) / 64), 2), dim3(256), 0, s, a.part, a.B, a.G,
                      mm0, mm1);
   return check_launch("hyb_mm_reduce_kernel");

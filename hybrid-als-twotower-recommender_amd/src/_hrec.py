@@ -111,6 +111,9 @@ _SIGNATURES.update({
                                           _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_prune_topk": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp,
                                         _c_i64, _c_i32, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_prune_local": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp,
+                                         _c_i64, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_sz,
+                                         _vp]),
     "hrec_hybrid_prune_fallback_taken": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_hybrid_prune_survivors": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
@@ -703,6 +706,21 @@ class HybridPrune:
             int(bool(als_wins)), self.top_k, int(idx_offset), _vp(out_i.data_ptr()), _vp(out_v.data_ptr()),
             _vp(self.ws.data_ptr()), self.need, _stream()))
         return out_i, out_v
+
+    def local(self, als_wins, idx_offset=0):
+        """Both phases for ONE item shard (hrec_hybrid_prune_local): the same
+        (ids, fused) as minmax() + topk() with one launch fewer; returns
+        (ids, fused, als_mm, tt_mm)."""
+        dev = self.Va.device
+        a_mm = torch.empty((2, self.B), dtype=torch.float32, device=dev)
+        t_mm = torch.empty((2, self.B), dtype=torch.float32, device=dev)
+        out_i = torch.empty((self.B, self.kk), dtype=torch.int64, device=dev)
+        out_v = torch.empty((self.B, self.kk), dtype=torch.float64, device=dev)
+        _check("hrec_hybrid_prune_local", lib().hrec_hybrid_prune_local(
+            *self._users(), int(bool(als_wins)), self.top_k, int(idx_offset), _vp(a_mm.data_ptr()),
+            _vp(t_mm.data_ptr()), _vp(out_i.data_ptr()), _vp(out_v.data_ptr()), _vp(self.ws.data_ptr()), self.need,
+            _stream()))
+        return out_i, out_v, a_mm, t_mm
 
     def survivors(self):
         """Survivors of the last topk()'s heavy-model filter per user (int32 [B])."""

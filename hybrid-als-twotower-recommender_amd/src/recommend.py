@@ -69,8 +69,9 @@ class ShardedRecommender:
     models' scores on the bf16 matrix cores (f32 accumulation) from bf16
     copies of the factors / item vectors made once here; pass V_local (the
     shard's ALS item factor rows) instead of Vt_local. For top_k <= 8 the bf16
-    path is the pruned one (hrec_hybrid_prune_*: no score matrix in HBM,
-    exact fallback gated on the device); pruned=False keeps the score
+    path is the pruned one (hrec_hybrid_prune_*: no score matrix in HBM, the
+    exact path inside the survivor kernel for the users that need it; one
+    shard: hrec_hybrid_prune_local); pruned=False keeps the score
     matrices (hrec_hybrid_scores + hrec_fuse_rows_topk); all three bf16
     paths return the same bits."""
 
@@ -161,6 +162,10 @@ class ShardedRecommender:
                     self.U, user_rows, user_vecs, self.V_op, self.iv_op, top_k)
             else:
                 hp.rebind(user_rows, user_vecs)
+            if self.world == 1:  # one shard: both phases in one call (no C2 between them)
+                idx, val, _, _ = hp.local(als_wins, self.offset)
+                self.last_prune = hp
+                return idx, val
             a_mm, t_mm = hp.minmax()
         else:
             inf = float("inf")

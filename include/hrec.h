@@ -488,6 +488,15 @@ int hrec_hybrid_prune_topk(const float* als_users, int64_t als_ld, const int64_t
                            void* workspace, size_t workspace_bytes, void* stream);
 int hrec_hybrid_prune_fallback_taken(const void* workspace, int n_users, int64_t n_items, int dk,
                                      int top_k, int* out, void* stream);
+/* Both phases for ONE item shard (no cross-shard min / max to combine): the
+ * same results as hrec_hybrid_prune_minmax + hrec_hybrid_prune_topk (als_mm /
+ * tt_mm are outputs here, [2, n_users] f32) with one launch fewer (the bound
+ * kernel reduces the extremes). Same workspace. */
+int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, const int64_t* als_rows, int64_t n_als_rows,
+                            int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
+                            const void* als_items, const void* tt_items, int64_t n_items, int dk, int als_wins,
+                            int top_k, int64_t idx_offset, float* als_mm, float* tt_mm, int64_t* out_idx,
+                            double* out_val, void* workspace, size_t workspace_bytes, void* stream);
 /* Diagnostics of the last phase 2: the survivors of the heavy-model filter per
  * user (out: n_users int32, device). */
 int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,

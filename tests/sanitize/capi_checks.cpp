@@ -93,6 +93,8 @@ int main() {
   INVALID(hrec_hybrid_prune_topk(nullptr, 64, nullptr, 4, 64, nullptr, 64, 64, 4, nullptr, nullptr, 10, 64, nullptr,
                                  nullptr, 1, 9, 0, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_prune_fallback_taken(nullptr, 1, 1, 64, 5, nullptr, nullptr));
+  INVALID(hrec_hybrid_prune_local(nullptr, 64, nullptr, 4, 64, nullptr, 64, 64, 4, nullptr, nullptr, 10, 64, 0, 9, 0,
+                                  nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_prune_survivors(nullptr, 1, 1, 64, 5, nullptr, nullptr));
 
   // workspace-size queries over a sweep of shapes (UBSan: no signed overflow)

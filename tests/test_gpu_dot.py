@@ -418,13 +418,18 @@ def test_hybrid_prune_equals_unfused(device, dk, B, N, ka, kt, k):
         assert torch.equal(gv, ev)
         if N >= 1000:
             assert not hp.fallback_taken()
+        # one shard: both phases in one call (the bound kernel folds the extremes)
+        li, lv, la, lt = hp.local(wins, 11)
+        assert torch.equal(li, ei) and torch.equal(lv, ev)
+        assert torch.equal(la, ea) and torch.equal(lt, et)
 
 
 def test_hybrid_prune_fallback_cases(device):
-    """The gated exact path answers (same bits as the unfused path) when the
-    pruned one cannot: every item identical (all fused scores tie: the
-    survivor list overflows), an unknown ALS row (NaN scores) and a catalogue
-    with tied maxima."""
+    """The exact path (inside the survivor kernel, per user) answers with the
+    same bits as the unfused path when the pruned one cannot: every item
+    identical (all fused scores tie: the survivor list overflows), an unknown
+    ALS row (NaN scores) and a catalogue with tied maxima — through both the
+    two-phase calls and the one-shard call."""
     h = _h()
     rng = np.random.default_rng(12)
     B, N, dk = 40, 30_000, 128
@@ -443,6 +448,10 @@ def test_hybrid_prune_fallback_cases(device):
         assert hp.fallback_taken()
         assert torch.equal(gi, ei)
         np.testing.assert_array_equal(gv.cpu().numpy(), ev.cpu().numpy())  # NaN == NaN position-wise
+        li, lv, _, _ = hp.local(wins)
+        assert hp.fallback_taken()
+        assert torch.equal(li, ei)
+        np.testing.assert_array_equal(lv.cpu().numpy(), ev.cpu().numpy())
 
 
 def test_recommender_bf16_paths_agree(device):
