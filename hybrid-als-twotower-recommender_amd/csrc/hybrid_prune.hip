@@ -188,6 +188,29 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   if (b == 0 && tid == 0) *flag = 0;
   if (tid == 0) cn[b] = 0;
   float* th_row = theta + (int64_t)b * G;
+  // every load the bound needs besides the seeds' rows, issued before the
+  // extremes are known (one round trip): the user's bf16 rows (B operands of
+  // the seed MFMAs), the heavy group maxima (+ their slices), the light ones
+  const char* uh = reinterpret_cast<const char*>(uop + ((int64_t)hm * B + b) * DK);
+  const char* ul = reinterpret_cast<const char*>(uop + ((int64_t)(1 - hm) * B + b) * DK);
+  HpFrag fh[KS], fl[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    fh[ks].i = *reinterpret_cast<const int4*>(uh + 16 * g + 64 * ks);
+    fl[ks].i = *reinterpret_cast<const int4*>(ul + 16 * g + 64 * ks);
+  }
+  const int lm = 1 - hm;
+  float lmx = -INFINITY;
+  if (tid < 128) {
+    float v = -INFINITY;
+    if (tid < G) {
+      const int ap = argpos[((int64_t)hm * G + tid) * B + b];
+      const float pv = part[(((int64_t)hm * G + tid) * 2 + 1) * B + b];
+      lmx = part[(((int64_t)lm * G + tid) * 2 + 1) * B + b];
+      v = ap >= 0 ? pv : -INFINITY;
+    }
+    smax[tid] = v;
+  }
   float amin, amax, tmin, tmax;
   if constexpr (LOCAL) {
     // thread t: model t >> 7, group t & 127 (G <= 128); fminf / fmaxf as
@@ -231,29 +254,6 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   }
   const HpScale sc = hp_scale(amin, amax, tmin, tmax);
   const int64_t per = ((N + G - 1) / G + 15) / 16 * 16;  // hyb_scores_kernel's group range
-  // the user's bf16 rows (B operands of the seed MFMAs)
-  const char* uh = reinterpret_cast<const char*>(uop + ((int64_t)hm * B + b) * DK);
-  const char* ul = reinterpret_cast<const char*>(uop + ((int64_t)(1 - hm) * B + b) * DK);
-  HpFrag fh[KS], fl[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    fh[ks].i = *reinterpret_cast<const int4*>(uh + 16 * g + 64 * ks);
-    fl[ks].i = *reinterpret_cast<const int4*>(ul + 16 * g + 64 * ks);
-  }
-  // every load the bound needs besides the seeds' rows, issued together: the
-  // heavy group maxima (+ their slices) and the light ones (for theta)
-  const int lm = 1 - hm;
-  float lmx = -INFINITY;
-  if (tid < 128) {
-    float v = -INFINITY;
-    if (tid < G) {
-      const int ap = argpos[((int64_t)hm * G + tid) * B + b];
-      const float pv = part[(((int64_t)hm * G + tid) * 2 + 1) * B + b];
-      lmx = part[(((int64_t)lm * G + tid) * 2 + 1) * B + b];
-      v = ap >= 0 ? pv : -INFINITY;
-    }
-    smax[tid] = v;
-  }
   for (int q = tid; q < kSlots; q += 256) sitem[q] = -1;
   if (tid == 0) s_tau = -INFINITY;
   __syncthreads();
