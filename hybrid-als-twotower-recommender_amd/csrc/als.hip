@@ -26,7 +26,7 @@
 #define HREC_ALS_CH0 8
 #endif
 #ifndef HREC_ALS_ABLATE
-#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip factor+solve, 3 = skip the substitutions, 4 = skip the Gramian
+#define HREC_ALS_ABLATE 0  // timing-only builds: 1 = skip factor+solve, 3 = skip the back substitution, 4 = skip the Gramian
 #endif
 #ifndef HREC_ALS_SOLVE_UNROLL
 #define HREC_ALS_SOLVE_UNROLL 8  // unroll of the two 64-step triangular-solve loops
@@ -723,6 +723,12 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
   // and each of the 2 x KP substitution steps is one broadcast + one masked fma.
   // (Spark's dppsv factors A = U^T U with U = D^1/2 Ut: the same solution.)
   auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
+  // The forward substitution Ut^T w = b rides along the panels: at pivot pv
+  // lane c > pv holds Ut[pv][c] (= ut) and w_pv is lane pv's b, final since
+  // pivot pv - 1, so b_c -= Ut[pv][c] w_pv is one broadcast + one fma off the
+  // panel's critical chain — the same operands in the same (pv ascending)
+  // order as a separate substitution loop, so the same bits.
+  double bs = 0.0;
 #pragma unroll
   for (int J = 0; J < NT; ++J) {
     // (a) block row J -> LDS (only q <= c: the upper triangle)
@@ -735,6 +741,7 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
       }
     }
     wave_lds_sync();
+    if (J == 0) bs = lane < KP ? bsh[lane] : 0.0;
     // (b) lane c >= 16J owns column c of block row J
     const int c = lane;
     const bool own = c >= 16 * J && c < KP;
@@ -777,6 +784,8 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
           dsh[pv] = piv;
           rdsh[pv] = r;
         }
+        const double wq = bcast(bs, pv);
+        if (own && c > pv) bs = fma(-ut, wq, bs);
         if (i < 15) {
 #pragma unroll
           for (int m0 = i + 1; m0 < 16; ++m0) a[m0] = fma(-u[m0], ut, a[m0]);
@@ -802,6 +811,10 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
       if (c == pv) {
         dsh[pv] = piv;
         rdsh[pv] = r;
+      }
+      {
+        const double wq = bcast(bs, pv);
+        if (own && c > pv) bs = fma(-ut, wq, bs);
       }
       if (i < 15) {
         if constexpr (kRl2) {  // bit-identical: u1 is the value lane pv + 1 stored to cb
@@ -855,15 +868,7 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
     if (lane < KP) out[lane] = (float)(myrd + Up[tri(lane)]);
     return;
   }
-  // forward  Ut^T w = b   (step q: lanes c > q subtract Ut[q][c] * w_q)
-  double bi = lane < KP ? bsh[lane] : 0.0;
-#pragma unroll HREC_ALS_SOLVE_UNROLL
-  for (int q = 0; q < KP; ++q) {
-    const double u = Up[tri(lc) + q];  // in bounds; used by lanes > q only
-    const double wq = bcast(bi, q);
-    if (lane > q) bi = fma(-u, wq, bi);
-  }
-  bi *= myrd;  // v = D^-1 w
+  double bi = bs * myrd;  // v = D^-1 w (w from the panels)
   // back     Ut x = v     (step q: lanes c < q subtract Ut[c][q] * x_q)
 #pragma unroll HREC_ALS_SOLVE_UNROLL
   for (int q = KP - 1; q >= 0; --q) {
