@@ -41,6 +41,9 @@
 #ifndef HREC_WIDE_WAVES
 #define HREC_WIDE_WAVES(NT) 8
 #endif
+#ifndef HREC_WIDE_G
+#define HREC_WIDE_G 4  // Gramian tile slots per operand-read group (reads of group g + 1 overlap group g's MFMAs)
+#endif
 #ifndef HREC_WIDE_CUT
 #define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
 #endif
@@ -69,6 +72,9 @@ __device__ unsigned long long g_wide_stamps[8];
 #endif
 
 typedef double wd4 __attribute__((ext_vector_type(4)));
+
+__device__ float wide_sbuf_load_f1(hrec_rsrc_t rsrc, int vindex, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.struct.buffer.load.f32");
 
 // Waves per row: 8 for kp <= 128; 16 for kp >= 192, so that each wave's
 // share of the register-resident Gramian tiles (<= 9 x 8 VGPRs) fits the
@@ -160,25 +166,75 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   double bacc = 0.0;  // b[tid] for tid < KP
   float4 ld[S::F4_PER_T];
   float lr = 0.f;     // this thread's rating slot (tid < WR)
-  const int64_t nwin = (n + WR - 1) / WR;
-  auto load_window = [&](int64_t win) {
+  const int nwin = (int)((n + WR - 1) / WR);
+  // Two-stage window prefetch: the source-row indices of window w + 2 are
+  // loaded while window w computes, the rows (and ratings) of window w + 1
+  // from indices already in registers — so no window start waits on a
+  // dependent index -> row round trip. Loads are unconditional (clamped
+  // addresses, results selected), so no branch splits the issue.
+  // Every validity test is applied where the loaded value is consumed (the
+  // rows at the conversion, the indices when the rows are issued), so no
+  // wait follows a load.
+  int ixn[S::F4_PER_T];  // raw source rows of the next window's float4 slots (kUniRow: slot lane & 1)
+  bool okq[S::F4_PER_T];  // slot q of the window in `ld` holds a real row
+  bool okr = false;       // the rating in `lr` is real
+  // indices / ratings of this row through buffer resources based at the
+  // row's first entry (32-bit element offsets in VGPRs, the 64-bit bases in
+  // SGPRs: no per-lane 64-bit address pairs)
+  const hrec_rsrc_t irs = rows_rsrc(indices, beg, 4, end);
+  const hrec_rsrc_t vrs = rows_rsrc(values, beg, 4, end);
+  const int n32 = (int)n;  // ratings of this row (< 2^31)
+  // kp 256 at 8 waves: a float4 slot's window row is wave-uniform (64 float4
+  // per row), so the index loads need no per-thread row arithmetic
+  constexpr bool kUniRow = KP / 4 == 64 && S::F4 % kWideThreads == 0;
+  auto load_idx = [&](int win, int (&ix)[S::F4_PER_T]) {
 #pragma unroll
     for (int q = 0; q < S::F4_PER_T; ++q) {
-      const int e = tid + q * kWideThreads;
-      ld[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < S::F4) {
-        const int r = e / (KP / 4), c4 = e % (KP / 4);
-        const int64_t p = beg + win * WR + r;
-        if (p < end) {
-          const int64_t sr = indices[p];
-          if (sr >= 0 && sr < n_src) ld[q] = *reinterpret_cast<const float4*>(src + sr * KP + 4 * c4);
-        }
+      int p;
+      if constexpr (kUniRow) {
+        // one source row per wave and slot (row w + 8 q of the window): lane
+        // l loads slot l & 1's index, read back by v_readlane when the rows
+        // are issued (a per-lane address keeps the value in a VGPR, so
+        // nothing waits for it here)
+        static_assert(S::F4_PER_T == 2, "two slots per thread");
+        if (q > 0) break;
+        p = win * WR + w + (kWideThreads / 64) * (__lane_id() & 1);
+      } else {
+        const int e = tid + q * kWideThreads;
+        p = win * WR + (e < S::F4 ? e / (KP / 4) : 0);
       }
+      ix[q] = __float_as_int(wide_sbuf_load_f1(irs, p < n32 ? p : n32 - 1, 0, 0, 0));
     }
-    if (tid < WR) {
-      const int64_t p = beg + win * WR + tid;
-      lr = p < end ? values[p] : 0.f;
+  };
+  auto load_rows = [&](int win, const int (&ix)[S::F4_PER_T]) {
+#pragma unroll
+    for (int q = 0; q < S::F4_PER_T; ++q) {
+      int c4, p, iq = ix[q];
+      bool inw;
+      if constexpr (kUniRow) {
+        c4 = __lane_id();
+        p = win * WR + w + (kWideThreads / 64) * q;
+        iq = __builtin_amdgcn_readlane(ix[0], q);
+        inw = true;
+      } else {
+        const int e = tid + q * kWideThreads;
+        c4 = e % (KP / 4);
+        p = win * WR + (e < S::F4 ? e / (KP / 4) : 0);
+        inw = e < S::F4;
+      }
+      okq[q] = inw && p < n32 && iq >= 0 && iq < n_src;
+      ld[q] = *reinterpret_cast<const float4*>(src + (int64_t)(okq[q] ? iq : 0) * KP + 4 * c4);
     }
+    // the ratings: consumed at the window's conversion, so one window ahead
+    const int l = kUniRow ? __lane_id() : tid;  // the rating slots are lanes 0..WR-1 of wave 0
+    const int pr = win * WR + (l < WR ? l : 0);
+    lr = wide_sbuf_load_f1(vrs, pr < n32 ? pr : n32 - 1, 0, 0, 0);
+    okr = tid < WR && win * WR + l < n32;
+  };
+  auto load_window = [&](int win) {  // window `win` now (prologue)
+    int ix[S::F4_PER_T];
+    load_idx(win, ix);
+    load_rows(win, ix);
   };
   auto store_window = [&](int b) {
 #pragma unroll
@@ -187,18 +243,23 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       if (e < S::F4) {
         const int r = e / (KP / 4), c4 = e % (KP / 4);
         double* d = &buf[b][r * LD + 4 * c4];
-        *reinterpret_cast<double2*>(d) = make_double2((double)ld[q].x, (double)ld[q].y);
-        *reinterpret_cast<double2*>(d + 2) = make_double2((double)ld[q].z, (double)ld[q].w);
+        const float4 t = okq[q] ? ld[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<double2*>(d) = make_double2((double)t.x, (double)t.y);
+        *reinterpret_cast<double2*>(d + 2) = make_double2((double)t.z, (double)t.w);
       }
     }
-    if (tid < WR) rsh[b][tid] = lr;
+    if (tid < WR) rsh[b][tid] = okr ? lr : 0.f;
   };
   load_window(0);
+  if (nwin > 1) load_idx(1, ixn);
   store_window(0);
   __syncthreads();
-  for (int64_t win = 0; win < nwin; ++win) {
+  for (int win = 0; win < nwin; ++win) {
     const int cb = (int)(win & 1);
-    if (win + 1 < nwin) load_window(win + 1);
+    if (win + 1 < nwin) {  // wave-uniform
+      load_rows(win + 1, ixn);
+      if (win + 2 < nwin) load_idx(win + 2, ixn);
+    }
     const double* wb = buf[cb];
 #pragma unroll 1
     for (int st = 0; st < WR / 4; ++st) {
@@ -207,7 +268,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       // into a register nobody reads). Slots go in groups of G: the operand
       // reads of group g + 1 are issued before the MFMAs of group g, so the
       // LDS latency hides behind G MFMAs (64 cycles each).
-      constexpr int G = 6, NG = (S::SLOTS + G - 1) / G;
+      constexpr int G = HREC_WIDE_G, NG = (S::SLOTS + G - 1) / G;
       double ra[2][G], rb[2][G];
       auto rd = [&](int g, int bsel) {
 #pragma unroll
@@ -419,54 +480,70 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 #endif
   WSTAMP(3);
   // ---------------------------------------------------------------- phase 3
-  // The owner of diagonal tile (J, J) stages it in its scratch: T[q][c].
-  auto stage_diag = [&](int s) {
-    double* T = tri[w];
+  // Backward substitution U x = v (v in bsh; the forward one ran inside the
+  // factorisation), one barrier per block: wave 0 runs the dependent chain
+  // x_M = U_MM^-1 (v_M - U_M,M+1 x_M+1) from the diagonal and
+  // super-diagonal tiles staged in the (now free) window buffers, while the
+  // owners of the other tiles of column M + 1 apply U_I,M+1 x_M+1 to the
+  // rows I < M. Each row still receives its column contributions in
+  // descending column order and every partial sum keeps its 16-lane
+  // butterfly order, so x is bit-identical to the two-barrier form.
+  double* const Dg = &buf[0][0];     // tile (M, M) at Dg + 272 M, row-major 16 x 17
+  double* const Sd = Dg + 272 * NT;  // tile (M - 1, M) at Sd + 272 M
+  static_assert(2 * 272 * NT <= 2 * S::BUF, "diagonal + super-diagonal tiles fit the window buffers");
 #pragma unroll
-    for (int r = 0; r < 4; ++r) T[(sub + 4 * r) * 17 + col] = acc[s][r];
-    wave_sync_lds();
-  };
-  // (the forward substitution ran inside the factorisation: bsh holds v)
-  // backward: U x = v (v in bsh, x -> xsh)
-#pragma unroll 1
-  for (int M = NT - 1; M >= 0; --M) {
+  for (int s = 0; s < S::SLOTS; ++s) {
+    if (pij[s] >= 0) {
+      const int I = pij[s] & 255, K = pij[s] >> 8;
+      if (K == I || K == I + 1) {
+        double* T = (K == I ? Dg : Sd) + 272 * K;
 #pragma unroll
-    for (int s = 0; s < S::SLOTS; ++s) {
-      if (pij[s] >= 0) {
-        const int I = pij[s] & 255, K = pij[s] >> 8;
-        if (I == M && K == M) {
-          stage_diag(s);
-          const double* T = tri[w];
-          double tr[16];  // row `lane` of U_MM
-#pragma unroll
-          for (int q = 0; q < 16; ++q) tr[q] = T[col * 17 + q];
-          double bi = lane < 16 ? bsh[16 * M + lane] : 0.0;
-#pragma unroll
-          for (int q = 15; q >= 0; --q) {
-            const double xq = wbcast(bi, q);
-            if (lane < q) bi = fma(-tr[q], xq, bi);
-          }
-          if (lane < 16) xsh[16 * M + lane] = bi;
-        }
+        for (int r = 0; r < 4; ++r) T[(sub + 4 * r) * 17 + col] = acc[s][r];
       }
     }
-    __syncthreads();
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int M = NT - 1; M >= 0; --M) {
+    if (w == 0) {
+      double bi = lane < 16 ? bsh[16 * M + lane] : 0.0;
+      if (M + 1 < NT) {  // v_M -= U_M,M+1 x_M+1 (lane i < 16: row i; butterfly order)
+        const double* T = Sd + 272 * (M + 1) + col * 17;
+        const double* xm = xsh + 16 * (M + 1);
+        // products rounded on their own (no contraction into the adds), the
+        // pairwise tree built as the products arrive (few live registers)
+        auto pr = [&](int q) { return __dmul_rn(T[q], xm[q]); };
+        auto quad = [&](int q) { return __dadd_rn(__dadd_rn(pr(q), pr(q + 1)), __dadd_rn(pr(q + 2), pr(q + 3))); };
+        const double lo = __dadd_rn(quad(0), quad(4));
+        const double hi = __dadd_rn(quad(8), quad(12));
+        bi = __dsub_rn(bi, __dadd_rn(lo, hi));
+      }
+      const double* T = Dg + 272 * M + col * 17;  // row `lane` of U_MM
+#pragma unroll 4
+      for (int q = 15; q >= 0; --q) {
+        const double xq = wbcast(bi, q);
+        if (lane < q) bi = fma(-T[q], xq, bi);
+      }
+      if (lane < 16) xsh[16 * M + lane] = bi;
+    }
+    if (M + 1 < NT) {
 #pragma unroll
-    for (int s = 0; s < S::SLOTS; ++s) {
-      if (pij[s] >= 0) {
-        const int I = pij[s] & 255, K = pij[s] >> 8;
-        if (K == M && I < M) {  // v_I -= U_IM x_M
-          const double xm = xsh[16 * M + col];
-          double part[4];
+      for (int s = 0; s < S::SLOTS; ++s) {
+        if (pij[s] >= 0) {
+          const int I = pij[s] & 255, K = pij[s] >> 8;
+          if (K == M + 1 && I < M) {  // v_I -= U_I,M+1 x_M+1
+            const double xm = xsh[16 * K + col];
+            double part[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            part[r] = acc[s][r] * xm;
+            for (int r = 0; r < 4; ++r) {
+              part[r] = acc[s][r] * xm;
 #pragma unroll
-            for (int off = 1; off < 16; off <<= 1) part[r] += __shfl_xor(part[r], off, kWave);
-          }
-          if (col == 0) {
+              for (int off = 1; off < 16; off <<= 1) part[r] += __shfl_xor(part[r], off, kWave);
+            }
+            if (col == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) bsh[16 * I + sub + 4 * r] -= part[r];
+              for (int r = 0; r < 4; ++r) bsh[16 * I + sub + 4 * r] -= part[r];
+            }
           }
         }
       }

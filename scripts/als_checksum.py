@@ -11,12 +11,13 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from src import synthetic  # noqa: E402
 from src.als_engine import DeviceALS  # noqa: E402
 
-n_users, n_items = 200_000, 20_000
+rank = int(sys.argv[1]) if len(sys.argv) > 1 else 64  # > 64: the wide kernel (csrc/als_wide.hip)
+n_users, n_items = (200_000, 20_000) if rank <= 64 else (40_000, 8_000)
 csr = synthetic.generate(n_users, n_items, 0.005, False)
 csc = synthetic.generate(n_users, n_items, 0.005, True)
-eng = DeviceALS(n_users, n_items, 64, 0.1, csr, csc)
+eng = DeviceALS(n_users, n_items, rank, 0.1, csr, csc)
 eng.init_user_factors(7)
 eng.fit(2)
 torch.cuda.synchronize()
 h = hashlib.sha256(eng.U.cpu().numpy().tobytes() + eng.V.cpu().numpy().tobytes()).hexdigest()
-print(os.path.basename(os.environ.get("HREC_LIB", "default")), h[:16])
+print(os.path.basename(os.environ.get("HREC_LIB", "default")), "rank", rank, h[:16])
