@@ -44,6 +44,9 @@
 #ifndef HREC_WIDE_G
 #define HREC_WIDE_G 4  // Gramian tile slots per operand-read group (reads of group g + 1 overlap group g's MFMAs)
 #endif
+#ifndef HREC_WIDE_BDEFER
+#define HREC_WIDE_BDEFER 0  // 1 = a window's rhs accumulation runs during the next window's MFMAs (3 window buffers; measured 640 -> 645 ms per rank-256 epoch, off)
+#endif
 #ifndef HREC_WIDE_CUT
 #define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
 #endif
@@ -52,8 +55,9 @@ namespace hrec {
 
 #ifdef HREC_WIDE_STAMPS
 // Diagnostic build only: per-phase cycle sums (s_memtime) of wave 0 of every
-// block: [0] Gramian, [1] panel write + barrier, [2] panels, [3] trailing
-// updates (+ barrier), [4] substitutions.
+// block: [0] Gramian, [1] trailing updates + panel write + barrier, [2]
+// panels, [3] tile staging, [4] x store; backward substitution per block:
+// [5] wave 0's chain, [6] its column updates, [7] barrier.
 __device__ unsigned long long g_wide_stamps[8];
 #define WSTAMP_DECL unsigned long long _ws_prev = 0
 #define WSTAMP(i)                                                                              \
@@ -118,6 +122,15 @@ __device__ __forceinline__ double wbcast(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+// A double moved across lanes by one DPP pattern (two 32-bit v_mov_dpp).
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -130,12 +143,16 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     int64_t n_rows, const float* __restrict__ src, int64_t n_src, int k, double reg, float* __restrict__ dst) {
   using S = WideShape<NT>;
   constexpr int KP = S::KP, LD = S::LD, WR = S::WR, kWideWaves = S::WAVES, kWideThreads = S::THREADS;
-  __shared__ __attribute__((aligned(16))) double buf[2][S::BUF];
+  // window buffers: NB = 3 rotates current / next / previous window (the
+  // previous one's rhs accumulation overlaps the current one's MFMAs);
+  // phase 2 uses buffers 0, 1 as its double-buffered panel
+  constexpr int NB = HREC_WIDE_BDEFER ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) double buf[NB][S::BUF];
   __shared__ double bsh[KP];      // b, then w (forward), then v / x
   __shared__ double dsh[KP];      // pivots D
   __shared__ double rdsh[KP];     // 1 / D
   __shared__ double xsh[KP];      // x blocks (backward)
-  __shared__ float rsh[2][WR];    // ratings of the two windows
+  __shared__ float rsh[NB][WR];   // ratings of the windows in buf
   __shared__ __attribute__((aligned(16))) double tri[kWideWaves][16 * 17];  // per-wave scratch: pivot rows / diagonal tile
   __shared__ double udg[16 * 17];              // U_JJ of the current block row
   const int tid = threadIdx.x, lane = tid & 63;
@@ -254,12 +271,25 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   if (nwin > 1) load_idx(1, ixn);
   store_window(0);
   __syncthreads();
+  // b over one window's ratings (threads t < kp, ratings in order)
+  auto rhs_window = [&](int b) {
+    if (tid < KP) {
+#pragma unroll 4
+      for (int r = 0; r < WR; ++r) bacc = fma((double)rsh[b][r], buf[b][r * LD + tid], bacc);
+    }
+  };
+  int cb = 0;  // buffer of window `win`
   for (int win = 0; win < nwin; ++win) {
-    const int cb = (int)(win & 1);
+    const int nb = cb + 1 == NB ? 0 : cb + 1;  // next window's buffer
     if (win + 1 < nwin) {  // wave-uniform
       load_rows(win + 1, ixn);
       if (win + 2 < nwin) load_idx(win + 2, ixn);
     }
+    // HREC_WIDE_BDEFER: the previous window's b (buffer nb + 1 mod 3) before
+    // this window's MFMAs — on waves 0..3, whose SIMD partners (waves 4..7)
+    // keep the matrix pipe busy meanwhile — instead of after them on the
+    // path to the barrier
+    if (HREC_WIDE_BDEFER && win > 0) rhs_window(nb + 1 == NB ? 0 : nb + 1);
     const double* wb = buf[cb];
 #pragma unroll 1
     for (int st = 0; st < WR / 4; ++st) {
@@ -293,12 +323,11 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (tid < KP) {
-#pragma unroll 4
-      for (int r = 0; r < WR; ++r) bacc = fma((double)rsh[cb][r], wb[r * LD + tid], bacc);
-    }
-    if (win + 1 < nwin) store_window(cb ^ 1);
+    // (the last window's b before the barrier: phase 2 reuses buffers 0, 1)
+    if (!HREC_WIDE_BDEFER || win + 1 == nwin) rhs_window(cb);
+    if (win + 1 < nwin) store_window(nb);
     __syncthreads();
+    cb = nb;
   }
   // lambda = numExplicits * regParam on the diagonal (1.0 on padding columns)
   const double lambda = (double)n * reg;
@@ -506,6 +535,10 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 #pragma unroll 1
   for (int M = NT - 1; M >= 0; --M) {
     if (w == 0) {
+      const double* Td = Dg + 272 * M + col * 17;  // row `lane` of U_MM
+      double tr[16];  // loaded first: their LDS latency hides behind the GEMV below
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tr[q] = Td[q];
       double bi = lane < 16 ? bsh[16 * M + lane] : 0.0;
       if (M + 1 < NT) {  // v_M -= U_M,M+1 x_M+1 (lane i < 16: row i; butterfly order)
         const double* T = Sd + 272 * (M + 1) + col * 17;
@@ -518,14 +551,14 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         const double hi = __dadd_rn(quad(8), quad(12));
         bi = __dsub_rn(bi, __dadd_rn(lo, hi));
       }
-      const double* T = Dg + 272 * M + col * 17;  // row `lane` of U_MM
-#pragma unroll 4
+#pragma unroll
       for (int q = 15; q >= 0; --q) {
         const double xq = wbcast(bi, q);
-        if (lane < q) bi = fma(-T[q], xq, bi);
+        if (lane < q) bi = fma(-tr[q], xq, bi);
       }
       if (lane < 16) xsh[16 * M + lane] = bi;
     }
+    WSTAMP(5);
     if (M + 1 < NT) {
 #pragma unroll
       for (int s = 0; s < S::SLOTS; ++s) {
@@ -537,8 +570,14 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               part[r] = acc[s][r] * xm;
-#pragma unroll
-              for (int off = 1; off < 16; off <<= 1) part[r] += __shfl_xor(part[r], off, kWave);
+              // 16-lane butterfly by DPP moves (no LDS round trips): swaps
+              // inside quads, then the half-row and row mirrors — lane 0
+              // (the only reader) adds exactly the partial sums the xor
+              // butterfly would (the mirrored lanes hold the same bits)
+              part[r] += dpp64<0xB1>(part[r]);   // quad_perm [1,0,3,2]
+              part[r] += dpp64<0x4E>(part[r]);   // quad_perm [2,3,0,1]
+              part[r] += dpp64<0x141>(part[r]);  // row_half_mirror
+              part[r] += dpp64<0x140>(part[r]);  // row_mirror
             }
             if (col == 0) {
 #pragma unroll
@@ -548,7 +587,9 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         }
       }
     }
+    WSTAMP(6);
     __syncthreads();
+    WSTAMP(7);
   }
   if (tid < KP) out[tid] = (float)xsh[tid];
   WSTAMP(4);

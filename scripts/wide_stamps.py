@@ -31,10 +31,10 @@ def main():
         sweep()
         torch.cuda.synchronize()
         fn(buf, 1)
-        v = [buf[i] / n for i in range(5)]
+        v = [buf[i] / n for i in range(8)]
         tot = sum(v)
         print(f"rank {k} {name}: cycles/row (s_memtime ticks) " +
-              " ".join(f"{lbl}={x:.0f}" for lbl, x in zip(["gram", "trail+write", "panel", "last", "subst"], v)) +
+              " ".join(f"{lbl}={x:.0f}" for lbl, x in zip(["gram", "trail+write", "panel", "p2tail", "xstore", "bs_chain", "bs_update", "bs_barrier"], v)) +
               f" total={tot:.0f}", flush=True)
 
 
