@@ -64,6 +64,9 @@
 #ifndef HREC_ALS_ROT1DPP
 #define HREC_ALS_ROT1DPP 1  // f32 sources: rotation by 4 by DPP moves of the converted operands (0: rotated load + conversion)
 #endif
+#ifndef HREC_ALS_ROT1DPP64
+#define HREC_ALS_ROT1DPP64 0  // f64 sources: rotation by 4 by DPP moves of the gathered operands (0: rotated loads; 1 measured 41.6 -> 41.9 ms user side, bit-identical)
+#endif
 #ifndef HREC_ALS_PR
 #define HREC_ALS_PR 2  // DIAG4 = 3: prefetch distance of the rotated loads (steps)
 #endif
@@ -365,7 +368,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
   constexpr bool kAhead = HREC_ALS_DIAG4 == 2 && MODE == 0;
   constexpr bool kMemRot = HREC_ALS_DIAG4 == 3 && MODE == 0;
   constexpr int PR = kMemRot ? HREC_ALS_PR : 1;  // rotated-load prefetch distance (steps)
-  constexpr bool kRot1Dpp = kMemRot && !S64 && HREC_ALS_ROT1DPP;
+  constexpr bool kRot1Dpp = kMemRot && (S64 ? HREC_ALS_ROT1DPP64 : HREC_ALS_ROT1DPP);
   static_assert(PR < PF, "rotated loads are issued from the current windows");
   const int voff1 = (S64 ? 8 : 4) * NT * ((col + 4) & 15), voff2 = (S64 ? 8 : 4) * NT * ((col + 8) & 15);
   auto rot_load = [&](int vi, int vo) -> RingT {
@@ -460,7 +463,7 @@ __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, con
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           if constexpr (S64) {
-            ar1[t] = rot1[s % PR].x[t];
+            ar1[t] = kRot1Dpp ? row_ror<12>(a[t]) : rot1[s % PR].x[t];
             if constexpr (!kPair8) ar2[t] = rot2[s % PR].x[t];
           } else {
             // ROT1DPP: the rotation by 4 lanes of the converted operand (two
