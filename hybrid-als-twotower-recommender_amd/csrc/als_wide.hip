@@ -140,6 +140,31 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Backward substitution: the wave that runs block M's chain also applies its
+// own tiles of column M + 1 right after it (on the critical path), so pick,
+// per block, the wave owning the fewest such tiles (I, M + 1), I < M
+// (pair p -> wave p % WAVES). Packed 3 bits per block at compile time.
+template <int NT, int WAVES>
+constexpr unsigned long long chain_waves_packed() {
+  unsigned long long packed = 0;
+  for (int M = 0; M < NT; ++M) {
+    int best = 0, bestc = 1 << 30;
+    for (int w = 0; w < WAVES; ++w) {
+      int c = 0;
+      for (int I = 0; M + 1 < NT && I < M; ++I) {
+        const int p = I * NT - I * (I - 1) / 2 + (M + 1 - I);
+        if (p % WAVES == w) ++c;
+      }
+      if (c < bestc) {
+        bestc = c;
+        best = w;
+      }
+    }
+    packed |= (unsigned long long)best << (3 * M);
+  }
+  return packed;
+}
+
 template <int NT>
 __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, const float* __restrict__ values,
@@ -554,7 +579,8 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   WSTAMP(3);
   // ---------------------------------------------------------------- phase 3
   // Backward substitution U x = v (v in bsh; the forward one ran inside the
-  // factorisation), one barrier per block: wave 0 runs the dependent chain
+  // factorisation), one barrier per block: one wave (per block the one with
+  // the fewest own column updates) runs the dependent chain
   // x_M = U_MM^-1 (v_M - U_M,M+1 x_M+1) from the diagonal and
   // super-diagonal tiles staged in the (now free) window buffers, while the
   // owners of the other tiles of column M + 1 apply U_I,M+1 x_M+1 to the
@@ -576,9 +602,11 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     }
   }
   __syncthreads();
+  static_assert(kWideWaves <= 8 && 3 * NT <= 64, "chain-wave table: 3 bits per block");
+  constexpr unsigned long long kChain = chain_waves_packed<NT, kWideWaves>();
 #pragma unroll 1
   for (int M = NT - 1; M >= 0; --M) {
-    if (w == 0) {
+    if (w == (int)((kChain >> (3 * M)) & 7)) {
       const double* Td = Dg + 272 * M + col * 17;  // row `lane` of U_MM
       double tr[16];  // loaded first: their LDS latency hides behind the GEMV below
 #pragma unroll
