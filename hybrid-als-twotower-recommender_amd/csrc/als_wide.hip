@@ -50,6 +50,9 @@
 #ifndef HREC_WIDE_PANEL_UNROLL
 #define HREC_WIDE_PANEL_UNROLL 0  // 1 = panel pivot loop unrolled (in-place column, b128 pivot-row reads: 147 spilled VGPRs, rank-256 epoch 644 -> 808 ms); 0 = rolled, shifted
 #endif
+#ifndef HREC_WIDE_WR_WIDE
+#define HREC_WIDE_WR_WIDE 16  // ratings per window at kp >= 192 (multiple of 4; LDS: two windows of WR x (kp + 16) doubles)
+#endif
 #ifndef HREC_WIDE_CUT
 #define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
 #endif
@@ -94,7 +97,7 @@ struct WideShape {
   static constexpr int NPAIR = NT * (NT + 1) / 2;
   static constexpr int SLOTS = (NPAIR + WAVES - 1) / WAVES;
   static constexpr int LD = KP + 16;                     // f64 row stride of windows and panels
-  static constexpr int WR = KP >= 192 ? 16 : 32;         // ratings per window
+  static constexpr int WR = KP >= 192 ? HREC_WIDE_WR_WIDE : 32;  // ratings per window
   static constexpr int WIN = WR * LD;                    // doubles per window buffer
   static constexpr int PANEL = 16 * LD;                  // doubles per panel buffer
   static constexpr int BUF = WIN > PANEL ? WIN : PANEL;  // windows and panels share two buffers
@@ -238,12 +241,11 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       int p;
       if constexpr (kUniRow) {
         // one source row per wave and slot (row w + 8 q of the window): lane
-        // l loads slot l & 1's index, read back by v_readlane when the rows
+        // l loads slot l % F4_PER_T's index, read back by v_readlane when the rows
         // are issued (a per-lane address keeps the value in a VGPR, so
         // nothing waits for it here)
-        static_assert(S::F4_PER_T == 2, "two slots per thread");
         if (q > 0) break;
-        p = win * WR + w + (kWideThreads / 64) * (__lane_id() & 1);
+        p = win * WR + w + (kWideThreads / 64) * (__lane_id() % S::F4_PER_T);
       } else {
         const int e = tid + q * kWideThreads;
         p = win * WR + (e < S::F4 ? e / (KP / 4) : 0);
