@@ -47,9 +47,6 @@
 #ifndef HREC_WIDE_BDEFER
 #define HREC_WIDE_BDEFER 0  // 1 = a window's rhs accumulation runs during the next window's MFMAs (3 window buffers; measured 640 -> 645 ms per rank-256 epoch, off)
 #endif
-#ifndef HREC_WIDE_PANEL_UNROLL
-#define HREC_WIDE_PANEL_UNROLL 0  // 1 = panel pivot loop unrolled (in-place column, b128 pivot-row reads: 147 spilled VGPRs, rank-256 epoch 644 -> 808 ms); 0 = rolled, shifted
-#endif
 #ifndef HREC_WIDE_WR_WIDE
 #define HREC_WIDE_WR_WIDE 16  // ratings per window at kp >= 192 (multiple of 4; LDS: two windows of WR x (kp + 16) doubles)
 #endif
@@ -417,46 +414,6 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       double a[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) a[m] = pc[m * LD];
-#if HREC_WIDE_PANEL_UNROLL
-      // pivot loop unrolled: a[m] updated in place (compile-time indices), the
-      // pivot row read back as aligned ds_read_b128 pairs, the per-pivot
-      // stores under compile-time lane conditions — the same fma on the same
-      // operands per entry as the rolled, shifted form (bit-identical)
-      wave_sync_lds();
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const double ai = a[i];
-        const double piv = wbcast(ai, i);  // lane i: column 16 J + i, row 16 J + i
-        const double r0 = __builtin_amdgcn_rcp(piv);
-        const double rp = fma(r0, fma(-piv, r0, 1.0), r0);
-        const double ut = ai * rp;  // U[16 J + i][c]
-        if (i == 15) {
-          if (own && lane >= 16) P[i * LD + c] = ut;
-          if (w == 0 && lane < 16) udg[i * 17 + lane] = lane == i ? 1.0 : 0.0;
-          if (w == 0 && lane == i) {
-            dsh[16 * J + i] = piv;
-            rdsh[16 * J + i] = rp;
-          }
-          break;
-        }
-        double* cbw = tri[w] + 16 * (i & 1);  // the pivot row of the diagonal block
-        if (lane < 16) cbw[lane] = ai;
-        if (own && lane >= 16) P[i * LD + c] = ut;  // the panel column's row i becomes U
-        if (w == 0 && lane < 16) udg[i * 17 + lane] = lane > i ? ut : (lane == i ? 1.0 : 0.0);
-        if (w == 0 && lane == i) {
-          dsh[16 * J + i] = piv;
-          rdsh[16 * J + i] = rp;
-        }
-        wave_sync_lds();
-#pragma unroll
-        for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(cbw + m0);
-          if (m0 > i) a[m0] = fma(-u.x, ut, a[m0]);
-          a[m0 + 1] = fma(-u.y, ut, a[m0 + 1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // no hoisting across pivots (register pressure)
-      }
-#else
       if (lane < 32) tri[w][16 + lane + 16 * (lane >> 4)] = 0.0;  // entries 16..31 of both buffers
       wave_sync_lds();
 #pragma unroll 1
@@ -485,7 +442,6 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 #pragma unroll
         for (int j = 0; j < 15; ++j) a[j] = fma(-u[j], ut, a[j + 1]);
       }
-#endif
       // forward substitution of block J (U_JJ^T w_J = b_J, b_J final: every
       // earlier block already subtracted its part) by wave 0, which has just
       // written U_JJ to udg; v_J = w_J / D
