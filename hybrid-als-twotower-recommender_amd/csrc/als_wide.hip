@@ -48,7 +48,7 @@
 #define HREC_WIDE_BDEFER 0  // 1 = a window's rhs accumulation runs during the next window's MFMAs (3 window buffers; measured 640 -> 645 ms per rank-256 epoch, off)
 #endif
 #ifndef HREC_WIDE_WR_WIDE
-#define HREC_WIDE_WR_WIDE 16  // ratings per window at kp >= 192 (multiple of 4; LDS: two windows of WR x (kp + 16) doubles)
+#define HREC_WIDE_WR_WIDE 32  // ratings per window at kp >= 192 (16: 641 ms, 32: 638 ms per rank-256 epoch) (multiple of 4; LDS: two windows of WR x (kp + 16) doubles)
 #endif
 #ifndef HREC_WIDE_CUT
 #define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   __shared__ double rdsh[KP];     // 1 / D
   __shared__ double xsh[KP];      // x blocks (backward)
   __shared__ float rsh[NB][WR];   // ratings of the windows in buf
-  __shared__ __attribute__((aligned(16))) double tri[kWideWaves][16 * 17];  // per-wave scratch: pivot rows / diagonal tile
+  __shared__ __attribute__((aligned(16))) double tri[kWideWaves][64];  // per-wave scratch: the panel's two 32-entry pivot-row buffers
   __shared__ double udg[16 * 17];              // U_JJ of the current block row
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -258,8 +258,7 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       if constexpr (kUniRow) {
         c4 = __lane_id();
         p = win * WR + w + (kWideThreads / 64) * q;
-        iq = __builtin_amdgcn_readlane(ix[0], q);
-        inw = true;
+        inw = true;  // ix[q]: slot q's index, already wave-uniform
       } else {
         const int e = tid + q * kWideThreads;
         c4 = e % (KP / 4);
@@ -276,9 +275,11 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     okr = tid < WR && win * WR + l < n32;
   };
   auto load_window = [&](int win) {  // window `win` now (prologue)
-    int ix[S::F4_PER_T];
+    int ix[S::F4_PER_T], iu[S::F4_PER_T];
     load_idx(win, ix);
-    load_rows(win, ix);
+#pragma unroll
+    for (int q = 0; q < S::F4_PER_T; ++q) iu[q] = kUniRow ? __builtin_amdgcn_readlane(ix[0], q) : ix[q];
+    load_rows(win, iu);
   };
   auto store_window = [&](int b) {
 #pragma unroll
@@ -309,8 +310,16 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
   for (int win = 0; win < nwin; ++win) {
     const int nb = cb + 1 == NB ? 0 : cb + 1;  // next window's buffer
     if (win + 1 < nwin) {  // wave-uniform
-      load_rows(win + 1, ixn);
+      // the index loads first: a value reloaded from scratch on the way
+      // (vmcnt counts in issue order) then waits for them, not for the rows
+      // (kp 256: the per-slot indices leave the VGPR by v_readlane first, so
+      // the next index load reuses its register — no loop-carried copy that
+      // would wait for it)
+      int ixc[S::F4_PER_T];
+#pragma unroll
+      for (int q = 0; q < S::F4_PER_T; ++q) ixc[q] = kUniRow ? __builtin_amdgcn_readlane(ixn[0], q) : ixn[q];
       if (win + 2 < nwin) load_idx(win + 2, ixn);
+      load_rows(win + 1, ixc);
     }
     // HREC_WIDE_BDEFER: the previous window's b (buffer nb + 1 mod 3) before
     // this window's MFMAs — on waves 0..3, whose SIMD partners (waves 4..7)

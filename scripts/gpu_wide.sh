@@ -13,3 +13,5 @@ for k in 256 128; do
   for lib in hybrid-als-twotower-recommender_amd/lib/abw/*.so; do HREC_LIB=$lib timeout -k 10 120 python scripts/als_checksum.py $k; done
   timeout -k 10 120 python scripts/als_checksum.py $k
 done
+# parity of each variant library (the wide tests through HREC_LIB)
+for lib in hybrid-als-twotower-recommender_amd/lib/abw/*.so; do HREC_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_als_wide.py -q -x --timeout 240 --timeout-method thread 2>&1 | tail -1; done
