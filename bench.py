@@ -4,9 +4,13 @@ Workload (BASELINE.json configs[1], SURVEY §8d "c2"): synthetic 1,000,000 users
 x 100,000 items at 0.5 % density (nnz ~ 5.0e8, ratings 0..18), rank 64,
 reg 0.1. One step = one ALS epoch = item half-sweep + user half-sweep
 (Spark's iteration order), generated and kept on the device (inputs resident
-in HBM before the timed region). With N ranks (torchrun), users and items are
+in HBM before the timed region). With N ranks, users and items are
 row-sharded and the factors replicated by RCCL all-gathers after each
-half-sweep; the total work is fixed (scaling "strong").
+half-sweep; the total work is fixed (scaling "strong"). `--gpus N` without
+torchrun starts the N rank processes itself (torch.distributed.run, before
+any GPU call). With 8 or more ranks the line also carries `als_c3`
+(BASELINE configs[2]: 10M x 1M at 1 %, rank 64, user-sharded with chunked
+RCCL all-gathers); `--config c3` makes c3 the headline (8 ranks required).
 
 Also measured in the same run (not the headline value):
   * scoring: B users x all items, JVM-exact ALS dot + stable top-5 on the
@@ -49,7 +53,16 @@ F32_VALU_MULADD_TFLOPS = 78.6
 CONFIGS = {
     "c2": dict(users=1_000_000, items=100_000, density=0.005, rank=64),
     "c2s": dict(users=100_000, items=20_000, density=0.005, rank=64),  # quick check
+    # BASELINE configs[2]: one rank's shard (~200 GB of CSR + CSC) is sized
+    # for 8 GPUs
+    "c3": dict(users=10_000_000, items=1_000_000, density=0.01, rank=64, min_world=8, layout="equal"),
 }
+# HREC_BENCH_C3_REHEARSAL="W:f": c3's flow at f x its users and items from W
+# ranks (the one-GPU gloo rehearsal of the 8-GPU sub-line; labelled in the line)
+if os.environ.get("HREC_BENCH_C3_REHEARSAL"):
+    _w, _f = os.environ["HREC_BENCH_C3_REHEARSAL"].split(":")
+    CONFIGS["c3"].update(users=int(CONFIGS["c3"]["users"] * float(_f)), items=int(CONFIGS["c3"]["items"] * float(_f)),
+                         min_world=int(_w), rehearsal=True)
 
 
 def algo_flops(nnz, n_dst, k):
@@ -454,6 +467,164 @@ def WANT_CPU(args, rank, world):
     return rank == 0 and world == 1 and not args.no_cpu_baseline
 
 
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher (WORLD_SIZE unset): start N fresh rank
+    processes through torch.distributed.run — before this process touches
+    the GPU — and return their exit status. Each rank gets its own device
+    (LOCAL_RANK) and RCCL; HREC_BENCH_BACKEND / HREC_BENCH_DEVICE pass
+    through for the one-GPU gloo rehearsal."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def max_over_ranks(x, world):
+    t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_als(cfg, world, rank, group, chunks, steps, warmup, accum_mode, stream):
+    """One configuration's ALS fit timed: this rank's CSR / CSC shard
+    generated on the device, `warmup` untimed + `steps` timed epochs (barrier
+    + synchronize on both sides, max over ranks), then one compute-only epoch
+    (the same kernels without the all-gathers) for the collective time that
+    is not hidden. Returns (engine, csr, csc, facts)."""
+    k = cfg["rank"]
+    n_users, n_items = cfg["users"], cfg["items"]
+    # ALS shards: chunk-interleaved when W > 1 so each chunk's all-gather
+    # overlaps the next chunk's half-sweep. Parts balanced on cost = nnz + a
+    # per-row solve term (RowLayout.balanced over every row's rating count)
+    # when counting is cheap (the count is a hash over every (user, item)
+    # pair: 1e11 at c2); at c3 (1e13 pairs, layout "equal") equal-count parts
+    # of the uniform hash matrix, balanced in expectation (the nnz ratio is
+    # reported)
+    if world > 1 and cfg.get("layout") != "equal":
+        u_lay = RowLayout.balanced(synthetic.row_counts(n_users, n_items, cfg["density"], False).cpu().numpy(),
+                                   world, chunks)
+        i_lay = RowLayout.balanced(synthetic.row_counts(n_users, n_items, cfg["density"], True).cpu().numpy(),
+                                   world, 1)
+        layout = "nnz-balanced contiguous parts"
+    else:
+        u_lay, i_lay = RowLayout.equal(n_users, world, chunks), RowLayout.equal(n_items, world, 1)
+        layout = "equal-count contiguous parts" if world > 1 else "one shard"
+    g0 = time.perf_counter()
+    csr = synthetic.generate_layout(n_users, n_items, cfg["density"], False, u_lay, rank)
+    csc = synthetic.generate_layout(n_users, n_items, cfg["density"], True, i_lay, rank)
+    eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group,
+                    accum_mode=accum_mode, chunks=chunks, user_layout=u_lay, item_layout=i_lay)
+    eng.init_user_factors(synthetic.SEED_INIT)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - g0
+
+    nnz_local = torch.tensor([csr.nnz, csc.nnz], dtype=torch.int64, device="cuda")
+    per_rank = torch.tensor([csr.nnz + csc.nnz], dtype=torch.int64, device="cuda")
+    per_rank_nnz = [int(per_rank.item())]
+    if world > 1:
+        dist.all_reduce(nnz_local)
+        allr = torch.zeros(world, dtype=torch.int64, device="cuda")
+        dist.all_gather_into_tensor(allr, per_rank)
+        per_rank_nnz = allr.tolist()
+    nnz_user, nnz_item = (int(x) for x in nnz_local.tolist())
+
+    for _ in range(warmup):
+        eng.epoch()
+
+    # Timed region: K epochs, barrier + synchronize on both sides.
+    ev = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        # events on the launch stream; at W = 1 they bracket exactly the two
+        # half-sweep kernels, at W > 1 also the all-gathers not hidden
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
+        eng.item_half_sweep()
+        e[1].record(stream)
+        eng.user_half_sweep()
+        e[2].record(stream)
+        ev.append(e)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    item_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+    user_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
+
+    # the same epoch's kernels without the collectives (after the timed region)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record(stream)
+    eng.compute_only_epoch()
+    c1.record(stream)
+    torch.cuda.synchronize()
+    compute_ms = max_over_ranks(c0.elapsed_time(c1), world)
+    ms_per_step = elapsed / steps * 1e3
+    facts = dict(k=k, n_users=n_users, n_items=n_items, elapsed=elapsed, ms_per_step=ms_per_step,
+                 item_ms=item_ms, user_ms=user_ms, nnz_user=nnz_user, nnz_item=nnz_item, per_rank_nnz=per_rank_nnz,
+                 layout=layout, gen_s=gen_s,
+                 u0=u_lay.part_rows(rank)[0][0], u_per=csr.n_rows,
+                 u_real=sum(c for _, c in u_lay.part_rows(rank)), i_real=sum(c for _, c in i_lay.part_rows(rank)),
+                 collectives={"world_size": world, "epoch_ms": ms_per_step,
+                              "compute_only_epoch_ms_max_over_ranks": compute_ms,
+                              "collective_ms_not_hidden_per_epoch": max(0.0, ms_per_step - compute_ms),
+                              "allgather_bytes_per_epoch_replicated": (eng.U.numel() + eng.V.numel()) * 4
+                              if world > 1 else 0,
+                              "note": ("epoch wall time (max over ranks) minus the same epoch's half-sweep "
+                                       "kernels alone (one compute-only epoch, HIP events, max over ranks)")})
+    return eng, csr, csc, facts
+
+
+def c3_line(world, rank, group, chunks, epochs, stream):
+    """The c3 sub-line: run_als on BASELINE configs[2] with `epochs` timed
+    epochs (1 warmup), or the reason it was skipped (not enough free device
+    memory on some rank for its CSR + CSC shard, decided on every rank)."""
+    cfg = CONFIGS["c3"]
+    k = cfg["rank"]
+    nnz_rank = cfg["density"] * cfg["users"] * cfg["items"] / world
+    need = 2 * nnz_rank * 8 * 1.02 + (cfg["users"] + cfg["items"]) * k * 4 * 3
+    ok = torch.tensor([1 if torch.cuda.mem_get_info()[0] >= need else 0], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if not int(ok.item()):
+        return {"skipped": True, "reason": f"a rank has less than {need / 1e9:.0f} GB of free device memory "
+                                           f"for its c3 shard (+ factors)"}
+    e3, csr3, csc3, f = run_als(cfg, world, rank, group, chunks, epochs, 1, 0, stream)
+    fl = algo_flops(csc3.nnz, f["i_real"], k) + algo_flops(csr3.nnz, f["u_real"], k)
+    by = algo_bytes(csc3.nnz, f["i_real"], k) + algo_bytes(csr3.nnz, f["u_real"], k)
+    ks = (f["item_ms"] + f["user_ms"]) / 1e3
+    tf = fl / ks / 1e12
+    tf_min = -max_over_ranks(-tf, world)  # the slowest rank's rate
+    out = {"epochs_per_s": epochs / f["elapsed"], "ms_per_epoch": f["ms_per_step"], "epochs": epochs,
+           "warmup": 1, "world_size": world, "rehearsal": bool(cfg.get("rehearsal")),
+           "config": {"users": cfg["users"], "items": cfg["items"], "density": cfg["density"], "rank": k,
+                      "nnz": f["nnz_user"], "nnz_check_csc": f["nnz_item"],
+                      "shard_nnz_max_over_min": max(f["per_rank_nnz"]) / max(1, min(f["per_rank_nnz"])),
+                      "shard_layout": f["layout"], "user_chunks_per_rank": chunks,
+                      "generate_s": f["gen_s"]},
+           "collectives": f["collectives"],
+           "roofline": roofline("mfma", fl / 2, (f["item_ms"] + f["user_ms"]) / 2, F64_MFMA_PEAK_TFLOPS, "TFLOP/s",
+                                "als_half_sweep_f64_kernel (item + user launches, rank 0's shard)",
+                                slowest_rank_TFLOPs=tf_min,
+                                kernel_ms_per_epoch={"item": f["item_ms"], "user": f["user_ms"]},
+                                gather_view={"algorithmic_GBps": by / ks / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
+                                             "frac": by / ks / 1e9 / HBM_PEAK_GBS}),
+           "north_star": {"target_epochs_per_s": 50, "note": (
+               "the exact f64-accumulated ALS flops of one c3 epoch (1.07e14 per GPU) bound 8 MI355X at "
+               "~0.73 epochs/s on the f64 matrix cores (DESIGN §5); the rate here is that bound's fraction")}}
+    del e3, csr3, csc3
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -466,15 +637,20 @@ def main():
     ap.add_argument("--c4-items", type=int, default=50_000_000,
                     help="two-tower scoring (c4): candidate items in total over all ranks (0 = skip)")
     ap.add_argument("--c4-users", type=int, default=1024)
-    ap.add_argument("--c5-users", type=int, default=256,
-                    help="users per batch of the c5 hybrid top-5 (rank 256 + d 256, bf16; 0 = skip)")
+    ap.add_argument("--c5-users", type=int, default=None,
+                    help="users per batch of the c5 hybrid top-5 (rank 256 + d 256, bf16; 0 = skip; "
+                         "default 256, 0 with --config c3)")
     ap.add_argument("--cpu-user-rows", type=int, default=600000)
     ap.add_argument("--cpu-item-rows", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-score-users", type=int, default=1024,
                     help="users of the scoring batch timed by the C JVM-exact scoring baseline")
-    ap.add_argument("--rank256-epochs", type=int, default=1,
-                    help="timed rank-256 ALS epochs on the same matrix (BASELINE c5's ALS half; 0 = skip)")
+    ap.add_argument("--rank256-epochs", type=int, default=None,
+                    help="timed rank-256 ALS epochs on the same matrix (BASELINE c5's ALS half; 0 = skip; "
+                         "default 1, 0 with --config c3)")
+    ap.add_argument("--c3-epochs", type=int, default=None,
+                    help="timed epochs of the c3 sub-line (BASELINE configs[2]: 10M x 1M, 1 %%, rank 64, "
+                         "8 GPUs), run after the c2 lines when 8 or more ranks are present; default 2")
     ap.add_argument("--api-reps", type=int, default=20,
                     help="users timed through HybridRecommendationSystem.get_hybrid_recommendations (0 = skip)")
     ap.add_argument("--chunks", type=int, default=4,
@@ -490,11 +666,26 @@ def main():
                     help="0: f64 matrix-core Gramian; 1: f32 matrix cores, f64 across 16-rating chunks")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    cfg = CONFIGS[args.config]
+    if world < cfg.get("min_world", 1):
+        raise SystemExit(f"--config {args.config} ({cfg['users']} x {cfg['items']}, density {cfg['density']}) is "
+                         f"BASELINE's {cfg['min_world']}-GPU configuration: one rank's share is sized for "
+                         f"{cfg['min_world']} ranks (one GPU each); run it with --gpus {cfg['min_world']}, "
+                         f"got {world}")
+    big = args.config == "c3"
+    if args.c5_users is None:
+        args.c5_users = 0 if big else 256
+    if args.rank256_epochs is None:
+        args.rank256_epochs = 0 if big else 1
+    if args.c3_epochs is None:
+        args.c3_epochs = 2
     # HREC_BENCH_BACKEND=gloo + HREC_BENCH_DEVICE=0: rehearsal of the W > 1
     # flow with every rank on one GPU (RCCL refuses two ranks per device);
     # the driver's multi-GPU runs use the defaults (RCCL, one GPU per rank).
@@ -509,75 +700,20 @@ def main():
             dist.init_process_group(backend)
         group = dist.group.WORLD
 
-    cfg = CONFIGS[args.config]
-    k = cfg["rank"]
-    n_users, n_items = cfg["users"], cfg["items"]
-    u0, u_per = shard_range(n_users, world, rank)
-    i0, i_per = shard_range(n_items, world, rank)
-    # ALS shards: chunk-interleaved when W > 1 so each chunk's all-gather
-    # overlaps the next chunk's half-sweep, users and items in contiguous
-    # parts balanced on cost = nnz + a per-row solve term (RowLayout.balanced
-    # over every row's rating count; src/als_engine.py)
-    chunks = args.chunks if world > 1 else 1
-    if world > 1:
-        u_lay = RowLayout.balanced(synthetic.row_counts(n_users, n_items, cfg["density"], False).cpu().numpy(),
-                                   world, chunks)
-        i_lay = RowLayout.balanced(synthetic.row_counts(n_users, n_items, cfg["density"], True).cpu().numpy(),
-                                   world, 1)
-    else:
-        u_lay, i_lay = RowLayout.equal(n_users, 1, 1), RowLayout.equal(n_items, 1, 1)
-    csr = synthetic.generate_layout(n_users, n_items, cfg["density"], False, u_lay, rank)
-    csc = synthetic.generate_layout(n_users, n_items, cfg["density"], True, i_lay, rank)
-    shard_nnz = torch.tensor([csr.nnz + csc.nnz], dtype=torch.int64, device="cuda")
-    eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc, world=world, rank=rank, group=group,
-                    accum_mode=args.accum_mode, chunks=chunks, user_layout=u_lay, item_layout=i_lay)
-    eng.init_user_factors(synthetic.SEED_INIT)
-    torch.cuda.synchronize()
-
-    nnz_local = torch.tensor([csr.nnz, csc.nnz], dtype=torch.int64, device="cuda")
-    if world > 1:
-        dist.all_reduce(nnz_local)
-    nnz_user, nnz_item = (int(x) for x in nnz_local.tolist())
-    per_rank_nnz = [int(shard_nnz.item())]
-    if world > 1:
-        allr = torch.zeros(world, dtype=torch.int64, device="cuda")
-        dist.all_gather_into_tensor(allr, shard_nnz)
-        per_rank_nnz = allr.tolist()
-
-    for _ in range(args.warmup):
-        eng.epoch()
-
-    # Timed region: K epochs, barrier + synchronize on both sides.
     stream = torch.cuda.current_stream()
-    ev = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        # events on the launch stream; at W = 1 they bracket exactly the two
-        # half-sweep kernels, at W > 1 also the all-gathers not hidden
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        e[0].record(stream)
-        eng.item_half_sweep()
-        e[1].record(stream)
-        eng.user_half_sweep()
-        e[2].record(stream)
-        ev.append(e)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
-    item_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
-    user_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
-    # per-rank algorithmic work of one epoch (both launches of the kernel)
-    flops = algo_flops(csc.nnz, i_per, k) + algo_flops(csr.nnz, u_per, k)
-    bytes_ = algo_bytes(csc.nnz, i_per, k) + algo_bytes(csr.nnz, u_per, k)
+    chunks = args.chunks if world > 1 else 1
+    eng, csr, csc, als = run_als(cfg, world, rank, group, chunks, args.steps, args.warmup, args.accum_mode, stream)
+    k, n_users, n_items = als["k"], als["n_users"], als["n_items"]
+    u0, u_per = als["u0"], als["u_per"]
+    u_real, i_real = als["u_real"], als["i_real"]
+    item_ms, user_ms, elapsed = als["item_ms"], als["user_ms"], als["elapsed"]
+    nnz_user, nnz_item, per_rank_nnz = als["nnz_user"], als["nnz_item"], als["per_rank_nnz"]
+    # per-rank algorithmic work of one epoch (both launches of the kernel; the
+    # rank's real rows, its layout padding excluded)
+    flops = algo_flops(csc.nnz, i_real, k) + algo_flops(csr.nnz, u_real, k)
+    bytes_ = algo_bytes(csc.nnz, i_real, k) + algo_bytes(csr.nnz, u_real, k)
+    # item shards of the scoring / hybrid lines (equal contiguous ranges)
+    i0, i_per = shard_range(n_items, world, rank)
     kern_s = (item_ms + user_ms) / 1e3
     achieved_tf = flops / kern_s / 1e12
 
@@ -702,7 +838,7 @@ def main():
     if args.rank256_epochs > 0:
         k256 = 256
         e256 = DeviceALS(n_users, n_items, k256, 0.1, csr, csc, world=world, rank=rank, group=group, chunks=chunks,
-                         user_layout=u_lay, item_layout=i_lay)
+                         user_layout=eng.u_layout, item_layout=eng.i_layout)
         e256.init_user_factors(synthetic.SEED_INIT)
         e256.epoch()
         if world > 1:
@@ -724,7 +860,7 @@ def main():
             dist.all_reduce(wt, op=dist.ReduceOp.MAX)
         it_ms = sum(e[0].elapsed_time(e[1]) for e in ev256) / len(ev256)
         ut_ms = sum(e[1].elapsed_time(e[2]) for e in ev256) / len(ev256)
-        fl256 = algo_flops(csc.nnz, i_per, k256) + algo_flops(csr.nnz, u_per, k256)
+        fl256 = algo_flops(csc.nnz, i_real, k256) + algo_flops(csr.nnz, u_real, k256)
         als256 = {"epochs_per_s": 1.0 / float(wt.item()), "ms_per_epoch": float(wt.item()) * 1e3, "rank": k256,
                   "epochs": args.rank256_epochs, "kernel_ms_per_epoch": {"item": it_ms, "user": ut_ms},
                   "roofline": roofline("mfma", fl256 / 2, (it_ms + ut_ms) / 2, F64_MFMA_PEAK_TFLOPS, "TFLOP/s",
@@ -992,6 +1128,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(eng, cfg, min(args.cpu_user_rows, n_users), min(args.cpu_item_rows, n_items))
 
+    # BASELINE configs[2] (c3: 10M x 1M, 1 %, rank 64, user-sharded ALS with
+    # RCCL all-gathers on 8 GPUs) as a sub-line of every run with >= 8 ranks,
+    # after the c2 lines (their buffers freed): the headline stays c2 at every
+    # N so the driver's 1/2/4/8 values compare the same workload.
+    als_c3 = None
+    if world >= CONFIGS["c3"]["min_world"] and args.config != "c3" and args.c3_epochs > 0:
+        del eng, csr, csc
+        torch.cuda.empty_cache()
+        als_c3 = c3_line(world, rank, group, chunks, args.c3_epochs, stream)
+
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         line = {
@@ -1013,11 +1159,14 @@ def main():
                 "users": n_users, "items": n_items, "density": cfg["density"], "rank": k,
                 "nnz": nnz_user, "nnz_check_csc": nnz_item,
                 "shard_nnz_max_over_min": max(per_rank_nnz) / max(1, min(per_rank_nnz)),
+                "shard_layout": als["layout"],
                 "parallelism": (f"dp{world} (users/items in contiguous parts balanced on nnz + per-row solve cost; "
                                 f"user side in {chunks} chunks per rank, each chunk's RCCL all-gather overlapping "
                                 f"the next chunk's half-sweep)"
                                 if world > 1 else "dp1 (single GPU, no collectives)"),
             },
+            "world_size": world,
+            "collectives": als["collectives"],
             "roofline": {
                 "kernel": "als_half_sweep_f64_kernel (item + user launches)",
                 "bound": "mfma",
@@ -1049,11 +1198,13 @@ def main():
             "tt_train": tt_train,
             "api_hybrid_call": api,
             "als_rank256": als256,
+            "als_c3": als_c3,
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -2,7 +2,8 @@
 #include <stdarg.h>
 
 #include <mutex>
-#include <unordered_set>
+#include <set>
+#include <utility>
 
 #include "common.h"
 
@@ -27,14 +28,17 @@ int check_launch(const char* what) {
 }
 
 // Kernels that take more than 64 KiB of dynamic LDS need the attribute raised
-// once (per process: the attribute belongs to the kernel, not the launch).
+// once per (device, kernel): it is set through the current device, so a
+// process that drives several GPUs (hipSetDevice) raises it on each.
 bool allow_max_lds_ptr(const void* kfn) {
   static std::mutex mu;
-  static std::unordered_set<const void*> done;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
   std::lock_guard<std::mutex> lock(mu);
-  if (done.count(kfn)) return true;
+  if (done.count({dev, kfn})) return true;
   if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
-  done.insert(kfn);
+  done.insert({dev, kfn});
   return true;
 }
 

@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
     const char* __restrict__ U, int B, int UB, const char* __restrict__ V, int64_t n_rows, int64_t n_items,
     int64_t item_step, int n_ut, float* __restrict__ out, int64_t ldo, const float* __restrict__ thr, int thr_stride,
     int64_t thr_per, int cap, float* __restrict__ cand_v, int64_t* __restrict__ cand_i, int* __restrict__ cand_n,
-    int64_t idx_offset, int sbuf) {
+    int64_t idx_offset, int sbuf, int inf_none) {
   using S = DotShape<BF16, DK>;
   // NI = 4: 32-user chunks (8 MFMAs per 2 user-fragment reads, as 4 x 4
   // would be, at the register budget of two waves per SIMD)
@@ -359,7 +359,9 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
         float t = __builtin_nanf("");  // absent user: never passes
         if (b0 + o < B) {
           t = thr[(int64_t)(b0 + o) * thr_stride];
-          t = t == t ? (t == INFINITY ? __builtin_nanf("") : t) : -INFINITY;  // NaN admits all, +inf none
+          // NaN admits all; +inf admits scores >= +inf, or none (inf_none:
+          // the pruned hybrid's dead users, whose chunks are then skipped)
+          t = t == t ? (inf_none && t == INFINITY ? __builtin_nanf("") : t) : -INFINITY;
         }
         ths[o] = t;
       }
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
             const float x = tr[gq];
             t = fminf(t, x == x ? x : -INFINITY);
           }
-          if (t == INFINITY) t = __builtin_nanf("");  // +inf admits none: the chunks skip this user
+          if (inf_none && t == INFINITY) t = __builtin_nanf("");  // every group dead: the chunks skip this user
         }
         ths[o] = t;
       }
@@ -583,7 +585,7 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
           const int64_t j = it * kItems + (int64_t)((x >> 12) & 1023u);
           float t = thr[(int64_t)(b0 + (int)(x >> 22)) * thr_stride + j / thr_per];
           t = t == t ? t : -INFINITY;
-          if (!(buf_s[e] >= t)) {
+          if (!(buf_s[e] >= t) || (inf_none && t == INFINITY)) {
             buf[e] = 0xffffffffu;  // dropped (no user 1023: UB <= 1023)
             continue;
           }
@@ -703,7 +705,8 @@ static auto dot_res_pick(int ni) {
 template <bool FILTER>
 static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
                           int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
-                          int64_t* ci, int* cn, int64_t off, hipStream_t s, int64_t thr_per = 0) {
+                          int64_t* ci, int* cn, int64_t off, hipStream_t s, int64_t thr_per = 0,
+                          int inf_none = 0) {
   const int row_b = dk * (bf16 ? 2 : 4);
   const int row_lds = row_b >= 256 ? row_b : row_b + 16;
   int ub_max = kResUserBytes / row_lds;
@@ -734,7 +737,7 @@ static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, i
     if (!allow_max_lds(kfn))                                                                                   \
       return check_launch("dot_res_kernel: LDS attribute");                                                   \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, u, B, UB, v, n_rows, n_items, step, n_ut, out, ldo, thr,         \
-                       thr_stride, thr_per, cap, cv, ci, cn, off, sbuf);                                       \
+                       thr_stride, thr_per, cap, cv, ci, cn, off, sbuf, inf_none);                             \
   } while (0)
   if (bf16) {
     switch (dk) {
@@ -791,7 +794,8 @@ static int64_t dot_sample(int64_t n, int kk) {
 // append (score, j) of every item j with score >= thr[b * thr_stride + j /
 // thr_per] to user b's list (cap entries; cn[b] counts every survivor, so
 // cn[b] > cap = overflow). Always the resident-user kernel (the only one with
-// per-group bounds).
+// per-group bounds). Here a +inf bound admits nothing (a dead group / user,
+// skipped); hrec_dot_topk's filter keeps +inf meaning "score >= +inf".
 int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr,
                    int thr_stride, int64_t thr_per, int cap, float* cv, int64_t* ci, int* cn, hipStream_t s) {
   if (!bf16 && dk > 128) {
@@ -799,7 +803,7 @@ int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk,
     return HREC_E_INVALID;
   }
   return dot_launch_res<true>(U, B, V, n_items, n_items, 1, dk, bf16, nullptr, 0, thr, thr_stride, cap, cv, ci, cn, 0,
-                              s, thr_per);
+                              s, thr_per, 1);
 }
 
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s) {

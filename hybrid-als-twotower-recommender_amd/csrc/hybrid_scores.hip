@@ -102,6 +102,8 @@ struct HsShape {
 #endif
   static constexpr int NI = DK == 64 ? 4 : (DK == 256 ? HREC_HS_NI256 : 2);  // item tiles per wave slice (VGPR budget)
   static constexpr int NU = NI == 4 ? 2 : 4;    // user tiles per chunk (NI 4: each user fragment feeds 4 MFMAs)
+  // hp_bound_kernel's seed slots hold 4 NI items per group in 16 slots
+  static_assert(NI >= 1 && NI <= 4, "item tiles per wave slice must be 1..4 (HREC_HS_NI256)");
 };
 
 // Modes: HS_FULL = score stores + per-block min / max (hrec_hybrid_scores);

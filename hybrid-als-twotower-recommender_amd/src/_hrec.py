@@ -101,11 +101,6 @@ _SIGNATURES.update({
     "hrec_hybrid_scores_workspace_bytes": (_c_sz, [_c_i32, _c_i64]),
     "hrec_hybrid_scores": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32,
                                     _vp, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
-    "hrec_hybrid_minmax_workspace_bytes": (_c_sz, [_c_i32]),
-    "hrec_hybrid_minmax": (_c_i32, [_vp, _vp, _c_i32, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
-    "hrec_hybrid_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
-    "hrec_hybrid_topk": (_c_i32, [_vp, _vp, _c_i32, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _c_i32, _vp, _c_i64,
-                                  _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_hybrid_prune_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32, _c_i32]),
     "hrec_hybrid_prune_minmax": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp,
                                           _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
@@ -123,7 +118,7 @@ _SIGNATURES.update({
                                       + [_vp]),
 })
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _LIB = None
 
 
@@ -592,23 +587,6 @@ def dot_filter(U, V, thr, thr_per=0, cap=8192):
     return cv, ci, cn
 
 
-def hybrid_minmax(als_user, tt_user, als_item, tt_item):
-    """Per-user [min; max] of both score rows (hrec_hybrid_minmax), as
-    rows_minmax would give for the two score matrices: ([2, B], [2, B]) f32."""
-    B, N = als_user.shape[0], als_item.shape[0]
-    dk = _hyb_args(als_user, tt_user, als_item, tt_item)
-    dev = als_user.device
-    a_mm = torch.empty((2, B), dtype=torch.float32, device=dev)
-    t_mm = torch.empty((2, B), dtype=torch.float32, device=dev)
-    need = int(lib().hrec_hybrid_minmax_workspace_bytes(B))
-    ws = torch.empty(need, dtype=torch.uint8, device=dev)
-    _check("hrec_hybrid_minmax", lib().hrec_hybrid_minmax(
-        _vp(als_user.data_ptr()), _vp(tt_user.data_ptr()), B, _vp(als_item.data_ptr()), _vp(tt_item.data_ptr()), N,
-        dk, _dev(a_mm, torch.float32, "als_mm"), _dev(t_mm, torch.float32, "tt_mm"), _dev(ws, torch.uint8, "ws"),
-        need, _stream()))
-    return a_mm, t_mm
-
-
 def hybrid_scores(als_users, als_rows, tt_users, als_item, tt_item):
     """Both bf16 score matrices of a hybrid batch and their per-row min/max
     in one launch (hrec_hybrid_scores): als_users [n, ka] f32 ALS factors
@@ -745,29 +723,6 @@ def _hyb_args(*ops):
     if dk not in (64, 128, 256):
         raise HrecError(f"hybrid: width {dk} must be 64, 128 or 256")
     return dk
-
-
-def hybrid_topk(als_user, tt_user, als_item, tt_item, als_mm, tt_mm, als_wins, top_k, idx_offset=0):
-    """Fused hybrid top-k (hrec_hybrid_topk). Returns (ids + idx_offset
-    [B, kk] int64, fused f64 [B, kk], overflowed: bool) — on overflow the
-    result is not exact and the caller reruns the unfused path."""
-    B, N = als_user.shape[0], als_item.shape[0]
-    dk = _hyb_args(als_user, tt_user, als_item, tt_item)
-    kk = min(int(top_k), int(N))
-    dev = als_user.device
-    out_i = torch.empty((B, kk), dtype=torch.int64, device=dev)
-    out_v = torch.empty((B, kk), dtype=torch.float64, device=dev)
-    if B == 0 or kk == 0:
-        return out_i, out_v, False
-    flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    need = int(lib().hrec_hybrid_topk_workspace_bytes(B, N, kk))
-    ws = torch.empty(need, dtype=torch.uint8, device=dev)
-    _check("hrec_hybrid_topk", lib().hrec_hybrid_topk(
-        _vp(als_user.data_ptr()), _vp(tt_user.data_ptr()), B, _vp(als_item.data_ptr()), _vp(tt_item.data_ptr()), N,
-        dk, _dev(als_mm, torch.float32, "als_mm"), _dev(tt_mm, torch.float32, "tt_mm"), int(bool(als_wins)), kk, None,
-        int(idx_offset), _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float64, "out_val"),
-        _dev(flag, torch.int32, "overflow"), _dev(ws, torch.uint8, "ws"), need, _stream()))
-    return out_i, out_v, bool(int(flag.item()))
 
 
 def _dot_topk_chunked(U, V, kk, idx_offset, chunk=1 << 20):

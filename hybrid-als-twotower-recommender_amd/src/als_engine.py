@@ -131,6 +131,36 @@ class RowLayout:
         return pos
 
 
+def shard_for_layout(csr, layout, rank):
+    """This rank's shard of a whole-matrix CSR (DeviceCSR over every row,
+    global column ids) under `layout`: its parts in chunk order, each part's
+    rows followed by empty rows up to layout.cs (the layout's padded slots),
+    indices / values copied (DeviceALS remaps the copy's column ids in place).
+    Pure torch ops, any device."""
+    ips, ixs, vs, off = [csr.indptr[:1] * 0], [], [], 0
+    ip_all = csr.indptr
+    for b, cnt in layout.part_rows(rank):
+        lo, hi = int(ip_all[b]), int(ip_all[b + cnt])
+        ip = torch.full((layout.cs,), hi - lo, dtype=torch.int64, device=ip_all.device)
+        ip[:cnt] = ip_all[b + 1: b + cnt + 1] - lo
+        ips.append(ip + off)
+        ixs.append(csr.indices[lo:hi])
+        vs.append(csr.values[lo:hi])
+        off += hi - lo
+    return DeviceCSR(torch.cat(ips), torch.cat(ixs).clone(), torch.cat(vs).clone(), layout.part_rows(rank)[0][0],
+                     layout.cs * layout.chunks, csr.n_cols)
+
+
+def process_group():
+    """(world, rank, group) of an initialised torch.distributed world with
+    more than one rank, else (1, 0, None). HREC_ALS_SHARD=0 keeps one rank's
+    fit unsharded even then."""
+    if os.environ.get("HREC_ALS_SHARD", "1") == "0" or not dist.is_available() or not dist.is_initialized():
+        return 1, 0, None
+    w = dist.get_world_size()
+    return (w, dist.get_rank(), dist.group.WORLD) if w > 1 else (1, 0, None)
+
+
 class DeviceALS:
     """Holds one rank's CSR shard (user rows), CSC shard (item rows) and the
     replicated factor matrices."""
@@ -267,6 +297,19 @@ class DeviceALS:
 
     def user_half_sweep(self):
         self._sweep(self.user_csr, self.V, self.U_local, self.U, self.u_cs, self.u_chunks)
+
+    def compute_only_epoch(self):
+        """The epoch's half-sweep kernels alone (this rank's rows, the same
+        chunk launches, no all-gathers: the replicated buffers are not
+        updated) — what an epoch would cost if the collectives were free
+        (bench.py: epoch time minus this = collective time not hidden)."""
+        for csr, src, local, cs, chunks in ((self.item_csc, self.U, self.V_local, self.i_cs, self.i_chunks),
+                                            (self.user_csr, self.V, self.U_local, self.u_cs, self.u_chunks)):
+            s64 = self._src64(src)
+            extra = {} if s64 is None else {"src64": s64}
+            for c in range(chunks):
+                self.sweep(csr.indptr[c * cs: (c + 1) * cs + 1], csr.indices, csr.values, src, self.k, self.reg,
+                           local[c * cs: (c + 1) * cs], self.accum_mode, **extra)
 
     def epoch(self):
         """One Spark iteration: items from users, then users from items."""

@@ -4,8 +4,15 @@ Same class, method names, arguments, return values and error sentinels as
 src/als_model.py:21-177; the Spark engine underneath (ALS.fit at :62,
 ALSModel.transform at :75) is replaced by libhrec's HIP kernels:
 
-  train            -> host CSR/CSC ingest + hrec_als_init_factors +
+  train            -> device CSR/CSC ingest + hrec_als_init_factors +
                       max_iter x (item half-sweep, user half-sweep)  [K1]
+                      (under an initialised torch.distributed world of W
+                      > 1 ranks — torchrun, one GPU per rank — every rank
+                      calls train with the same frame; the users and items
+                      are split into nnz-balanced row shards, the factors
+                      replicated by RCCL all-gathers after each half-sweep,
+                      and every rank ends with the full model: the factors
+                      are bit-identical to the one-rank fit)
   predict_for_user -> hrec_als_score (JVM-exact f32 dot, NaN for unknown
                       ids = coldStartStrategy "drop")                [K2]
                       + cold-start fallback via hrec_cosine_sim +
@@ -24,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _hrec
-from .als_engine import DeviceALS, padded_k
+from .als_engine import DeviceALS, RowLayout, padded_k, process_group, shard_for_layout
 from .data_preprocessing import get_item_features
 from .synthetic import DeviceCSR
 
@@ -187,6 +194,8 @@ def build_csr(rows, cols, vals, n_rows, n_cols):
 class ALSModel:
     """src/als_model.py:21 — same constructor signature (+ optional seed)."""
 
+    CHUNKS = 4  # W > 1: user-side row chunks per rank (overlapped all-gathers)
+
     def __init__(self, rank=10, max_iter=10, reg_param=0.1, cold_start_strategy="drop", seed=None):
         self.rank = rank
         self.max_iter = max_iter
@@ -228,17 +237,36 @@ class ALSModel:
         item_ids_t, irow = _hrec.encode_ids(items, rng(items_h))
         user_ids, item_ids = user_ids_t.cpu().numpy(), item_ids_t.cpu().numpy()
         k = int(self.rank)
-        csr = build_csr(urow, irow, ratings, len(user_ids), len(item_ids))
-        csc = build_csr(irow, urow, ratings, len(item_ids), len(user_ids))
-        eng = DeviceALS(len(user_ids), len(item_ids), k, float(self.reg_param), csr, csc)
+        n_u, n_i = len(user_ids), len(item_ids)
+        csr = build_csr(urow, irow, ratings, n_u, n_i)
+        csc = build_csr(irow, urow, ratings, n_i, n_u)
+        del urow, irow, ratings, users, items
+        world, rank, group = process_group()
+        if world > 1:
+            # nnz-balanced contiguous row shards (users in
+            # CHUNKS per rank: each chunk's all-gather overlaps the next
+            # chunk's sweep), this rank's parts cut out of the whole CSR/CSC
+            ulay = RowLayout.balanced((csr.indptr[1:] - csr.indptr[:-1]).cpu().numpy(), world, self.CHUNKS)
+            ilay = RowLayout.balanced((csc.indptr[1:] - csc.indptr[:-1]).cpu().numpy(), world, 1)
+            csr, csc = shard_for_layout(csr, ulay, rank), shard_for_layout(csc, ilay, rank)
+            eng = DeviceALS(n_u, n_i, k, float(self.reg_param), csr, csc, world=world, rank=rank, group=group,
+                            chunks=self.CHUNKS, item_chunks=1, user_layout=ulay, item_layout=ilay)
+        else:
+            eng = DeviceALS(n_u, n_i, k, float(self.reg_param), csr, csc)
         if U0 is not None:
             eng.set_user_factors(U0)
         else:
             seed = (hash(type(self).__name__) if self.seed is None else int(self.seed)) & ((1 << 63) - 1)
             eng.init_user_factors(seed)
         eng.fit(int(self.max_iter))
-        return DeviceALSFactors(user_ids, item_ids, eng.U[: len(user_ids)].contiguous(),
-                                eng.V[: len(item_ids)].contiguous(), k)
+        if world == 1:
+            U, V = eng.U[:n_u].contiguous(), eng.V[:n_i].contiguous()
+        else:  # every rank holds the replicated factors; back to global row order
+            U = torch.zeros((n_u, eng.kp), dtype=torch.float32, device=dev)
+            V = torch.zeros((n_i, eng.kp), dtype=torch.float32, device=dev)
+            U[:, :k] = eng.user_factors
+            V[:, :k] = eng.item_factors
+        return DeviceALSFactors(user_ids, item_ids, U, V, k)
 
     def train(self, data, initial_user_factors=None):
         """src/als_model.py:43-66. `initial_user_factors` (optional, [n_users, rank]

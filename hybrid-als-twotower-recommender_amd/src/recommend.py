@@ -9,13 +9,15 @@ items split into contiguous shards, one per rank (SURVEY §8e, rows
 
   1. local scores: JVM-exact ALS dot (hrec_als_score) and two-tower Dot on
      the matrix cores (hrec_tt_score) for the rank's item shard;
-  2. per-row min / max of both (hrec_rows_minmax_f32), made global by RCCL
-     all_reduce MIN / MAX (C2) — min and max are exact under any grouping;
+  2. per-row min / max of both (hrec_rows_minmax_f32), made global by ONE
+     RCCL all_reduce MIN over [min | -max] of both models (C2) — min and
+     max are exact under any grouping;
   3. fusion with the global scaler coefficients + local stable top-k with
      global item ids (hrec_fuse_rows_topk);
-  4. RCCL all_gather of the [B, k] candidates (C3) and a keyed stable top-k
-     merge (hrec_topk_f64_keyed): ties break on the global item id, so every
-     world size returns the same items and scores as one GPU.
+  4. ONE RCCL all_gather of the [B, k] candidates, ids and scores in one
+     buffer (C3), and a keyed stable top-k merge (hrec_topk_f64_keyed): ties
+     break on the global item id, so every world size returns the same items
+     and scores as one GPU. Two collectives per batch in all.
 
 ShardedScorer does the same for the two-tower scoring alone (BASELINE c4:
 d = 128 embeddings, 50M candidates over 8 GPUs): each rank ranks its item
@@ -51,9 +53,6 @@ class DeviceOps:
     def operand(x, dtype, dk=None):
         return _hrec.dot_operand(x, dtype, dk)
 
-    hybrid_minmax = staticmethod(_hrec.hybrid_minmax)
-    hybrid_topk = staticmethod(_hrec.hybrid_topk)
-
     dot_scores = staticmethod(_hrec.dot_scores)
     hybrid_scores = staticmethod(_hrec.hybrid_scores)
     hybrid_prune = staticmethod(_hrec.HybridPrune)
@@ -76,7 +75,7 @@ class ShardedRecommender:
     paths return the same bits."""
 
     def __init__(self, U, Vt_local, item_vecs_local, item_offset, k, world=1, rank=0, group=None, ops=None,
-                 precision="exact", V_local=None, fused=False, pruned=True):
+                 precision="exact", V_local=None, pruned=True):
         self.U = U                          # [n_users, kp] ALS user factors (replicated)
         self.Vt = Vt_local                  # [kp, ld] transposed ALS item factors of this shard
         self.iv = item_vecs_local           # [n_local, d] two-tower item vectors of this shard
@@ -93,11 +92,6 @@ class ShardedRecommender:
                 raise ValueError("precision='bf16' needs V_local (ALS item factor rows of the shard)")
             # one width for both models so the fused kernel can run them together
             self.dk = max(64, _hrec.dot_dk(V_local.shape[1]), _hrec.dot_dk(item_vecs_local.shape[1]))
-            # fused kernels: no score matrix in HBM (bit-identical results);
-            # off by default — at c5's 1e5-item shards the two score matrices
-            # are cheap and the fused path's per-batch overflow check (a host
-            # sync) costs more than it saves
-            self.fused = bool(fused) and hasattr(self.ops, "hybrid_topk")
             self.pruned = bool(pruned) and hasattr(self.ops, "hybrid_prune")
             self.V_op = self.ops.operand(V_local, torch.bfloat16, self.dk)
             self.iv_op = self.ops.operand(item_vecs_local, torch.bfloat16, self.dk)
@@ -114,37 +108,6 @@ class ShardedRecommender:
                     o.tt_scores(user_vecs, self.iv))
         u_als, u_tt = self._user_ops(user_rows, user_vecs)
         return o.dot_scores(u_als, self.V_op), o.dot_scores(u_tt, self.iv_op)
-
-    def _recommend_fused(self, user_rows, user_vecs, als_wins, top_k):
-        """bf16 path on the fused kernels (hrec_hybrid_minmax / _topk): no
-        score matrix is written; same results as the unfused path, which
-        answers a batch whose survivor list overflowed."""
-        o = self.ops
-        B = int(user_rows.shape[0])
-        dev = user_vecs.device
-        if self.n_local > 0:
-            u_als, u_tt = self._user_ops(user_rows, user_vecs)
-            a_mm, t_mm = o.hybrid_minmax(u_als, u_tt, self.V_op, self.iv_op)
-        else:
-            inf = float("inf")
-            a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
-            t_mm = a_mm.clone()
-        if self.world > 1:
-            for mm in (a_mm, t_mm):
-                dist.all_reduce(mm[0], op=dist.ReduceOp.MIN, group=self.group)
-                dist.all_reduce(mm[1], op=dist.ReduceOp.MAX, group=self.group)
-        if self.n_local > 0:
-            idx, val, over = o.hybrid_topk(u_als, u_tt, self.V_op, self.iv_op, a_mm, t_mm, als_wins, top_k,
-                                           self.offset)
-            if over:
-                idx, val = o.fuse_rows_topk(o.dot_scores(u_als, self.V_op), o.dot_scores(u_tt, self.iv_op),
-                                            a_mm, t_mm, als_wins, top_k, self.offset)
-        else:
-            idx = torch.empty((B, 0), dtype=torch.int64, device=dev)
-            val = torch.empty((B, 0), dtype=torch.float64, device=dev)
-        if self.world == 1:
-            return idx, val
-        return merge_candidates(idx, val, top_k, self.world, self.group, o)
 
     def _recommend_pruned(self, user_rows, user_vecs, als_wins, top_k):
         """bf16 path without score matrices (hrec_hybrid_prune_*): phase 1 gives
@@ -172,9 +135,7 @@ class ShardedRecommender:
             a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
             t_mm = a_mm.clone()
         if self.world > 1:
-            for mm in (a_mm, t_mm):
-                dist.all_reduce(mm[0], op=dist.ReduceOp.MIN, group=self.group)
-                dist.all_reduce(mm[1], op=dist.ReduceOp.MAX, group=self.group)
+            a_mm, t_mm = global_minmax(a_mm, t_mm, self.group)
         if self.n_local > 0:
             idx, val = hp.topk(a_mm, t_mm, als_wins, self.offset)
             self.last_prune = hp
@@ -188,8 +149,6 @@ class ShardedRecommender:
     def recommend(self, user_rows, user_vecs, als_wins, top_k):
         """user_rows: [B] int64 ALS rows; user_vecs: [B, d] two-tower user
         vectors. Returns (global item ids [B, k], fused scores f64 [B, k])."""
-        if self.precision == "bf16" and self.fused:
-            return self._recommend_fused(user_rows, user_vecs, als_wins, top_k)
         if self.precision == "bf16" and self.pruned and 1 <= int(top_k) <= _hrec.PRUNE_MAX_K:
             return self._recommend_pruned(user_rows, user_vecs, als_wins, top_k)
         o = self.ops
@@ -208,9 +167,7 @@ class ShardedRecommender:
             a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
             t_mm = a_mm.clone()
         if self.world > 1:
-            for mm in (a_mm, t_mm):
-                dist.all_reduce(mm[0], op=dist.ReduceOp.MIN, group=self.group)
-                dist.all_reduce(mm[1], op=dist.ReduceOp.MAX, group=self.group)
+            a_mm, t_mm = global_minmax(a_mm, t_mm, self.group)
         if self.n_local > 0:
             idx, val = o.fuse_rows_topk(als, tt, a_mm, t_mm, als_wins, top_k, self.offset)
         else:
@@ -221,23 +178,41 @@ class ShardedRecommender:
         return merge_candidates(idx, val, top_k, self.world, self.group, o)
 
 
+# Collective calls issued by this module (C2 + C3): two per sharded batch.
+COLLECTIVE_CALLS = [0]
+
+
+def global_minmax(a_mm, t_mm, group):
+    """C2: both models' per-user [min; max] rows made global in ONE
+    all_reduce(MIN): the maxima travel negated (-max(x) = min(-x), exact in
+    floating point), packed as [a_min | t_min | -a_max | -t_max] ([4, B] f32),
+    and are negated back. Returns (als_mm, tt_mm), [2, B] each."""
+    pack = torch.stack([a_mm[0], t_mm[0], -a_mm[1], -t_mm[1]])
+    COLLECTIVE_CALLS[0] += 1
+    dist.all_reduce(pack, op=dist.ReduceOp.MIN, group=group)
+    return torch.stack([pack[0], -pack[2]]), torch.stack([pack[1], -pack[3]])
+
+
 def merge_candidates(idx, val, top_k, world, group, ops):
     """C3: all_gather every rank's [B, <=k] candidates (global ids, -1 = empty
-    slot) and merge them by a keyed stable top-k (ties -> smaller id)."""
+    slot) and merge them by a keyed stable top-k (ties -> smaller id). Ids
+    (int64) and scores (f64, bit-cast to int64) travel as ONE [B, 2k] buffer."""
     B = idx.shape[0]
     dev = idx.device
     kk = int(top_k)
+    val = val.double()  # exact for f32 scores
     if idx.shape[1] < kk:  # every rank contributes k slots; -1 marks an empty one
         pad = kk - idx.shape[1]
         idx = torch.cat([idx, torch.full((B, pad), -1, dtype=torch.int64, device=dev)], 1)
         val = torch.cat([val, torch.full((B, pad), float("-inf"), dtype=val.dtype, device=dev)], 1)
-    # rank-major concatenation [W*B, k] (the layout every backend accepts)
-    g_idx = torch.empty((world * B, kk), dtype=idx.dtype, device=dev)
-    g_val = torch.empty((world * B, kk), dtype=val.dtype, device=dev)
-    dist.all_gather_into_tensor(g_idx, idx.contiguous(), group=group)
-    dist.all_gather_into_tensor(g_val, val.contiguous(), group=group)
-    cand_i = g_idx.view(world, B, kk).permute(1, 0, 2).reshape(B, world * kk).contiguous()
-    cand_v = g_val.view(world, B, kk).permute(1, 0, 2).reshape(B, world * kk).contiguous()
+    send = torch.cat([idx.to(torch.int64), val.view(torch.int64)], 1).contiguous()
+    # rank-major concatenation [W*B, 2k] (the layout every backend accepts)
+    got = torch.empty((world * B, 2 * kk), dtype=torch.int64, device=dev)
+    COLLECTIVE_CALLS[0] += 1
+    dist.all_gather_into_tensor(got, send, group=group)
+    got = got.view(world, B, 2 * kk).permute(1, 0, 2)
+    cand_i = got[:, :, :kk].reshape(B, world * kk).contiguous()
+    cand_v = got[:, :, kk:].contiguous().view(torch.float64).reshape(B, world * kk).contiguous()
     return ops.topk_keyed(cand_v, cand_i, top_k)
 
 

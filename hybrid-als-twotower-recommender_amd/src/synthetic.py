@@ -50,67 +50,67 @@ class DeviceCSR:
         return int(self.indices.numel())
 
 
+def generate_parts(n_users, n_items, density, transposed, parts, seed=SEED, seed2=SEED2, n_levels=N_LEVELS,
+                   device=None):
+    """One CSR over several row ranges of R (transposed=False: user rows over
+    items) or R^T (item rows over users), concatenated in order: parts =
+    [(row_begin, n_rows, n_real)], each range's rows past its first n_real
+    (or past the matrix) empty. The index / value arrays are allocated once
+    and every range is filled in place (no concatenation: a c3 shard is
+    ~100 GB per side, so a copy would not fit beside it)."""
+    _hrec.require_device()
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    total_rows = n_items if transposed else n_users
+    n_cols = n_users if transposed else n_items
+    thr = threshold(density)
+    spans, off = [], 0
+    for b, n, real in parts:
+        real = max(0, min(int(n), total_rows - int(b), int(real)))
+        spans.append((int(b), off, real))
+        off += int(n)
+    counts = torch.zeros(off, dtype=torch.int64, device=device)
+    for b, o, real in spans:
+        if real > 0:
+            _hrec.synth_row_counts(seed, thr, b, real, n_cols, transposed, counts[o: o + real])
+    indptr = _hrec.exclusive_scan(counts)
+    del counts
+    nnz = int(indptr[-1].item())
+    indices = torch.empty(max(nnz, 1), dtype=torch.int32, device=device)[:nnz]
+    values = torch.empty(max(nnz, 1), dtype=torch.float32, device=device)[:nnz]
+    if nnz > 0:
+        for b, o, real in spans:
+            if real > 0:  # indptr entries are absolute positions in indices / values
+                _hrec.synth_fill(seed, seed2, thr, b, real, n_cols, transposed, n_levels, indptr[o:],
+                                 indices, values)
+    return DeviceCSR(indptr, indices, values, parts[0][0] if parts else 0, off, n_cols)
+
+
 def generate(n_users, n_items, density, transposed, row_begin=0, n_rows=None, seed=SEED,
              seed2=SEED2, n_levels=N_LEVELS, device=None, n_real=None):
     """Generate rows [row_begin, row_begin+n_rows) of R (transposed=False:
     user rows over items) or of R^T (transposed=True: item rows over users).
     Rows past the end of the matrix, or past the first n_real rows, are empty
     (shard padding)."""
-    _hrec.require_device()
-    device = device or torch.device("cuda", torch.cuda.current_device())
     total_rows = n_items if transposed else n_users
-    n_cols = n_users if transposed else n_items
     if n_rows is None:
         n_rows = total_rows - row_begin
-    real = max(0, min(n_rows, total_rows - row_begin))
-    if n_real is not None:
-        real = min(real, int(n_real))
-    thr = threshold(density)
-    counts = torch.zeros(n_rows, dtype=torch.int64, device=device)
-    if real > 0:
-        _hrec.synth_row_counts(seed, thr, row_begin, real, n_cols, transposed, counts)
-    indptr = _hrec.exclusive_scan(counts)
-    nnz = int(indptr[-1].item())
-    indices = torch.empty(max(nnz, 1), dtype=torch.int32, device=device)[:nnz]
-    values = torch.empty(max(nnz, 1), dtype=torch.float32, device=device)[:nnz]
-    if real > 0 and nnz > 0:
-        _hrec.synth_fill(seed, seed2, thr, row_begin, real, n_cols, transposed, n_levels, indptr,
-                         indices, values)
-    del counts
-    return DeviceCSR(indptr, indices, values, row_begin, n_rows, n_cols)
+    real = n_rows if n_real is None else min(n_rows, int(n_real))
+    return generate_parts(n_users, n_items, density, transposed, [(row_begin, n_rows, real)], seed=seed,
+                          seed2=seed2, n_levels=n_levels, device=device)
 
 
 def generate_ranges(n_users, n_items, density, transposed, ranges, **kw):
     """One CSR over several row ranges [(row_begin, n_rows), ...] of R or R^T,
     concatenated in order (a chunk-interleaved shard, als_engine.shard_chunks)."""
-    parts = [generate(n_users, n_items, density, transposed, b, n, **kw) for b, n in ranges]
-    if len(parts) == 1:
-        return parts[0]
-    offs, ips = 0, [parts[0].indptr[:1]]
-    for p in parts:
-        ips.append(p.indptr[1:] + offs)
-        offs += p.nnz
-    indptr = torch.cat(ips)
-    indices = torch.cat([p.indices for p in parts])
-    values = torch.cat([p.values for p in parts])
-    return DeviceCSR(indptr, indices, values, ranges[0][0], sum(n for _, n in ranges), parts[0].n_cols)
-
+    return generate_parts(n_users, n_items, density, transposed, [(b, n, n) for b, n in ranges], **kw)
 
 
 def generate_layout(n_users, n_items, density, transposed, layout, rank, **kw):
     """This rank's shard under an als_engine.RowLayout: its parts (chunk
     order), each part's rows followed by empty rows up to the layout's cs,
     with GLOBAL column ids (DeviceALS remaps them)."""
-    parts = [generate(n_users, n_items, density, transposed, b, layout.cs, n_real=cnt, **kw)
-             for b, cnt in layout.part_rows(rank)]
-    if len(parts) == 1:
-        return parts[0]
-    offs, ips = 0, [parts[0].indptr[:1]]
-    for p in parts:
-        ips.append(p.indptr[1:] + offs)
-        offs += p.nnz
-    return DeviceCSR(torch.cat(ips), torch.cat([p.indices for p in parts]), torch.cat([p.values for p in parts]),
-                     parts[0].row_begin, layout.cs * len(parts), parts[0].n_cols)
+    return generate_parts(n_users, n_items, density, transposed,
+                          [(b, layout.cs, cnt) for b, cnt in layout.part_rows(rank)], **kw)
 
 
 def row_counts(n_users, n_items, density, transposed, seed=SEED, device=None):

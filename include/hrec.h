@@ -37,8 +37,10 @@
 extern "C" {
 #endif
 
-/* 2: hrec_fuse_topk gained out_minmax; hrec_hybrid_scores gained n_als_rows. */
-#define HREC_ABI_VERSION 2
+/* 2: hrec_fuse_topk gained out_minmax; hrec_hybrid_scores gained n_als_rows.
+ * 3: hrec_hybrid_minmax / hrec_hybrid_topk removed (the pruned hybrid
+ *    replaces them); hrec_dot_topk's +inf bound admits scores >= +inf. */
+#define HREC_ABI_VERSION 3
 
 #define HREC_OK 0
 #define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
@@ -398,38 +400,15 @@ int hrec_dot_topk(const void* user_vec, int n_users, const void* item_vec, int64
 /* The survivor filter of hrec_dot_topk / the pruned hybrid alone: append
  * (score, j) of every item j with <U[b], V[j]> >= thr[b * thr_stride + (thr_per
  * ? j / thr_per : 0)] to user b's list (cand_val / cand_idx [n_users, cap]; a
- * NaN bound admits every score, a +inf bound none; list order unspecified). cand_n[b], zeroed by
+ * NaN bound admits every score, a +inf bound none — a dead user or group,
+ * skipped; hrec_dot_topk's own filter instead admits scores >= +inf for a
+ * +inf bound; list order unspecified). cand_n[b], zeroed by
  * the caller, ends as the user's survivor count, or > cap when the list
  * overflowed (the list then holds an arbitrary subset). bf16 operands, or f32
  * at dk <= 128. */
 int hrec_dot_filter(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
                     int dtype, const float* thr, int thr_stride, int64_t thr_per, int cap, float* cand_val,
                     int64_t* cand_idx, int* cand_n, void* stream);
-
-/* ---------------------------------------------------------------------
- * Fused hybrid recommendation on bf16 operands (csrc/hybrid_fused.hip,
- * BASELINE config c5): ALS scores <als_user[b], als_item[j]> and two-tower
- * scores <tt_user[b], tt_item[j]> (both operands [*, dk] bf16, dk in
- * {64, 128, 256}, zero-padded), the reference's per-model MinMaxScaler
- * fusion and stable top-k (src/hybrid_system.py:57-75, :108) without writing
- * either score matrix. Same results as hrec_dot_scores x2 +
- * hrec_fuse_rows_topk. */
-size_t hrec_hybrid_minmax_workspace_bytes(int n_users);
-/* Per-user [min | max] of both score rows over items [0, n_items):
- * als_mm / tt_mm are [2, n_users] f32 (the hrec_rows_minmax_f32 layout). */
-int hrec_hybrid_minmax(const void* als_user, const void* tt_user, int n_users, const void* als_item,
-                       const void* tt_item, int64_t n_items, int dk, float* als_mm, float* tt_mm,
-                       void* workspace, size_t workspace_bytes, void* stream);
-size_t hrec_hybrid_topk_workspace_bytes(int n_users, int64_t n_items, int top_k);
-/* Fused scores with the scaler coefficients of als_mm / tt_mm (global
- * min/max when the items are sharded), weights (0.8, 0.2) if als_wins else
- * (0.2, 0.8); top_k per user, ties -> smaller item index; ids + idx_offset.
- * thr_in (optional, [n_users] f64): lower bound of each user's k-th best;
- * *overflow as hrec_dot_topk. */
-int hrec_hybrid_topk(const void* als_user, const void* tt_user, int n_users, const void* als_item,
-                     const void* tt_item, int64_t n_items, int dk, const float* als_mm, const float* tt_mm,
-                     int als_wins, int top_k, const double* thr_in, int64_t idx_offset, int64_t* out_idx,
-                     double* out_val, int* overflow, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------
  * Both score matrices of the bf16 hybrid in one launch (csrc/hybrid_scores.hip,
@@ -472,8 +451,13 @@ int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const int64_t* al
  *   survivors than k take the exact unfused path, gated on the device (no host
  *   round trip; hrec_hybrid_prune_fallback_taken copies that flag).
  * top_k in [1, 8]; the workspace (hrec_hybrid_prune_workspace_bytes, the same
- * dk and top_k) carries phase 1's state into phase 2 and holds the fallback's
- * two score matrices (2 n_users n_items floats). n_users < 65536. */
+ * dk and top_k) carries phase 1's state into phase 2: per item group G =
+ * ceil(n_items / group) the group partials and arg-slices (24 B per user and
+ * group), both bf16 user operands (4 dk B per user), the per-group bounds
+ * (4 B per user and group) and each user's survivor list of 8192 entries
+ * (96 KiB per user, whatever n_items is; the exact fallback runs inside the
+ * survivor kernel and needs no score matrices). About 100 KiB per user at
+ * c5: 25 MB for 256 users. n_users < 65536. */
 size_t hrec_hybrid_prune_workspace_bytes(int n_users, int64_t n_items, int dk, int top_k);
 int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, const int64_t* als_rows,
                              int64_t n_als_rows, int als_width, const float* tt_users, int64_t tt_ld,

@@ -83,9 +83,6 @@ int main() {
   INVALID(hrec_dot_topk(nullptr, 1, nullptr, 4, 64, 2, 5, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_dot_filter(nullptr, 1, nullptr, 4, 256, 0, nullptr, 1, 0, 8, nullptr, nullptr, nullptr, nullptr));
   INVALID(hrec_dot_filter(nullptr, 1, nullptr, 100, 64, 1, nullptr, 2, 32, -8, nullptr, nullptr, nullptr, nullptr));
-  INVALID(hrec_hybrid_minmax(nullptr, nullptr, 1, nullptr, nullptr, 4, 32, nullptr, nullptr, nullptr, 0, nullptr));
-  INVALID(hrec_hybrid_topk(nullptr, nullptr, 1, nullptr, nullptr, 4, 64, nullptr, nullptr, 1, 0, nullptr, 0, nullptr,
-                           nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_scores(nullptr, 64, nullptr, -1, 64, nullptr, 64, 64, 4, nullptr, nullptr, 10, 64, nullptr,
                              nullptr, 10, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_prune_minmax(nullptr, 64, nullptr, 4, 64, nullptr, 64, 64, 4, nullptr, nullptr, 10, 96,
@@ -108,8 +105,8 @@ int main() {
         acc += hrec_als_score_topk_workspace_bytes(b, n, k);
         acc += hrec_topk_workspace_bytes(b, n, k, 1) + hrec_topk_workspace_bytes(b, n, k, 0);
         acc += hrec_fuse_workspace_bytes(n, k) + hrec_fuse_rows_workspace_bytes(b, n, k);
-        acc += hrec_dot_topk_workspace_bytes(b, n, k) + hrec_hybrid_topk_workspace_bytes(b, n, k);
-        acc += hrec_hybrid_scores_workspace_bytes(b, n) + hrec_hybrid_minmax_workspace_bytes(b);
+        acc += hrec_dot_topk_workspace_bytes(b, n, k);
+        acc += hrec_hybrid_scores_workspace_bytes(b, n);
         if (k <= 8) acc += hrec_hybrid_prune_workspace_bytes(b, n, 256, k);
       }
   for (int64_t n : ns) {

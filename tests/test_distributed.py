@@ -190,6 +190,32 @@ def test_nnz_balanced_shards_match_unsharded(world, chunks):
         np.testing.assert_array_equal(Vr, V)
 
 
+def test_shard_for_layout_matches_host_shard():
+    """als_engine.shard_for_layout (what ALSModel.train cuts out of the
+    whole-frame CSR under W > 1) == the host shard builder of these tests,
+    for balanced chunked layouts, incl. empty parts (more parts than rows)."""
+    from src.als_engine import RowLayout, shard_for_layout
+    from src.synthetic import DeviceCSR
+
+    for transposed in (False, True):
+        ip, ix, v = _skewed_csr(transposed)
+        n_cols = SK_USERS if transposed else SK_ITEMS
+        full = DeviceCSR(torch.from_numpy(ip), torch.from_numpy(ix), torch.from_numpy(v), 0, len(ip) - 1, n_cols)
+        for world, chunks in ((2, 1), (3, 4), (5, 3)):
+            lay = RowLayout.balanced(np.diff(ip), world, chunks)
+            for r in range(world):
+                a, b = shard_for_layout(full, lay, r), _layout_shard((ip, ix, v), lay, r, n_cols)
+                assert torch.equal(a.indptr, b.indptr) and torch.equal(a.indices, b.indices)
+                assert torch.equal(a.values, b.values)
+                assert (a.row_begin, a.n_rows, a.n_cols) == (b.row_begin, b.n_rows, b.n_cols)
+                assert a.indices.data_ptr() != full.indices.data_ptr()  # remapped in place later: a copy
+    tiny = DeviceCSR(torch.tensor([0, 2, 3], dtype=torch.int64), torch.tensor([1, 0, 1], dtype=torch.int32),
+                     torch.tensor([1.0, 2.0, 3.0]), 0, 2, 2)
+    lay = RowLayout.balanced([2, 1], 3, 2)
+    shards = [shard_for_layout(tiny, lay, r) for r in range(3)]
+    assert sum(s.nnz for s in shards) == 3 and all(s.n_rows == lay.cs * 2 for s in shards)
+
+
 def test_row_layout_positions():
     from src.als_engine import RowLayout
 
@@ -290,20 +316,6 @@ class _CpuOps:
         return torch.from_numpy(np.array(out_i)), torch.from_numpy(np.array(out_v))
 
 
-class _CpuFusedOps(_CpuOps):
-    """Stand-ins for the fused kernels (same results as the unfused ops)."""
-
-    @staticmethod
-    def hybrid_minmax(ua, ut, va, vt):
-        return _CpuOps.rows_minmax(_CpuOps.dot_scores(ua, va)), _CpuOps.rows_minmax(_CpuOps.dot_scores(ut, vt))
-
-    @staticmethod
-    def hybrid_topk(ua, ut, va, vt, a_mm, t_mm, als_wins, top_k, offset):
-        i, v = _CpuOps.fuse_rows_topk(_CpuOps.dot_scores(ua, va), _CpuOps.dot_scores(ut, vt), a_mm, t_mm, als_wins,
-                                      top_k, offset)
-        return i, v, False
-
-
 def _hybrid_data():
     rng = np.random.default_rng(7)
     n_users, n_items, k, d = 12, 101, 8, 6
@@ -322,9 +334,8 @@ def _hybrid_run(world, rank, U, V, uv, iv, k, group=None, precision="exact"):
     Vl = V[i0: i0 + per]
     rec = ShardedRecommender(torch.from_numpy(U), torch.from_numpy(np.ascontiguousarray(Vl.T)),
                              torch.from_numpy(iv[i0: i0 + per]), i0, k, world=world, rank=rank, group=group,
-                             ops=_CpuFusedOps if precision == "bf16-fused" else _CpuOps,
-                             precision="bf16" if precision.startswith("bf16") else precision,
-                             V_local=torch.from_numpy(np.ascontiguousarray(Vl)), fused=precision == "bf16-fused")
+                             ops=_CpuOps, precision=precision,
+                             V_local=torch.from_numpy(np.ascontiguousarray(Vl)))
     rows = torch.tensor([0, 3, 5, 7, 11], dtype=torch.int64)
     return [t.numpy() for t in rec.recommend(rows, torch.from_numpy(uv), True, 7)]
 
@@ -332,13 +343,17 @@ def _hybrid_run(world, rank, U, V, uv, iv, k, group=None, precision="exact"):
 def _hybrid_worker(rank, world, port, q, precision="exact"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from src import recommend
+
     U, V, uv, iv, k = _hybrid_data()
-    q.put((rank, _hybrid_run(world, rank, U, V, uv, iv, k, dist.group.WORLD, precision)))
+    c0 = recommend.COLLECTIVE_CALLS[0]
+    out = _hybrid_run(world, rank, U, V, uv, iv, k, dist.group.WORLD, precision)
+    q.put((rank, out, recommend.COLLECTIVE_CALLS[0] - c0))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,precision", [(2, "exact"), (4, "exact"), (24, "exact"), (3, "bf16"),
-                                             (3, "bf16-fused"), (24, "bf16-fused")])
+                                             (24, "bf16")])
 def test_sharded_hybrid_topk_matches_single(world, precision):
     U, V, uv, iv, k = _hybrid_data()
     ref_i, ref_v = _hybrid_run(1, 0, U, V, uv, iv, k, precision=precision)
@@ -352,9 +367,10 @@ def test_sharded_hybrid_topk_matches_single(world, precision):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for _, (gi, gv) in res:
+    for _, (gi, gv), calls in res:
         np.testing.assert_array_equal(gi, ref_i)
         np.testing.assert_array_equal(gv, ref_v)
+        assert calls == 2  # C2 (one all_reduce) + C3 (one all_gather) per batch
 
 
 # ------------------------------------------- sharded two-tower top-k (c4, C3)
@@ -382,6 +398,27 @@ def _scorer_run(world, rank, uv, iv, group=None):
     sc = ShardedScorer(torch.from_numpy(iv[i0: i0 + per]), i0, world=world, rank=rank, group=group, ops=_CpuDotOps)
     i, v = sc.topk(torch.from_numpy(uv), 7)
     return i.numpy(), v.numpy().astype(np.float64)
+
+
+def test_global_minmax_packs_both_models():
+    """C2 packing: [a_min | t_min | -a_max | -t_max] reduced by MIN gives
+    both models' global min and max exactly (one rank: the identity), incl.
+    the +inf / -inf extremes of an empty shard."""
+    from src.recommend import global_minmax
+
+    a = torch.tensor([[1.5, float("inf"), -2.0], [3.0, -float("inf"), -0.0]])
+    t = torch.tensor([[-7.0, 0.25, float("inf")], [9.0, 0.5, -float("inf")]])
+
+    class _G:
+        pass
+
+    orig = dist.all_reduce
+    dist.all_reduce = lambda x, op=None, group=None: x  # world 1: MIN over one rank
+    try:
+        ga, gt = global_minmax(a, t, _G())
+    finally:
+        dist.all_reduce = orig
+    assert torch.equal(ga, a) and torch.equal(gt, t)
 
 
 def _scorer_worker(rank, world, port, q):

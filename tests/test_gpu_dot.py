@@ -142,6 +142,30 @@ def test_dot_filter_staging_overflow_keeps_lists_valid(device):
         np.testing.assert_array_equal(cv[b][~filler[b]], S[b, ids])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dot_topk_infinite_scores(device, dtype):
+    """k or more items scoring +inf (overflowing dots) put +inf in
+    the sample's k-th best, i.e. the filter bound; hrec_dot_topk must still
+    admit scores >= +inf (the +inf items, smaller index first), as the full
+    score matrix's stable top-k says."""
+    h = _h()
+    N, d, k = 20_000, 64, 5
+    rng = np.random.default_rng(31)
+    U = np.abs(rng.standard_normal((3, d))).astype(np.float32) + 0.5
+    V = rng.standard_normal((N, d)).astype(np.float32)
+    hot = np.arange(100, 1100, 100)  # 10 items on the sample's stride (even ids)
+    V[hot] = 3e38
+    Ud = h.dot_operand(torch.from_numpy(U).to(device), dtype)
+    Vd = h.dot_operand(torch.from_numpy(V).to(device), dtype)
+    full = h.dot_scores(Ud, Vd).cpu().numpy()
+    assert np.all(np.isposinf(full[:, hot]))
+    ei, ev = _stable_topk(full, k)
+    gi, gv = h.dot_topk(Ud, Vd, k)
+    np.testing.assert_array_equal(gi.cpu().numpy(), ei)
+    np.testing.assert_array_equal(gi.cpu().numpy(), np.tile(hot[:k], (3, 1)))
+    np.testing.assert_array_equal(gv.cpu().numpy(), ev)
+
+
 def test_dot_topk_ties_keep_candidate_order(device):
     """Duplicated item vectors score identically: the reference's stable sort
     keeps candidate (index) order among them."""
@@ -214,17 +238,20 @@ def test_dot_topk_matches_f64_ranking_outside_ties(device):
     assert checked >= B // 2
 
 
-def test_hybrid_bf16_mode_matches_f64_fusion(device):
+@pytest.mark.parametrize("n_items", [3000, 120_000])
+def test_hybrid_bf16_mode_matches_f64_fusion(device, n_items):
     """BASELINE c5 numerics: rank-200 ALS factors (kp 256) and d = 256 tower
     vectors in bf16, both score matrices on the bf16 matrix cores, then the
     reference fusion (per-model min-max, 0.2/0.8 weights, stable top-5).
     Checked against the f64 fusion of the bf16-ROUNDED operands: fused
     scores within 1e-4, indices equal wherever the oracle's consecutive
-    top-6 scores are separated by more than 1e-4."""
+    top-6 scores are separated by more than 1e-4. 120k items: the pruned
+    path's per-group bounds and survivor filter over more than the 16,384
+    items below which it scores everything (the path c5 serves)."""
     from src.recommend import ShardedRecommender
 
     rng = np.random.default_rng(21)
-    n_users, n_items, k, kp, d = 40, 3000, 200, 256, 256
+    n_users, k, kp, d = 40, 200, 256, 256
     U = np.zeros((n_users, kp), np.float32)
     U[:, :k] = rng.normal(size=(n_users, k)) / np.sqrt(k)
     V = np.zeros((n_items, kp), np.float32)
@@ -235,6 +262,8 @@ def test_hybrid_bf16_mode_matches_f64_fusion(device):
     rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, k,
                              precision="bf16", V_local=torch.from_numpy(V).to(device))
     gi, gv = rec.recommend(torch.from_numpy(rows).to(device), torch.from_numpy(uv).to(device), False, 5)
+    if n_items > 16384:
+        assert not rec.last_prune.fallback_taken()  # the pruned path itself answered
     als = _bf16_round(U[rows]).astype(np.float64) @ _bf16_round(V).astype(np.float64).T
     tt = _bf16_round(uv).astype(np.float64) @ _bf16_round(iv).astype(np.float64).T
 
@@ -251,36 +280,6 @@ def test_hybrid_bf16_mode_matches_f64_fusion(device):
         for j in range(5):
             if (j == 0 or f[j - 1] - f[j] > 1e-4) and f[j] - f[j + 1] > 1e-4:
                 assert gi[b, j] == order[b, j], (b, j)
-
-
-@pytest.mark.parametrize("n_users,n_items,k,d,B,wins", [(40, 3000, 200, 256, 8, False), (300, 40000, 50, 64, 130, True),
-                                                       (64, 70001, 120, 100, 33, False)])
-def test_hybrid_fused_equals_unfused(device, n_users, n_items, k, d, B, wins):
-    """The fused hybrid kernels (hrec_hybrid_minmax + hrec_hybrid_topk: no
-    score matrix written) return exactly what the unfused bf16 path (two
-    hrec_dot_scores + hrec_rows_minmax + hrec_fuse_rows_topk) returns — same
-    MFMA k order, same fusion arithmetic — incl. the sample-bound filter
-    (n_items > 16384), a user count that is not a multiple of the 128-user
-    block and widths padded to one dk."""
-    from src.recommend import ShardedRecommender
-
-    rng = np.random.default_rng(n_items)
-    kp = 256 if k > 128 else (128 if k > 64 else 64)
-    U = np.zeros((n_users, kp), np.float32)
-    U[:, :k] = rng.normal(size=(n_users, k)) / np.sqrt(k)
-    V = np.zeros((n_items, kp), np.float32)
-    V[:, :k] = rng.normal(size=(n_items, k)) / np.sqrt(k)
-    iv = (rng.normal(size=(n_items, d)) / 8).astype(np.float32)
-    uv = (rng.normal(size=(B, d)) / 8).astype(np.float32)
-    rows = torch.as_tensor(rng.integers(0, n_users, B), dtype=torch.int64, device=device)
-    rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, k,
-                             precision="bf16", V_local=torch.from_numpy(V).to(device), fused=True)
-    assert rec.fused
-    fi, fv = rec.recommend(rows, torch.from_numpy(uv).to(device), wins, 7)
-    rec.fused = False
-    ui, uv_ = rec.recommend(rows, torch.from_numpy(uv).to(device), wins, 7)
-    np.testing.assert_array_equal(fi.cpu().numpy(), ui.cpu().numpy())
-    np.testing.assert_array_equal(fv.cpu().numpy(), uv_.cpu().numpy())
 
 
 @pytest.mark.parametrize("dk,B,N,ka,kt", [(256, 256, 100_003, 256, 256), (256, 300, 1000, 200, 250),
@@ -332,31 +331,6 @@ def test_hybrid_scores_empty_catalogue(device):
     v = torch.empty((0, 64), dtype=torch.bfloat16, device=device)
     als, tt, a_mm, t_mm = h.hybrid_scores(U, torch.arange(4, device=device), U, v, v)
     assert als.shape == (4, 0) and torch.all(a_mm[0] == float("inf")) and torch.all(t_mm[1] == -float("inf"))
-
-
-def test_hybrid_fused_minmax_and_overflow(device):
-    """hrec_hybrid_minmax == hrec_rows_minmax of the two score matrices; a
-    catalogue of identical items (every fused score ties) overflows the
-    survivor list and the recommender falls back to the exact unfused path."""
-    h = _h()
-    from src.recommend import ShardedRecommender
-
-    rng = np.random.default_rng(5)
-    ua = h.dot_operand(torch.from_numpy(_vecs(70, 128, 1)).to(device), torch.bfloat16)
-    ut = h.dot_operand(torch.from_numpy(_vecs(70, 128, 2)).to(device), torch.bfloat16)
-    va = h.dot_operand(torch.from_numpy(_vecs(20001, 128, 3)).to(device), torch.bfloat16)
-    vt = h.dot_operand(torch.from_numpy(_vecs(20001, 128, 4)).to(device), torch.bfloat16)
-    a_mm, t_mm = h.hybrid_minmax(ua, ut, va, vt)
-    np.testing.assert_array_equal(a_mm.cpu().numpy(), h.rows_minmax(h.dot_scores(ua, va)).cpu().numpy())
-    np.testing.assert_array_equal(t_mm.cpu().numpy(), h.rows_minmax(h.dot_scores(ut, vt)).cpu().numpy())
-    V = np.tile(rng.normal(size=(1, 64)).astype(np.float32), (30000, 1))
-    iv = np.tile(rng.normal(size=(1, 64)).astype(np.float32), (30000, 1))
-    U = rng.normal(size=(10, 64)).astype(np.float32)
-    rec = ShardedRecommender(torch.from_numpy(U).to(device), None, torch.from_numpy(iv).to(device), 0, 64,
-                             precision="bf16", V_local=torch.from_numpy(V).to(device), fused=True)
-    rows = torch.arange(4, dtype=torch.int64, device=device)
-    i, v = rec.recommend(rows, torch.from_numpy(U[:4]).to(device), False, 5)
-    np.testing.assert_array_equal(i.cpu().numpy(), np.tile(np.arange(5), (4, 1)))
 
 
 @pytest.mark.parametrize("precision", ["exact", "bf16"])
@@ -455,8 +429,8 @@ def test_hybrid_prune_fallback_cases(device):
 
 
 def test_recommender_bf16_paths_agree(device):
-    """ShardedRecommender precision "bf16": pruned (default), unfused
-    (pruned=False) and K9f (fused=True) return the same ids and scores."""
+    """ShardedRecommender precision "bf16": pruned (default) and unfused
+    (pruned=False) return the same ids and scores."""
     from src.recommend import ShardedRecommender
 
     rng = np.random.default_rng(44)
@@ -467,7 +441,7 @@ def test_recommender_bf16_paths_agree(device):
     uv = torch.as_tensor(rng.normal(size=(B, d)).astype(np.float32), device=device)
     rows = torch.as_tensor(rng.choice(n_users, B, replace=False), device=device)
     recs = [ShardedRecommender(U, None, iv, 0, k, precision="bf16", V_local=V, **kw)
-            for kw in ({}, {"pruned": False}, {"fused": True})]
+            for kw in ({}, {"pruned": False})]
     for wins in (True, False):
         outs = [r.recommend(rows, uv, wins, 5) for r in recs]
         for i, v in outs[1:]:

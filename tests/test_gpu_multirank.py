@@ -15,8 +15,9 @@ over the whole item set:
   * "small": rank 0 holds 3 items and top_k = 5 exceeds that shard;
   * "empty": rank 1 holds no items.
 Precisions: ShardedRecommender "exact" (JVM-exact ALS + f32 Dot), "bf16"
-(one-launch hrec_hybrid_scores) and "bf16" fused (hrec_hybrid_minmax /
-hrec_hybrid_topk); ShardedScorer (hrec_dot_topk) on f32 and bf16 operands.
+pruned (hrec_hybrid_prune_minmax / _topk; top_k > 8: hrec_hybrid_scores) and
+"bf16" unfused (hrec_hybrid_scores + hrec_fuse_rows_topk); ShardedScorer
+(hrec_dot_topk) on f32 and bf16 operands.
 """
 import os
 import socket
@@ -28,7 +29,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 N_USERS, N_ITEMS, K, KP, D, B = 300, 5000, 32, 32, 24, 40
-CONFIGS = [("exact", False), ("bf16", False), ("bf16", True)]
+CONFIGS = [("exact", "plain", {}), ("bf16", "pruned", {}), ("bf16", "unfused", {"pruned": False})]
 
 
 def make_data(split):
@@ -65,13 +66,12 @@ def run_shard(U, V, uvec, ivec, rows, lo, hi, world, rank, group, top_k):
     V_loc, iv_loc = T(V[lo:hi]), T(ivec[lo:hi])
     Vt_loc = _hrec.transpose(V_loc) if hi > lo else V_loc.t().contiguous()
     out = {}
-    for prec, fused in CONFIGS:
+    for prec, tag, kw in CONFIGS:
         rec = ShardedRecommender(dU, Vt_loc, iv_loc, lo, K, world=world, rank=rank, group=group,
-                                 precision=prec, V_local=V_loc if prec == "bf16" else None, fused=fused)
+                                 precision=prec, V_local=V_loc if prec == "bf16" else None, **kw)
         for als_wins in (True, False):
             idx, val = rec.recommend(drows, duvec, als_wins, top_k)
-            out[f"rec_{prec}_{'fused' if fused else 'plain'}_{als_wins}"] = (idx.cpu().numpy(),
-                                                                           val.double().cpu().numpy())
+            out[f"rec_{prec}_{tag}_{als_wins}"] = (idx.cpu().numpy(), val.double().cpu().numpy())
     for dt in (torch.float32, torch.bfloat16):
         iv_op = _hrec.dot_operand(iv_loc, dt, 32) if hi > lo else torch.zeros((0, 32), dtype=dt, device=dev)
         sc = ShardedScorer(iv_op, lo, world=world, rank=rank, group=group)
@@ -130,3 +130,75 @@ def test_two_ranks_match_one_rank(device, case, split, top_k):
             i_got, v_got = res[r][name]
             np.testing.assert_array_equal(i_got, i_ref, err_msg=f"{case} {name} rank {r}")
             np.testing.assert_array_equal(v_got, v_ref, err_msg=f"{case} {name} rank {r}")
+
+
+# ------------------------------------------- ALSModel.train under torchrun
+def _als_frame():
+    """A power-law frame (skewed degrees: the nnz-balanced shards differ
+    from equal-count ones), duplicates kept, non-contiguous raw ids."""
+    import pandas as pd
+
+    rng = np.random.default_rng(77)
+    n_u, n_i, nnz = 1500, 900, 40_000
+    pu = 1 / (np.arange(n_u) + 1.0) ** 0.6
+    pi = 1 / (np.arange(n_i) + 1.0) ** 0.6
+    u = rng.choice(n_u, nnz, p=pu / pu.sum()) * 3 + 11
+    i = rng.choice(n_i, nnz, p=pi / pi.sum()) * 7 + 5
+    return pd.DataFrame({"userId": u, "itemId": i, "average_review_rating": rng.integers(0, 19, nnz),
+                         "manufacturer_id": 0, "category_id": 0, "price": 1.0})
+
+
+def _als_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.als_model import ALSModel
+
+        m = ALSModel(rank=24, max_iter=4, reg_param=0.1, seed=9)
+        assert m.train(_als_frame()) is True
+        s = m.predict_for_user(int(m.model.user_ids[5]), [int(x) for x in m.model.item_ids[:50]])
+        q.put((rank, (m.model.U.cpu().numpy(), m.model.V.cpu().numpy(), [v for _, v in s])))
+        dist.barrier()
+    except BaseException as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_als_model_train_two_ranks_matches_one(device):
+    """ALSModel.train under an initialised 2-rank world (the
+    reference's caller under torchrun, src/als_model.py:43-66) shards users
+    and items (nnz-balanced parts, 4 user chunks per rank, chunked
+    all-gathers through the HIP half-sweeps) and every rank ends with the
+    factors of the one-rank fit, bit for bit; predict_for_user serves the
+    same scores on every rank."""
+    import torch.multiprocessing as mp
+
+    from src.als_model import ALSModel
+
+    m = ALSModel(rank=24, max_iter=4, reg_param=0.1, seed=9)
+    assert m.train(_als_frame()) is True
+    U1, V1 = m.model.U.cpu().numpy(), m.model.V.cpu().numpy()
+    s1 = [v for _, v in m.predict_for_user(int(m.model.user_ids[5]), [int(x) for x in m.model.item_ids[:50]])]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_als_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert not isinstance(res[r], str), res[r]
+        assert procs[r].exitcode == 0
+        U, V, sc = res[r]
+        np.testing.assert_array_equal(U, U1)
+        np.testing.assert_array_equal(V, V1)
+        assert sc == s1
