@@ -128,6 +128,15 @@ int hs_slice_tiles(int dk);  // item tiles of 16 per wave slice (a slice = 16 * 
 int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr,
                    int thr_stride, int64_t thr_per, int cap, float* cv, int64_t* ci, int* cn, hipStream_t s);
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s);
+// csrc/dot_gemv.hip: the few-user (B <= 4) streaming scoring kernel, same
+// contract as the matrix-core launch of csrc/dot_topk.hip (FILTER: the
+// per-user survivor filter, thr_per == 0) — HREC_DOT_GEMV=0 turns it off.
+bool dot_gemv_applies(int B, int64_t step, int dk, int bf16);
+template <bool FILTER>
+int dot_gemv_run(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk, int bf16,
+                 float* out,
+                 int64_t ldo, const float* thr, int thr_stride, int cap, float* cv, int64_t* ci, int* cn, int64_t off,
+                 hipStream_t s);
 // csrc/score.hip: hrec_fuse_rows_topk's exact segment path, gated on *gate.
 size_t fuse_rows_exact_ws_bytes(int64_t n_rows, int64_t n, int kk);
 int fuse_rows_exact(const float* als, const float* tt, int64_t n_rows, int64_t n, int64_t ld, const float* als_mm,

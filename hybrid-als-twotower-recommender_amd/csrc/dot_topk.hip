@@ -761,6 +761,9 @@ template <bool FILTER>
 static int dot_launch(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
                       int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
                       int64_t* ci, int* cn, int64_t off, hipStream_t s) {
+  if (dot_gemv_applies(B, step, dk, bf16))  // a few users: the streaming GEMV kernel (csrc/dot_gemv.hip)
+    return dot_gemv_run<FILTER>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap, cv, ci, cn,
+                                off, s);
   const int choice = dot_tiling_choice();
   if (choice == 2 && (bf16 || dk <= 128))
     return dot_launch_res<FILTER>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap, cv, ci,

@@ -65,6 +65,33 @@ def test_dot_scores_vs_f64(device, dtype, B, N, d):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,d", [(1, 32), (1, 64), (1, 128), (1, 256), (2, 50), (2, 128), (3, 32), (4, 64)])
+def test_few_user_scores_and_topk(device, dtype, B, d):
+    """K8v (csrc/dot_gemv.hip: B <= 4 users, the reference's one-user call
+    shape; the streaming GEMV where its per-lane partials fit, the matrix-core
+    kernel otherwise): scores within the f32 bound of the f64 dot on a ragged
+    catalogue (not a multiple of the 64-row tile), and the sampled-bound top-k
+    (N > 16384) bit-exact against the same path's full score matrix."""
+    h = _h()
+    N = 70_001
+    U = _vecs(B, d, 40 + B)
+    V = _vecs(N, d, 41)
+    Ud = h.dot_operand(torch.from_numpy(U).to(device), dtype)
+    Vd = h.dot_operand(torch.from_numpy(V).to(device), dtype)
+    got = h.dot_scores(Ud, Vd).cpu().numpy()
+    if dtype == torch.bfloat16:
+        U, V = _bf16_round(U), _bf16_round(V)
+    ref = U.astype(np.float64) @ V.astype(np.float64).T
+    bound = 1e-6 * (np.abs(U).astype(np.float64) @ np.abs(V).astype(np.float64).T) + 1e-30
+    assert np.all(np.abs(got - ref) <= bound), np.max(np.abs(got - ref) / bound)
+    for k in (1, 5, 64):
+        ei, ev = _stable_topk(got, k)
+        gi, gv = h.dot_topk(Ud, Vd, k)
+        np.testing.assert_array_equal(gi.cpu().numpy(), ei)
+        np.testing.assert_array_equal(gv.cpu().numpy(), ev)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,N,d,k", [(7, 5000, 64, 5), (130, 40000, 128, 5), (3, 100003, 64, 10),
                                      (1, 20000, 256, 1), (200, 17000, 32, 64), (2, 3, 64, 5)])
 def test_dot_topk_bit_exact_vs_full_scores(device, dtype, B, N, d, k):
