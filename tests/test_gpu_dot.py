@@ -39,6 +39,17 @@ def _bf16_round(x):
     return r.astype(np.uint32).view(np.float32)
 
 
+def _mfma_scores(h, U, V):
+    """hrec_dot_scores on the matrix cores whatever the batch size: B <= 4
+    users take the streaming GEMV (another f32 summation order), so the batch
+    is padded to 5 rows and the extra rows dropped."""
+    B = U.shape[0]
+    if B > 4:
+        return h.dot_scores(U, V)
+    pad = torch.zeros((5 - B, U.shape[1]), dtype=U.dtype, device=U.device)
+    return h.dot_scores(torch.cat([U, pad]).contiguous(), V)[:B].contiguous()
+
+
 def _stable_topk(scores, k):
     """Python's sorted(..., reverse=True)[:k] order on each row: larger first,
     ties -> smaller index."""
@@ -329,7 +340,7 @@ def test_hybrid_scores_equals_dot_scores_and_minmax(device, dk, B, N, ka, kt):
     als, tt, a_mm, t_mm = h.hybrid_scores(U, rows, uv, va, vt)
     ua = h.dot_operand(U.index_select(0, rows), torch.bfloat16, dk)
     ut = h.dot_operand(uv, torch.bfloat16, dk)
-    ref_a, ref_t = h.dot_scores(ua, va), h.dot_scores(ut, vt)
+    ref_a, ref_t = _mfma_scores(h, ua, va), _mfma_scores(h, ut, vt)
     assert torch.equal(als, ref_a) and torch.equal(tt, ref_t)
     assert torch.equal(a_mm, h.rows_minmax(ref_a)) and torch.equal(t_mm, h.rows_minmax(ref_t))
 
@@ -346,7 +357,7 @@ def test_hybrid_scores_unknown_rows_are_nan(device):
     rows = torch.tensor([2, -1, 10, 1 << 40], dtype=torch.int64, device=device)
     als, tt, a_mm, _ = h.hybrid_scores(U, rows, uv, v, v)
     assert torch.isnan(als[1:]).all() and not torch.isnan(als[0]).any()
-    ref = h.dot_scores(h.dot_operand(U[2:3], torch.bfloat16), v)
+    ref = _mfma_scores(h, h.dot_operand(U[2:3], torch.bfloat16), v)
     assert torch.equal(als[0:1], ref)
     assert torch.all(a_mm[0, 1:] == float("inf")) and torch.all(a_mm[1, 1:] == -float("inf"))
     assert not torch.isnan(tt).any()
