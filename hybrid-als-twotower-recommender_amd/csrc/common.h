@@ -137,6 +137,13 @@ int dot_gemv_run(const void* U, int B, const void* V, int64_t n_rows, int64_t n_
                  float* out,
                  int64_t ldo, const float* thr, int thr_stride, int cap, float* cv, int64_t* ci, int* cn, int64_t off,
                  hipStream_t s);
+// csrc/scan.hip: inclusive / exclusive prefix sums (any n; workspace
+// scan_ws_bytes(n)) and the extremes of an int64 column (out[0] = min,
+// out[1] = max, device).
+size_t scan_ws_bytes(int64_t n);
+template <typename T>
+int scan_run(const T* in, T* out, int64_t n, bool exclusive, void* ws, hipStream_t s);
+int minmax_i64_run(const int64_t* x, int64_t n, int64_t* out, hipStream_t s);
 // csrc/score.hip: hrec_fuse_rows_topk's exact segment path, gated on *gate.
 size_t fuse_rows_exact_ws_bytes(int64_t n_rows, int64_t n, int kk);
 int fuse_rows_exact(const float* als, const float* tt, int64_t n_rows, int64_t n, int64_t ld, const float* als_mm,

@@ -26,7 +26,8 @@ __global__ __launch_bounds__(256) void iota_i32_kernel(int32_t* __restrict__ out
     out[i] = (int32_t)i;
 }
 
-// keys32[i] = ids[i] - lo (caller guarantees lo <= ids <= hi, hi - lo < 2^31)
+// keys32[i] = ids[i] - lo as 32 unsigned bits (caller guarantees lo <= ids <= hi,
+// hi - lo < 2^32)
 __global__ __launch_bounds__(256) void shift_keys_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
                                                          int32_t* __restrict__ keys32) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void scatter_codes_kernel(const K* __restrict_
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t c = incl[i] - 1;
     codes[pos[i]] = c;
-    if (flag[i]) uniq[c] = (int64_t)keys[i] + lo;
+    if (flag[i]) uniq[c] = (sizeof(K) == 4 ? (int64_t)(uint32_t)keys[i] : (int64_t)keys[i]) + lo;
     if (i == n - 1) *n_uniq = (int64_t)incl[i];
   }
 }
@@ -251,12 +252,6 @@ __global__ __launch_bounds__(256) void uniq_bits_kernel(const uint32_t* __restri
     const uint32_t wd = bits[v >> 5];
     if ((wd >> (v & 31)) & 1u) uniq[pre[v >> 5] + (uint32_t)__popc(wd & ((1u << (v & 31)) - 1u))] = v + lo;
   }
-}
-
-__global__ void minmax_store_kernel(const int64_t* __restrict__ mn, const int64_t* __restrict__ mx,
-                                    int64_t* __restrict__ out) {
-  out[0] = *mn;
-  out[1] = *mx;
 }
 
 // indptr from row-sorted keys: indptr[r] = first i with keys[i] >= r.
@@ -605,28 +600,6 @@ int bits_for(int64_t n_rows) {  // radix bits covering codes 0 .. n_rows-1
   return b;
 }
 
-// Workspace layout of hrec_encode_ids (all 256-B aligned). keys holds the
-// sorted 64-bit keys, or the shifted 32-bit keys and their sorted copy.
-struct EncodeWs {
-  size_t keys, pos, pos2, flag, incl, temp, total;
-  explicit EncodeWs(int64_t n) {
-    size_t sort_tmp = 0, sort32_tmp = 0, scan_tmp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const int64_t*)nullptr, (int64_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort32_tmp, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, scan_tmp, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-    if (sort32_tmp > sort_tmp) sort_tmp = sort32_tmp;
-    keys = 0;
-    pos = keys + align256(8 * (size_t)n);
-    pos2 = pos + align256(4 * (size_t)n);
-    flag = pos2 + align256(4 * (size_t)n);
-    incl = flag + align256(4 * (size_t)n);
-    temp = incl + align256(4 * (size_t)n);
-    total = temp + align256(sort_tmp > scan_tmp ? sort_tmp : scan_tmp);
-  }
-};
-
 // CSR build workspace: ping-pong keys / packed (col, rating) entries of the
 // intermediate passes, the (digit, tile) counts and the scan's chunk sums.
 struct CsrWs {
@@ -651,6 +624,88 @@ struct CsrWs {
     total = sums + align256(4 * (size_t)n_chunks);
   }
 };
+
+// The largest CsrWs over every key width (1 .. 32 bits).
+inline size_t csr_ws_max(int64_t n) {
+  size_t m = 0;
+  for (int b = 1; b <= 32; ++b) {
+    const size_t t = CsrWs(n, b).total;
+    m = t > m ? t : m;
+  }
+  return m;
+}
+
+// Workspace layout of hrec_encode_ids (all 256-B aligned): the shifted
+// 32-bit keys (or, for id spans past 2^32, the sorted 64-bit keys), the
+// position columns, the distinct flags and their scan, and a temp region for
+// the key sort (the in-tree radix sort's workspace; hipCUB's 64-bit sort
+// only for spans past 2^32) or the scan.
+struct EncodeWs {
+  size_t keys, pos, pos2, flag, incl, temp, total;
+  explicit EncodeWs(int64_t n) {
+    size_t sort64_tmp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort64_tmp, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+    size_t tmp = csr_ws_max(n) + align256(4 * (size_t)n);  // + the sort's value output
+    if (sort64_tmp > tmp) tmp = sort64_tmp;
+    if (scan_ws_bytes(n) > tmp) tmp = scan_ws_bytes(n);
+    keys = 0;
+    pos = keys + align256(8 * (size_t)n);
+    pos2 = pos + align256(4 * (size_t)n);
+    flag = pos2 + align256(4 * (size_t)n);
+    incl = flag + align256(4 * (size_t)n);
+    temp = incl + align256(4 * (size_t)n);
+    total = temp + align256(tmp);
+  }
+};
+
+// Stable sort of (key, col, val) by the low `bits` bits of the unsigned
+// keys: ceil(bits / 10) LSD passes. idx_out / val_out get the cols / vals in
+// key order; *sorted_keys points at the sorted keys (inside ws).
+int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, int64_t nnz, int bits, void* ws,
+                 int32_t* idx_out, float* val_out, const int32_t** sorted_keys, hipStream_t s) {
+  const CsrWs L(nnz, bits);
+  char* w = static_cast<char*>(ws);
+  int32_t* kbuf[2] = {reinterpret_cast<int32_t*>(w + L.ka), reinterpret_cast<int32_t*>(w + L.kb)};
+  uint64_t* pbuf[2] = {reinterpret_cast<uint64_t*>(w + L.pa), reinterpret_cast<uint64_t*>(w + L.pb)};
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
+  uint32_t* sums = reinterpret_cast<uint32_t*>(w + L.sums);
+  const unsigned nt = (unsigned)L.n_tiles;
+  // downsweep: persistent, one block per CU (its tile takes 118 KB of LDS)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const unsigned nd = (unsigned)(L.n_tiles < cus ? L.n_tiles : cus);
+  const int32_t* kin = keys;
+  const uint64_t* pin = nullptr;
+  int shift = 0;
+  for (int p = 0; p < L.passes; ++p) {
+    const int db = L.digit[p];
+    const int R = 1 << db;
+    const int64_t n_chunks = (L.n_tiles + kScanTiles - 1) / kScanTiles;
+    hipLaunchKernelGGL(sort_upsweep_kernel, dim3(nt), dim3(kSortThreads), 0, s, kin, nnz, shift, db, L.n_tiles, cnt);
+    hipLaunchKernelGGL(sort_colsum_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
+    hipLaunchKernelGGL(sort_colscan_top_kernel, dim3(1), dim3(1024), 0, s, sums, n_chunks, R);
+    hipLaunchKernelGGL(sort_colscan_apply_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
+    const bool first = p == 0, last = p == L.passes - 1;
+    int32_t* kout = kbuf[p & 1];
+    uint64_t* pout = pbuf[p & 1];
+#define HREC_DOWN(F, LST)                                                                                        \
+  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nd), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
+                     shift, db, L.n_tiles, cnt, kout, pout, idx_out, val_out)
+    if (first && last) HREC_DOWN(true, true);
+    else if (first) HREC_DOWN(true, false);
+    else if (last) HREC_DOWN(false, true);
+    else HREC_DOWN(false, false);
+#undef HREC_DOWN
+    const int rc = check_launch("radix sort pass");
+    if (rc) return rc;
+    kin = kout;
+    pin = pout;
+    shift += db;
+  }
+  *sorted_keys = kin;
+  return HREC_OK;
+}
 
 }  // namespace hrec
 
@@ -684,7 +739,8 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
   const unsigned g = grid_for(n);
   // A narrow id range sorts (id - lo) on only the bits it spans.
   const bool narrow = (uint64_t)id_hi - (uint64_t)id_lo < 0x7fffffffull;
-  const int64_t span = narrow ? (int64_t)((uint64_t)id_hi - (uint64_t)id_lo) + 1 : 0;
+  const bool span32 = (uint64_t)id_hi - (uint64_t)id_lo <= 0xffffffffull;
+  const int64_t span = span32 ? (int64_t)((uint64_t)id_hi - (uint64_t)id_lo) + 1 : 0;
   if (narrow && span <= n && span <= kBitsSpan) {
     // small dense range: LDS bitmaps (flag holds the bits, incl the word prefixes)
     const int nw = (int)((span + 31) >> 5);
@@ -706,65 +762,53 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
     if (hipMemsetAsync(flag, 0, (size_t)span * sizeof(int32_t), s) != hipSuccess)
       return check_launch("encode_ids: memset");
     hipLaunchKernelGGL(mark_present_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, flag);
-    if (hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, flag, incl, (int)span, s) != hipSuccess)
-      return check_launch("encode_ids: scan");
+    const int rc = scan_run<int32_t>(flag, incl, span, false, temp, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(codes_from_rank_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, incl, codes);
     hipLaunchKernelGGL(uniq_from_rank_kernel, dim3(grid_for(span)), dim3(256), 0, s, flag, incl, span, id_lo, uniq,
                        n_uniq);
     return check_launch("encode_ids: dense");
   }
   hipLaunchKernelGGL(iota_i32_kernel, dim3(g), dim3(256), 0, s, pos, n);
-  if (narrow) {
+  if (span32) {
+    // (id - lo) as 32-bit keys, sorted with their positions by the in-tree
+    // stable radix sort on the bits the span needs
     int32_t* k32 = reinterpret_cast<int32_t*>(w + L.keys);
-    int32_t* k32s = k32 + n;
-    const int bits = bits_for((int64_t)((uint64_t)id_hi - (uint64_t)id_lo) + 1);
+    const int bits = span > ((int64_t)1 << 31) ? 32 : bits_for(span);
     hipLaunchKernelGGL(shift_keys_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, k32);
-    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k32, k32s, pos, pos2, (int)n, 0, bits, s) != hipSuccess)
-      return check_launch("encode_ids: radix sort");
+    float* vdummy = reinterpret_cast<float*>(static_cast<char*>(temp) + csr_ws_max(n));
+    const int32_t* k32s = nullptr;
+    int rc = csr_sort_run(k32, pos, reinterpret_cast<const float*>(pos), n, bits, temp, pos2, vdummy, &k32s, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(distinct_flags_kernel<int32_t>, dim3(g), dim3(256), 0, s, k32s, n, flag);
-    temp_bytes = L.total - L.temp;
-    if (hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, flag, incl, (int)n, s) != hipSuccess)
-      return check_launch("encode_ids: scan");
+    rc = scan_run<int32_t>(flag, incl, n, false, temp, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(scatter_codes_kernel<int32_t>, dim3(g), dim3(256), 0, s, k32s, id_lo, pos2, flag, incl, n,
                        codes, uniq, n_uniq);
   } else {
+    // ids spanning more than 2^32 (only through the C-ABI: the drop-in API's
+    // ids are Spark Ints): hipCUB's 64-bit key sort
     int64_t* keys = reinterpret_cast<int64_t*>(w + L.keys);
     if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, ids, keys, pos, pos2, (int)n, 0, 64, s) != hipSuccess)
       return check_launch("encode_ids: radix sort");
     hipLaunchKernelGGL(distinct_flags_kernel<int64_t>, dim3(g), dim3(256), 0, s, keys, n, flag);
-    temp_bytes = L.total - L.temp;
-    if (hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, flag, incl, (int)n, s) != hipSuccess)
-      return check_launch("encode_ids: scan");
+    const int rc = scan_run<int32_t>(flag, incl, n, false, temp, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(scatter_codes_kernel<int64_t>, dim3(g), dim3(256), 0, s, keys, (int64_t)0, pos2, flag, incl,
                        n, codes, uniq, n_uniq);
   }
   return check_launch("encode_ids");
 }
 
-extern "C" size_t hrec_minmax_i64_workspace_bytes(int64_t n) {
-  if (n <= 0 || n >= 0x7fffffffll) return 0;
-  size_t a = 0, b = 0;
-  (void)hipcub::DeviceReduce::Min(nullptr, a, (const int64_t*)nullptr, (int64_t*)nullptr, (int)n);
-  (void)hipcub::DeviceReduce::Max(nullptr, b, (const int64_t*)nullptr, (int64_t*)nullptr, (int)n);
-  return 512 + align256(a > b ? a : b);
-}
+extern "C" size_t hrec_minmax_i64_workspace_bytes(int64_t n) { return n > 0 ? 256 : 0; }
 
 extern "C" int hrec_minmax_i64(const int64_t* x, int64_t n, int64_t* out, void* ws, size_t ws_bytes,
                                void* stream) {
-  HREC_REQUIRE(n > 0 && n < 0x7fffffffll, "minmax_i64: n=%lld out of range [1, 2^31-1)", (long long)n);
-  HREC_REQUIRE(x && out && ws, "minmax_i64: null pointer");
-  const size_t need = hrec_minmax_i64_workspace_bytes(n);
-  HREC_REQUIRE(ws_bytes >= need, "minmax_i64: workspace %zu < %zu bytes", ws_bytes, need);
-  hipStream_t s = as_stream(stream);
-  char* w = static_cast<char*>(ws);
-  int64_t* mn = reinterpret_cast<int64_t*>(w);
-  int64_t* mx = reinterpret_cast<int64_t*>(w + 256);
-  size_t tb = need - 512;
-  if (hipcub::DeviceReduce::Min(w + 512, tb, x, mn, (int)n, s) != hipSuccess) return check_launch("minmax_i64: min");
-  tb = need - 512;
-  if (hipcub::DeviceReduce::Max(w + 512, tb, x, mx, (int)n, s) != hipSuccess) return check_launch("minmax_i64: max");
-  hipLaunchKernelGGL(minmax_store_kernel, dim3(1), dim3(1), 0, s, mn, mx, out);
-  return check_launch("minmax_i64");
+  HREC_REQUIRE(n > 0, "minmax_i64: n=%lld must be >= 1", (long long)n);
+  HREC_REQUIRE(x && out, "minmax_i64: null pointer");
+  (void)ws;
+  (void)ws_bytes;  // no workspace needed (kept in the signature: ABI)
+  return minmax_i64_run(x, n, out, as_stream(stream));
 }
 
 extern "C" size_t hrec_coo_to_csr_workspace_bytes(int64_t nnz, int64_t n_rows) {
@@ -789,44 +833,9 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   const int bits = bits_for(n_rows);
   const CsrWs L(nnz, bits);
   HREC_REQUIRE(ws_bytes >= L.total, "coo_to_csr: workspace %zu < %zu bytes", ws_bytes, L.total);
-  char* w = static_cast<char*>(ws);
-  int32_t* kbuf[2] = {reinterpret_cast<int32_t*>(w + L.ka), reinterpret_cast<int32_t*>(w + L.kb)};
-  uint64_t* pbuf[2] = {reinterpret_cast<uint64_t*>(w + L.pa), reinterpret_cast<uint64_t*>(w + L.pb)};
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
-  uint32_t* sums = reinterpret_cast<uint32_t*>(w + L.sums);
-  const unsigned nt = (unsigned)L.n_tiles;
-  // downsweep: persistent, one block per CU (its tile takes 118 KB of LDS)
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const unsigned nd = (unsigned)(L.n_tiles < cus ? L.n_tiles : cus);
-  const int32_t* kin = rows;
-  const uint64_t* pin = nullptr;
-  int shift = 0;
-  for (int p = 0; p < L.passes; ++p) {
-    const int db = L.digit[p];
-    const int R = 1 << db;
-    const int64_t n_chunks = (L.n_tiles + kScanTiles - 1) / kScanTiles;
-    hipLaunchKernelGGL(sort_upsweep_kernel, dim3(nt), dim3(kSortThreads), 0, s, kin, nnz, shift, db, L.n_tiles, cnt);
-    hipLaunchKernelGGL(sort_colsum_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
-    hipLaunchKernelGGL(sort_colscan_top_kernel, dim3(1), dim3(1024), 0, s, sums, n_chunks, R);
-    hipLaunchKernelGGL(sort_colscan_apply_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
-    const bool first = p == 0, last = p == L.passes - 1;
-    int32_t* kout = kbuf[p & 1];
-    uint64_t* pout = pbuf[p & 1];
-#define HREC_DOWN(F, LST)                                                                                        \
-  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nd), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
-                     shift, db, L.n_tiles, cnt, kout, pout, indices, values)
-    if (first && last) HREC_DOWN(true, true);
-    else if (first) HREC_DOWN(true, false);
-    else if (last) HREC_DOWN(false, true);
-    else HREC_DOWN(false, false);
-#undef HREC_DOWN
-    const int rc = check_launch("coo_to_csr: radix pass");
-    if (rc) return rc;
-    kin = kout;
-    pin = pout;
-    shift += db;
-  }
+  const int32_t* kin = nullptr;
+  int rc = csr_sort_run(rows, cols, vals, nnz, bits, ws, indices, values, &kin, s);
+  if (rc) return rc;
   hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz / 4 + 1)), dim3(256), 0, s, kin, nnz, n_rows,
                      indptr);
   return check_launch("coo_to_csr");

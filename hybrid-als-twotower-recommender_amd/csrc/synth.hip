@@ -1,8 +1,6 @@
 // K10: synthetic interaction matrix (CSR / CSC shards) and ALS initial
 // factors, generated on the device from counter-based hashes so that any
 // shard layout (and the CPU oracle) sees bit-identical data.
-#include <hipcub/hipcub.hpp>
-
 #include "common.h"
 
 namespace hrec {
@@ -132,32 +130,19 @@ extern "C" int hrec_synth_fill(uint64_t seed, uint64_t seed2, uint64_t threshold
   return check_launch("synth_fill_kernel");
 }
 
-extern "C" size_t hrec_scan_workspace_bytes(int64_t n) {
-  size_t bytes = 0;
-  if (n <= 0) return 16;
-  if (hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int)n) !=
-      hipSuccess)
-    return 0;
-  return bytes + 16;
-}
+extern "C" size_t hrec_scan_workspace_bytes(int64_t n) { return scan_ws_bytes(n); }
 
 extern "C" int hrec_exclusive_scan_i64(const int64_t* counts, int64_t n, int64_t* out, void* workspace,
                                        size_t workspace_bytes, void* stream) {
-  HREC_REQUIRE(n >= 0 && n < 0x7fffffffll, "exclusive_scan: n out of range");
+  HREC_REQUIRE(n >= 0, "exclusive_scan: n out of range");
   HREC_REQUIRE(out != nullptr, "exclusive_scan: null out");
   hipStream_t s = as_stream(stream);
   if (hipMemsetAsync(out, 0, sizeof(int64_t), s) != hipSuccess) return check_launch("scan memset");
   if (n == 0) return HREC_OK;
   HREC_REQUIRE(counts && workspace, "exclusive_scan: null pointer");
-  size_t need = hrec_scan_workspace_bytes(n);
+  const size_t need = hrec_scan_workspace_bytes(n);
   HREC_REQUIRE(workspace_bytes >= need, "exclusive_scan: workspace %zu < %zu", workspace_bytes, need);
-  size_t bytes = workspace_bytes;
-  hipError_t e = hipcub::DeviceScan::InclusiveSum(workspace, bytes, counts, out + 1, (int)n, s);
-  if (e != hipSuccess) {
-    set_error("exclusive_scan: %s", hipGetErrorString(e));
-    return HREC_E_LAUNCH;
-  }
-  return check_launch("exclusive_scan");
+  return scan_run<int64_t>(counts, out + 1, n, false, workspace, s);
 }
 
 extern "C" int hrec_als_init_factors(uint64_t seed, int64_t row_begin, int64_t n_rows, int k, int kp,

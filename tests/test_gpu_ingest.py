@@ -125,3 +125,24 @@ def test_synthetic_csc_from_csr_via_ingest(device):
     urow = torch.repeat_interleave(torch.arange(n_u, dtype=torch.int32), counts).to(device)
     ip, ix, v = h.coo_to_csr(csr.indices, urow, csr.values, n_i)
     assert torch.equal(ip, csc.indptr) and torch.equal(ix, csc.indices) and torch.equal(v, csc.values)
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 1_000_003, 5_000_000])
+def test_exclusive_scan_matches_cumsum(device, n):
+    """The in-tree reduce-then-scan (csrc/scan.hip: tile sums, one block over
+    the sums, tile scans from their offsets) behind the generator's indptr:
+    exact int64 prefix sums at tile boundaries and across many tiles."""
+    h = _hrec()
+    rng = np.random.default_rng(n)
+    c = rng.integers(0, 1 << 40, n, dtype=np.int64)
+    got = h.exclusive_scan(torch.as_tensor(c, device=device)).cpu().numpy()
+    np.testing.assert_array_equal(got, np.concatenate([[0], np.cumsum(c)]))
+
+
+def test_minmax_extremes(device):
+    h = _hrec()
+    x = np.array([5, -(2 ** 63), 2 ** 63 - 1, 0], np.int64)
+    assert h.minmax_i64(torch.as_tensor(x, device=device)) == (-(2 ** 63), 2 ** 63 - 1)
+    y = np.full(3_000_001, 7, np.int64)
+    y[2_999_999] = -1
+    assert h.minmax_i64(torch.as_tensor(y, device=device)) == (-1, 7)
