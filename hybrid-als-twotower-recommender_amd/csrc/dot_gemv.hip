@@ -70,6 +70,9 @@ __device__ __forceinline__ void gemv_unpack(const int4 v, float* x) {
 #ifndef HREC_GEMV_WAVES
 #define HREC_GEMV_WAVES 4
 #endif
+#ifndef HREC_GEMV_AUX
+#define HREC_GEMV_AUX 2  // cache-policy bits of the item loads: non-temporal (the operand streams once)
+#endif
 constexpr int kGemvBatch = HREC_GEMV_BATCH;
 
 typedef int gemv_v4i __attribute__((ext_vector_type(4)));
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(kGemvThreads, HREC_GEMV_WAVES) void dot_gemv_kernel
     for (int t0 = 0; t0 < L; t0 += T) {
       gemv_v4i raw[T];
 #pragma unroll
-      for (int q = 0; q < T; ++q) raw[q] = gemv_raw_load(rs, lane_off + (uint32_t)(t0 + q) * load_step, 0, 0);
+      for (int q = 0; q < T; ++q) raw[q] = gemv_raw_load(rs, lane_off + (uint32_t)(t0 + q) * load_step, 0, HREC_GEMV_AUX);
 #pragma unroll
       for (int q = 0; q < T; ++q) {
         float x[E];
@@ -256,11 +259,17 @@ static bool gemv_fits_rt(int nb, int dk, int bf16) {
   return nb * L <= 32;
 }
 
+// Measured on the c4 one-user call (50M x 128, scripts/gpu_gemv_ab.sh): f32
+// 6.15 ms on the matrix cores (16x16x4 f32 tiles, 15 of 16 users empty) ->
+// 3.95 ms here (non-temporal loads; 4.35 cached); bf16 2.23 ms on the matrix
+// cores vs 2.29-2.59 here, so bf16 operands keep the matrix-core path.
+// HREC_DOT_GEMV=0 turns the kernel off, =2 also takes bf16 operands.
 bool dot_gemv_applies(int B, int64_t step, int dk, int bf16) {
-  static const bool on = [] {
+  static const int mode = [] {
     const char* e = getenv("HREC_DOT_GEMV");
-    return !(e && atoi(e) == 0);
+    return e ? atoi(e) : 1;
   }();
+  const bool on = mode == 2 || (mode == 1 && !bf16);
   // a tile's 64 rows x step must stay within one 32-bit buffer offset
   const int64_t tile_bytes = 64 * step * (int64_t)dk * (bf16 ? 2 : 4);
   return on && B >= 1 && B <= kGemvMaxB && gemv_fits_rt(gemv_nb(B), dk, bf16) && tile_bytes < ((int64_t)1 << 32);
