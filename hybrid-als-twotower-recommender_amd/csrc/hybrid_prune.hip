@@ -7,10 +7,11 @@
 // The fusion needs each user's min / max of BOTH score rows before any fused
 // score exists, so the scores are computed twice, the second time for one
 // model only:
-//   phase 1 (hrec_hybrid_prune_minmax): the user rows gathered + converted to
-//     bf16 operands once; both GEMMs (hyb_scores_kernel, mode HS_PRUNE: no
-//     stores) -> per-user min / max of both rows, and per item group (block)
-//     both models' group maxima + the 16-NI item slice holding the heavy one;
+//   phase 1 (hrec_hybrid_prune_minmax): both GEMMs (hyb_scores_kernel, mode
+//     HS_PRUNE: no stores; every block gathers + converts its users to bf16,
+//     the item group 0 blocks also leave those operands for phase 2) -> per-
+//     user min / max of both rows, and per item group (block) both models'
+//     group maxima + the 16-NI item slice holding the heavy one;
 //   [the caller all-reduces the min / max across item shards (C2)]
 //   phase 2 (hrec_hybrid_prune_topk), three launches:
 //     a. bound: per user, the slices of the 16 groups with the largest maxima
@@ -21,8 +22,9 @@
 //        scaled, hence a raw heavy score >= theta_g (f64, lowered by a
 //        relative margin); +inf where the group's heavy maximum is below it;
 //     b. the heavy model's GEMM alone with the per-group survivor filter
-//        (dot_res_kernel FILTER, K8, survivors staged in LDS per tile): item
-//        ids + exact heavy scores per user;
+//        (hyb_scores_kernel HS_FILTER: one block per item group, so a user's
+//        bound is one LDS value per block; survivors staged in LDS and
+//        flushed once per block): item ids + exact heavy scores per user;
 //     c. each survivor's light score with the same bf16 MFMA k order (A =
 //        the gathered item rows, B = the user row), the fused score with
 //        fuse_rows_kernel's arithmetic (ALS branch f64, two-tower f32, numpy
@@ -36,6 +38,7 @@
 // the same MFMA chain and every fused score the same arithmetic.
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -92,32 +95,6 @@ __device__ __forceinline__ double hp_fuse(const HpScale& s, float a, float t, do
   const double an = (double)a * s.ascale + s.amin_;
   const float tn = t * s.tscale + s.tmin_;
   return w0 * an + w1 * (double)tn;
-}
-
-// 1. bf16 user operands [2][B][dk]: the ALS rows gathered by als_rows (a row
-// outside [0, n_als_rows) reads as NaN, as hyb_scores_kernel stages it) and
-// the two-tower rows, columns >= width zero — hyb_scores_kernel's staging.
-__global__ __launch_bounds__(256) void hp_user_ops_kernel(const float* __restrict__ als_users, int64_t als_ld,
-                                                          const int64_t* __restrict__ als_rows, int64_t n_als_rows,
-                                                          int als_width, const float* __restrict__ tt_users,
-                                                          int64_t tt_ld, int tt_width, int B, int dk,
-                                                          uint16_t* __restrict__ uop) {
-  const int b = blockIdx.x, m = blockIdx.y;
-  const float* src = m ? tt_users : als_users;
-  const int64_t ld = m ? tt_ld : als_ld;
-  const int wd = m ? tt_width : als_width;
-  int64_t row = b;
-  bool bad = false;
-  if (m == 0 && als_rows) {
-    row = als_rows[b];
-    bad = row < 0 || row >= n_als_rows;
-  }
-  uint16_t* out = uop + ((int64_t)m * B + b) * dk;
-  for (int c = threadIdx.x; c < dk; c += blockDim.x) {
-    float v = 0.f;
-    if (c < wd) v = bad ? __builtin_nanf("") : src[row * ld + c];
-    out[c] = (uint16_t)hp_bf16(v);
-  }
 }
 
 // Order of the fused top-k (score.hip's better()): larger first, equal ->
@@ -571,6 +548,16 @@ struct HpWs {
   size_t total;
 };
 
+// HREC_HP_FILTER: 1 (default) = the per-group filter on the phase-1 GEMM
+// (hyb_scores_kernel HS_FILTER), 0 = the K8 resident-user filter.
+static int hp_filter_choice() {
+  static const int v = [] {
+    const char* e = getenv("HREC_HP_FILTER");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static HpWs hp_layout(char* base, int B, int64_t N, int dk, int kk) {
   HpWs w{};
   size_t off = 0;
@@ -635,17 +622,15 @@ extern "C" int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, 
   HREC_REQUIRE(workspace_bytes >= need, "hybrid_prune_minmax: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t s = as_stream(stream);
   const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, 1);
-  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
-                     n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
-  rc = check_launch("hp_user_ops_kernel");
-  if (rc) return rc;
   if (n_items == 0)  // no items: min = +inf, max = -inf (hrec_hybrid_scores of an empty shard)
     return hrec_hybrid_scores(als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users,
                               als_items, tt_items, 0, dk, nullptr, nullptr, 0, als_mm, tt_mm, w.part,
                               (size_t)2 * 2 * n_users * 4 + 256, stream);
+  // the users are gathered + converted by the GEMM launch itself; its item
+  // group 0 blocks leave the bf16 operands for phase 2 (no user-ops launch)
   return hybrid_scores_run(1 /* HS_PRUNE */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
                            tt_width, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, 0, als_mm, tt_mm,
-                           w.part, w.argpos, nullptr, s, w.uop);
+                           w.part, w.argpos, s, nullptr, w.uop);
 }
 
 // Phase 2 launches (a - c). local: the bound kernel reduces the extremes
@@ -681,11 +666,20 @@ static int hp_phase2(bool local, int n_users, const void* als_items, const void*
 #undef HREC_HP_BOUND
   int rc = check_launch("hp_bound_kernel");
   if (rc) return rc;
-  // b. the heavy model's scores, survivors of the per-group bounds
-  const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
-  const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
-  rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
-                      w.cn, s);
+  // b. the heavy model's scores, survivors of the per-group bounds: one
+  //    block per item group (the bound is one LDS value per user), the
+  //    phase-1 GEMM's tiling and k order (the same scores)
+  if (hp_filter_choice() == 1) {
+    const HsFilter f{w.theta, hm, kHpCap, w.cv, w.ci, w.cn};
+    rc = hybrid_scores_run(2 /* HS_FILTER */, nullptr, 0, nullptr, 0, 0, nullptr, 0, 0, n_users, als_items, tt_items,
+                           n_items, dk, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, s, w.uop, nullptr,
+                           &f);
+  } else {  // the K8 resident-user filter (round 3)
+    const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
+    const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
+    rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
+                        w.cn, s);
+  }
   if (rc) return rc;
   // c. light scores + fusion of the survivors, exact top-k; the exact path in
   //    the same block for the users that need it
@@ -745,14 +739,11 @@ extern "C" int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, c
   HREC_REQUIRE(workspace_bytes >= need, "hybrid_prune_local: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t s = as_stream(stream);
   const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, 1);
-  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
-                     n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
-  rc = check_launch("hp_user_ops_kernel");
-  if (rc) return rc;
-  // phase 1 without its min / max reduce launch (the bound kernel folds it)
+  // phase 1 (user gather + conversion inside, operands left for phase 2)
+  // without its min / max reduce launch (the bound kernel folds it)
   rc = hybrid_scores_run(1 /* HS_PRUNE */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
                          tt_width, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, 0, nullptr, nullptr,
-                         w.part, w.argpos, nullptr, s, w.uop);
+                         w.part, w.argpos, s, nullptr, w.uop);
   if (rc) return rc;
   return hp_phase2(true, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, als_mm, tt_mm, als_wins, top_k,
                    idx_offset, out_idx, out_val, workspace, s);

@@ -56,8 +56,17 @@ struct HybScoresArgs {
   int64_t ldo;
   float* part;             // [2][G][2][B]: per-block min / max
   int* argpos;             // HS_PRUNE: [2][G][B] slice of each block's max ((jb / 16) * 4 + g), -1 = none
-  const int* gate;         // HS_GATED: skip the launch while *gate == 0
   const uint16_t* uop;     // optional: the batch's bf16 user operands [2][B][DK] (staged as is)
+  uint16_t* uop_out;       // optional (f32 staging): the blocks of item group 0 also write their
+                           // model's bf16 user operands there ([2][B][DK], row-major)
+  // HS_FILTER: the heavy model hm's scores against per-(user, group) bounds
+  const float* theta;      // [B][G]: a score >= theta survives; +inf / NaN: nothing of the group
+  int hm;
+  int cap;                 // survivor list length per user
+  float* cv;               // [B][cap] survivor scores
+  int64_t* ci;             // [B][cap] survivor item ids
+  int* cn;                 // [B] survivors counted (zeroed by the caller; > cap: the list overflowed)
+  int sbuf;                // HS_FILTER: survivors a block stages in LDS
   int G;                   // item groups per (model, user tile)
   int UB;                  // users per tile (multiple of 64)
   int n_ut;
@@ -73,6 +82,13 @@ struct HybScoresArgs {
 
 constexpr int kHsThreads = 512;
 constexpr int kHsMaxUserBytes = 128 * 1024;
+constexpr size_t kHsMaxLds = 160 * 1024;
+
+// HS_FILTER: LDS bytes before the staged survivors (users, bounds, counts,
+// overflow marks, the staging counter), 16-B aligned
+__host__ __device__ inline size_t hs_filter_head(int UB, int row_b) {
+  return ((size_t)UB * row_b + (size_t)UB * 12 + 4 + 15) & ~(size_t)15;
+}
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN): hrec_f32_to_bf16.
 __device__ __forceinline__ uint32_t hs_bf16(float v) {
@@ -108,16 +124,17 @@ struct HsShape {
 
 // Modes: HS_FULL = score stores + per-block min / max (hrec_hybrid_scores);
 // HS_PRUNE = no stores, min / max + the item slice holding each block's max
-// (pass 1 of the pruned hybrid top-k, csrc/hybrid_prune.hip); HS_GATED =
-// score stores only, skipped unless *gate (that path's exact fallback).
-enum { HS_FULL = 0, HS_PRUNE = 1, HS_GATED = 2 };
+// (pass 1 of the pruned hybrid top-k, csrc/hybrid_prune.hip); HS_FILTER =
+// the heavy model alone, survivors of the per-(user, group) bounds appended
+// to per-user lists (pass 2's filter: one block per item group, so a user's
+// bound is one LDS value per block and its survivors leave in one flush).
+enum { HS_FULL = 0, HS_PRUNE = 1, HS_FILTER = 2 };
 
 // NCH: user chunks of CU = 16 NU users in the tile (compile-time, so the
 // per-lane running min / max of every chunk stays in registers and the last
 // chunk's item refills are unconditional).
 template <int DK, int NCH, int MODE>
 __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a) {
-  if (MODE == HS_GATED && *a.gate == 0) return;  // block-uniform
   using S = HsShape<DK>;
   constexpr int KS = S::KS, NI = S::NI, NU = S::NU, CU = 16 * NU;
   constexpr int kRowB = S::kRowB;
@@ -126,10 +143,21 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   uint32_t* mmk = reinterpret_cast<uint32_t*>(dsm + (size_t)a.UB * kRowB);  // [UB][2]: ~key(min), key(max)
   // HS_PRUNE: [UB] key(max) << 32 | ~slice (ds_max_u64: the larger max, then the earlier slice)
   unsigned long long* amk = reinterpret_cast<unsigned long long*>(dsm + (size_t)a.UB * kRowB + (size_t)a.UB * 8);
+  // HS_FILTER (in place of the two above): [UB] bounds, [UB] survivor counts
+  // (then list bases), [UB] overflow marks, the staging counter, then the
+  // staged survivors (meta = user << 24 | item offset in the group, score,
+  // rank among the user's survivors of the block)
+  float* ths = reinterpret_cast<float*>(dsm + (size_t)a.UB * kRowB);
+  int* cnt_l = reinterpret_cast<int*>(ths + a.UB);
+  int* ovf_l = cnt_l + a.UB;
+  int* bn = ovf_l + a.UB;
+  uint32_t* sb_meta = reinterpret_cast<uint32_t*>(dsm + hs_filter_head(a.UB, kRowB));
+  float* sb_val = reinterpret_cast<float*>(sb_meta + a.sbuf);
+  int* sb_rank = reinterpret_cast<int*>(sb_val + a.sbuf);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int model = blockIdx.x & 1;
-  const int rest = blockIdx.x >> 1;
+  const int model = MODE == HS_FILTER ? a.hm : (blockIdx.x & 1);
+  const int rest = MODE == HS_FILTER ? (int)blockIdx.x : (int)(blockIdx.x >> 1);
   const int ut = rest % a.n_ut, grp = rest / a.n_ut;
   const int64_t per = ((a.N + a.G - 1) / a.G + 15) / 16 * 16;
   const int64_t i0 = (int64_t)grp * per;
@@ -188,9 +216,6 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         *reinterpret_cast<int4*>(us + r * kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v[j];
       }
     }
-    for (int o = threadIdx.x; o < 2 * a.UB; o += kHsThreads) mmk[o] = 0u;
-    if (MODE == HS_PRUNE)
-      for (int o = threadIdx.x; o < a.UB; o += kHsThreads) amk[o] = 0ull;
   } else {
     const float* src = a.users[model];
     const int64_t ld = a.ld[model];
@@ -212,7 +237,8 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
           const float* p = src + row * ld + 8 * q;
           if (row < 0 || row >= a.n_rows[model]) {  // unknown / stale row: NaN scores (as hrec_als_score's -1)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) f[j][e] = __builtin_nanf("");
+            for (int e = 0; e < 8; ++e)
+              if (8 * q + e < wd) f[j][e] = __builtin_nanf("");
           } else if (vec && 8 * q + 8 <= wd) {
             const float4 x0 = *reinterpret_cast<const float4*>(p);
             const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
@@ -236,8 +262,26 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         const int4 v = {(int)(h[0] | (h[1] << 16)), (int)(h[2] | (h[3] << 16)), (int)(h[4] | (h[5] << 16)),
                         (int)(h[6] | (h[7] << 16))};
         *reinterpret_cast<int4*>(us + r * kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v;
+        // the operands the later passes read (hp_user_ops_kernel's layout), once per model
+        if (a.uop_out && grp == 0 && r < ub)
+          *reinterpret_cast<int4*>(a.uop_out + ((int64_t)model * a.B + b0 + r) * DK + 8 * q) = v;
       }
     }
+  }
+  if constexpr (MODE == HS_FILTER) {
+    for (int o = threadIdx.x; o < a.UB; o += kHsThreads) {
+      float t = __builtin_nanf("");  // absent user: nothing passes
+      if (o < ub) {
+        t = a.theta[(int64_t)(b0 + o) * a.G + grp];
+        // +inf: a dead (user, group) — nothing passes; NaN admits every score
+        t = t == t ? (t == __builtin_inff() ? __builtin_nanf("") : t) : -__builtin_inff();
+      }
+      ths[o] = t;
+      cnt_l[o] = 0;
+      ovf_l[o] = 0;
+    }
+    if (threadIdx.x == 0) *bn = 0;
+  } else {
     for (int o = threadIdx.x; o < 2 * a.UB; o += kHsThreads) mmk[o] = 0u;
     if (MODE == HS_PRUNE)
       for (int o = threadIdx.x; o < a.UB; o += kHsThreads) amk[o] = 0ull;
@@ -333,6 +377,35 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
             const bool gt = mx > hi[ch][u];
             hi[ch][u] = gt ? mx : hi[ch][u];
             hp[ch][u] = gt ? (int)(jb >> 4) : hp[ch][u];
+          } else if constexpr (MODE == HS_FILTER) {
+            // the user's bound for this group (LDS); scores past the range are
+            // never compared
+            const float th = ths[bl];
+            float mx = -__builtin_inff();
+#pragma unroll
+            for (int t = 0; t < NI; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (full || jb + 16 * t + 4 * g + r < i1) mx = fmaxf(mx, acc[u][t][r]);
+            if (__ballot(mx >= th)) {  // rare: stage this lane's survivors
+#pragma unroll
+              for (int t = 0; t < NI; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int64_t j = jb + 16 * t + 4 * g + r;
+                  if ((full || j < i1) && acc[u][t][r] >= th) {
+                    const int e = atomicAdd(bn, 1);
+                    const int rk = atomicAdd(&cnt_l[bl], 1);
+                    if (e < a.sbuf) {
+                      sb_meta[e] = ((uint32_t)bl << 24) | (uint32_t)(j - i0);
+                      sb_val[e] = acc[u][t][r];
+                      sb_rank[e] = rk;
+                    } else {
+                      ovf_l[bl] = 1;  // staging full: the user's list is marked overflowing at the flush
+                    }
+                  }
+                }
+            }
           } else if constexpr (MODE == HS_FULL) {
             if (full) {
 #pragma unroll
@@ -351,7 +424,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
                   }
             }
           }
-          if (MODE != HS_PRUNE && HREC_HS_ABLATE == 0 && bl < ub) {
+          if (MODE == HS_FULL && HREC_HS_ABLATE == 0 && bl < ub) {
             float* o = out + (int64_t)(b0 + bl) * a.ldo;
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
@@ -374,7 +447,35 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       }
     }
   }
-  if constexpr (MODE == HS_GATED) return;  // scores only (the mm are known)
+  if constexpr (MODE == HS_FILTER) {
+    // flush: one list reservation per user (global atomic), then the entries
+    __syncthreads();
+    for (int o = threadIdx.x; o < ub; o += kHsThreads) {
+      const int k = cnt_l[o];
+      int base = 0;
+      if (ovf_l[o]) {
+        atomicAdd(&a.cn[b0 + o], a.cap + 1);  // > cap: the exact path answers this user
+      } else if (k > 0) {
+        base = atomicAdd(&a.cn[b0 + o], k);
+      }
+      cnt_l[o] = ovf_l[o] ? -1 : base;
+    }
+    __syncthreads();
+    const int ne = *bn < a.sbuf ? *bn : a.sbuf;
+    for (int e = threadIdx.x; e < ne; e += kHsThreads) {
+      const uint32_t m = sb_meta[e];
+      const int ul = (int)(m >> 24);
+      const int base = cnt_l[ul];
+      if (base < 0) continue;
+      const int p = base + sb_rank[e];
+      if (p < a.cap) {
+        const int64_t b = b0 + ul;
+        a.cv[b * a.cap + p] = sb_val[e];
+        a.ci[b * a.cap + p] = i0 + (int64_t)(m & 0xffffffu);
+      }
+    }
+    return;
+  }
   // fold the lanes' running min / max per user into the block's LDS slots
   if (HREC_HS_ABLATE < 2 && ub > 0) {
 #pragma unroll
@@ -485,7 +586,8 @@ static int hs_launch_n(HybScoresArgs& a, size_t lds, hipStream_t s) {
   const auto kfn = hyb_scores_kernel<DK, NCH, MODE>;
   if (!allow_max_lds(kfn))
     return check_launch("hyb_scores_kernel: LDS attribute");
-  hipLaunchKernelGGL(kfn, dim3((unsigned)(2 * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
+  const int models = MODE == HS_FILTER ? 1 : 2;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)(models * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
   return check_launch("hyb_scores_kernel");
 }
 
@@ -494,7 +596,13 @@ static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
   constexpr int CU = 16 * HsShape<DK>::NU;
   a.UB = hs_user_tile<DK>(a.B);
   a.n_ut = (a.B + a.UB - 1) / a.UB;
-  const size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * (MODE == HS_PRUNE ? 16 : 8);
+  size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * (MODE == HS_PRUNE ? 16 : 8);
+  if (MODE == HS_FILTER) {  // the rest of the 160 KiB stages survivors (12 B each)
+    const size_t head = hs_filter_head(a.UB, HsShape<DK>::kRowB);
+    a.sbuf = head < kHsMaxLds ? (int)((kHsMaxLds - head) / 12) : 0;
+    if (a.sbuf > 8192) a.sbuf = 8192;
+    lds = head + (size_t)a.sbuf * 12;
+  }
   int rc;
   switch (a.UB / CU) {
     case 1: rc = hs_launch_n<DK, 1, MODE>(a, lds, s); break;
@@ -502,7 +610,7 @@ static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
     case 3: rc = hs_launch_n<DK, 3, MODE>(a, lds, s); break;
     default: rc = hs_launch_n<DK, 4, MODE>(a, lds, s); break;
   }
-  if (rc || MODE == HS_GATED || mm0 == nullptr) return rc;  // no extremes wanted: the caller folds the partials
+  if (rc || MODE == HS_FILTER || mm0 == nullptr) return rc;  // no extremes wanted: the caller folds the partials
   hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((a.B + 63) / 64), 2), dim3(256), 0, s, a.part, a.B, a.G,
                      mm0, mm1);
   return check_launch("hyb_mm_reduce_kernel");
@@ -523,9 +631,18 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
                       int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                       const void* als_items, const void* tt_items, int64_t n_items, int dk, float* als_out,
                       float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm, float* part, int* argpos,
-                      const int* gate, hipStream_t s, const uint16_t* uop) {
+                      hipStream_t s, const uint16_t* uop, uint16_t* uop_out, const HsFilter* filt) {
   HybScoresArgs a{};
   a.uop = uop;
+  a.uop_out = uop_out;
+  if (filt) {
+    a.theta = filt->theta;
+    a.hm = filt->hm;
+    a.cap = filt->cap;
+    a.cv = filt->cv;
+    a.ci = filt->ci;
+    a.cn = filt->cn;
+  }
   a.users[0] = als_users;
   a.users[1] = tt_users;
   a.ld[0] = als_ld;
@@ -545,11 +662,10 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
   a.ldo = ld_out;
   a.part = part;
   a.argpos = argpos;
-  a.gate = gate;
   a.G = hs_groups(n_items);
   switch (mode) {
     case HS_PRUNE: return hs_dispatch<HS_PRUNE>(a, dk, als_mm, tt_mm, s);
-    case HS_GATED: return hs_dispatch<HS_GATED>(a, dk, als_mm, tt_mm, s);
+    case HS_FILTER: return hs_dispatch<HS_FILTER>(a, dk, als_mm, tt_mm, s);
     default: return hs_dispatch<HS_FULL>(a, dk, als_mm, tt_mm, s);
   }
 }
@@ -594,5 +710,5 @@ extern "C" int hrec_hybrid_scores(const float* als_users, int64_t als_ld, const 
   }
   return hybrid_scores_run(HS_FULL, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld, tt_width,
                            n_users, als_items, tt_items, n_items, dk, als_out, tt_out, ld_out, als_mm, tt_mm,
-                           static_cast<float*>(workspace), nullptr, nullptr, s);
+                           static_cast<float*>(workspace), nullptr, s);
 }
