@@ -117,7 +117,7 @@ namespace hrec {
 // (0 = scores + per-row min / max, 1 = min / max + per-block max slice, no
 // stores, 2 = the heavy model's survivors of per-(user, item group) bounds:
 // filt) and its item-group count. uop: pre-converted bf16 user rows to stage
-// as is; uop_out: write the converted rows there (f32 staging, modes 0 / 1).
+// as is.
 struct HsFilter {
   const float* theta;  // [B][G] bounds (+inf: nothing of the group, NaN: every score)
   int hm;              // the heavy model (0 = ALS, 1 = two-tower)
@@ -130,8 +130,7 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
                       int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                       const void* als_items, const void* tt_items, int64_t n_items, int dk, float* als_out,
                       float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm, float* part, int* argpos,
-                      hipStream_t s, const uint16_t* uop = nullptr, uint16_t* uop_out = nullptr,
-                      const HsFilter* filt = nullptr);
+                      hipStream_t s, const uint16_t* uop = nullptr, const HsFilter* filt = nullptr);
 int hs_groups(int64_t n_items);
 int hs_slice_tiles(int dk);  // item tiles of 16 per wave slice (a slice = 16 * tiles items)
 // csrc/dot_topk.hip: the matrix-core survivor filter (score >= thr[b]) and

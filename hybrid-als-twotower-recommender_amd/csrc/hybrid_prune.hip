@@ -7,11 +7,10 @@
 // The fusion needs each user's min / max of BOTH score rows before any fused
 // score exists, so the scores are computed twice, the second time for one
 // model only:
-//   phase 1 (hrec_hybrid_prune_minmax): both GEMMs (hyb_scores_kernel, mode
-//     HS_PRUNE: no stores; every block gathers + converts its users to bf16,
-//     the item group 0 blocks also leave those operands for phase 2) -> per-
-//     user min / max of both rows, and per item group (block) both models'
-//     group maxima + the 16-NI item slice holding the heavy one;
+//   phase 1 (hrec_hybrid_prune_minmax): the user rows gathered + converted to
+//     bf16 operands once; both GEMMs (hyb_scores_kernel, mode HS_PRUNE: no
+//     stores) -> per-user min / max of both rows, and per item group (block)
+//     both models' group maxima + the 16-NI item slice holding the heavy one;
 //   [the caller all-reduces the min / max across item shards (C2)]
 //   phase 2 (hrec_hybrid_prune_topk), three launches:
 //     a. bound: per user, the slices of the 16 groups with the largest maxima
@@ -95,6 +94,35 @@ __device__ __forceinline__ double hp_fuse(const HpScale& s, float a, float t, do
   const double an = (double)a * s.ascale + s.amin_;
   const float tn = t * s.tscale + s.tmin_;
   return w0 * an + w1 * (double)tn;
+}
+
+// 1. bf16 user operands [2][B][dk]: the ALS rows gathered by als_rows (a row
+// outside [0, n_als_rows) reads as NaN, as hyb_scores_kernel stages it) and
+// the two-tower rows, columns >= width zero — hyb_scores_kernel's staging.
+// (Folding this into phase 1 — every GEMM block gathering and converting its
+// f32 rows — measured slower: phase 1 35.7 -> 47.7 us against this launch's
+// 5.4 us, round 4.)
+__global__ __launch_bounds__(256) void hp_user_ops_kernel(const float* __restrict__ als_users, int64_t als_ld,
+                                                          const int64_t* __restrict__ als_rows, int64_t n_als_rows,
+                                                          int als_width, const float* __restrict__ tt_users,
+                                                          int64_t tt_ld, int tt_width, int B, int dk,
+                                                          uint16_t* __restrict__ uop) {
+  const int b = blockIdx.x, m = blockIdx.y;
+  const float* src = m ? tt_users : als_users;
+  const int64_t ld = m ? tt_ld : als_ld;
+  const int wd = m ? tt_width : als_width;
+  int64_t row = b;
+  bool bad = false;
+  if (m == 0 && als_rows) {
+    row = als_rows[b];
+    bad = row < 0 || row >= n_als_rows;
+  }
+  uint16_t* out = uop + ((int64_t)m * B + b) * dk;
+  for (int c = threadIdx.x; c < dk; c += blockDim.x) {
+    float v = 0.f;
+    if (c < wd) v = bad ? __builtin_nanf("") : src[row * ld + c];
+    out[c] = (uint16_t)hp_bf16(v);
+  }
 }
 
 // Order of the fused top-k (score.hip's better()): larger first, equal ->
@@ -626,11 +654,13 @@ extern "C" int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, 
     return hrec_hybrid_scores(als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users,
                               als_items, tt_items, 0, dk, nullptr, nullptr, 0, als_mm, tt_mm, w.part,
                               (size_t)2 * 2 * n_users * 4 + 256, stream);
-  // the users are gathered + converted by the GEMM launch itself; its item
-  // group 0 blocks leave the bf16 operands for phase 2 (no user-ops launch)
+  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
+                     n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
+  rc = check_launch("hp_user_ops_kernel");
+  if (rc) return rc;
   return hybrid_scores_run(1 /* HS_PRUNE */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
                            tt_width, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, 0, als_mm, tt_mm,
-                           w.part, w.argpos, s, nullptr, w.uop);
+                           w.part, w.argpos, s, w.uop);
 }
 
 // Phase 2 launches (a - c). local: the bound kernel reduces the extremes
@@ -672,8 +702,7 @@ static int hp_phase2(bool local, int n_users, const void* als_items, const void*
   if (hp_filter_choice() == 1) {
     const HsFilter f{w.theta, hm, kHpCap, w.cv, w.ci, w.cn};
     rc = hybrid_scores_run(2 /* HS_FILTER */, nullptr, 0, nullptr, 0, 0, nullptr, 0, 0, n_users, als_items, tt_items,
-                           n_items, dk, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, s, w.uop, nullptr,
-                           &f);
+                           n_items, dk, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, s, w.uop, &f);
   } else {  // the K8 resident-user filter (round 3)
     const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
     const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
@@ -739,11 +768,14 @@ extern "C" int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, c
   HREC_REQUIRE(workspace_bytes >= need, "hybrid_prune_local: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t s = as_stream(stream);
   const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, 1);
-  // phase 1 (user gather + conversion inside, operands left for phase 2)
-  // without its min / max reduce launch (the bound kernel folds it)
+  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
+                     n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
+  rc = check_launch("hp_user_ops_kernel");
+  if (rc) return rc;
+  // phase 1 without its min / max reduce launch (the bound kernel folds it)
   rc = hybrid_scores_run(1 /* HS_PRUNE */, als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld,
                          tt_width, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, 0, nullptr, nullptr,
-                         w.part, w.argpos, s, nullptr, w.uop);
+                         w.part, w.argpos, s, w.uop);
   if (rc) return rc;
   return hp_phase2(true, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, als_mm, tt_mm, als_wins, top_k,
                    idx_offset, out_idx, out_val, workspace, s);

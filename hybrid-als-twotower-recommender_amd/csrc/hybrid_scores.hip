@@ -57,8 +57,6 @@ struct HybScoresArgs {
   float* part;             // [2][G][2][B]: per-block min / max
   int* argpos;             // HS_PRUNE: [2][G][B] slice of each block's max ((jb / 16) * 4 + g), -1 = none
   const uint16_t* uop;     // optional: the batch's bf16 user operands [2][B][DK] (staged as is)
-  uint16_t* uop_out;       // optional (f32 staging): the blocks of item group 0 also write their
-                           // model's bf16 user operands there ([2][B][DK], row-major)
   // HS_FILTER: the heavy model hm's scores against per-(user, group) bounds
   const float* theta;      // [B][G]: a score >= theta survives; +inf / NaN: nothing of the group
   int hm;
@@ -67,6 +65,7 @@ struct HybScoresArgs {
   int64_t* ci;             // [B][cap] survivor item ids
   int* cn;                 // [B] survivors counted (zeroed by the caller; > cap: the list overflowed)
   int sbuf;                // HS_FILTER: survivors a block stages in LDS
+  int fsplit;              // HS_FILTER: blocks per item group
   int G;                   // item groups per (model, user tile)
   int UB;                  // users per tile (multiple of 64)
   int n_ut;
@@ -158,10 +157,19 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   const int g = lane >> 4, c = lane & 15;
   const int model = MODE == HS_FILTER ? a.hm : (blockIdx.x & 1);
   const int rest = MODE == HS_FILTER ? (int)blockIdx.x : (int)(blockIdx.x >> 1);
-  const int ut = rest % a.n_ut, grp = rest / a.n_ut;
+  const int ut = rest % a.n_ut;
+  const int grp = MODE == HS_FILTER ? rest / a.n_ut / a.fsplit : rest / a.n_ut;
   const int64_t per = ((a.N + a.G - 1) / a.G + 15) / 16 * 16;
-  const int64_t i0 = (int64_t)grp * per;
-  const int64_t i1 = i0 + per < a.N ? i0 + per : a.N;
+  int64_t i0 = (int64_t)grp * per;
+  int64_t i1 = i0 + per < a.N ? i0 + per : a.N;
+  if constexpr (MODE == HS_FILTER) {  // part of the group: fsplit blocks share its bound
+    const int part = rest / a.n_ut % a.fsplit;
+    constexpr int64_t kSl = 16 * S::NI;
+    const int64_t sub = (per + a.fsplit * kSl - 1) / (a.fsplit * kSl) * kSl;
+    const int64_t g1 = i1;
+    i0 = i0 + part * sub < g1 ? i0 + part * sub : g1;
+    i1 = i0 + sub < g1 ? i0 + sub : g1;
+  }
   const int b0 = ut * a.UB;
   const int ub = a.B - b0 < a.UB ? a.B - b0 : a.UB;
 
@@ -262,9 +270,6 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         const int4 v = {(int)(h[0] | (h[1] << 16)), (int)(h[2] | (h[3] << 16)), (int)(h[4] | (h[5] << 16)),
                         (int)(h[6] | (h[7] << 16))};
         *reinterpret_cast<int4*>(us + r * kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v;
-        // the operands the later passes read (hp_user_ops_kernel's layout), once per model
-        if (a.uop_out && grp == 0 && r < ub)
-          *reinterpret_cast<int4*>(a.uop_out + ((int64_t)model * a.B + b0 + r) * DK + 8 * q) = v;
       }
     }
   }
@@ -587,7 +592,8 @@ static int hs_launch_n(HybScoresArgs& a, size_t lds, hipStream_t s) {
   if (!allow_max_lds(kfn))
     return check_launch("hyb_scores_kernel: LDS attribute");
   const int models = MODE == HS_FILTER ? 1 : 2;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)(models * a.n_ut * a.G)), dim3(kHsThreads), lds, s, a);
+  const int per_group = MODE == HS_FILTER ? a.fsplit : 1;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)(models * a.n_ut * a.G * per_group)), dim3(kHsThreads), lds, s, a);
   return check_launch("hyb_scores_kernel");
 }
 
@@ -602,6 +608,16 @@ static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
     a.sbuf = head < kHsMaxLds ? (int)((kHsMaxLds - head) / 12) : 0;
     if (a.sbuf > 8192) a.sbuf = 8192;
     lds = head + (size_t)a.sbuf * 12;
+    // one model: split each item group over enough blocks to fill the CUs
+    static const int cus = [] {
+      int dev = 0, n = 256;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n > 0 ? n : 256;
+    }();
+    const int64_t slices = ((a.N + a.G - 1) / a.G + 16 * HsShape<DK>::NI - 1) / (16 * HsShape<DK>::NI);
+    int fs = (cus + a.n_ut * a.G - 1) / (a.n_ut * a.G);
+    if (fs > slices / 8) fs = (int)(slices / 8);  // >= one round of the 8 waves per block
+    a.fsplit = fs < 1 ? 1 : fs;
   }
   int rc;
   switch (a.UB / CU) {
@@ -631,10 +647,9 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
                       int als_width, const float* tt_users, int64_t tt_ld, int tt_width, int n_users,
                       const void* als_items, const void* tt_items, int64_t n_items, int dk, float* als_out,
                       float* tt_out, int64_t ld_out, float* als_mm, float* tt_mm, float* part, int* argpos,
-                      hipStream_t s, const uint16_t* uop, uint16_t* uop_out, const HsFilter* filt) {
+                      hipStream_t s, const uint16_t* uop, const HsFilter* filt) {
   HybScoresArgs a{};
   a.uop = uop;
-  a.uop_out = uop_out;
   if (filt) {
     a.theta = filt->theta;
     a.hm = filt->hm;
