@@ -64,6 +64,29 @@ __device__ __forceinline__ uint32_t hp_bf16(float v) {
 }
 __device__ __forceinline__ float hp_f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
+#ifdef HREC_HP_STAMPS
+// Diagnostic builds only: per block (thread 0) s_memtime at the kernel's
+// phase points, [kernel 0 = bound, 1 = survivors][block][point], plain stores.
+constexpr int kHpStampBlocks = 1024;
+__device__ unsigned long long g_hp_stamps[2][kHpStampBlocks][8];
+#define HP_STAMP_DECL unsigned long long hp_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define HP_STAMP(i)                                          \
+  do {                                                       \
+    if (threadIdx.x == 0) hp_t[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define HP_STAMP_OUT(kid)                                                            \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < kHpStampBlocks) {                           \
+      hp_t[7] = __builtin_amdgcn_s_memtime();                                        \
+      for (int _q = 0; _q < 8; ++_q) g_hp_stamps[kid][blockIdx.x][_q] = hp_t[_q];    \
+    }                                                                                \
+  } while (0)
+#else
+#define HP_STAMP_DECL
+#define HP_STAMP(i)
+#define HP_STAMP_OUT(kid)
+#endif
+
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -189,6 +212,8 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   __shared__ double s_tau;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
+  HP_STAMP_DECL;
+  HP_STAMP(0);
   const int b = blockIdx.x;
   if (b == 0 && tid == 0) *flag = 0;
   if (tid == 0) cn[b] = 0;
@@ -206,10 +231,11 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   }
   const int lm = 1 - hm;
   float lmx = -INFINITY;
+  int ap = -1;  // the group's max slice (kept for the seed slots below: no second load)
   if (tid < 128) {
     float v = -INFINITY;
     if (tid < G) {
-      const int ap = argpos[((int64_t)hm * G + tid) * B + b];
+      ap = argpos[((int64_t)hm * G + tid) * B + b];
       const float pv = part[(((int64_t)hm * G + tid) * 2 + 1) * B + b];
       lmx = part[(((int64_t)lm * G + tid) * 2 + 1) * B + b];
       v = ap >= 0 ? pv : -INFINITY;
@@ -237,6 +263,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
       red[wv][1] = hi;
     }
     __syncthreads();
+    HP_STAMP(1);
     amin = fminf(red[0][0], red[1][0]);
     amax = fmaxf(red[0][1], red[1][1]);
     tmin = fminf(red[2][0], red[3][0]);
@@ -255,6 +282,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     // exact path ranks them; nothing survives the filter
     for (int gi = tid; gi < G; gi += 256) th_row[gi] = INFINITY;
     if (tid == 0) uflag[b] = 1;
+    HP_STAMP_OUT(0);
     return;  // block-uniform
   }
   const HpScale sc = hp_scale(amin, amax, tmin, tmax);
@@ -262,6 +290,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   for (int q = tid; q < kSlots; q += 256) sitem[q] = -1;
   if (tid == 0) s_tau = -INFINITY;
   __syncthreads();
+  HP_STAMP(2);
   // the kHpMaxGroups largest group maxima (value desc, group asc) -> seed slots
   const int per_g = 4 * slice_ni;
   if (tid < G) {
@@ -273,7 +302,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
         rank += (o > v || (o == v && q < tid)) ? 1 : 0;
       }
       if (rank < kHpMaxGroups) {
-        const int pos = argpos[((int64_t)hm * G + tid) * B + b];
+        const int pos = ap;
         const int64_t jb = (int64_t)(pos >> 2) * 16;
         const int gq = pos & 3;
         const int64_t i1 = (int64_t)tid * per + per < N ? (int64_t)tid * per + per : N;
@@ -286,6 +315,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     }
   }
   __syncthreads();
+  HP_STAMP(3);
   // exact fused scores of the seeds: 16 per MFMA group, both models, two
   // groups' rows in flight per wave
   const char* vh = reinterpret_cast<const char*>(hm ? tt_items : als_items);
@@ -316,6 +346,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     }
   }
   __syncthreads();
+  HP_STAMP(4);
   // tau = the kk-th largest (the seed items are distinct)
   for (int q = tid; q < n_slots; q += 256) {
     const double v = sfl[q];
@@ -328,10 +359,12 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     if (rank == kk - 1) s_tau = v;
   }
   __syncthreads();
+  HP_STAMP(5);
   const double tau = s_tau;
   if (tau == -INFINITY) {  // fewer than kk numeric seeds: the exact path
     for (int gi = tid; gi < G; gi += 256) th_row[gi] = INFINITY;
     if (tid == 0) uflag[b] = 1;
+    HP_STAMP_OUT(0);
     return;
   }
   if (tid == 0) uflag[b] = 0;
@@ -359,6 +392,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     if (gi < 128 && (double)th > (double)smax[gi]) th = INFINITY;
     th_row[gi] = th;
   }
+  HP_STAMP_OUT(0);
 }
 
 // 2c. Survivors of user blockIdx.x (8 waves, 16 survivors per MFMA group):
@@ -389,6 +423,8 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   __shared__ int s_full;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
+  HP_STAMP_DECL;
+  HP_STAMP(0);
   const int b = blockIdx.x;
   const float* cvb = cv + (int64_t)b * cap;
   const int64_t* cib = ci + (int64_t)b * cap;
@@ -502,6 +538,7 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
     }
     __syncthreads();
   };
+  HP_STAMP(1);
   reset();
   if (!flagged) {
     // two survivor groups per wave in flight (q0, q0 + 8); the next pair's
@@ -535,8 +572,13 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
       }
     }
   }
+  HP_STAMP(2);
   merge(!flagged);
-  if (!flagged && s_full == 0) return;  // block-uniform
+  HP_STAMP(3);
+  if (!flagged && s_full == 0) {  // block-uniform
+    HP_STAMP_OUT(1);
+    return;
+  }
   // the exact path for this user
   if (tid == 0) *flag = 1;
   if (!(amin <= amax) || !(tmin <= tmax)) {
@@ -780,6 +822,12 @@ extern "C" int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, c
   return hp_phase2(true, n_users, als_items, tt_items, n_items, dk, nullptr, nullptr, als_mm, tt_mm, als_wins, top_k,
                    idx_offset, out_idx, out_val, workspace, s);
 }
+
+#ifdef HREC_HP_STAMPS
+extern "C" int hrec_debug_hp_stamps(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hp_stamps), sizeof(g_hp_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,
                                            int32_t* out, void* stream) {

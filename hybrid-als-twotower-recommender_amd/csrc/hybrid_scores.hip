@@ -79,6 +79,13 @@ struct HybScoresArgs {
 #define HREC_HS_NT 0  // 1 = non-temporal score stores
 #endif
 
+#ifndef HREC_HS_STAGE_BATCH
+#define HREC_HS_STAGE_BATCH 16  // 16-B user-operand loads per thread in flight while staging
+#endif
+#ifndef HREC_HS_STAGE_ROT
+#define HREC_HS_STAGE_ROT 1  // rotate each block's staging start (spreads the shared rows' L2 lines)
+#endif
+
 constexpr int kHsThreads = 512;
 constexpr int kHsMaxUserBytes = 128 * 1024;
 constexpr size_t kHsMaxLds = 160 * 1024;
@@ -129,6 +136,16 @@ struct HsShape {
 // bound is one LDS value per block and its survivors leave in one flush).
 enum { HS_FULL = 0, HS_PRUNE = 1, HS_FILTER = 2 };
 
+#ifdef HREC_HS_STAMPS
+// Diagnostic builds only (plain stores per block, no contended atomics):
+// [mode][block][0..3] = wave 0's s_memtime at entry, after the staging, after
+// its main loop, at the end; [4 + w / 2] = (w even: low, odd: high 32 bits)
+// the main-loop ticks of wave w.
+constexpr int kHsStampBlocks = 1024;
+__device__ unsigned long long g_hs_stamps[3][kHsStampBlocks][8];
+#define HS_T() __builtin_amdgcn_s_memtime()
+#endif
+
 // NCH: user chunks of CU = 16 NU users in the tile (compile-time, so the
 // per-lane running min / max of every chunk stays in registers and the last
 // chunk's item refills are unconditional).
@@ -137,6 +154,9 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   using S = HsShape<DK>;
   constexpr int KS = S::KS, NI = S::NI, NU = S::NU, CU = 16 * NU;
   constexpr int kRowB = S::kRowB;
+#ifdef HREC_HS_STAMPS
+  const unsigned long long t_start = HS_T();
+#endif
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   char* us = dsm;
   uint32_t* mmk = reinterpret_cast<uint32_t*>(dsm + (size_t)a.UB * kRowB);  // [UB][2]: ~key(min), key(max)
@@ -204,22 +224,29 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   // width). Batches of chunks (8 floats each) per thread: all loads are
   // issued before the first conversion (16-B loads when the row allows).
   if (a.uop) {  // pre-converted rows (hp_user_ops_kernel): 16-B copies
+    // every block of a launch reads the same rows: each block of an XCD
+    // starts at another 1/16 of them (the same L2 lines are not requested
+    // by all 32 CUs at once), and the whole tile is in flight at once at d >= 128
     const char* src = reinterpret_cast<const char*>(a.uop) + ((int64_t)model * a.B + b0) * (DK * 2);
-    constexpr int kBatch = 8;
+    constexpr int kBatch = HREC_HS_STAGE_BATCH;
     const int n_chunks = a.UB * S::kChunks;
+    const int rot = HREC_HS_STAGE_ROT ? (int)((blockIdx.x >> 3) & 15) * (n_chunks >> 4) : 0;
     for (int o0 = threadIdx.x; o0 < n_chunks; o0 += kBatch * kHsThreads) {
       int4 v[kBatch];
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
-        const int o = o0 + j * kHsThreads;
+        int o = o0 + j * kHsThreads + rot;
+        o = o >= n_chunks ? o - n_chunks : o;
         const int r = o / S::kChunks, q = o % S::kChunks;
         v[j] = int4{0, 0, 0, 0};
-        if (o < n_chunks && r < ub) v[j] = *reinterpret_cast<const int4*>(src + (int64_t)r * (DK * 2) + 16 * q);
+        if (o0 + j * kHsThreads < n_chunks && r < ub)
+          v[j] = *reinterpret_cast<const int4*>(src + (int64_t)r * (DK * 2) + 16 * q);
       }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
-        const int o = o0 + j * kHsThreads;
-        if (o >= n_chunks) break;
+        if (o0 + j * kHsThreads >= n_chunks) break;
+        int o = o0 + j * kHsThreads + rot;
+        o = o >= n_chunks ? o - n_chunks : o;
         const int r = o / S::kChunks, q = o % S::kChunks;
         *reinterpret_cast<int4*>(us + r * kRowB + 16 * (S::kSwz ? q ^ (r & 15) : q)) = v[j];
       }
@@ -292,6 +319,9 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       for (int o = threadIdx.x; o < a.UB; o += kHsThreads) amk[o] = 0ull;
   }
   __syncthreads();
+#ifdef HREC_HS_STAMPS
+  const unsigned long long t_staged = HS_T();
+#endif
 
   // running min / max of this lane's scores per (chunk, user tile): the
   // lane's user is CU ch + 16 u + c in every slice; folded across lanes once
@@ -452,6 +482,25 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       }
     }
   }
+#ifdef HREC_HS_STAMPS
+  const unsigned long long t_loop = HS_T();
+  __shared__ uint32_t s_wloop[8];
+  if ((threadIdx.x & 63) == 0) s_wloop[w] = (uint32_t)(t_loop - t_staged);
+  auto stamp_end = [&]() {
+    if (threadIdx.x == 0 && blockIdx.x < kHsStampBlocks) {
+      const unsigned long long t3 = HS_T();
+      unsigned long long* o = g_hs_stamps[MODE][blockIdx.x];
+      o[0] = t_start;
+      o[1] = t_staged;
+      o[2] = t_loop;
+      o[3] = t3;
+      for (int q = 0; q < 4; ++q) o[4 + q] = (unsigned long long)s_wloop[2 * q] | ((unsigned long long)s_wloop[2 * q + 1] << 32);
+    }
+  };
+#define HS_STAMP_END() stamp_end()
+#else
+#define HS_STAMP_END()
+#endif
   if constexpr (MODE == HS_FILTER) {
     // flush: one list reservation per user (global atomic), then the entries
     __syncthreads();
@@ -479,6 +528,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         a.ci[b * a.cap + p] = i0 + (int64_t)(m & 0xffffffu);
       }
     }
+    HS_STAMP_END();
     return;
   }
   // fold the lanes' running min / max per user into the block's LDS slots
@@ -525,6 +575,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       a.argpos[(int64_t)(model * a.G + grp) * a.B + b0 + o] = k ? (int)~(uint32_t)k : -1;
     }
   }
+  HS_STAMP_END();
 }
 
 // mm[model][0 / 1][b] = min / max over the G item groups' partials: a block
@@ -688,6 +739,14 @@ int hybrid_scores_run(int mode, const float* als_users, int64_t als_ld, const in
 }  // namespace hrec
 
 using namespace hrec;
+
+#ifdef HREC_HS_STAMPS
+extern "C" int hrec_debug_hs_stamps(unsigned long long* host_out, int reset) {
+  (void)reset;
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hs_stamps), sizeof(g_hs_stamps)) != hipSuccess) return -2;
+  return 0;
+}
+#endif
 
 extern "C" size_t hrec_hybrid_scores_workspace_bytes(int n_users, int64_t n_items) {
   const size_t B = (size_t)(n_users > 0 ? n_users : 0);
