@@ -111,6 +111,11 @@ _SIGNATURES.update({
                                          _vp]),
     "hrec_hybrid_prune_fallback_taken": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_hybrid_prune_survivors": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
+    "hrec_comm_get_unique_id": (_c_i32, [_vp]),
+    "hrec_comm_init": (_c_i32, [_c_i32, _c_i32, _vp, ctypes.POINTER(_vp)]),
+    "hrec_comm_destroy": (_c_i32, [_vp]),
+    "hrec_allgather": (_c_i32, [_vp, _vp, _vp, _c_sz, _c_i32, _vp]),
+    "hrec_allreduce_minmax": (_c_i32, [_vp, _vp, _c_i32, _c_i64, _vp]),
     "hrec_adam_sparse": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp] +
                          [ctypes.c_float] * 6 + [_vp]),
     "hrec_adam_sparse_tables": (_c_i32, [ctypes.POINTER(SparseTable), _c_i32] + [ctypes.c_float] * 6 + [_vp]),
@@ -118,7 +123,7 @@ _SIGNATURES.update({
                                       + [_vp]),
 })
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _LIB = None
 
 
@@ -874,3 +879,52 @@ def topk_keyed(vals, keys, top_k):
         _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float64, "out_val"), _dev(ws, torch.uint8, "ws"),
         need, _stream()))
     return out_i, out_v
+
+
+# ------------------------------------------------------- multi-GPU (C-ABI)
+_COMM_DTYPES = {torch.float32: 0, torch.float64: 1, torch.int32: 2, torch.int64: 3, torch.uint8: 4}
+
+
+class Comm:
+    """The C-ABI's RCCL communicator (hrec_comm_*), for hosts that drive the
+    exchange steps through libhrec instead of torch.distributed: rank 0's
+    unique_id() goes to every rank by the host's own channel, then every
+    rank constructs Comm(rank, world, uid)."""
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * 128)()
+        _check("hrec_comm_get_unique_id", lib().hrec_comm_get_unique_id(ctypes.cast(buf, _vp)))
+        return bytes(buf)
+
+    def __init__(self, rank, world, uid):
+        if len(uid) != 128:
+            raise HrecError("Comm: the unique id has 128 bytes")
+        self._id = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        self.h = _vp()
+        self.rank, self.world = int(rank), int(world)
+        _check("hrec_comm_init", lib().hrec_comm_init(self.rank, self.world, ctypes.cast(self._id, _vp),
+                                                      ctypes.byref(self.h)))
+
+    def allgather(self, send, recv=None):
+        """recv [world * n] = every rank's send [n] (rank-major)."""
+        if send.dtype not in _COMM_DTYPES or not send.is_cuda or not send.is_contiguous():
+            raise HrecError("Comm.allgather: a contiguous device tensor of f32/f64/i32/i64/u8")
+        if recv is None:
+            recv = torch.empty((self.world,) + tuple(send.shape), dtype=send.dtype, device=send.device)
+        _check("hrec_allgather", lib().hrec_allgather(self.h, _vp(send.data_ptr()), _dev(recv, send.dtype, "recv"),
+                                                      send.numel(), _COMM_DTYPES[send.dtype], _stream()))
+        return recv
+
+    def allreduce_minmax(self, mm):
+        """mm [n_rows, 2, B] f32 (each model's [min; max]) -> global extremes, in place."""
+        if mm.dim() != 3 or mm.shape[1] != 2:
+            raise HrecError("Comm.allreduce_minmax: mm must be [n_rows, 2, B]")
+        _check("hrec_allreduce_minmax", lib().hrec_allreduce_minmax(
+            self.h, _dev(mm, torch.float32, "mm"), mm.shape[0], mm.shape[2], _stream()))
+        return mm
+
+    def close(self):
+        if self.h:
+            _check("hrec_comm_destroy", lib().hrec_comm_destroy(self.h))
+            self.h = _vp()

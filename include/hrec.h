@@ -39,8 +39,9 @@ extern "C" {
 
 /* 2: hrec_fuse_topk gained out_minmax; hrec_hybrid_scores gained n_als_rows.
  * 3: hrec_hybrid_minmax / hrec_hybrid_topk removed (the pruned hybrid
- *    replaces them); hrec_dot_topk's +inf bound admits scores >= +inf. */
-#define HREC_ABI_VERSION 3
+ *    replaces them); hrec_dot_topk's +inf bound admits scores >= +inf.
+ * 4: the RCCL exchange steps (hrec_comm_*, hrec_allgather, hrec_allreduce_minmax). */
+#define HREC_ABI_VERSION 4
 
 #define HREC_OK 0
 #define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
@@ -485,6 +486,27 @@ int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, const int64_
  * user (out: n_users int32, device). */
 int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,
                                 int32_t* out, void* stream);
+
+/* ---------------------------------------------------------------------
+ * Multi-GPU exchange steps (csrc/comm.hip) for hosts without
+ * torch.distributed: one process per GPU, RCCL over xGMI (bound with dlopen
+ * at hrec_comm_init; a process that already loaded librccl.so.1 — PyTorch —
+ * shares that copy). Rank 0 calls hrec_comm_get_unique_id and hands the 128
+ * bytes to every rank (the host's own channel); every rank then calls
+ * hrec_comm_init (collective). HREC_E_UNSUPPORTED when RCCL is absent.
+ *   C1: hrec_allgather of a rank's factor rows after a half-sweep (recv =
+ *       world x count elements, rank-major: the replicated matrix);
+ *   C2: hrec_allreduce_minmax — mm is [n_rows][2][n_users] f32 (each model's
+ *       [min; max] rows, the hrec_rows_minmax_f32 layout, models consecutive),
+ *       replaced in place by the minima / maxima over all ranks (one MIN
+ *       all-reduce with the maxima negated);
+ *   C3: hrec_allgather (dtype 4 = bytes) of the per-shard top-k candidates. */
+int hrec_comm_get_unique_id(uint8_t* id_out /* 128 bytes */);
+int hrec_comm_init(int rank, int world, const uint8_t* id /* 128 bytes */, void** comm_out);
+int hrec_comm_destroy(void* comm);
+/* dtype: 0 f32, 1 f64, 2 i32, 3 i64, 4 u8; count = elements per rank. */
+int hrec_allgather(void* comm, const void* send, void* recv, size_t count, int dtype, void* stream);
+int hrec_allreduce_minmax(void* comm, float* mm, int n_rows, int64_t n_users, void* stream);
 
 #ifdef __cplusplus
 }

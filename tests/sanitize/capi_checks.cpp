@@ -94,6 +94,12 @@ int main() {
                                   nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr));
   INVALID(hrec_hybrid_prune_survivors(nullptr, 1, 1, 64, 5, nullptr, nullptr));
 
+  // RCCL exchange steps (argument checks only: no communicator exists here)
+  INVALID(hrec_comm_get_unique_id(nullptr));
+  INVALID(hrec_comm_init(0, 1, nullptr, nullptr));
+  INVALID(hrec_allgather(nullptr, nullptr, nullptr, 4, 0, nullptr));
+  INVALID(hrec_allreduce_minmax(nullptr, nullptr, 1, 4, nullptr));
+
   // workspace-size queries over a sweep of shapes (UBSan: no signed overflow)
   size_t acc = 0;
   const int64_t ns[] = {0, 1, 17, 1000, 100003, 50000000};

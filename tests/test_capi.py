@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared if not hasattr(lib, n)]
     assert not missing, missing
     lib.hrec_abi_version.restype = ctypes.c_int
-    assert lib.hrec_abi_version() == 3
+    assert lib.hrec_abi_version() == 4
 
 
 def test_python_binding_covers_the_header():
@@ -53,6 +53,17 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert f(None, 9, *args) == -1
     assert b"tables" in lib.hrec_last_error()
     assert f(None, 0, *args) == 0  # nothing to update
+    # the RCCL exchange steps: argument checks before RCCL is touched
+    lib.hrec_allgather.restype = ctypes.c_int
+    assert lib.hrec_allgather(None, None, None, ctypes.c_size_t(4), 0, None) == -1
+    assert b"null communicator" in lib.hrec_last_error()
+    lib.hrec_comm_init.restype = ctypes.c_int
+    idb = (ctypes.c_uint8 * 128)()
+    out = ctypes.c_void_p()
+    assert lib.hrec_comm_init(2, 2, idb, ctypes.byref(out)) == -1
+    assert b"rank 2 of world 2" in lib.hrec_last_error()
+    lib.hrec_allreduce_minmax.restype = ctypes.c_int
+    assert lib.hrec_allreduce_minmax(ctypes.c_void_p(8), None, 0, ctypes.c_int64(3), None) == -1
     # phased sparse Adam: phase range and table count before any device work
     fp = lib.hrec_adam_sparse_tables_phase
     fp.restype = ctypes.c_int
