@@ -84,9 +84,24 @@ class TwoTowerModel:
         self.seed = seed
 
     def _build_item_tower(self):
-        """Describes the item tower (:38-66); the computation is K4."""
+        """(:38-66) -> (inputs, item_vec) as the reference returns them: the
+        four inputs by their Input-layer names, and the tower itself —
+        item_vec = LN(Dense(d)(concat[E_item, E_man(8), E_cat(8),
+        relu(Dense(16)(numeric))])) — as a function of those inputs on the
+        device (K4, csrc/tt_mfma.hip; the parameters build_model allocates)."""
         inputs = ["item_id_in", "manufacturer_in", "category_in", "numeric_in"]
-        return inputs, "item_vec = LN(Dense(d)(concat[E_item, E_man(8), E_cat(8), relu(Dense(16)(numeric))]))"
+
+        def item_vec(item_id_in, manufacturer_in, category_in, numeric_in):
+            if self.model is None:
+                raise RuntimeError("item tower: call build_model() first (it owns the tower's weights)")
+            dev, sz = self.model.device, self.model.sizes
+            ids = [torch.as_tensor(_ids(x, sz[t], name), device=dev)
+                   for x, t, name in ((item_id_in, "item_emb", "item_id_in"), (manufacturer_in, "man_emb", "manufacturer_in"),
+                                      (category_in, "cat_emb", "category_in"))]
+            num = np.ascontiguousarray(np.asarray(numeric_in, dtype=np.float32).reshape(-1, 2))
+            return self.model.item_vectors(*ids, torch.as_tensor(num, device=dev))
+
+        return inputs, item_vec
 
     def build_model(self, init=None):
         """Allocate the parameters (Keras initialisers) on the device (:68-89)."""

@@ -495,6 +495,11 @@ def test_twotower_api_train_predict_save_load(device, tmp_path):
     c = ott.forward(p, np.full(len(cand), 5), cand["itemId"].to_numpy(), cand["manufacturer_id"].to_numpy(),
                     cand["category_id"].to_numpy(), num)
     np.testing.assert_allclose([s for _, s in preds], c["yhat"], rtol=1e-5, atol=1e-4)
+    # _build_item_tower (:38-66): (the four inputs, the tower as a function of them)
+    names, item_vec = tt._build_item_tower()
+    assert names == ["item_id_in", "manufacturer_in", "category_in", "numeric_in"]
+    iv = item_vec(cand["itemId"].to_numpy(), cand["manufacturer_id"].to_numpy(), cand["category_id"].to_numpy(), num)
+    np.testing.assert_allclose(iv.cpu().numpy(), c["ivec"], rtol=1e-5, atol=2e-5)
     path = str(tmp_path / "models" / "twotower.keras")
     tt.save_model(path)
     tt2 = TwoTowerModel.load_model(path)
