@@ -720,7 +720,10 @@ static int hp_phase2(bool local, int n_users, const void* als_items, const void*
   const int G = hs_groups(n_items);
   const uint16_t* ai = static_cast<const uint16_t*>(als_items);
   const uint16_t* ti = static_cast<const uint16_t*>(tt_items);
-#define HREC_HP_BOUND(DK, L)                                                                                       \
+  // hp_bound_kernel's LDS slots hold kHpMaxGroups x 16 items: 16 per group = 4 tiles of 4 (HREC_HS_NI* builds)
+  HREC_REQUIRE(hs_slice_tiles(dk) <= 4, "hybrid_prune: slice of %d tiles exceeds the bound kernel's 4",
+               hs_slice_tiles(dk));
+#define HREC_HP_BOUND(DK, L)                                                                                 \
   hipLaunchKernelGGL((hp_bound_kernel<DK, L>), dim3((unsigned)n_users), dim3(256), 0, s, w.part, w.argpos, G,        \
                      n_items, n_users, hm, als_mm, tt_mm, als_mm_out, tt_mm_out, w0, w1, kk, hs_slice_tiles(DK),   \
                      w.uop, ai, ti, w.theta, w.cn, w.uflag, w.flag)
