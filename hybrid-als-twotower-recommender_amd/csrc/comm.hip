@@ -136,7 +136,7 @@ extern "C" int hrec_allgather(void* comm, const void* send, void* recv, size_t c
   HREC_REQUIRE(dtype >= 0 && dtype <= 4, "allgather: dtype must be 0 (f32), 1 (f64), 2 (i32), 3 (i64) or 4 (u8)");
   if (count == 0) return HREC_OK;
   HREC_REQUIRE(send && recv, "allgather: null buffer");
-  static const int kRcclType[5] = {7 /* ncclFloat32 */, 9 /* ncclFloat64 */, 2 /* ncclInt32 */, 4 /* ncclInt64 */,
+  static const int kRcclType[5] = {7 /* ncclFloat32 */, 8 /* ncclFloat64 */, 2 /* ncclInt32 */, 4 /* ncclInt64 */,
                                    1 /* ncclUint8 */};
   const Comm* c = static_cast<const Comm*>(comm);
   const Rccl* r = rccl();
