@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -139,3 +141,20 @@ def test_topk_workspace_query_terminates_for_large_k():
     f.restype = ctypes.c_size_t
     f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
     assert f(2, 100000, 3000) > 0
+
+
+def test_comm_rccl_enum_values_match_header():
+    """csrc/comm.hip restates the few rccl.h enum values it passes (dtype and
+    ncclMin) as literals: each must equal the header's value."""
+    import re
+    hdr = "/opt/rocm/include/rccl/rccl.h"
+    if not os.path.exists(hdr):
+        pytest.skip("rccl.h not present")
+    text = open(hdr).read()
+    src = open(os.path.join(ROOT, "hybrid-als-twotower-recommender_amd", "csrc", "comm.hip")).read()
+    pairs = re.findall(r"(\d+) /\* (nccl\w+) \*/", src)
+    assert {n for _, n in pairs} >= {"ncclFloat32", "ncclFloat64", "ncclInt32", "ncclInt64", "ncclUint8", "ncclMin"}
+    for val, name in pairs:
+        m = re.search(r"\b%s\s*=\s*(\d+)" % name, text)
+        assert m, name
+        assert int(val) == int(m.group(1)), (name, val, m.group(1))
