@@ -675,7 +675,9 @@ struct EncodeWs {
     size_t sort64_tmp = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort64_tmp, (const int64_t*)nullptr, (int64_t*)nullptr,
                                              (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-    size_t tmp = csr_ws_max(n) + align256(4 * (size_t)n);  // + the sort's value output
+    // the in-tree sort's workspace (its sorted keys stay there), the sort's
+    // value output, then the scan's workspace (must not overlap the keys)
+    size_t tmp = csr_ws_max(n) + align256(4 * (size_t)n) + align256(scan_ws_bytes(n));
     if (sort64_tmp > tmp) tmp = sort64_tmp;
     if (scan_ws_bytes(n) > tmp) tmp = scan_ws_bytes(n);
     keys = 0;
@@ -816,7 +818,9 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
     int rc = csr_sort_run(k32, pos, reinterpret_cast<const float*>(pos), n, bits, temp, pos2, vdummy, &k32s, s);
     if (rc) return rc;
     hipLaunchKernelGGL(distinct_flags_kernel<int32_t>, dim3(g), dim3(256), 0, s, k32s, n, flag);
-    rc = scan_run<int32_t>(flag, incl, n, false, temp, s);
+    // the sorted keys live at the start of temp: the scan works past them
+    void* scan_ws = static_cast<char*>(temp) + csr_ws_max(n) + align256(4 * (size_t)n);
+    rc = scan_run<int32_t>(flag, incl, n, false, scan_ws, s);
     if (rc) return rc;
     hipLaunchKernelGGL(scatter_codes_kernel<int32_t>, dim3(g), dim3(256), 0, s, k32s, id_lo, pos2, flag, incl, n,
                        codes, uniq, n_uniq);
