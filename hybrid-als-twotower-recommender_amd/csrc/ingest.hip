@@ -15,8 +15,6 @@
 // encode_ids: a marked table + scan for dense id ranges (hipCUB radix sort of
 // (id, position) otherwise); coo_to_csr: a hand-written stable LSD radix sort
 // of the dense row codes (below); plus O(n) integer passes. HBM-bound.
-#include <stdlib.h>
-
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -295,9 +293,9 @@ __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* 
 //   2. a column scan of the tile-major counts (sort_colsum / colscan_*): the
 //      output offset of every (tile, digit) — digits ascending, tiles in
 //      input order;
-//   3. downsweep (persistent, one block per CU; two register sets, so the
-//      next tile's entries load while a whole tile is ranked, sorted and
-//      written): each wave takes a contiguous 1/8 of the block's tile into
+//   3. downsweep (persistent, one block per CU; the next tile's entries load
+//      while a tile is written out): each wave takes a contiguous 1/8 of the
+//      block's tile into
 //      registers and ranks its entries among its own same-digit entries in
 //      input order (per 64-entry round: the lanes below with the same digit,
 //      from `bits` ballots, plus the wave's running per-digit count in LDS —
@@ -391,7 +389,7 @@ __global__ __launch_bounds__(512) void sort_colscan_apply_kernel(uint32_t* __res
   }
 }
 
-template <bool FIRST, bool LAST, bool DB>
+template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
     const int32_t* __restrict__ keys_in, const int32_t* __restrict__ cols_in, const float* __restrict__ vals_in,
     const uint64_t* __restrict__ pay_in, int64_t n, int shift, int bits, int64_t n_tiles,
@@ -408,44 +406,46 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
   // wave w takes tile entries [w PW, (w + 1) PW), 64 per round (coalesced)
-  struct Regs {
-    int32_t key[kSortIPT];
-    uint64_t pay[kSortIPT];
-    uint32_t go[2];  // offsets of digits t, t + 512 (R <= 1024)
-  };
-  auto load = [&](Regs& x, int64_t tile) {
+  int32_t key[kSortIPT];
+  uint64_t pay[kSortIPT];
+  auto load = [&](int64_t tile) {
     const int64_t base = tile * kSortTile;
 #pragma unroll
     for (int r = 0; r < kSortIPT; ++r) {
       const int64_t i = base + w * PW + r * 64 + lane;
-      x.key[r] = 0;
-      x.pay[r] = 0;
+      key[r] = 0;
+      pay[r] = 0;
       if (tile < n_tiles && i < n) {
-        x.key[r] = keys_in[i];
+        key[r] = keys_in[i];
         if constexpr (FIRST) {
-          x.pay[r] = (uint64_t)(uint32_t)cols_in[i] | ((uint64_t)__float_as_uint(vals_in[i]) << 32);
+          pay[r] = (uint64_t)(uint32_t)cols_in[i] | ((uint64_t)__float_as_uint(vals_in[i]) << 32);
         } else {
-          x.pay[r] = pay_in[i];
+          pay[r] = pay_in[i];
         }
       }
     }
+  };
+  // persistent blocks (one per CU: the tile takes 118 KB of LDS); the next
+  // tile's entries and digit offsets load while this tile is written out
+  uint32_t go[2];  // offsets of digits t, t + 512 (R <= 1024)
+  auto load_offs = [&](int64_t tile) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int d = threadIdx.x + h * kSortThreads;
-      x.go[h] = (tile < n_tiles && d < R) ? offs[tile * R + d] : 0u;
+      go[h] = (tile < n_tiles && d < R) ? offs[tile * R + d] : 0u;
     }
   };
-  // one tile: rank, sort into LDS, write out; `after_lds` runs once the
-  // tile's registers are consumed (the single-set kernel loads the next tile
-  // there)
-  auto process = [&](Regs& x, int64_t tile, auto&& after_lds) {
+  int64_t tile = blockIdx.x;
+  load(tile);
+  load_offs(tile);
+  for (; tile < n_tiles; tile += gridDim.x) {
     const int64_t base = tile * kSortTile;
     const int tn = (int)(n - base < kSortTile ? n - base : kSortTile);  // entries of this tile
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int d = threadIdx.x + h * kSortThreads;
       if (d < R) {
-        goff[d] = x.go[h];
+        goff[d] = go[h];
 #pragma unroll
         for (int q = 0; q < NW; ++q) wh[q][d] = 0;
       }
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
 #pragma unroll
     for (int r = 0; r < kSortIPT; ++r) {
       const bool active = w * PW + r * 64 + lane < tn;
-      const uint32_t dg = ((uint32_t)x.key[r] >> shift) & dmask;
+      const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
       uint64_t peers = __ballot(active);
       for (int b = 0; b < bits; ++b) {
         const uint64_t m = __ballot((dg >> b) & 1u);
@@ -489,15 +489,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
           c[h][q] = d0 + h < R ? wh[q][d0 + h] : 0;
           tot += c[h][q];
         }
-      uint32_t y = tot;
+      uint32_t x = tot;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t z = __shfl_up(y, off, 64);
-        if (lane >= off) y += z;
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
       }
-      if (lane == 63) scan_sh[w] = y;
+      if (lane == 63) scan_sh[w] = x;
       __syncthreads();
-      uint32_t run = y - tot;
+      uint32_t run = x - tot;
       for (int q = 0; q < w; ++q) run += scan_sh[q];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -508,18 +508,19 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
         }
     }
     __syncthreads();
-    // 3. the tile sorted into LDS
+    // 3. the tile sorted into LDS; then the next tile's loads are issued
 #pragma unroll
     for (int r = 0; r < kSortIPT; ++r) {
       if (w * PW + r * 64 + lane < tn) {
-        const uint32_t dg = ((uint32_t)x.key[r] >> shift) & dmask;
+        const uint32_t dg = ((uint32_t)key[r] >> shift) & dmask;
         const uint32_t q = wh[w][dg] + rk[r];
-        sk[q] = x.key[r];
-        sp[q] = x.pay[r];
+        sk[q] = key[r];
+        sp[q] = pay[r];
       }
     }
     __syncthreads();
-    after_lds();
+    load(tile + gridDim.x);
+    load_offs(tile + gridDim.x);
     // 4. write out: consecutive LDS entries of one digit go to consecutive
     //    output positions (coalesced runs); a digit's first LDS slot is its
     //    wave-0 offset
@@ -540,27 +541,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
       }
     }
     __syncthreads();
-  };
-  // persistent blocks (one per CU: the tile takes 118 KB of LDS)
-  const int64_t step = gridDim.x;
-  int64_t tile = blockIdx.x;
-  if constexpr (DB) {
-    // two register sets: tile t + step's loads are issued before tile t is
-    // ranked, so a whole tile of work covers their latency
-    Regs a, b;
-    load(a, tile);
-    for (; tile < n_tiles; tile += 2 * step) {
-      load(b, tile + step);
-      process(a, tile, [] {});
-      if (tile + step >= n_tiles) break;
-      load(a, tile + 2 * step);
-      process(b, tile + step, [] {});
-    }
-  } else {
-    // one set: the next tile's entries load while this tile is written out
-    Regs a;
-    load(a, tile);
-    for (; tile < n_tiles; tile += step) process(a, tile, [&] { load(a, tile + step); });
   }
 }
 
@@ -605,15 +585,6 @@ __global__ __launch_bounds__(256) void copy_entries_kernel(const int32_t* __rest
         values[i0 + u * stride] = v[u];
       }
   }
-}
-
-// HREC_SORT_DB: 1 (default) = the downsweep's two register sets, 0 = one set
-static bool sort_double_buffer() {
-  static const bool v = [] {
-    const char* e = getenv("HREC_SORT_DB");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
 }
 
 inline unsigned grid_for(int64_t n) {
@@ -720,19 +691,13 @@ int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, in
     const bool first = p == 0, last = p == L.passes - 1;
     int32_t* kout = kbuf[p & 1];
     uint64_t* pout = pbuf[p & 1];
-#define HREC_DOWN(F, LST, DB)                                                                                     \
-  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST, DB>), dim3(nd), dim3(kSortThreads), 0, s, kin, cols, vals, pin,  \
-                     nnz, shift, db, L.n_tiles, cnt, kout, pout, idx_out, val_out)
-#define HREC_DOWN2(F, LST)          \
-  if (sort_double_buffer())         \
-    HREC_DOWN(F, LST, true);        \
-  else                              \
-    HREC_DOWN(F, LST, false)
-    if (first && last) HREC_DOWN2(true, true);
-    else if (first) HREC_DOWN2(true, false);
-    else if (last) HREC_DOWN2(false, true);
-    else HREC_DOWN2(false, false);
-#undef HREC_DOWN2
+#define HREC_DOWN(F, LST)                                                                                        \
+  hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nd), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
+                     shift, db, L.n_tiles, cnt, kout, pout, idx_out, val_out)
+    if (first && last) HREC_DOWN(true, true);
+    else if (first) HREC_DOWN(true, false);
+    else if (last) HREC_DOWN(false, true);
+    else HREC_DOWN(false, false);
 #undef HREC_DOWN
     const int rc = check_launch("radix sort pass");
     if (rc) return rc;

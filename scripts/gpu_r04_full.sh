@@ -8,8 +8,3 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | g
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err
 rc=$?; tail -c 300 gpurun_out/r04_bench.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/r04_bench.err; exit $rc; }
 HREC_LIB=hybrid-als-twotower-recommender_amd/lib/variants/libhrec_hsstamps.so timeout -k 10 300 python -u scripts/hs_stamps.py 2>&1 | grep -v amdgpu.ids
-rc=$?; [ $rc -eq 0 ] || exit $rc
-for db in 0 1; do
-  echo "== HREC_SORT_DB=$db"
-  HREC_SORT_DB=$db timeout -k 10 200 python -u scripts/ingest_probe.py 2>&1 | grep -v amdgpu.ids || exit 1
-done
