@@ -88,7 +88,11 @@ struct HybScoresArgs {
 
 constexpr int kHsThreads = 512;
 constexpr int kHsMaxUserBytes = 128 * 1024;
+#ifdef HREC_HS_STAMPS
+constexpr size_t kHsMaxLds = 160 * 1024 - 256;  // the stamp build's static per-wave slots take LDS too
+#else
 constexpr size_t kHsMaxLds = 160 * 1024;
+#endif
 
 // HS_FILTER: LDS bytes before the staged survivors (users, bounds, counts,
 // overflow marks, the staging counter), 16-B aligned
