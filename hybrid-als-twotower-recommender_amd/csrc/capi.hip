@@ -37,7 +37,11 @@ bool allow_max_lds_ptr(const void* kfn) {
   if (hipGetDevice(&dev) != hipSuccess) return false;
   std::lock_guard<std::mutex> lock(mu);
   if (done.count({dev, kfn})) return true;
-  if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
+  // the CU's 160 KiB less the kernel's static LDS (the attribute bounds the sum)
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, kfn) != hipSuccess) return false;
+  const int dyn = 160 * 1024 - (int)fa.sharedSizeBytes;
+  if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess) return false;
   done.insert({dev, kfn});
   return true;
 }
