@@ -55,6 +55,7 @@ constexpr int kHpCap = 8192;      // survivors per user (expected: a few hundred
 static_assert(kHpCap >= 256, "hp_cand_topk_kernel reads the first 256 slots unconditionally");
 constexpr int kHpMaxK = 8;        // top_k handled here (kFuseK of the exact path)
 constexpr int kHpMaxGroups = 16;  // heavy-model groups whose max slices seed the bound
+constexpr int kHpRankMax = 1024;  // survivor lists up to this long are ranked in LDS (hp_cand_topk_kernel)
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN): hrec_f32_to_bf16.
 __device__ __forceinline__ uint32_t hp_bf16(float v) {
@@ -161,21 +162,30 @@ __device__ __forceinline__ bool hp_better(double va, int64_t ia, double vb, int6
 // the k order of hyb_scores_kernel / dot_res_kernel (bit-identical scores).
 // A padding slot (item < 0) reads row 0; its result is dropped.
 template <int DK>
-__device__ __forceinline__ hp_f4 hp_gather_dot(const char* __restrict__ vbase, int64_t item, int64_t N, int g,
-                                               const HpFrag (&uf)[DK / 32]) {
+__device__ __forceinline__ void hp_gather_load(const char* __restrict__ vbase, int64_t item, int64_t N, int g,
+                                               HpFrag (&it)[DK / 32]) {
   constexpr int KS = DK / 32;
   // survivors are arbitrary rows: 64-bit addresses (a buffer resource spans at most 4 GiB)
   const char* row = vbase + (item >= 0 && item < N ? item : 0) * (int64_t)(DK * 2);
-  HpFrag it[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) it[ks].i = *reinterpret_cast<const int4*>(row + 16 * g + 64 * ks);
+}
+
+template <int DK>
+__device__ __forceinline__ hp_f4 hp_dot(const HpFrag (&it)[DK / 32], const HpFrag (&uf)[DK / 32]) {
   hp_f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+  for (int ks = 0; ks < DK / 32; ++ks)
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hp_bf8, it[ks].i),
                                                   __builtin_bit_cast(hp_bf8, uf[ks].i), acc, 0, 0, 0);
   return acc;
 }
+
+// Order point between a batch of row loads and the MFMAs that use them: left
+// to itself the scheduler interleaves each load with the MFMA of the one
+// before (a few loads in flight, one round trip per k-step); with every load
+// of the batch issued first, the batch costs one round trip.
+__device__ __forceinline__ void hp_loads_issued() { __builtin_amdgcn_sched_barrier(0); }
 
 __device__ __forceinline__ float hp_pick(const hp_f4& a, int r) {
   return r == 0 ? a[0] : (r == 1 ? a[1] : (r == 2 ? a[2] : a[3]));
@@ -206,9 +216,9 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
 #pragma clang fp contract(off)
   constexpr int KS = DK / 32;
   constexpr int kSlots = kHpMaxGroups * 16;  // <= 16 groups x (4 NI <= 16) items
-  __shared__ float smax[128];
+  __shared__ __attribute__((aligned(16))) float smax[128];
   __shared__ int sitem[kSlots];
-  __shared__ double sfl[kSlots];
+  __shared__ __attribute__((aligned(16))) double sfl[kSlots];
   __shared__ double s_tau;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -296,10 +306,16 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   if (tid < G) {
     const float v = smax[tid];
     if (v != -INFINITY) {
+      // all 128 slots (those >= G hold -inf, never counted): 32 broadcast
+      // 16-B reads in flight instead of a chain of G dependent ones
       int rank = 0;
-      for (int q = 0; q < G; ++q) {
-        const float o = smax[q];
-        rank += (o > v || (o == v && q < tid)) ? 1 : 0;
+#pragma unroll
+      for (int q = 0; q < 128; q += 4) {
+        const float4 o = *reinterpret_cast<const float4*>(smax + q);
+        rank += (o.x > v || (o.x == v && q < tid)) ? 1 : 0;
+        rank += (o.y > v || (o.y == v && q + 1 < tid)) ? 1 : 0;
+        rank += (o.z > v || (o.z == v && q + 2 < tid)) ? 1 : 0;
+        rank += (o.w > v || (o.w == v && q + 3 < tid)) ? 1 : 0;
       }
       if (rank < kHpMaxGroups) {
         const int pos = ap;
@@ -316,8 +332,8 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   }
   __syncthreads();
   HP_STAMP(3);
-  // exact fused scores of the seeds: 16 per MFMA group, both models, two
-  // groups' rows in flight per wave
+  // exact fused scores of the seeds: 16 per MFMA group, both models; wave w
+  // takes groups w and w + 8 (the second only when the slice holds 4 tiles)
   const char* vh = reinterpret_cast<const char*>(hm ? tt_items : als_items);
   const char* vl = reinterpret_cast<const char*>(hm ? als_items : tt_items);
   const int n_slots = kHpMaxGroups * per_g;
@@ -330,19 +346,23 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
       sfl[slot] = (it_s >= 0 && f == f) ? f : -INFINITY;
     }
   };
-  for (int q = wv; 16 * q < n_slots; q += 8) {
-    const int q2 = q + 4;
+  for (int q = wv; 16 * q < n_slots; q += 16) {
+    const int q2 = q + 8;
     const int item = sitem[16 * q + c];
     const int item2 = 16 * q2 < n_slots ? sitem[16 * q2 + c] : -1;
-    const hp_f4 ah = hp_gather_dot<DK>(vh, item, N, g, fh);
-    const hp_f4 al = hp_gather_dot<DK>(vl, item, N, g, fl);
+    HpFrag rh[KS], rl[KS];
+    hp_gather_load<DK>(vh, item, N, g, rh);
+    hp_gather_load<DK>(vl, item, N, g, rl);
     if (16 * q2 < n_slots) {  // wave-uniform
-      const hp_f4 ah2 = hp_gather_dot<DK>(vh, item2, N, g, fh);
-      const hp_f4 al2 = hp_gather_dot<DK>(vl, item2, N, g, fl);
-      seed(q, ah, al, item);
-      seed(q2, ah2, al2, item2);
+      HpFrag rh2[KS], rl2[KS];
+      hp_gather_load<DK>(vh, item2, N, g, rh2);
+      hp_gather_load<DK>(vl, item2, N, g, rl2);
+      hp_loads_issued();
+      seed(q, hp_dot<DK>(rh, fh), hp_dot<DK>(rl, fl), item);
+      seed(q2, hp_dot<DK>(rh2, fh), hp_dot<DK>(rl2, fl), item2);
     } else {
-      seed(q, ah, al, item);
+      hp_loads_issued();
+      seed(q, hp_dot<DK>(rh, fh), hp_dot<DK>(rl, fl), item);
     }
   }
   __syncthreads();
@@ -352,9 +372,13 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
     const double v = sfl[q];
     if (v == -INFINITY) continue;
     int rank = 0;
-    for (int o = 0; o < n_slots; ++o) {
-      const double x = sfl[o];
-      rank += (x > v || (x == v && o < q)) ? 1 : 0;
+    for (int o0 = 0; o0 < n_slots; o0 += 16) {  // n_slots: a multiple of 16; 8 broadcast 16-B reads in flight
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(sfl + o0 + e);
+        rank += (x.x > v || (x.x == v && o0 + e < q)) ? 1 : 0;
+        rank += (x.y > v || (x.y == v && o0 + e + 1 < q)) ? 1 : 0;
+      }
     }
     if (rank == kk - 1) s_tau = v;
   }
@@ -421,6 +445,13 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   __shared__ double rv[8 * KK];
   __shared__ int64_t ri[8 * KK];
   __shared__ int s_full;
+  // short lists (nb <= kHpRankMax): every survivor's fused score and item in
+  // LDS, ranked by counting (padding: NaN / INT32_MAX, never better)
+  __shared__ __attribute__((aligned(16))) double sv[kHpRankMax];
+  __shared__ __attribute__((aligned(16))) int si[kHpRankMax];
+  __shared__ double sel_v[KK];
+  __shared__ int64_t sel_i[KK];
+  __shared__ int s_bad;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   HP_STAMP_DECL;
@@ -540,13 +571,23 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   };
   HP_STAMP(1);
   reset();
+  const bool small = !flagged && nb <= kHpRankMax;  // block-uniform
+  if (tid == 0) s_bad = 0;
   if (!flagged) {
     // two survivor groups per wave in flight (q0, q0 + 8); the next pair's
     // ids and heavy scores load while this pair's rows are gathered
     auto take = [&](const hp_f4& acc, int q, int64_t item, float h) {
       const int p = 16 * q + hs;
       const int64_t pid = __shfl(item, hs, kWave);
-      if (c < 4 && p < nb) insert(fused(h, hp_pick(acc, c)), pid);
+      if (c < 4 && p < nb) {
+        const double f = fused(h, hp_pick(acc, c));
+        if (small) {
+          sv[p] = f;
+          si[p] = (int)pid;  // an item of the shard: < 2^31
+        } else {
+          insert(f, pid);
+        }
+      }
     };
     for (; 16 * q0 < nb; q0 += 16) {
       const int q1 = q0 + 8;
@@ -562,20 +603,64 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
           n_h1 = cvb[16 * (qn + 8) + hs];
         }
       }
-      const hp_f4 a0 = hp_gather_dot<DK>(vl, it0, N, g, uf);
+      HpFrag r0[KS];
+      hp_gather_load<DK>(vl, it0, N, g, r0);
       if (16 * q1 < nb) {  // wave-uniform
-        const hp_f4 a1 = hp_gather_dot<DK>(vl, it1, N, g, uf);
-        take(a0, q0, it0, h0);
-        take(a1, q1, it1, h1);
+        HpFrag r1[KS];
+        hp_gather_load<DK>(vl, it1, N, g, r1);
+        hp_loads_issued();
+        take(hp_dot<DK>(r0, uf), q0, it0, h0);
+        take(hp_dot<DK>(r1, uf), q1, it1, h1);
       } else {
-        take(a0, q0, it0, h0);
+        hp_loads_issued();
+        take(hp_dot<DK>(r0, uf), q0, it0, h0);
       }
     }
   }
   HP_STAMP(2);
-  merge(!flagged);
+  bool done;
+  if (small) {
+    // rank = the survivors better than this one (hp_better is a strict total
+    // order over distinct items); ranks < kk are the user's top kk in order
+    const int nbp = (nb + 7) & ~7;
+    for (int p = nb + tid; p < nbp; p += 512) {
+      sv[p] = __builtin_nan("");
+      si[p] = 0x7fffffff;
+    }
+    __syncthreads();
+    for (int p = tid; p < nb; p += 512) {
+      const double v = sv[p];
+      const int64_t i = si[p];
+      int rank = 0;
+      for (int o0 = 0; o0 < nbp; o0 += 8) {
+        const int4 ia = *reinterpret_cast<const int4*>(si + o0);
+        const int4 ib = *reinterpret_cast<const int4*>(si + o0 + 4);
+        const int io[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const double2 x = *reinterpret_cast<const double2*>(sv + o0 + e);
+          rank += hp_better(x.x, io[e], v, i) ? 1 : 0;
+          rank += hp_better(x.y, io[e + 1], v, i) ? 1 : 0;
+        }
+      }
+      if (rank < kk) {
+        sel_v[rank] = v;
+        sel_i[rank] = i;
+        if (v != v) s_bad = 1;  // a NaN among the kk: the exact path orders them
+      }
+    }
+    __syncthreads();
+    done = s_bad == 0;
+    if (done && tid < kk) {
+      out_idx[(int64_t)b * kk + tid] = sel_i[tid] + idx_offset;
+      out_val[(int64_t)b * kk + tid] = sel_v[tid];
+    }
+  } else {
+    merge(!flagged);
+    done = !flagged && s_full == 0;
+  }
   HP_STAMP(3);
-  if (!flagged && s_full == 0) {  // block-uniform
+  if (done) {  // block-uniform
     HP_STAMP_OUT(1);
     return;
   }
@@ -597,8 +682,12 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   reset();
   for (int64_t q = wv; 16 * q < N; q += 8) {
     const int64_t item = 16 * q + c < N ? 16 * q + c : -1;
-    const hp_f4 ah = hp_gather_dot<DK>(vh, item, N, g, uh);
-    const hp_f4 al = hp_gather_dot<DK>(vl, item, N, g, uf);
+    HpFrag rh[KS], rl[KS];
+    hp_gather_load<DK>(vh, item, N, g, rh);
+    hp_gather_load<DK>(vl, item, N, g, rl);
+    hp_loads_issued();
+    const hp_f4 ah = hp_dot<DK>(rh, uh);
+    const hp_f4 al = hp_dot<DK>(rl, uf);
     const int64_t p = 16 * q + hs;
     if (c < 4 && p < N) insert(fused(hp_pick(ah, c), hp_pick(al, c)), p);
   }
