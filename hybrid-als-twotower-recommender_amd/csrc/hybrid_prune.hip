@@ -332,8 +332,9 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   }
   __syncthreads();
   HP_STAMP(3);
-  // exact fused scores of the seeds: 16 per MFMA group, both models; wave w
-  // takes groups w and w + 8 (the second only when the slice holds 4 tiles)
+  // exact fused scores of the seeds: 16 per MFMA group, both models; the 4
+  // waves take groups (w, w + 4), then (w + 8, w + 12) when the slices hold 4
+  // tiles, all rows of a pair in flight at once
   const char* vh = reinterpret_cast<const char*>(hm ? tt_items : als_items);
   const char* vl = reinterpret_cast<const char*>(hm ? als_items : tt_items);
   const int n_slots = kHpMaxGroups * per_g;
@@ -346,8 +347,8 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
       sfl[slot] = (it_s >= 0 && f == f) ? f : -INFINITY;
     }
   };
-  for (int q = wv; 16 * q < n_slots; q += 16) {
-    const int q2 = q + 8;
+  for (int q = wv; 16 * q < n_slots; q += 8) {
+    const int q2 = q + 4;
     const int item = sitem[16 * q + c];
     const int item2 = 16 * q2 < n_slots ? sitem[16 * q2 + c] : -1;
     HpFrag rh[KS], rl[KS];
@@ -439,7 +440,8 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
                                                            const void* __restrict__ tt_items, int64_t N, int B,
                                                            const float* __restrict__ als_mm,
                                                            const float* __restrict__ tt_mm, double w0, double w1,
-                                                           int kk, int64_t idx_offset, int64_t* __restrict__ out_idx,
+                                                           int kk, int rank_max, int64_t idx_offset,
+                                                           int64_t* __restrict__ out_idx,
                                                            double* __restrict__ out_val, int* __restrict__ flag) {
   constexpr int KS = DK / 32, KK = kHpMaxK;
   __shared__ double rv[8 * KK];
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   };
   HP_STAMP(1);
   reset();
-  const bool small = !flagged && nb <= kHpRankMax;  // block-uniform
+  const bool small = !flagged && nb <= rank_max;  // block-uniform (rank_max <= kHpRankMax)
   if (tid == 0) s_bad = 0;
   if (!flagged) {
     // two survivor groups per wave in flight (q0, q0 + 8); the next pair's
@@ -717,6 +719,16 @@ static int hp_filter_choice() {
   return v;
 }
 
+// HREC_HP_RANK: 1 (default) = survivor lists up to kHpRankMax ranked in LDS,
+// 0 = every list through the per-lane lists and the wave merges
+static int hp_rank_max() {
+  static const int v = [] {
+    const char* e = getenv("HREC_HP_RANK");
+    return (e && atoi(e) == 0) ? 0 : kHpRankMax;
+  }();
+  return v;
+}
+
 static HpWs hp_layout(char* base, int B, int64_t N, int dk, int kk) {
   HpWs w{};
   size_t off = 0;
@@ -851,7 +863,7 @@ static int hp_phase2(bool local, int n_users, const void* als_items, const void*
 #define HREC_HP_CAND(DK)                                                                                           \
   hipLaunchKernelGGL(hp_cand_topk_kernel<DK>, dim3((unsigned)n_users), dim3(512), 0, s, w.cn, kHpCap, w.cv, w.ci,   \
                      w.uflag, w.uop, hm, als_items, tt_items, n_items, n_users, amm, tmm, w0, w1, kk,              \
-                     idx_offset, out_idx, out_val, w.flag)
+                     hp_rank_max(), idx_offset, out_idx, out_val, w.flag)
   switch (dk) {
     case 64: HREC_HP_CAND(64); break;
     case 128: HREC_HP_CAND(128); break;
