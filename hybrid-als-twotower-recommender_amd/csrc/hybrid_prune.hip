@@ -55,7 +55,7 @@ constexpr int kHpCap = 8192;      // survivors per user (expected: a few hundred
 static_assert(kHpCap >= 256, "hp_cand_topk_kernel reads the first 256 slots unconditionally");
 constexpr int kHpMaxK = 8;        // top_k handled here (kFuseK of the exact path)
 constexpr int kHpMaxGroups = 16;  // heavy-model groups whose max slices seed the bound
-constexpr int kHpRankMax = 1024;  // survivor lists up to this long are ranked in LDS (hp_cand_topk_kernel)
+constexpr int kHpRankMax = 512;  // survivor lists up to this long are ranked in LDS (hp_cand_topk_kernel)
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN): hrec_f32_to_bf16.
 __device__ __forceinline__ uint32_t hp_bf16(float v) {
@@ -155,6 +155,15 @@ __device__ __forceinline__ bool hp_better(double va, int64_t ia, double vb, int6
   const bool na = va != va, nb = vb != vb;
   if (na || nb) return !na && nb ? true : (na && nb ? ia < ib : false);
   return va > vb || (va == vb && ia < ib);
+}
+
+// hp_better as 0 / 1 without branches (the LDS ranking evaluates it for
+// every pair: a branch per pair would also wait for each read)
+__device__ __forceinline__ int hp_better_bits(double va, int ia, double vb, int64_t ib) {
+  const int na = (int)(va != va), nb = (int)(vb != vb), lt = (int)((int64_t)ia < ib);
+  const int num = (1 - na) & (1 - nb) & ((int)(va > vb) | ((int)(va == vb) & lt));
+  const int nan = ((1 - na) & nb) | (na & nb & lt);
+  return num | nan;
 }
 
 // 16 gathered item rows (A, row c = item c) against one user row (B, every
@@ -312,10 +321,11 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
 #pragma unroll
       for (int q = 0; q < 128; q += 4) {
         const float4 o = *reinterpret_cast<const float4*>(smax + q);
-        rank += (o.x > v || (o.x == v && q < tid)) ? 1 : 0;
-        rank += (o.y > v || (o.y == v && q + 1 < tid)) ? 1 : 0;
-        rank += (o.z > v || (o.z == v && q + 2 < tid)) ? 1 : 0;
-        rank += (o.w > v || (o.w == v && q + 3 < tid)) ? 1 : 0;
+        // non-short-circuit forms: a branch per element would wait for each read
+        rank += (int)(o.x > v) | ((int)(o.x == v) & (int)(q < tid));
+        rank += (int)(o.y > v) | ((int)(o.y == v) & (int)(q + 1 < tid));
+        rank += (int)(o.z > v) | ((int)(o.z == v) & (int)(q + 2 < tid));
+        rank += (int)(o.w > v) | ((int)(o.w == v) & (int)(q + 3 < tid));
       }
       if (rank < kHpMaxGroups) {
         const int pos = ap;
@@ -377,8 +387,8 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {
         const double2 x = *reinterpret_cast<const double2*>(sfl + o0 + e);
-        rank += (x.x > v || (x.x == v && o0 + e < q)) ? 1 : 0;
-        rank += (x.y > v || (x.y == v && o0 + e + 1 < q)) ? 1 : 0;
+        rank += (int)(x.x > v) | ((int)(x.x == v) & (int)(o0 + e < q));
+        rank += (int)(x.y > v) | ((int)(x.y == v) & (int)(o0 + e + 1 < q));
       }
     }
     if (rank == kk - 1) s_tau = v;
@@ -641,8 +651,8 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           const double2 x = *reinterpret_cast<const double2*>(sv + o0 + e);
-          rank += hp_better(x.x, io[e], v, i) ? 1 : 0;
-          rank += hp_better(x.y, io[e + 1], v, i) ? 1 : 0;
+          rank += hp_better_bits(x.x, io[e], v, i);
+          rank += hp_better_bits(x.y, io[e + 1], v, i);
         }
       }
       if (rank < kk) {
