@@ -461,6 +461,7 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   // LDS, ranked by counting (padding: NaN / INT32_MAX, never better)
   __shared__ __attribute__((aligned(16))) double sv[kHpRankMax];
   __shared__ __attribute__((aligned(16))) int si[kHpRankMax];
+  __shared__ int rk_cnt[kHpRankMax];
   __shared__ double sel_v[KK];
   __shared__ int64_t sel_i[KK];
   __shared__ int s_bad;
@@ -639,25 +640,38 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
       sv[p] = __builtin_nan("");
       si[p] = 0x7fffffff;
     }
+    for (int p = tid; p < nb; p += 512) rk_cnt[p] = 0;
     __syncthreads();
-    for (int p = tid; p < nb; p += 512) {
+    // S threads per survivor (nb * S <= 512), each counting over a 1/S slice
+    // of the list (a multiple of 8 entries), summed by LDS atomics
+    const int S = nb >= 512 ? 1 : 512 / nb;
+    const int seg_len = (nbp / S + 7) & ~7;
+    if (tid < nb * S) {
+      const int p = tid / S, seg = tid - p * S;
       const double v = sv[p];
       const int64_t i = si[p];
-      int rank = 0;
-      for (int o0 = 0; o0 < nbp; o0 += 8) {
+      const int o_end = (seg + 1) * seg_len < nbp ? (seg + 1) * seg_len : nbp;
+      int part = 0;
+      for (int o0 = seg * seg_len; o0 < o_end; o0 += 8) {
         const int4 ia = *reinterpret_cast<const int4*>(si + o0);
         const int4 ib = *reinterpret_cast<const int4*>(si + o0 + 4);
         const int io[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           const double2 x = *reinterpret_cast<const double2*>(sv + o0 + e);
-          rank += hp_better_bits(x.x, io[e], v, i);
-          rank += hp_better_bits(x.y, io[e + 1], v, i);
+          part += hp_better_bits(x.x, io[e], v, i);
+          part += hp_better_bits(x.y, io[e + 1], v, i);
         }
       }
+      if (part) atomicAdd(&rk_cnt[p], part);
+    }
+    __syncthreads();
+    for (int p = tid; p < nb; p += 512) {
+      const int rank = rk_cnt[p];
       if (rank < kk) {
+        const double v = sv[p];
         sel_v[rank] = v;
-        sel_i[rank] = i;
+        sel_i[rank] = si[p];
         if (v != v) s_bad = 1;  // a NaN among the kk: the exact path orders them
       }
     }

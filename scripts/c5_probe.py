@@ -37,5 +37,8 @@ for _ in range(reps):
     rec5.recommend(hu5, uv5, False, 5)
 e.record()
 torch.cuda.synchronize()
+sv = rec5.last_prune.survivors().double()
+q = torch.quantile(sv.cpu(), torch.tensor([0.5, 0.9, 0.99], dtype=torch.float64)).tolist()
 print(f"c5 batch {s.elapsed_time(e) / reps * 1e3:.1f} us, fallback {rec5.last_prune.fallback_taken()}, "
-      f"survivors mean {rec5.last_prune.survivors().double().mean().item():.0f}", flush=True)
+      f"survivors mean {sv.mean().item():.0f} (p50 {q[0]:.0f}, p90 {q[1]:.0f}, p99 {q[2]:.0f}, "
+      f"max {sv.max().item():.0f})", flush=True)
