@@ -645,7 +645,7 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
     // S threads per survivor (nb * S <= 512), each counting over a 1/S slice
     // of the list (a multiple of 8 entries), summed by LDS atomics
     const int S = nb >= 512 ? 1 : 512 / nb;
-    const int seg_len = (nbp / S + 7) & ~7;
+    const int seg_len = ((nbp + S - 1) / S + 7) & ~7;  // >= 8: S * seg_len >= nbp
     if (tid < nb * S) {
       const int p = tid / S, seg = tid - p * S;
       const double v = sv[p];
