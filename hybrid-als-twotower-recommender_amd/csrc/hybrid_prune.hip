@@ -55,7 +55,6 @@ constexpr int kHpCap = 8192;      // survivors per user (expected: a few hundred
 static_assert(kHpCap >= 256, "hp_cand_topk_kernel reads the first 256 slots unconditionally");
 constexpr int kHpMaxK = 8;        // top_k handled here (kFuseK of the exact path)
 constexpr int kHpMaxGroups = 16;  // heavy-model groups whose max slices seed the bound
-constexpr int kHpRankMax = 512;  // survivor lists up to this long are ranked in LDS (hp_cand_topk_kernel)
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN): hrec_f32_to_bf16.
 __device__ __forceinline__ uint32_t hp_bf16(float v) {
@@ -155,15 +154,6 @@ __device__ __forceinline__ bool hp_better(double va, int64_t ia, double vb, int6
   const bool na = va != va, nb = vb != vb;
   if (na || nb) return !na && nb ? true : (na && nb ? ia < ib : false);
   return va > vb || (va == vb && ia < ib);
-}
-
-// hp_better as 0 / 1 without branches (the LDS ranking evaluates it for
-// every pair: a branch per pair would also wait for each read)
-__device__ __forceinline__ int hp_better_bits(double va, int ia, double vb, int64_t ib) {
-  const int na = (int)(va != va), nb = (int)(vb != vb), lt = (int)((int64_t)ia < ib);
-  const int num = (1 - na) & (1 - nb) & ((int)(va > vb) | ((int)(va == vb) & lt));
-  const int nan = ((1 - na) & nb) | (na & nb & lt);
-  return num | nan;
 }
 
 // 16 gathered item rows (A, row c = item c) against one user row (B, every
@@ -450,21 +440,12 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
                                                            const void* __restrict__ tt_items, int64_t N, int B,
                                                            const float* __restrict__ als_mm,
                                                            const float* __restrict__ tt_mm, double w0, double w1,
-                                                           int kk, int rank_max, int64_t idx_offset,
-                                                           int64_t* __restrict__ out_idx,
+                                                           int kk, int64_t idx_offset, int64_t* __restrict__ out_idx,
                                                            double* __restrict__ out_val, int* __restrict__ flag) {
   constexpr int KS = DK / 32, KK = kHpMaxK;
   __shared__ double rv[8 * KK];
   __shared__ int64_t ri[8 * KK];
   __shared__ int s_full;
-  // short lists (nb <= kHpRankMax): every survivor's fused score and item in
-  // LDS, ranked by counting (padding: NaN / INT32_MAX, never better)
-  __shared__ __attribute__((aligned(16))) double sv[kHpRankMax];
-  __shared__ __attribute__((aligned(16))) int si[kHpRankMax];
-  __shared__ int rk_cnt[kHpRankMax];
-  __shared__ double sel_v[KK];
-  __shared__ int64_t sel_i[KK];
-  __shared__ int s_bad;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   HP_STAMP_DECL;
@@ -584,23 +565,13 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   };
   HP_STAMP(1);
   reset();
-  const bool small = !flagged && nb <= rank_max;  // block-uniform (rank_max <= kHpRankMax)
-  if (tid == 0) s_bad = 0;
   if (!flagged) {
     // two survivor groups per wave in flight (q0, q0 + 8); the next pair's
     // ids and heavy scores load while this pair's rows are gathered
     auto take = [&](const hp_f4& acc, int q, int64_t item, float h) {
       const int p = 16 * q + hs;
       const int64_t pid = __shfl(item, hs, kWave);
-      if (c < 4 && p < nb) {
-        const double f = fused(h, hp_pick(acc, c));
-        if (small) {
-          sv[p] = f;
-          si[p] = (int)pid;  // an item of the shard: < 2^31
-        } else {
-          insert(f, pid);
-        }
-      }
+      if (c < 4 && p < nb) insert(fused(h, hp_pick(acc, c)), pid);
     };
     for (; 16 * q0 < nb; q0 += 16) {
       const int q1 = q0 + 8;
@@ -631,60 +602,8 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
     }
   }
   HP_STAMP(2);
-  bool done;
-  if (small) {
-    // rank = the survivors better than this one (hp_better is a strict total
-    // order over distinct items); ranks < kk are the user's top kk in order
-    const int nbp = (nb + 7) & ~7;
-    for (int p = nb + tid; p < nbp; p += 512) {
-      sv[p] = __builtin_nan("");
-      si[p] = 0x7fffffff;
-    }
-    for (int p = tid; p < nb; p += 512) rk_cnt[p] = 0;
-    __syncthreads();
-    // S threads per survivor (nb * S <= 512), each counting over a 1/S slice
-    // of the list (a multiple of 8 entries), summed by LDS atomics
-    const int S = nb >= 512 ? 1 : 512 / nb;
-    const int seg_len = ((nbp + S - 1) / S + 7) & ~7;  // >= 8: S * seg_len >= nbp
-    if (tid < nb * S) {
-      const int p = tid / S, seg = tid - p * S;
-      const double v = sv[p];
-      const int64_t i = si[p];
-      const int o_end = (seg + 1) * seg_len < nbp ? (seg + 1) * seg_len : nbp;
-      int part = 0;
-      for (int o0 = seg * seg_len; o0 < o_end; o0 += 8) {
-        const int4 ia = *reinterpret_cast<const int4*>(si + o0);
-        const int4 ib = *reinterpret_cast<const int4*>(si + o0 + 4);
-        const int io[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const double2 x = *reinterpret_cast<const double2*>(sv + o0 + e);
-          part += hp_better_bits(x.x, io[e], v, i);
-          part += hp_better_bits(x.y, io[e + 1], v, i);
-        }
-      }
-      if (part) atomicAdd(&rk_cnt[p], part);
-    }
-    __syncthreads();
-    for (int p = tid; p < nb; p += 512) {
-      const int rank = rk_cnt[p];
-      if (rank < kk) {
-        const double v = sv[p];
-        sel_v[rank] = v;
-        sel_i[rank] = si[p];
-        if (v != v) s_bad = 1;  // a NaN among the kk: the exact path orders them
-      }
-    }
-    __syncthreads();
-    done = s_bad == 0;
-    if (done && tid < kk) {
-      out_idx[(int64_t)b * kk + tid] = sel_i[tid] + idx_offset;
-      out_val[(int64_t)b * kk + tid] = sel_v[tid];
-    }
-  } else {
-    merge(!flagged);
-    done = !flagged && s_full == 0;
-  }
+  merge(!flagged);
+  const bool done = !flagged && s_full == 0;
   HP_STAMP(3);
   if (done) {  // block-uniform
     HP_STAMP_OUT(1);
@@ -739,16 +658,6 @@ static int hp_filter_choice() {
   static const int v = [] {
     const char* e = getenv("HREC_HP_FILTER");
     return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-// HREC_HP_RANK: 1 (default) = survivor lists up to kHpRankMax ranked in LDS,
-// 0 = every list through the per-lane lists and the wave merges
-static int hp_rank_max() {
-  static const int v = [] {
-    const char* e = getenv("HREC_HP_RANK");
-    return (e && atoi(e) == 0) ? 0 : kHpRankMax;
   }();
   return v;
 }
@@ -887,7 +796,7 @@ static int hp_phase2(bool local, int n_users, const void* als_items, const void*
 #define HREC_HP_CAND(DK)                                                                                           \
   hipLaunchKernelGGL(hp_cand_topk_kernel<DK>, dim3((unsigned)n_users), dim3(512), 0, s, w.cn, kHpCap, w.cv, w.ci,   \
                      w.uflag, w.uop, hm, als_items, tt_items, n_items, n_users, amm, tmm, w0, w1, kk,              \
-                     hp_rank_max(), idx_offset, out_idx, out_val, w.flag)
+                     idx_offset, out_idx, out_val, w.flag)
   switch (dk) {
     case 64: HREC_HP_CAND(64); break;
     case 128: HREC_HP_CAND(128); break;
