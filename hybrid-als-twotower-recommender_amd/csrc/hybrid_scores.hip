@@ -585,17 +585,19 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
 
 // ---------------------------------------------------------------- K9s2
 // The d = 256 pruned passes (HS_PRUNE, HS_FILTER) with the roles turned
-// round: a 4-wave block (one wave per SIMD) keeps its <= 256 users' bf16
-// fragments in REGISTERS (wave w: users 64 w .. 64 w + 63, 128 VGPRs) and
-// streams the item range through an LDS ring of kStStages 16-item tiles,
-// filled by LDS-DMA (global_load_lds_dwordx4: no VGPRs, one tile issued per
-// tile consumed, kStStages - 1 tiles in flight across the barriers). Each
-// item fragment read from LDS feeds 4 MFMAs (the user tiles), half the LDS
-// traffic per MFMA of hyb_scores_kernel, and no wave waits on its own item
-// loads. Same MFMA chains (A = items, B = users, k-steps ascending), so the
-// same scores; the same slices (32 items = 2 tiles) for the per-block max
-// position; the same survivor staging and flush.
-constexpr int kStThreads = 256;
+// round: the block's <= 256 users' bf16 fragments stay in REGISTERS (wave
+// w and w + 4: users 64 (w & 3) .. + 63, 128 VGPRs) and the item range
+// streams through an LDS ring of kStStages 16-item tiles filled by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs; kStStages - 2 tiles in flight across
+// the barriers). Waves 0-3 take the even tiles, waves 4-7 the odd ones, so
+// each SIMD runs two independent MFMA streams. Each item fragment read from
+// LDS feeds 4 MFMAs (the user tiles), half the LDS traffic per MFMA of
+// hyb_scores_kernel. Same MFMA chains (A = items, B = users, k-steps
+// ascending), so the same scores; the same slices (32 items = 2 tiles) for
+// the per-block max position (the two wave groups' results are folded with
+// the same rule: larger max, then the smaller position); the same survivor
+// staging and flush.
+constexpr int kStThreads = 512;
 constexpr int kStStages = 8;
 constexpr int kStRowB = 512;             // one d = 256 bf16 item row
 constexpr int kStTileB = 16 * kStRowB;   // 8 KiB: one 16-item tile
@@ -625,8 +627,9 @@ __device__ __forceinline__ void hs_glds16(const void* src, uint32_t lds) {
       : "memory");
 }
 
-// LDS bytes of the stream kernel's filter head (bounds, counts, overflow
-// marks, the staging counter), 16-B aligned, after the ring
+// LDS bytes after the ring: HS_FILTER's head (bounds, counts, overflow marks,
+// the staging counter) or HS_PRUNE's hand-over of the odd-tile waves'
+// extremes (min, max, position per user), 16-B aligned
 __host__ __device__ inline size_t hs_stream_head(int UB) { return ((size_t)UB * 12 + 4 + 15) & ~(size_t)15; }
 
 template <int MODE>
@@ -644,6 +647,7 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
   float* sb_val = reinterpret_cast<float*>(sb_meta + a.sbuf);
   int* sb_rank = reinterpret_cast<int*>(sb_val + a.sbuf);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wu = w & 3, par = w >> 2;  // user quarter, tile parity
   const int g = lane >> 4, c = lane & 15;
   const int model = MODE == HS_FILTER ? a.hm : (blockIdx.x & 1);
   const int rest = MODE == HS_FILTER ? (int)blockIdx.x : (int)(blockIdx.x >> 1);
@@ -680,43 +684,40 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
     if (threadIdx.x == 0) *bn = 0;
     __syncthreads();  // before any LDS-DMA is in flight (this barrier waits for every load)
   }
-  // this wave's users: fragments of user 64 w + 16 u + c, k-chunk g (B operands)
+  // this wave's users: fragments of user 64 wu + 16 u + c, k-chunk g (B
+  // operands); rows past the batch load row 0 and are zeroed (their scores
+  // are never used)
   HsFrag uf[NU][KS];
   float th[NU];
   {
     const char* ub_base = reinterpret_cast<const char*>(a.uop) + ((int64_t)model * a.B + b0) * (DK * 2);
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int bl = 64 * w + 16 * u + c;
+      const int bl = 64 * wu + 16 * u + c;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {  // unconditional loads (row 0 past the batch), zeroed after
+      for (int ks = 0; ks < KS; ++ks) {
         const int4 v = *reinterpret_cast<const int4*>(ub_base + (int64_t)(bl < ub ? bl : 0) * (DK * 2) + 64 * ks + 16 * g);
         uf[u][ks].i = bl < ub ? v : int4{0, 0, 0, 0};
       }
       if constexpr (MODE == HS_FILTER) th[u] = bl < ub ? ths[bl] : __builtin_nanf("");  // NaN: nothing passes
     }
   }
-  // tile t -> ring stage t % kStStages: wave w issues the 1-KiB pieces 2 w,
-  // 2 w + 1 (rows 4 w .. 4 w + 3). LDS slot 32 r + s (16 B) of a tile holds
-  // chunk s ^ (r & 15) of row r (XOR swizzle on the SOURCE address: the
-  // DMA writes lane-linear), so the 16 rows a ds_read_b128 touches fall in
-  // distinct banks. Tiles past the range re-read the last one (a uniform
+  // tile t -> ring stage t % kStStages; every wave issues piece w (1 KiB =
+  // rows 2 w, 2 w + 1) of every tile. LDS slot 32 r + s (16 B) of a tile
+  // holds chunk s ^ (r & 15) of row r (XOR swizzle on the SOURCE address:
+  // the DMA writes lane-linear), so the 16 rows a ds_read_b128 touches fall
+  // in distinct banks. Tiles past the range re-read the last one (a uniform
   // number of loads per iteration keeps the counted waits constant).
   const char* items = a.items[model];
   const uint32_t ring_lds = (uint32_t)(uintptr_t)(hs_lds_char*)ring;
+  const int slot = 64 * w + lane;
+  const int sr = slot >> 5, ssl = slot & 31;
   auto issue = [&](int t) {
     const int tt = t < T ? t : T - 1;
-    const uint32_t dst = ring_lds + (uint32_t)((t % kStStages) * kStTileB);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int piece = 2 * w + h;
-      const int slot = 64 * piece + lane;
-      const int r = slot >> 5, sl = slot & 31;
-      int64_t j = i0 + 16 * (int64_t)tt + r;
-      j = j < i1 ? j : i1 - 1;
-      const char* src = items + j * kStRowB + 16 * (sl ^ (r & 15));
-      hs_glds16(src, __builtin_amdgcn_readfirstlane(dst + (uint32_t)piece * 1024u));
-    }
+    int64_t j = i0 + 16 * (int64_t)tt + sr;
+    j = j < i1 ? j : i1 - 1;
+    const char* src = items + j * kStRowB + 16 * (ssl ^ (sr & 15));
+    hs_glds16(src, __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)((t % kStStages) * kStTileB + w * 1024)));
   };
   float lo[NU], hi[NU];
   int hp[NU];
@@ -727,62 +728,70 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
     hp[u] = -1;
   }
   if (T > 0 && ub > 0) {  // block-uniform
+    // prologue: tiles 0 .. kStStages - 3; iteration i consumes tiles 2 i
+    // (waves 0-3) and 2 i + 1 (waves 4-7) and issues 2 i + kStStages - 2,
+    // 2 i + kStStages - 1 into the stages iteration i - 1 read
 #pragma unroll
-    for (int t = 0; t < kStStages - 1; ++t) issue(t);
-    for (int t = 0; t < T; ++t) {
-      // tile t landed: this wave's pieces by the counted wait (2 per tile,
-      // kStStages - 2 tiles stay in flight), every wave's by the barrier,
-      // which also retires every read of the stage refilled next
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * (kStStages - 2)) : "memory");
+    for (int t = 0; t < kStStages - 2; ++t) issue(t);
+    const int iters = (T + 1) / 2;
+    for (int i = 0; i < iters; ++i) {
+      // tiles 2 i, 2 i + 1 landed: this wave's pieces by the counted wait
+      // (kStStages - 4 tiles stay in flight), every wave's by the barrier,
+      // which also retires every read of the stages refilled next
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kStStages - 4) : "memory");
       __builtin_amdgcn_s_barrier();
-      issue(t + kStStages - 1);
-      const char* tile = ring + (t % kStStages) * kStTileB;
-      hs_f4 acc[NU];
+      issue(2 * i + kStStages - 2);
+      issue(2 * i + kStStages - 1);
+      const int t = 2 * i + par;
+      if (t < T) {  // wave-uniform
+        const char* tile = ring + (t % kStStages) * kStTileB;
+        hs_f4 acc[NU];
 #pragma unroll
-      for (int u = 0; u < NU; ++u) acc[u] = hs_f4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < NU; ++u) acc[u] = hs_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        HsFrag it;
-        it.i = *reinterpret_cast<const int4*>(tile + c * kStRowB + 16 * ((4 * ks + g) ^ c));
+        for (int ks = 0; ks < KS; ++ks) {
+          HsFrag it;
+          it.i = *reinterpret_cast<const int4*>(tile + c * kStRowB + 16 * ((4 * ks + g) ^ c));
 #pragma unroll
-        for (int u = 0; u < NU; ++u)
-          acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it.i),
-                                                           __builtin_bit_cast(hs_bf8, uf[u][ks].i), acc[u], 0, 0, 0);
-      }
-      // C/D: lane holds user 64 w + 16 u + c, items i0 + 16 t + 4 g + r
-      const int64_t jt = i0 + 16 * (int64_t)t;
-      const bool full = jt + 16 <= i1;  // block-uniform
+          for (int u = 0; u < NU; ++u)
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it.i),
+                                                             __builtin_bit_cast(hs_bf8, uf[u][ks].i), acc[u], 0, 0, 0);
+        }
+        // C/D: lane holds user 64 wu + 16 u + c, items i0 + 16 t + 4 g + r
+        const int64_t jt = i0 + 16 * (int64_t)t;
+        const bool full = jt + 16 <= i1;  // wave-uniform
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        float mx = -__builtin_inff(), mn = __builtin_inff();
+        for (int u = 0; u < NU; ++u) {
+          float mx = -__builtin_inff(), mn = __builtin_inff();
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (full || jt + 4 * g + r < i1) {
-            mx = fmaxf(mx, acc[u][r]);
-            mn = fminf(mn, acc[u][r]);
-          }
-        if constexpr (MODE == HS_PRUNE) {
-          lo[u] = fminf(lo[u], mn);
-          // slice (32 items = tiles 2 m, 2 m + 1) of the lane's max: the
-          // earlier slice on ties, as hyb_scores_kernel's strict compare
-          const bool gt = mx > hi[u];
-          hi[u] = gt ? mx : hi[u];
-          hp[u] = gt ? (int)((i0 + 32 * (int64_t)(t >> 1)) >> 4) : hp[u];
-        } else {
-          if (__ballot(mx >= th[u])) {  // rare: stage this lane's survivors
-            const int bl = 64 * w + 16 * u + c;
+          for (int r = 0; r < 4; ++r)
+            if (full || jt + 4 * g + r < i1) {
+              mx = fmaxf(mx, acc[u][r]);
+              mn = fminf(mn, acc[u][r]);
+            }
+          if constexpr (MODE == HS_PRUNE) {
+            lo[u] = fminf(lo[u], mn);
+            // slice (32 items = tiles 2 m, 2 m + 1) of the lane's max: the
+            // earlier slice on ties, as hyb_scores_kernel's strict compare
+            const bool gt = mx > hi[u];
+            hi[u] = gt ? mx : hi[u];
+            hp[u] = gt ? (int)((i0 + 32 * (int64_t)(t >> 1)) >> 4) : hp[u];
+          } else {
+            if (__ballot(mx >= th[u])) {  // rare: stage this lane's survivors
+              const int bl = 64 * wu + 16 * u + c;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int64_t j = jt + 4 * g + r;
-              if ((full || j < i1) && acc[u][r] >= th[u]) {
-                const int e = atomicAdd(bn, 1);
-                const int rk = atomicAdd(&cnt_l[bl], 1);
-                if (e < a.sbuf) {
-                  sb_meta[e] = ((uint32_t)bl << 24) | (uint32_t)(j - i0);
-                  sb_val[e] = acc[u][r];
-                  sb_rank[e] = rk;
-                } else {
-                  ovf_l[bl] = 1;  // staging full: the user's list is marked overflowing at the flush
+              for (int r = 0; r < 4; ++r) {
+                const int64_t j = jt + 4 * g + r;
+                if ((full || j < i1) && acc[u][r] >= th[u]) {
+                  const int e = atomicAdd(bn, 1);
+                  const int rk = atomicAdd(&cnt_l[bl], 1);
+                  if (e < a.sbuf) {
+                    sb_meta[e] = ((uint32_t)bl << 24) | (uint32_t)(j - i0);
+                    sb_val[e] = acc[u][r];
+                    sb_rank[e] = rk;
+                  } else {
+                    ovf_l[bl] = 1;  // staging full: the user's list is marked overflowing at the flush
+                  }
                 }
               }
             }
@@ -790,7 +799,7 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the LDS goes
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the LDS is reused
   }
   if constexpr (MODE == HS_FILTER) {
     // flush: one list reservation per user (global atomic), then the entries
@@ -821,26 +830,56 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
     }
   } else {
     // per user: fold the 4 lane groups (min; larger max, then the smaller
-    // position slice * 4 + g) and write the block's partials
+    // position slice * 4 + g), the odd-tile waves hand theirs over in LDS,
+    // the even-tile waves fold them in and write the block's partials
+    float* xl = reinterpret_cast<float*>(head);
+    float* xh = xl + a.UB;
+    int* xp = reinterpret_cast<int*>(xh + a.UB);
+    float l[NU], h[NU];
+    int p[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      float l = lo[u], h = hi[u];
-      int p = hp[u] < 0 ? 0x7fffffff : hp[u] * 4 + g;
+      l[u] = lo[u];
+      h[u] = hi[u];
+      p[u] = hp[u] < 0 ? 0x7fffffff : hp[u] * 4 + g;
 #pragma unroll
       for (int off = 16; off < 64; off <<= 1) {
-        l = fminf(l, __shfl_xor(l, off, kWave));
-        const float oh = __shfl_xor(h, off, kWave);
-        const int op = __shfl_xor(p, off, kWave);
-        const bool take = oh > h || (oh == h && op < p);
-        h = take ? oh : h;
-        p = take ? op : p;
+        l[u] = fminf(l[u], __shfl_xor(l[u], off, kWave));
+        const float oh = __shfl_xor(h[u], off, kWave);
+        const int op = __shfl_xor(p[u], off, kWave);
+        const bool take = oh > h[u] || (oh == h[u] && op < p[u]);
+        h[u] = take ? oh : h[u];
+        p[u] = take ? op : p[u];
       }
-      const int bl = 64 * w + 16 * u + c;
-      if (g == 0 && bl < ub) {
-        float* pp = a.part + ((int64_t)(model * a.G + grp) * 2) * a.B + b0 + bl;
-        pp[0] = l;
-        pp[a.B] = h;
-        a.argpos[(int64_t)(model * a.G + grp) * a.B + b0 + bl] = p == 0x7fffffff ? -1 : p;
+    }
+    if (par == 1 && g == 0) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int bl = 64 * wu + 16 * u + c;
+        if (bl < a.UB) {
+          xl[bl] = l[u];
+          xh[bl] = h[u];
+          xp[bl] = p[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (par == 0 && g == 0) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int bl = 64 * wu + 16 * u + c;
+        if (bl < ub) {
+          const float ol = xl[bl], oh = xh[bl];
+          const int op = xp[bl];
+          const float fl = fminf(l[u], ol);
+          const bool take = oh > h[u] || (oh == h[u] && op < p[u]);
+          const float fh = take ? oh : h[u];
+          const int fp = take ? op : p[u];
+          float* pp = a.part + ((int64_t)(model * a.G + grp) * 2) * a.B + b0 + bl;
+          pp[0] = fl;
+          pp[a.B] = fh;
+          a.argpos[(int64_t)(model * a.G + grp) * a.B + b0 + bl] = fp == 0x7fffffff ? -1 : fp;
+        }
       }
     }
   }
@@ -932,7 +971,7 @@ static int hs_stream_launch(HybScoresArgs& a, hipStream_t s) {
   const int n_ut = (a.B + 255) / 256;
   a.UB = (a.B + n_ut - 1) / n_ut;
   a.n_ut = n_ut;
-  size_t lds = (size_t)kStStages * kStTileB;
+  size_t lds = (size_t)kStStages * kStTileB + hs_stream_head(a.UB);  // PRUNE: the hand-over after the ring
   int blocks = 2 * a.n_ut * a.G;
   if (MODE == HS_FILTER) {
     const size_t head = lds + hs_stream_head(a.UB);
