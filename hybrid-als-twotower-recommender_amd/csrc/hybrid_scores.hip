@@ -598,7 +598,11 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
 // the same rule: larger max, then the smaller position); the same survivor
 // staging and flush.
 constexpr int kStThreads = 512;
-constexpr int kStStages = 8;
+// ring stages: HS_PRUNE 16 (128 KiB, 14 tiles in flight per CU: enough bytes
+// to cover the HBM latency at the full rate), HS_FILTER 12 (the rest of the
+// LDS stages survivors)
+template <int MODE>
+constexpr int st_stages() { return MODE == HS_PRUNE ? 16 : 12; }
 constexpr int kStRowB = 512;             // one d = 256 bf16 item row
 constexpr int kStTileB = 16 * kStRowB;   // 8 KiB: one 16-item tile
 
@@ -634,7 +638,7 @@ __host__ __device__ inline size_t hs_stream_head(int UB) { return ((size_t)UB * 
 
 template <int MODE>
 __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a) {
-  constexpr int DK = 256, KS = DK / 32, NU = 4;
+  constexpr int DK = 256, KS = DK / 32, NU = 4, kStStages = st_stages<MODE>();
   static_assert(MODE == HS_PRUNE || MODE == HS_FILTER, "the stream kernel has no score stores");
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   char* ring = dsm;
@@ -971,10 +975,10 @@ static int hs_stream_launch(HybScoresArgs& a, hipStream_t s) {
   const int n_ut = (a.B + 255) / 256;
   a.UB = (a.B + n_ut - 1) / n_ut;
   a.n_ut = n_ut;
-  size_t lds = (size_t)kStStages * kStTileB + hs_stream_head(a.UB);  // PRUNE: the hand-over after the ring
+  size_t lds = (size_t)st_stages<MODE>() * kStTileB + hs_stream_head(a.UB);  // PRUNE: the hand-over after the ring
   int blocks = 2 * a.n_ut * a.G;
   if (MODE == HS_FILTER) {
-    const size_t head = lds + hs_stream_head(a.UB);
+    const size_t head = lds;  // ring + the filter head
     a.sbuf = head < kHsMaxLds ? (int)((kHsMaxLds - head) / 12) : 0;
     if (a.sbuf > 8192) a.sbuf = 8192;
     lds = head + (size_t)a.sbuf * 12;
