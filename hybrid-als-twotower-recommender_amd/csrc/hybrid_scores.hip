@@ -752,14 +752,21 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
         hs_f4 acc[NU];
 #pragma unroll
         for (int u = 0; u < NU; ++u) acc[u] = hs_f4{0.f, 0.f, 0.f, 0.f};
+        // every k-step's item fragment read first, then the MFMAs k-step by
+        // k-step with the 4 user tiles interleaved (left to itself the
+        // scheduler chains one tile's 8 dependent MFMAs back to back)
+        HsFrag it[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          it[ks].i = *reinterpret_cast<const int4*>(tile + c * kStRowB + 16 * ((4 * ks + g) ^ c));
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          HsFrag it;
-          it.i = *reinterpret_cast<const int4*>(tile + c * kStRowB + 16 * ((4 * ks + g) ^ c));
 #pragma unroll
           for (int u = 0; u < NU; ++u)
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it.i),
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it[ks].i),
                                                              __builtin_bit_cast(hs_bf8, uf[u][ks].i), acc[u], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
         // C/D: lane holds user 64 wu + 16 u + c, items i0 + 16 t + 4 g + r
         const int64_t jt = i0 + 16 * (int64_t)t;
