@@ -640,6 +640,9 @@ template <int MODE>
 __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a) {
   constexpr int DK = 256, KS = DK / 32, NU = 4, kStStages = st_stages<MODE>();
   static_assert(MODE == HS_PRUNE || MODE == HS_FILTER, "the stream kernel has no score stores");
+#ifdef HREC_HS_STAMPS
+  unsigned long long st_t[5] = {HS_T(), 0, 0, 0, 0};
+#endif
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   char* ring = dsm;
   char* head = dsm + kStStages * kStTileB;
@@ -737,6 +740,9 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
     // 2 i + kStStages - 1 into the stages iteration i - 1 read
 #pragma unroll
     for (int t = 0; t < kStStages - 2; ++t) issue(t);
+#ifdef HREC_HS_STAMPS
+    st_t[1] = HS_T();
+#endif
     const int iters = (T + 1) / 2;
     for (int i = 0; i < iters; ++i) {
       // tiles 2 i, 2 i + 1 landed: this wave's pieces by the counted wait
@@ -744,6 +750,9 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
       // which also retires every read of the stages refilled next
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kStStages - 4) : "memory");
       __builtin_amdgcn_s_barrier();
+#ifdef HREC_HS_STAMPS
+      if (i == 0) st_t[2] = HS_T();
+#endif
       issue(2 * i + kStStages - 2);
       issue(2 * i + kStStages - 1);
       const int t = 2 * i + par;
@@ -811,6 +820,9 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the LDS is reused
+#ifdef HREC_HS_STAMPS
+    st_t[3] = HS_T();
+#endif
   }
   if constexpr (MODE == HS_FILTER) {
     // flush: one list reservation per user (global atomic), then the entries
@@ -894,8 +906,15 @@ __global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a)
       }
     }
   }
+#ifdef HREC_HS_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < kHsStampBlocks) {
+    st_t[4] = HS_T();
+    unsigned long long* o = g_hs_stamps[MODE][blockIdx.x];
+    for (int q = 0; q < 5; ++q) o[q] = st_t[q];
+    o[5] = 0xffffull;  // marks a stream-kernel record
+  }
+#endif
 }
-
 // HREC_HS_STREAM (env): 1 (default) = hyb_stream_kernel for the d = 256
 // pruned passes, 0 = hyb_scores_kernel
 static bool hs_stream_on() {
