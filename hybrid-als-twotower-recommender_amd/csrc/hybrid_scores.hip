@@ -25,7 +25,6 @@
 // uint keys, ds_max_u32); every block writes its partials, and a tiny
 // second kernel reduces them per user (no global atomics, deterministic).
 #include <float.h>
-#include <stdlib.h>
 
 #include <type_traits>
 
@@ -583,348 +582,6 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   HS_STAMP_END();
 }
 
-// ---------------------------------------------------------------- K9s2
-// The d = 256 pruned passes (HS_PRUNE, HS_FILTER) with the roles turned
-// round: the block's <= 256 users' bf16 fragments stay in REGISTERS (wave
-// w and w + 4: users 64 (w & 3) .. + 63, 128 VGPRs) and the item range
-// streams through an LDS ring of kStStages 16-item tiles filled by LDS-DMA
-// (global_load_lds_dwordx4: no VGPRs; kStStages - 2 tiles in flight across
-// the barriers). Waves 0-3 take the even tiles, waves 4-7 the odd ones, so
-// each SIMD runs two independent MFMA streams. Each item fragment read from
-// LDS feeds 4 MFMAs (the user tiles), half the LDS traffic per MFMA of
-// hyb_scores_kernel. Same MFMA chains (A = items, B = users, k-steps
-// ascending), so the same scores; the same slices (32 items = 2 tiles) for
-// the per-block max position (the two wave groups' results are folded with
-// the same rule: larger max, then the smaller position); the same survivor
-// staging and flush.
-constexpr int kStThreads = 512;
-// ring stages: HS_PRUNE 16 (128 KiB, 14 tiles in flight per CU: enough bytes
-// to cover the HBM latency at the full rate), HS_FILTER 12 (the rest of the
-// LDS stages survivors)
-template <int MODE>
-constexpr int st_stages() { return MODE == HS_PRUNE ? 16 : 12; }
-constexpr int kStRowB = 512;             // one d = 256 bf16 item row
-constexpr int kStTileB = 16 * kStRowB;   // 8 KiB: one 16-item tile
-
-#ifndef HREC_HS_STREAM
-#define HREC_HS_STREAM 1
-#endif
-
-typedef __attribute__((address_space(3))) char hs_lds_char;
-
-// One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
-// [lds, lds + 1 KiB) (lds wave-uniform). Issued from inline asm so the
-// compiler's wait insertion does not see a pending LDS write: the builtin
-// form makes it wait for the whole DMA queue before every LDS read of the
-// ring (every read may alias it); the kernel counts the pieces itself. M0 is
-// set and restored inside the statement.
-__device__ __forceinline__ void hs_glds16(const void* src, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds)
-      : "memory");
-}
-
-// LDS bytes after the ring: HS_FILTER's head (bounds, counts, overflow marks,
-// the staging counter) or HS_PRUNE's hand-over of the odd-tile waves'
-// extremes (min, max, position per user), 16-B aligned
-__host__ __device__ inline size_t hs_stream_head(int UB) { return ((size_t)UB * 12 + 4 + 15) & ~(size_t)15; }
-
-template <int MODE>
-__global__ __launch_bounds__(kStThreads) void hyb_stream_kernel(HybScoresArgs a) {
-  constexpr int DK = 256, KS = DK / 32, NU = 4, kStStages = st_stages<MODE>();
-  static_assert(MODE == HS_PRUNE || MODE == HS_FILTER, "the stream kernel has no score stores");
-#ifdef HREC_HS_STAMPS
-  unsigned long long st_t[5] = {HS_T(), 0, 0, 0, 0};
-#endif
-  extern __shared__ __attribute__((aligned(16))) char dsm[];
-  char* ring = dsm;
-  char* head = dsm + kStStages * kStTileB;
-  float* ths = reinterpret_cast<float*>(head);
-  int* cnt_l = reinterpret_cast<int*>(ths + a.UB);
-  int* ovf_l = cnt_l + a.UB;
-  int* bn = ovf_l + a.UB;
-  uint32_t* sb_meta = reinterpret_cast<uint32_t*>(head + hs_stream_head(a.UB));
-  float* sb_val = reinterpret_cast<float*>(sb_meta + a.sbuf);
-  int* sb_rank = reinterpret_cast<int*>(sb_val + a.sbuf);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wu = w & 3, par = w >> 2;  // user quarter, tile parity
-  const int g = lane >> 4, c = lane & 15;
-  const int model = MODE == HS_FILTER ? a.hm : (blockIdx.x & 1);
-  const int rest = MODE == HS_FILTER ? (int)blockIdx.x : (int)(blockIdx.x >> 1);
-  const int ut = rest % a.n_ut;
-  const int grp = MODE == HS_FILTER ? rest / a.n_ut / a.fsplit : rest / a.n_ut;
-  const int64_t per = ((a.N + a.G - 1) / a.G + 15) / 16 * 16;
-  int64_t i0 = (int64_t)grp * per;
-  int64_t i1 = i0 + per < a.N ? i0 + per : a.N;
-  if constexpr (MODE == HS_FILTER) {  // part of the group (slices of 32 items, as hyb_scores_kernel)
-    const int part = rest / a.n_ut % a.fsplit;
-    constexpr int64_t kSl = 32;
-    const int64_t sub = (per + a.fsplit * kSl - 1) / (a.fsplit * kSl) * kSl;
-    const int64_t g1 = i1;
-    i0 = i0 + part * sub < g1 ? i0 + part * sub : g1;
-    i1 = i0 + sub < g1 ? i0 + sub : g1;
-  }
-  const int b0 = ut * a.UB;
-  const int ub = a.B - b0 < a.UB ? a.B - b0 : a.UB;
-  const int64_t n_it = i1 > i0 ? i1 - i0 : 0;
-  const int T = (int)((n_it + 15) / 16);
-
-  if constexpr (MODE == HS_FILTER) {
-    for (int o = threadIdx.x; o < a.UB; o += kStThreads) {
-      float t = __builtin_nanf("");  // absent user: nothing passes
-      if (o < ub) {
-        t = a.theta[(int64_t)(b0 + o) * a.G + grp];
-        // +inf: a dead (user, group) — nothing passes; NaN admits every score
-        t = t == t ? (t == __builtin_inff() ? __builtin_nanf("") : t) : -__builtin_inff();
-      }
-      ths[o] = t;
-      cnt_l[o] = 0;
-      ovf_l[o] = 0;
-    }
-    if (threadIdx.x == 0) *bn = 0;
-    __syncthreads();  // before any LDS-DMA is in flight (this barrier waits for every load)
-  }
-  // this wave's users: fragments of user 64 wu + 16 u + c, k-chunk g (B
-  // operands); rows past the batch load row 0 and are zeroed (their scores
-  // are never used)
-  HsFrag uf[NU][KS];
-  float th[NU];
-  {
-    const char* ub_base = reinterpret_cast<const char*>(a.uop) + ((int64_t)model * a.B + b0) * (DK * 2);
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int bl = 64 * wu + 16 * u + c;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int4 v = *reinterpret_cast<const int4*>(ub_base + (int64_t)(bl < ub ? bl : 0) * (DK * 2) + 64 * ks + 16 * g);
-        uf[u][ks].i = bl < ub ? v : int4{0, 0, 0, 0};
-      }
-      if constexpr (MODE == HS_FILTER) th[u] = bl < ub ? ths[bl] : __builtin_nanf("");  // NaN: nothing passes
-    }
-  }
-  // tile t -> ring stage t % kStStages; every wave issues piece w (1 KiB =
-  // rows 2 w, 2 w + 1) of every tile. LDS slot 32 r + s (16 B) of a tile
-  // holds chunk s ^ (r & 15) of row r (XOR swizzle on the SOURCE address:
-  // the DMA writes lane-linear), so the 16 rows a ds_read_b128 touches fall
-  // in distinct banks. Tiles past the range re-read the last one (a uniform
-  // number of loads per iteration keeps the counted waits constant).
-  const char* items = a.items[model];
-  const uint32_t ring_lds = (uint32_t)(uintptr_t)(hs_lds_char*)ring;
-  const int slot = 64 * w + lane;
-  const int sr = slot >> 5, ssl = slot & 31;
-  auto issue = [&](int t) {
-    const int tt = t < T ? t : T - 1;
-    int64_t j = i0 + 16 * (int64_t)tt + sr;
-    j = j < i1 ? j : i1 - 1;
-    const char* src = items + j * kStRowB + 16 * (ssl ^ (sr & 15));
-    hs_glds16(src, __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)((t % kStStages) * kStTileB + w * 1024)));
-  };
-  float lo[NU], hi[NU];
-  int hp[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    lo[u] = __builtin_inff();
-    hi[u] = -__builtin_inff();
-    hp[u] = -1;
-  }
-  if (T > 0 && ub > 0) {  // block-uniform
-    // prologue: tiles 0 .. kStStages - 3; iteration i consumes tiles 2 i
-    // (waves 0-3) and 2 i + 1 (waves 4-7) and issues 2 i + kStStages - 2,
-    // 2 i + kStStages - 1 into the stages iteration i - 1 read
-#pragma unroll
-    for (int t = 0; t < kStStages - 2; ++t) issue(t);
-#ifdef HREC_HS_STAMPS
-    st_t[1] = HS_T();
-#endif
-    const int iters = (T + 1) / 2;
-    for (int i = 0; i < iters; ++i) {
-      // tiles 2 i, 2 i + 1 landed: this wave's pieces by the counted wait
-      // (kStStages - 4 tiles stay in flight), every wave's by the barrier,
-      // which also retires every read of the stages refilled next
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kStStages - 4) : "memory");
-      __builtin_amdgcn_s_barrier();
-#ifdef HREC_HS_STAMPS
-      if (i == 0) st_t[2] = HS_T();
-#endif
-      issue(2 * i + kStStages - 2);
-      issue(2 * i + kStStages - 1);
-      const int t = 2 * i + par;
-      if (t < T) {  // wave-uniform
-        const char* tile = ring + (t % kStStages) * kStTileB;
-        hs_f4 acc[NU];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) acc[u] = hs_f4{0.f, 0.f, 0.f, 0.f};
-        // every k-step's item fragment read first, then the MFMAs k-step by
-        // k-step with the 4 user tiles interleaved (left to itself the
-        // scheduler chains one tile's 8 dependent MFMAs back to back)
-        HsFrag it[KS];
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          it[ks].i = *reinterpret_cast<const int4*>(tile + c * kStRowB + 16 * ((4 * ks + g) ^ c));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-          for (int u = 0; u < NU; ++u)
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it[ks].i),
-                                                             __builtin_bit_cast(hs_bf8, uf[u][ks].i), acc[u], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        // C/D: lane holds user 64 wu + 16 u + c, items i0 + 16 t + 4 g + r
-        const int64_t jt = i0 + 16 * (int64_t)t;
-        const bool full = jt + 16 <= i1;  // wave-uniform
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-          float mx = -__builtin_inff(), mn = __builtin_inff();
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (full || jt + 4 * g + r < i1) {
-              mx = fmaxf(mx, acc[u][r]);
-              mn = fminf(mn, acc[u][r]);
-            }
-          if constexpr (MODE == HS_PRUNE) {
-            lo[u] = fminf(lo[u], mn);
-            // slice (32 items = tiles 2 m, 2 m + 1) of the lane's max: the
-            // earlier slice on ties, as hyb_scores_kernel's strict compare
-            const bool gt = mx > hi[u];
-            hi[u] = gt ? mx : hi[u];
-            hp[u] = gt ? (int)((i0 + 32 * (int64_t)(t >> 1)) >> 4) : hp[u];
-          } else {
-            if (__ballot(mx >= th[u])) {  // rare: stage this lane's survivors
-              const int bl = 64 * wu + 16 * u + c;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int64_t j = jt + 4 * g + r;
-                if ((full || j < i1) && acc[u][r] >= th[u]) {
-                  const int e = atomicAdd(bn, 1);
-                  const int rk = atomicAdd(&cnt_l[bl], 1);
-                  if (e < a.sbuf) {
-                    sb_meta[e] = ((uint32_t)bl << 24) | (uint32_t)(j - i0);
-                    sb_val[e] = acc[u][r];
-                    sb_rank[e] = rk;
-                  } else {
-                    ovf_l[bl] = 1;  // staging full: the user's list is marked overflowing at the flush
-                  }
-                }
-              }
-            }
-          }
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the LDS is reused
-#ifdef HREC_HS_STAMPS
-    st_t[3] = HS_T();
-#endif
-  }
-  if constexpr (MODE == HS_FILTER) {
-    // flush: one list reservation per user (global atomic), then the entries
-    __syncthreads();
-    for (int o = threadIdx.x; o < ub; o += kStThreads) {
-      const int k = cnt_l[o];
-      int base = 0;
-      if (ovf_l[o]) {
-        atomicAdd(&a.cn[b0 + o], a.cap + 1);  // > cap: the exact path answers this user
-      } else if (k > 0) {
-        base = atomicAdd(&a.cn[b0 + o], k);
-      }
-      cnt_l[o] = ovf_l[o] ? -1 : base;
-    }
-    __syncthreads();
-    const int ne = *bn < a.sbuf ? *bn : a.sbuf;
-    for (int e = threadIdx.x; e < ne; e += kStThreads) {
-      const uint32_t m = sb_meta[e];
-      const int ul = (int)(m >> 24);
-      const int base = cnt_l[ul];
-      if (base < 0) continue;
-      const int p = base + sb_rank[e];
-      if (p < a.cap) {
-        const int64_t b = b0 + ul;
-        a.cv[b * a.cap + p] = sb_val[e];
-        a.ci[b * a.cap + p] = i0 + (int64_t)(m & 0xffffffu);
-      }
-    }
-  } else {
-    // per user: fold the 4 lane groups (min; larger max, then the smaller
-    // position slice * 4 + g), the odd-tile waves hand theirs over in LDS,
-    // the even-tile waves fold them in and write the block's partials
-    float* xl = reinterpret_cast<float*>(head);
-    float* xh = xl + a.UB;
-    int* xp = reinterpret_cast<int*>(xh + a.UB);
-    float l[NU], h[NU];
-    int p[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      l[u] = lo[u];
-      h[u] = hi[u];
-      p[u] = hp[u] < 0 ? 0x7fffffff : hp[u] * 4 + g;
-#pragma unroll
-      for (int off = 16; off < 64; off <<= 1) {
-        l[u] = fminf(l[u], __shfl_xor(l[u], off, kWave));
-        const float oh = __shfl_xor(h[u], off, kWave);
-        const int op = __shfl_xor(p[u], off, kWave);
-        const bool take = oh > h[u] || (oh == h[u] && op < p[u]);
-        h[u] = take ? oh : h[u];
-        p[u] = take ? op : p[u];
-      }
-    }
-    if (par == 1 && g == 0) {
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int bl = 64 * wu + 16 * u + c;
-        if (bl < a.UB) {
-          xl[bl] = l[u];
-          xh[bl] = h[u];
-          xp[bl] = p[u];
-        }
-      }
-    }
-    __syncthreads();
-    if (par == 0 && g == 0) {
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int bl = 64 * wu + 16 * u + c;
-        if (bl < ub) {
-          const float ol = xl[bl], oh = xh[bl];
-          const int op = xp[bl];
-          const float fl = fminf(l[u], ol);
-          const bool take = oh > h[u] || (oh == h[u] && op < p[u]);
-          const float fh = take ? oh : h[u];
-          const int fp = take ? op : p[u];
-          float* pp = a.part + ((int64_t)(model * a.G + grp) * 2) * a.B + b0 + bl;
-          pp[0] = fl;
-          pp[a.B] = fh;
-          a.argpos[(int64_t)(model * a.G + grp) * a.B + b0 + bl] = fp == 0x7fffffff ? -1 : fp;
-        }
-      }
-    }
-  }
-#ifdef HREC_HS_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < kHsStampBlocks) {
-    st_t[4] = HS_T();
-    unsigned long long* o = g_hs_stamps[MODE][blockIdx.x];
-    for (int q = 0; q < 5; ++q) o[q] = st_t[q];
-    o[5] = 0xffffull;  // marks a stream-kernel record
-  }
-#endif
-}
-// HREC_HS_STREAM (env): 1 (default) = hyb_stream_kernel for the d = 256
-// pruned passes, 0 = hyb_scores_kernel
-static bool hs_stream_on() {
-  static const bool v = [] {
-    const char* e = getenv("HREC_HS_STREAM");
-    return e ? atoi(e) != 0 : HREC_HS_STREAM != 0;
-  }();
-  return v;
-}
-
 // mm[model][0 / 1][b] = min / max over the G item groups' partials: a block
 // of 256 threads takes 64 users of one model, 4 stripes of groups per user
 // (8 loads in flight per thread), then folds the stripes in LDS.
@@ -995,48 +652,9 @@ static int hs_launch_n(HybScoresArgs& a, size_t lds, hipStream_t s) {
   return check_launch("hyb_scores_kernel");
 }
 
-template <int MODE>
-static int hs_stream_launch(HybScoresArgs& a, hipStream_t s) {
-  // 256 users per tile (4 waves x 64)
-  const int n_ut = (a.B + 255) / 256;
-  a.UB = (a.B + n_ut - 1) / n_ut;
-  a.n_ut = n_ut;
-  size_t lds = (size_t)st_stages<MODE>() * kStTileB + hs_stream_head(a.UB);  // PRUNE: the hand-over after the ring
-  int blocks = 2 * a.n_ut * a.G;
-  if (MODE == HS_FILTER) {
-    const size_t head = lds;  // ring + the filter head
-    a.sbuf = head < kHsMaxLds ? (int)((kHsMaxLds - head) / 12) : 0;
-    if (a.sbuf > 8192) a.sbuf = 8192;
-    lds = head + (size_t)a.sbuf * 12;
-    static const int cus = [] {
-      int dev = 0, n = 256;
-      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      return n > 0 ? n : 256;
-    }();
-    const int64_t slices = ((a.N + a.G - 1) / a.G + 31) / 32;
-    int fs = (cus + a.n_ut * a.G - 1) / (a.n_ut * a.G);
-    if (fs > slices / 4) fs = (int)(slices / 4);  // >= 4 slices (8 tiles) per block
-    a.fsplit = fs < 1 ? 1 : fs;
-    blocks = a.n_ut * a.G * a.fsplit;
-  }
-  const auto kfn = hyb_stream_kernel<MODE>;
-  if (!allow_max_lds(kfn)) return check_launch("hyb_stream_kernel: LDS attribute");
-  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kStThreads), lds, s, a);
-  return check_launch("hyb_stream_kernel");
-}
-
 template <int DK, int MODE>
 static int hs_launch(HybScoresArgs& a, float* mm0, float* mm1, hipStream_t s) {
   constexpr int CU = 16 * HsShape<DK>::NU;
-  if constexpr (DK == 256 && MODE != HS_FULL) {
-    if (a.uop && hs_stream_on()) {
-      const int rc = hs_stream_launch<MODE>(a, s);
-      if (rc || MODE == HS_FILTER || mm0 == nullptr) return rc;
-      hipLaunchKernelGGL(hyb_mm_reduce_kernel, dim3((unsigned)((a.B + 63) / 64), 2), dim3(256), 0, s, a.part, a.B,
-                         a.G, mm0, mm1);
-      return check_launch("hyb_mm_reduce_kernel");
-    }
-  }
   a.UB = hs_user_tile<DK>(a.B);
   a.n_ut = (a.B + a.UB - 1) / a.UB;
   size_t lds = (size_t)a.UB * HsShape<DK>::kRowB + (size_t)a.UB * (MODE == HS_PRUNE ? 16 : 8);

@@ -19,9 +19,7 @@ buf = np.zeros((3, 1024, 8), np.uint64)
 lib.hrec_debug_hs_stamps(buf.ctypes.data, 0)
 for mode, name in ((1, "HS_PRUNE (phase 1)"), (2, "HS_FILTER (pass 2b)")):
     b = buf[mode].astype(np.int64)
-    b = b[(b[:, 0] > 0) & (b[:, 5] != 0xffff)]
-    if len(b) == 0:
-        continue
+    b = b[b[:, 0] > 0]
     t0 = b[:, 0].min()
     st, lp, ep = b[:, 1] - b[:, 0], b[:, 2] - b[:, 1], b[:, 3] - b[:, 2]
     wl = np.concatenate([(b[:, 4 + q] & 0xffffffff, b[:, 4 + q] >> 32) for q in range(4)])
@@ -50,16 +48,3 @@ if hasattr(lib, "hrec_debug_hp_stamps"):
             prev = cur
         d = t[:, 7] - prev
         print(f"  -> {'(to end)':12s} p50 {np.percentile(d, 50):7.0f}  p90 {np.percentile(d, 90):7.0f}")
-
-# hyb_stream_kernel (K9s2) records: [0] entry, [1] users loaded + prologue
-# issued, [2] first tile landed, [3] loop done, [4] end; [5] = 0xffff
-for mode, name in ((1, "K9s2 HS_PRUNE"), (2, "K9s2 HS_FILTER")):
-    b = buf[mode].astype(np.int64)
-    b = b[(b[:, 0] > 0) & (b[:, 5] == 0xffff)]
-    if len(b) == 0:
-        continue
-    q = lambda x: "p10 %6d  p50 %6d  p90 %6d" % tuple(np.percentile(x, [10, 50, 90]))  # noqa: E731
-    print(f"{name}: {len(b)} blocks; start spread {b[:, 0].max() - b[:, 0].min()}, end spread "
-          f"{b[:, 4].max() - b[:, 4].min()}\n  users+prologue {q(b[:, 1] - b[:, 0])}\n  first tile     "
-          f"{q(b[:, 2] - b[:, 1])}\n  loop           {q(b[:, 3] - b[:, 2])}\n  epilogue       {q(b[:, 4] - b[:, 3])}",
-          flush=True)
