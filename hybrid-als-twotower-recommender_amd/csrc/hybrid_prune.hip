@@ -186,6 +186,43 @@ __device__ __forceinline__ hp_f4 hp_dot(const HpFrag (&it)[DK / 32], const HpFra
 // of the batch issued first, the batch costs one round trip.
 __device__ __forceinline__ void hp_loads_issued() { __builtin_amdgcn_sched_barrier(0); }
 
+// hp_better's order as one unsigned key (larger = better; ties -> the smaller
+// item): 0 = an empty slot (idx INT64_MAX), 1 = NaN, numbers above by their
+// ordered bits (-0 folded into +0, equal values share a key).
+__device__ __forceinline__ uint64_t hp_order_key(double v, int64_t idx) {
+  const double z = v + 0.0;  // -0 + 0 = +0
+  const uint64_t u = (uint64_t)__double_as_longlong(z);
+  const uint64_t ord = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  return idx == INT64_MAX ? 0ull : (v != v ? 1ull : ord);
+}
+
+// 64-bit moves across lanes: DPP (CTRL: gfx9 dpp_ctrl, all sources valid)
+// and readlane, as two 32-bit halves.
+template <int CTRL, typename T>
+__device__ __forceinline__ T hp_dpp64(T x) {
+  static_assert(sizeof(T) == 8, "64-bit values");
+  uint64_t u;
+  __builtin_memcpy(&u, &x, 8);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  u = ((uint64_t)hi << 32) | lo;
+  T r;
+  __builtin_memcpy(&r, &u, 8);
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ T hp_readlane64(T x, int src) {
+  static_assert(sizeof(T) == 8, "64-bit values");
+  uint64_t u;
+  __builtin_memcpy(&u, &x, 8);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+  u = ((uint64_t)hi << 32) | lo;
+  T r;
+  __builtin_memcpy(&r, &u, 8);
+  return r;
+}
+
 __device__ __forceinline__ float hp_pick(const hp_f4& a, int r) {
   return r == 0 ? a[0] : (r == 1 ? a[1] : (r == 2 ? a[2] : a[3]));
 }
@@ -491,15 +528,39 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
     }
   };
   auto fused = [&](float h, float l) { return hm ? hp_fuse(sc, l, h, w0, w1) : hp_fuse(sc, h, l, w0, w1); };
+  // the wave's best (bv, bi) into every lane (empty slots: bi == INT64_MAX,
+  // worse than everything): the order as one integer key per entry, reduced
+  // by DPP within each 16-lane row (quad swaps, half-row and row mirrors:
+  // register moves, no LDS round trip) and across the 4 rows by readlanes
   auto wave_best = [&](double& bv, int64_t& bi) {
+    uint64_t k = hp_order_key(bv, bi);
+    int64_t i = bi;
+    double v = bv;
+    auto fold = [&](uint64_t ok, int64_t oi, double ov) {
+      const bool tk = (ok > k) | ((ok == k) & (oi < i));
+      k = tk ? ok : k;
+      i = tk ? oi : i;
+      v = tk ? ov : v;
+    };
+    fold(hp_dpp64<0xB1>(k), hp_dpp64<0xB1>(i), hp_dpp64<0xB1>(v));     // quad_perm [1,0,3,2]
+    fold(hp_dpp64<0x4E>(k), hp_dpp64<0x4E>(i), hp_dpp64<0x4E>(v));     // quad_perm [2,3,0,1]
+    fold(hp_dpp64<0x141>(k), hp_dpp64<0x141>(i), hp_dpp64<0x141>(v));  // row_half_mirror
+    fold(hp_dpp64<0x140>(k), hp_dpp64<0x140>(i), hp_dpp64<0x140>(v));  // row_mirror
+    uint64_t bk = hp_readlane64(k, 0);
+    int64_t bi2 = hp_readlane64(i, 0);
+    double bv2 = hp_readlane64(v, 0);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double yv = __shfl_xor(bv, off, kWave);
-      const int64_t yi = __shfl_xor(bi, off, kWave);
-      const bool tk = bi == INT64_MAX ? yi != INT64_MAX : (yi != INT64_MAX && hp_better(yv, yi, bv, bi));
-      bv = tk ? yv : bv;
-      bi = tk ? yi : bi;
+    for (int r = 1; r < 4; ++r) {
+      const uint64_t ok = hp_readlane64(k, 16 * r);
+      const int64_t oi = hp_readlane64(i, 16 * r);
+      const double ov = hp_readlane64(v, 16 * r);
+      const bool tk = (ok > bk) | ((ok == bk) & (oi < bi2));
+      bk = tk ? ok : bk;
+      bi2 = tk ? oi : bi2;
+      bv2 = tk ? ov : bv2;
     }
+    bv = bv2;
+    bi = bi2;
   };
   // the lanes' lists -> each wave's best kk (LDS) -> wave 0's merge; writes
   // the outputs when `write`; returns (in s_full) whether a NaN or a missing
