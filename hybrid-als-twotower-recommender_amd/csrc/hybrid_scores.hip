@@ -107,6 +107,25 @@ __device__ __forceinline__ uint32_t hs_bf16(float v) {
   return (x + 0x7fffu + ((x >> 16) & 1u)) >> 16;
 }
 
+// The value of lane ^ 16 / lane ^ 32 by the gfx950 row / half swaps
+// (v_permlane16_swap / v_permlane32_swap: VALU, no LDS round trip): with the
+// same register as both operands, the swap leaves the partner's value in the
+// first result for lanes with that bit set and in the second for the others.
+template <typename T>
+__device__ __forceinline__ T hs_xor16(T x) {
+  static_assert(sizeof(T) == 4, "32-bit values");
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(T, (uint32_t)((threadIdx.x & 16) ? r[0] : r[1]));
+}
+template <typename T>
+__device__ __forceinline__ T hs_xor32(T x) {
+  static_assert(sizeof(T) == 4, "32-bit values");
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(T, (uint32_t)((threadIdx.x & 32) ? r[0] : r[1]));
+}
+
 // Order-preserving float <-> uint keys (larger float -> larger key); the
 // LDS slots start at 0, below every key.
 __device__ __forceinline__ uint32_t hs_key(float f) {
@@ -543,15 +562,21 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       for (int u = 0; u < NU; ++u) {
         const int bl = CU * ch + 16 * u + c;
         float l = lo[ch][u], h = hi[ch][u];
-        l = fminf(l, __shfl_xor(l, 16, kWave));
-        l = fminf(l, __shfl_xor(l, 32, kWave));
+        l = fminf(l, hs_xor16(l));
+        l = fminf(l, hs_xor32(l));
         if constexpr (MODE == HS_PRUNE) {
           // (max, slice * 4 + g) of the 4 lane groups: larger max, then the smaller position
           int p = hp[ch][u] < 0 ? 0x7fffffff : hp[ch][u] * 4 + g;
-#pragma unroll
-          for (int off = 16; off < 64; off <<= 1) {
-            const float oh = __shfl_xor(h, off, kWave);
-            const int op = __shfl_xor(p, off, kWave);
+          {
+            const float oh = hs_xor16(h);
+            const int op = hs_xor16(p);
+            const bool take = oh > h || (oh == h && op < p);
+            h = take ? oh : h;
+            p = take ? op : p;
+          }
+          {
+            const float oh = hs_xor32(h);
+            const int op = hs_xor32(p);
             const bool take = oh > h || (oh == h && op < p);
             h = take ? oh : h;
             p = take ? op : p;
@@ -559,8 +584,8 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
           if (g == 0 && bl < ub && p != 0x7fffffff)
             atomicMax(&amk[bl], ((unsigned long long)hs_key(h) << 32) | (uint32_t)~p);
         } else {
-          h = fmaxf(h, __shfl_xor(h, 16, kWave));
-          h = fmaxf(h, __shfl_xor(h, 32, kWave));
+          h = fmaxf(h, hs_xor16(h));
+          h = fmaxf(h, hs_xor32(h));
         }
         if (g == 0 && bl < ub) {
           atomicMax(&mmk[2 * bl], ~hs_key(l));
