@@ -1,12 +1,12 @@
-# c5 pruned hybrid: per-kernel durations (kernel trace) of the probe, for each
-# HREC_HP_RANK setting given (default: 1 0)
+# c5 pruned hybrid: per-kernel durations (kernel trace) of the probe (an
+# optional list of labels runs it once per label)
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for r in ${@:-1 0}; do
-  echo "== HREC_HP_RANK=$r"
-  HREC_HP_RANK=$r timeout -k 10 200 python -u scripts/c5_probe.py 30 2>&1 | grep -v amdgpu.ids
-  HREC_HP_RANK=$r timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5tr_$r -o t -- python scripts/c5_probe.py 20 > /dev/null 2>&1
+for r in ${@:-1}; do
+  echo "== run $r"
+  timeout -k 10 200 python -u scripts/c5_probe.py 30 2>&1 | grep -v amdgpu.ids
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5tr_$r -o t -- python scripts/c5_probe.py 20 > /dev/null 2>&1
   python scripts/pmc_table.py gpurun_out/c5tr_$r --match hp_ | cut -c1-150
   python scripts/pmc_table.py gpurun_out/c5tr_$r --match hyb_ | cut -c1-150
 done
