@@ -405,20 +405,25 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   }
   __syncthreads();
   HP_STAMP(4);
-  // tau = the kk-th largest (the seed items are distinct)
-  for (int q = tid; q < n_slots; q += 256) {
+  // tau = the kk-th largest (the seed items are distinct): the thread pair
+  // (2 q, 2 q + 1) ranks slot q over the two halves of the list
+  const int half = n_slots / 2;  // a multiple of 16
+  for (int qq = tid; qq < 2 * n_slots; qq += 256) {
+    const int q = qq >> 1, h = qq & 1;
     const double v = sfl[q];
-    if (v == -INFINITY) continue;
     int rank = 0;
-    for (int o0 = 0; o0 < n_slots; o0 += 16) {  // n_slots: a multiple of 16; 8 broadcast 16-B reads in flight
+    if (v != -INFINITY) {
+      for (int o0 = h * half; o0 < (h + 1) * half; o0 += 16) {  // 8 broadcast 16-B reads in flight
 #pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        const double2 x = *reinterpret_cast<const double2*>(sfl + o0 + e);
-        rank += (int)(x.x > v) | ((int)(x.x == v) & (int)(o0 + e < q));
-        rank += (int)(x.y > v) | ((int)(x.y == v) & (int)(o0 + e + 1 < q));
+        for (int e = 0; e < 16; e += 2) {
+          const double2 x = *reinterpret_cast<const double2*>(sfl + o0 + e);
+          rank += (int)(x.x > v) | ((int)(x.x == v) & (int)(o0 + e < q));
+          rank += (int)(x.y > v) | ((int)(x.y == v) & (int)(o0 + e + 1 < q));
+        }
       }
     }
-    if (rank == kk - 1) s_tau = v;
+    rank += __shfl_xor(rank, 1, kWave);
+    if (h == 0 && v != -INFINITY && rank == kk - 1) s_tau = v;
   }
   __syncthreads();
   HP_STAMP(5);
