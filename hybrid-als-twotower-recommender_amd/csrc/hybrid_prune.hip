@@ -210,6 +210,22 @@ __device__ __forceinline__ T hp_dpp64(T x) {
   __builtin_memcpy(&r, &u, 8);
   return r;
 }
+template <int CTRL>
+__device__ __forceinline__ float hp_dpp32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+// lane ^ 16 / lane ^ 32 by v_permlane16_swap / v_permlane32_swap (see
+// csrc/hybrid_scores.hip hs_xor16)
+__device__ __forceinline__ float hp_xor16(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float hp_xor32(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
 template <typename T>
 __device__ __forceinline__ T hp_readlane64(T x, int src) {
   static_assert(sizeof(T) == 8, "64-bit values");
@@ -253,6 +269,7 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   constexpr int KS = DK / 32;
   constexpr int kSlots = kHpMaxGroups * 16;  // <= 16 groups x (4 NI <= 16) items
   __shared__ __attribute__((aligned(16))) float smax[128];
+  __shared__ int srank[128];
   __shared__ int sitem[kSlots];
   __shared__ __attribute__((aligned(16))) double sfl[kSlots];
   __shared__ double s_tau;
@@ -299,11 +316,20 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
       lo = part[(((int64_t)m * G + gi) * 2) * B + b];
       hi = part[(((int64_t)m * G + gi) * 2 + 1) * B + b];
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      lo = fminf(lo, __shfl_xor(lo, off, kWave));
-      hi = fmaxf(hi, __shfl_xor(hi, off, kWave));
-    }
+    // wave min / max without LDS permutes: DPP within rows (quad swaps, half-
+    // row and row mirrors), then the row / half swaps of gfx950
+    lo = fminf(lo, hp_dpp32<0xB1>(lo));
+    hi = fmaxf(hi, hp_dpp32<0xB1>(hi));
+    lo = fminf(lo, hp_dpp32<0x4E>(lo));
+    hi = fmaxf(hi, hp_dpp32<0x4E>(hi));
+    lo = fminf(lo, hp_dpp32<0x141>(lo));
+    hi = fmaxf(hi, hp_dpp32<0x141>(hi));
+    lo = fminf(lo, hp_dpp32<0x140>(lo));
+    hi = fmaxf(hi, hp_dpp32<0x140>(hi));
+    lo = fminf(lo, hp_xor16(lo));
+    hi = fmaxf(hi, hp_xor16(hi));
+    lo = fminf(lo, hp_xor32(lo));
+    hi = fmaxf(hi, hp_xor32(hi));
     if (lane == 0) {
       red[wv][0] = lo;
       red[wv][1] = hi;
@@ -337,23 +363,29 @@ __global__ __launch_bounds__(256) void hp_bound_kernel(const float* __restrict__
   if (tid == 0) s_tau = -INFINITY;
   __syncthreads();
   HP_STAMP(2);
-  // the kHpMaxGroups largest group maxima (value desc, group asc) -> seed slots
+  // the kHpMaxGroups largest group maxima (value desc, group asc) -> seed
+  // slots. Group gi's rank over all 128 slots (those >= G hold -inf, never
+  // counted) in two halves: thread gi the lower, thread 128 + gi the upper,
+  // 16 broadcast 16-B reads each; non-short-circuit forms (a branch per
+  // element would wait for each read)
   const int per_g = 4 * slice_ni;
-  if (tid < G) {
-    const float v = smax[tid];
-    if (v != -INFINITY) {
-      // all 128 slots (those >= G hold -inf, never counted): 32 broadcast
-      // 16-B reads in flight instead of a chain of G dependent ones
-      int rank = 0;
+  {
+    const int gi = tid & 127, h = tid >> 7;
+    const float v = smax[gi];
+    int part_rank = 0;
 #pragma unroll
-      for (int q = 0; q < 128; q += 4) {
-        const float4 o = *reinterpret_cast<const float4*>(smax + q);
-        // non-short-circuit forms: a branch per element would wait for each read
-        rank += (int)(o.x > v) | ((int)(o.x == v) & (int)(q < tid));
-        rank += (int)(o.y > v) | ((int)(o.y == v) & (int)(q + 1 < tid));
-        rank += (int)(o.z > v) | ((int)(o.z == v) & (int)(q + 2 < tid));
-        rank += (int)(o.w > v) | ((int)(o.w == v) & (int)(q + 3 < tid));
-      }
+    for (int q0 = 0; q0 < 64; q0 += 4) {
+      const int q = 64 * h + q0;
+      const float4 o = *reinterpret_cast<const float4*>(smax + q);
+      part_rank += (int)(o.x > v) | ((int)(o.x == v) & (int)(q < gi));
+      part_rank += (int)(o.y > v) | ((int)(o.y == v) & (int)(q + 1 < gi));
+      part_rank += (int)(o.z > v) | ((int)(o.z == v) & (int)(q + 2 < gi));
+      part_rank += (int)(o.w > v) | ((int)(o.w == v) & (int)(q + 3 < gi));
+    }
+    if (h == 1) srank[gi] = part_rank;
+    __syncthreads();
+    if (h == 0 && gi < G && v != -INFINITY) {
+      const int rank = part_rank + srank[gi];
       if (rank < kHpMaxGroups) {
         const int pos = ap;
         const int64_t jb = (int64_t)(pos >> 2) * 16;
