@@ -365,11 +365,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       ua[u].i = *reinterpret_cast<const int4*>(us + (16 * u + c) * kRowB + off);
     }
     float* const out = a.out[model];
-    // one slice; LT = its live item tiles (a group's last slice may hold one
-    // tile of 16 items: its other tiles' MFMAs are skipped, a compile-time
-    // choice so no branch splits the scheduled MFMA stream)
-    auto slice = [&](auto lt) {
-      constexpr int LT = decltype(lt)::value;
+    for (; jb < i1; jb += kStride) {
       rows_of(jb + kStride, vnext);
       const bool full = jb + kSlice <= i1;  // wave-uniform: every item of the slice is in range
       auto user_frag = [&](int ch, int u, int ks) {
@@ -399,10 +395,9 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
           for (int u = 0; u < NU; ++u)
 #pragma unroll
             for (int t = 0; t < NI; ++t)
-              if (t < LT)
-                acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it_f[ks][t].i),
-                                                                    __builtin_bit_cast(hs_bf8, f[u].i), acc[u][t], 0,
-                                                                    0, 0);
+              acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hs_bf8, it_f[ks][t].i),
+                                                                  __builtin_bit_cast(hs_bf8, f[u].i), acc[u][t], 0,
+                                                                  0, 0);
           if (last) {  // step ks of this slice is done: refill it with the next slice's
 #pragma unroll
             for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
@@ -410,7 +405,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
 #pragma unroll
           for (int u = 0; u < NU; ++u) {
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-            __builtin_amdgcn_sched_group_barrier(0x008, LT, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x008, NI, 0);  // MFMA
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -507,16 +502,6 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
             }
           }
         }
-      }
-        };
-    for (; jb < i1; jb += kStride) {
-      if constexpr (NI == 1 || MODE == HS_FULL) {  // (HS_FULL: one variant keeps its registers)
-        slice(std::integral_constant<int, NI>{});
-      } else {
-        if (jb + 16 < i1)  // wave-uniform
-          slice(std::integral_constant<int, NI>{});
-        else
-          slice(std::integral_constant<int, 1>{});
       }
     }
   }
