@@ -130,13 +130,7 @@ __global__ __launch_bounds__(256) void hp_user_ops_kernel(const float* __restric
                                                           int als_width, const float* __restrict__ tt_users,
                                                           int64_t tt_ld, int tt_width, int B, int dk,
                                                           uint16_t* __restrict__ uop) {
-  // 4 consecutive columns per thread (one 16-B load when the row allows, one
-  // 8-B store): 256 / (dk / 4) users per block
-  const int m = blockIdx.y;
-  const int tpu = dk / 4;  // threads per user
-  const int b = blockIdx.x * (256 / tpu) + threadIdx.x / tpu;
-  const int c0 = 4 * (threadIdx.x % tpu);
-  if (b >= B) return;
+  const int b = blockIdx.x, m = blockIdx.y;
   const float* src = m ? tt_users : als_users;
   const int64_t ld = m ? tt_ld : als_ld;
   const int wd = m ? tt_width : als_width;
@@ -146,18 +140,12 @@ __global__ __launch_bounds__(256) void hp_user_ops_kernel(const float* __restric
     row = als_rows[b];
     bad = row < 0 || row >= n_als_rows;
   }
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* p = src + (bad ? 0 : row) * ld + c0;
-  if (!bad && c0 + 4 <= wd && ((ld & 3) == 0) && (((uintptr_t)src & 15) == 0)) {
-    const float4 x = *reinterpret_cast<const float4*>(p);
-    v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (c0 + e < wd) v[e] = bad ? __builtin_nanf("") : p[e];
+  uint16_t* out = uop + ((int64_t)m * B + b) * dk;
+  for (int c = threadIdx.x; c < dk; c += blockDim.x) {
+    float v = 0.f;
+    if (c < wd) v = bad ? __builtin_nanf("") : src[row * ld + c];
+    out[c] = (uint16_t)hp_bf16(v);
   }
-  const uint32_t lo = hp_bf16(v[0]) | (hp_bf16(v[1]) << 16), hi = hp_bf16(v[2]) | (hp_bf16(v[3]) << 16);
-  *reinterpret_cast<uint2*>(uop + ((int64_t)m * B + b) * dk + c0) = make_uint2(lo, hi);
 }
 
 // Order of the fused top-k (score.hip's better()): larger first, equal ->
@@ -840,9 +828,7 @@ extern "C" int hrec_hybrid_prune_minmax(const float* als_users, int64_t als_ld, 
     return hrec_hybrid_scores(als_users, als_ld, als_rows, n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users,
                               als_items, tt_items, 0, dk, nullptr, nullptr, 0, als_mm, tt_mm, w.part,
                               (size_t)2 * 2 * n_users * 4 + 256, stream);
-  const int upb = 256 / (dk / 4);  // users per hp_user_ops block
-  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)((n_users + upb - 1) / upb), 2), dim3(256), 0, s, als_users,
-                     als_ld, als_rows,
+  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
                      n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
   rc = check_launch("hp_user_ops_kernel");
   if (rc) return rc;
@@ -959,9 +945,7 @@ extern "C" int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, c
   HREC_REQUIRE(workspace_bytes >= need, "hybrid_prune_local: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t s = as_stream(stream);
   const HpWs w = hp_layout((char*)workspace, n_users, n_items, dk, 1);
-  const int upb = 256 / (dk / 4);  // users per hp_user_ops block
-  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)((n_users + upb - 1) / upb), 2), dim3(256), 0, s, als_users,
-                     als_ld, als_rows,
+  hipLaunchKernelGGL(hp_user_ops_kernel, dim3((unsigned)n_users, 2), dim3(256), 0, s, als_users, als_ld, als_rows,
                      n_als_rows, als_width, tt_users, tt_ld, tt_width, n_users, dk, w.uop);
   rc = check_launch("hp_user_ops_kernel");
   if (rc) return rc;
