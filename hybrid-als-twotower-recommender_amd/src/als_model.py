@@ -335,11 +335,13 @@ class ALSModel:
 
     def _predict_device(self, user_id, all_items):
         """For HybridRecommendationSystem's array path: (items, keys, f32
-        device scores) when every score is a transform output (no cold-start
-        row), else the predict_for_user list itself (same prints, same [])."""
+        device scores), else the predict_for_user list itself (same prints,
+        same []). Cold-start rows stay NaN here (no host sync to look for
+        them): the array path sends any non-finite score to the list path,
+        which applies the fallback through _predictions."""
         try:
             items, keys, scores = self._score_device(user_id, all_items)
-            if scores is not None and not bool(torch.isnan(scores).any()):
+            if scores is not None:
                 return items, keys, scores
             return self._predictions(items, scores)
         except Exception as e:

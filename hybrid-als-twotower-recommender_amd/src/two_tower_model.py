@@ -216,7 +216,11 @@ class TwoTowerModel:
         the device scores, (item_features, f32 device scores [n]); [] for an
         empty frame. Raises where predict_for_user raises."""
         inputs = {
-            "user_in": np.full(len(item_features), user_id),
+            # the reference's np.full(len(item_features), user_id) column holds
+            # one id n times, and one user vector serves every row
+            # (_score_device): that id alone is converted and range-checked
+            # (the same cast, the same error) and sent to the device
+            "user_in": np.full(1, user_id),
             "item_id_in": item_features["itemId"].values,
             "manufacturer_in": item_features["manufacturer_id"].values,
             "category_in": item_features["category_id"].values,
