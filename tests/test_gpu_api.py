@@ -528,7 +528,12 @@ def test_twotower_golden_input_assembly(device):
         tt._device_inputs = spy
         out = tt.predict_for_user(31, cand)
         for k, v in case["inputs"].items():
-            assert np.asarray(seen[k]).tolist() == v, k
+            if k == "user_in":
+                # the reference's column repeats one id n times; the device path
+                # converts and sends that id once (one user vector serves every row)
+                assert len(set(v)) == 1 and np.asarray(seen[k]).tolist() == v[:1], k
+            else:
+                assert np.asarray(seen[k]).tolist() == v, k
         assert [i for i, _ in out] == [i for i, _ in dec_pairs(case["result"])]
 
 
