@@ -520,8 +520,6 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
   __shared__ double rv[8 * KK];
   __shared__ int64_t ri[8 * KK];
   __shared__ int s_full;
-  __shared__ uint64_t mk[64];  // merge: the slots' order keys
-  __shared__ int64_t mi[64];   // and items
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   HP_STAMP_DECL;
@@ -624,36 +622,41 @@ __global__ __launch_bounds__(512) void hp_cand_topk_kernel(const int* __restrict
     }
     __syncthreads();
     if (wv == 0) {
-      // the 8 waves' best kk (one slot per lane: 8 KK = 64) ranked at once:
-      // each lane counts the slots ahead of its own in hp_better's order (an
-      // integer key + the item), so rank r's lane writes output r — no kk
-      // dependent arg-best rounds. Empty slots (key 0) and NaNs (key 1) among
-      // the first kk mark the list as not final (the exact path then answers).
-      static_assert(8 * KK == 64, "one merge slot per lane of wave 0");
-      const bool valid = (lane % KK) < kk;
-      const double v = valid ? rv[lane] : 0.0;
-      const int64_t i = valid ? ri[lane] : INT64_MAX;
-      const uint64_t key = hp_order_key(v, i);
-      mk[lane] = key;
-      mi[lane] = i;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      int rank = 0;
-#pragma unroll 8
-      for (int o = 0; o < 64; ++o) {
-        const uint64_t ko = mk[o];
-        const int64_t io = mi[o];
-        // equal (key, item) only between empty slots: ordered by lane, so
-        // every rank below 64 has one writer (-1 / 0 for a missing entry)
-        rank += (int)(ko > key) | ((int)(ko == key) & ((int)(io < i) | ((int)(io == i) & (int)(o < lane))));
+      // lane l holds candidates l (and l + 64 when 8 kk > 64), better one first
+      double v0 = 0.0, v1 = 0.0;
+      int64_t i0 = INT64_MAX, i1 = INT64_MAX;
+      if (lane < 8 * KK && (lane % KK) < kk) {
+        v0 = rv[lane];
+        i0 = ri[lane];
       }
-      const bool top = rank < kk;
-      if (write && top) {
-        out_idx[(int64_t)b * kk + rank] = i == INT64_MAX ? -1 : i + idx_offset;
-        out_val[(int64_t)b * kk + rank] = i == INT64_MAX ? 0.0 : v;
+      if (lane + 64 < 8 * KK && ((lane + 64) % KK) < kk) {
+        v1 = rv[lane + 64];
+        i1 = ri[lane + 64];
       }
-      const bool bad = __ballot(top && key <= 1ull) != 0;
+      if (i1 != INT64_MAX && (i0 == INT64_MAX || hp_better(v1, i1, v0, i0))) {
+        const double tv = v0;
+        const int64_t ti = i0;
+        v0 = v1;
+        i0 = i1;
+        v1 = tv;
+        i1 = ti;
+      }
+      bool bad = false;
+      for (int r = 0; r < kk; ++r) {
+        double bv = v0;
+        int64_t bi = i0;
+        wave_best(bv, bi);
+        if (bi == INT64_MAX || bv != bv) bad = true;
+        if (write && lane == 0) {
+          out_idx[(int64_t)b * kk + r] = bi == INT64_MAX ? -1 : bi + idx_offset;
+          out_val[(int64_t)b * kk + r] = bi == INT64_MAX ? 0.0 : bv;
+        }
+        if (bi != INT64_MAX && i0 == bi) {
+          v0 = v1;
+          i0 = i1;
+          i1 = INT64_MAX;
+        }
+      }
       if (lane == 0) s_full = bad ? 1 : 0;
     }
     __syncthreads();
