@@ -123,7 +123,26 @@ _SIGNATURES.update({
                                       + [_vp]),
 })
 
-ABI_VERSION = 4
+class HybridBatch(ctypes.Structure):
+    """hrec_hybrid_batch (include/hrec.h)."""
+    _fields_ = [("als_users", _vp), ("als_rows", _vp), ("tt_users", _vp), ("als_items", _vp), ("tt_items", _vp),
+                ("prepared", _vp), ("als_ld", _c_i64), ("n_als_rows", _c_i64), ("tt_ld", _c_i64),
+                ("als_items_ld", _c_i64), ("tt_items_ld", _c_i64), ("n_items", _c_i64), ("als_width", _c_i32),
+                ("tt_width", _c_i32), ("n_users", _c_i32), ("dk", _c_i32)]
+
+
+_HBP = ctypes.POINTER(HybridBatch)
+_SIGNATURES.update({
+    "hrec_hybrid_exact_items_bytes": (_c_sz, [_c_i64, _c_i32]),
+    "hrec_hybrid_exact_prepare": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _c_i32, _c_i64, _c_i32, _vp, _vp]),
+    "hrec_hybrid_exact_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
+    "hrec_hybrid_exact_minmax": (_c_i32, [_HBP, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_exact_topk": (_c_i32, [_HBP, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_exact_local": (_c_i32, [_HBP, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_hybrid_exact_counts": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
+})
+
+ABI_VERSION = 5
 _LIB = None
 
 
@@ -720,6 +739,131 @@ class HybridPrune:
         return bool(int(out.item()))
 
 
+EXACT_MAX_K = 8
+EXACT_TT_WIDTHS = (32, 64, 128)
+
+
+def exact_dk(als_width, tt_width):
+    """The bf16 operand width of the exact pruned hybrid (64 or 128), or None
+    when the shapes are outside it (the materialised path answers)."""
+    if tt_width not in EXACT_TT_WIDTHS or not 1 <= als_width <= 128:
+        return None
+    return 64 if max(als_width, tt_width) <= 64 else 128
+
+
+class HybridExactItems:
+    """One item shard prepared for the exact pruned hybrid
+    (hrec_hybrid_exact_prepare): the f32 rows the exact chains read (ALS item
+    factor rows [n, >= k], row stride a multiple of 4; two-tower item vectors
+    [n, d], d in 32/64/128) and their bf16 operands + norm bounds."""
+
+    def __init__(self, als_items, k, tt_items):
+        self.k, self.d = int(k), int(tt_items.shape[1])
+        self.dk = exact_dk(self.k, self.d)
+        if self.dk is None:
+            raise HrecError(f"hybrid_exact: widths (k={self.k}, d={self.d}) outside the exact pruned path")
+        for t, name in ((als_items, "als_items"), (tt_items, "tt_items")):
+            if t.dtype != torch.float32 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 4 \
+                    or t.data_ptr() % 16:
+                raise HrecError(f"hybrid_exact: {name} must be a 16-B aligned row-major float32 device matrix "
+                                "with a row stride that is a multiple of 4")
+        if als_items.shape[0] != tt_items.shape[0] or als_items.stride(0) < -(-self.k // 4) * 4:
+            raise HrecError("hybrid_exact: item counts differ or ALS rows narrower than k rounded up to 4")
+        self.Va, self.Vt, self.N = als_items, tt_items, int(tt_items.shape[0])
+        self.buf = torch.empty(int(lib().hrec_hybrid_exact_items_bytes(self.N, self.dk)), dtype=torch.uint8,
+                               device=tt_items.device)
+        _check("hrec_hybrid_exact_prepare", lib().hrec_hybrid_exact_prepare(
+            _vp(als_items.data_ptr()), als_items.stride(0), self.k, _vp(tt_items.data_ptr()), tt_items.stride(0),
+            self.d, self.N, self.dk, _vp(self.buf.data_ptr()), _stream()))
+
+
+class HybridExact:
+    """The exact pruned hybrid top-k (hrec_hybrid_exact_*) for one batch shape:
+    minmax() -> (als_mm, tt_mm) [2, B] (all-reduce them across item shards),
+    then topk(als_mm, tt_mm, als_wins, idx_offset) -> (ids [B, kk] int64,
+    fused f64 [B, kk]); local() does both for one shard. Bit for bit
+    als_score + tt_score + rows_minmax + fuse_rows_topk (batches of >= 8
+    users). als_users [n, >= k] f32 (rows als_rows [B] int64 used), tt_users
+    [B, d] f32; items: a HybridExactItems."""
+
+    def __init__(self, als_users, als_rows, tt_users, items, top_k):
+        if not 1 <= int(top_k) <= EXACT_MAX_K:
+            raise HrecError(f"hybrid_exact: top_k must be in [1, {EXACT_MAX_K}]")
+        for t, name in ((als_users, "als_users"), (tt_users, "tt_users")):
+            if t.dtype != torch.float32 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+                raise HrecError(f"hybrid_exact: {name} must be a row-major float32 device matrix")
+        if als_users.shape[1] < items.k or tt_users.shape[1] != items.d:
+            raise HrecError("hybrid_exact: user widths differ from the prepared items'")
+        self.items = items
+        self.B, self.N, self.dk = int(als_rows.shape[0]), items.N, items.dk
+        if tt_users.shape[0] != self.B:
+            raise HrecError("hybrid_exact: batch sizes differ")
+        self.top_k = int(top_k)
+        self.kk = min(self.top_k, self.N)
+        self.U = als_users
+        self.need = int(lib().hrec_hybrid_exact_workspace_bytes(self.B, self.N, self.dk))
+        self.ws = torch.empty(self.need, dtype=torch.uint8, device=tt_users.device)
+        self.rebind(als_rows, tt_users)
+
+    def rebind(self, als_rows, tt_users):
+        """The same batch shape with other users (the workspace is reused)."""
+        if int(als_rows.shape[0]) != self.B or tuple(tt_users.shape) != (self.B, self.items.d) or \
+                tt_users.dtype != torch.float32 or tt_users.stride(1) != 1 or not tt_users.is_cuda:
+            raise HrecError("hybrid_exact.rebind: batch shape differs from the one the workspace was sized for")
+        self.rows = als_rows if als_rows.dtype == torch.int64 and als_rows.is_contiguous() else \
+            als_rows.to(torch.int64).contiguous()
+        self.T = tt_users
+        it = self.items
+        self.arg = HybridBatch(_vp(self.U.data_ptr()), _vp(self.rows.data_ptr()), _vp(self.T.data_ptr()),
+                               _vp(it.Va.data_ptr()), _vp(it.Vt.data_ptr()), _vp(it.buf.data_ptr()),
+                               self.U.stride(0), self.U.shape[0], self.T.stride(0), it.Va.stride(0), it.Vt.stride(0),
+                               self.N, it.k, it.d, self.B, self.dk)
+        return self
+
+    def _mm(self):
+        dev = self.ws.device
+        return (torch.empty((2, self.B), dtype=torch.float32, device=dev),
+                torch.empty((2, self.B), dtype=torch.float32, device=dev))
+
+    def _out(self):
+        dev = self.ws.device
+        return (torch.empty((self.B, self.kk), dtype=torch.int64, device=dev),
+                torch.empty((self.B, self.kk), dtype=torch.float64, device=dev))
+
+    def minmax(self):
+        a_mm, t_mm = self._mm()
+        _check("hrec_hybrid_exact_minmax", lib().hrec_hybrid_exact_minmax(
+            ctypes.byref(self.arg), _vp(a_mm.data_ptr()), _vp(t_mm.data_ptr()), _vp(self.ws.data_ptr()), self.need,
+            _stream()))
+        return a_mm, t_mm
+
+    def topk(self, als_mm, tt_mm, als_wins, idx_offset=0):
+        out_i, out_v = self._out()
+        _check("hrec_hybrid_exact_topk", lib().hrec_hybrid_exact_topk(
+            ctypes.byref(self.arg), _dev(als_mm, torch.float32, "als_mm"), _dev(tt_mm, torch.float32, "tt_mm"),
+            int(bool(als_wins)), self.top_k, int(idx_offset), _vp(out_i.data_ptr()), _vp(out_v.data_ptr()),
+            _vp(self.ws.data_ptr()), self.need, _stream()))
+        return out_i, out_v
+
+    def local(self, als_wins, idx_offset=0):
+        """Both phases for ONE item shard: (ids, fused, als_mm, tt_mm)."""
+        a_mm, t_mm = self._mm()
+        out_i, out_v = self._out()
+        _check("hrec_hybrid_exact_local", lib().hrec_hybrid_exact_local(
+            ctypes.byref(self.arg), int(bool(als_wins)), self.top_k, int(idx_offset), _vp(a_mm.data_ptr()),
+            _vp(t_mm.data_ptr()), _vp(out_i.data_ptr()), _vp(out_v.data_ptr()), _vp(self.ws.data_ptr()), self.need,
+            _stream()))
+        return out_i, out_v, a_mm, t_mm
+
+    def counts(self):
+        """(groups rescored per user for the extremes [B], for the top-k [B],
+        whether some user rescored every group) of the last call."""
+        out = torch.empty(2 * self.B + 1, dtype=torch.int32, device=self.ws.device)
+        _check("hrec_hybrid_exact_counts", lib().hrec_hybrid_exact_counts(
+            _vp(self.ws.data_ptr()), self.B, self.N, self.dk, _vp(out.data_ptr()), _stream()))
+        return out[: self.B], out[self.B: 2 * self.B], bool(int(out[2 * self.B].item()))
+
+
 def _hyb_args(*ops):
     dk = ops[0].shape[1]
     for t in ops:
@@ -912,6 +1056,10 @@ class Comm:
             raise HrecError("Comm.allgather: a contiguous device tensor of f32/f64/i32/i64/u8")
         if recv is None:
             recv = torch.empty((self.world,) + tuple(send.shape), dtype=send.dtype, device=send.device)
+        elif recv.numel() != self.world * send.numel() or recv.device != send.device:
+            # hrec_allgather writes world x count elements: a smaller buffer is an out-of-bounds write
+            raise HrecError(f"Comm.allgather: recv holds {recv.numel()} elements on {recv.device}, "
+                            f"need {self.world} x {send.numel()} on {send.device}")
         _check("hrec_allgather", lib().hrec_allgather(self.h, _vp(send.data_ptr()), _dev(recv, send.dtype, "recv"),
                                                       send.numel(), _COMM_DTYPES[send.dtype], _stream()))
         return recv
@@ -920,6 +1068,8 @@ class Comm:
         """mm [n_rows, 2, B] f32 (each model's [min; max]) -> global extremes, in place."""
         if mm.dim() != 3 or mm.shape[1] != 2:
             raise HrecError("Comm.allreduce_minmax: mm must be [n_rows, 2, B]")
+        if not mm.is_cuda or mm.dtype != torch.float32:
+            raise HrecError("Comm.allreduce_minmax: mm must be a float32 device tensor")
         _check("hrec_allreduce_minmax", lib().hrec_allreduce_minmax(
             self.h, _dev(mm, torch.float32, "mm"), mm.shape[0], mm.shape[2], _stream()))
         return mm

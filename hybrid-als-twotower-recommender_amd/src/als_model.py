@@ -191,6 +191,21 @@ def build_csr(rows, cols, vals, n_rows, n_cols):
     return DeviceCSR(indptr, indices, values, 0, int(n_rows), int(n_cols))
 
 
+def java_string_hash(s):
+    """java.lang.String.hashCode (s[0] 31^(n-1) + ... + s[n-1], int32)."""
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
+def default_seed():
+    """Spark ALS's default seed, HasSeed's this.getClass.getName.hashCode:
+    the same in every process (Python's str hash is salted per process, so a
+    torchrun world would start each rank from other factors)."""
+    return java_string_hash("org.apache.spark.ml.recommendation.ALS") & ((1 << 63) - 1)
+
+
 class ALSModel:
     """src/als_model.py:21 — same constructor signature (+ optional seed)."""
 
@@ -256,7 +271,11 @@ class ALSModel:
         if U0 is not None:
             eng.set_user_factors(U0)
         else:
-            seed = (hash(type(self).__name__) if self.seed is None else int(self.seed)) & ((1 << 63) - 1)
+            seed = default_seed() if self.seed is None else int(self.seed) & ((1 << 63) - 1)
+            if world > 1:  # every rank starts from rank 0's factors
+                t = torch.tensor([seed], dtype=torch.int64, device=dev)
+                torch.distributed.broadcast(t, 0, group=group)
+                seed = int(t.item())
             eng.init_user_factors(seed)
         eng.fit(int(self.max_iter))
         if world == 1:
@@ -351,6 +370,17 @@ class ALSModel:
     def predict_for_user(self, user_id, all_items):
         try:
             items, _, scores = self._score_device(user_id, all_items)
+            return self._predictions(items, scores)
+        except Exception as e:
+            print(f"Prediction error: {str(e)}")
+            return []
+
+    def _predictions_guarded(self, items, scores):
+        """_predictions under predict_for_user's own error contract (:68-91):
+        a failing cold-start fallback prints 'Prediction error: ...' and gives
+        [] for the ALS side only — for callers that took the scores through
+        _predict_device and finish the list later (the hybrid's list path)."""
+        try:
             return self._predictions(items, scores)
         except Exception as e:
             print(f"Prediction error: {str(e)}")

@@ -187,7 +187,7 @@ class HybridRecommendationSystem:
                 if top is not None:
                     return top
             if isinstance(als_preds, tuple):  # the lists predict_for_user returns (:101-102)
-                als_preds = self.als_model._predictions(als_preds[0], als_preds[2])
+                als_preds = self.als_model._predictions_guarded(als_preds[0], als_preds[2])
             if isinstance(tt_preds, tuple):
                 tt_preds = self.twotower_model._predictions(*tt_preds)
             try:

@@ -53,6 +53,14 @@ class DeviceOps:
     def operand(x, dtype, dk=None):
         return _hrec.dot_operand(x, dtype, dk)
 
+    @staticmethod
+    def hybrid_exact_items(Vt_local, n_local, k, item_vecs_local):
+        """The shard's ALS item factor rows (row-major again: the exact chain
+        reads one row per item) + two-tower rows, prepared for hrec_hybrid_exact_*."""
+        rows = _hrec.transpose(Vt_local.contiguous())[:n_local]
+        return _hrec.HybridExactItems(rows, k, item_vecs_local.contiguous())
+
+    hybrid_exact = staticmethod(_hrec.HybridExact)
     dot_scores = staticmethod(_hrec.dot_scores)
     hybrid_scores = staticmethod(_hrec.hybrid_scores)
     hybrid_prune = staticmethod(_hrec.HybridPrune)
@@ -63,7 +71,13 @@ class DeviceOps:
 
 class ShardedRecommender:
     """precision "exact": JVM-exact ALS scores (Spark's f32 mul/add chain) and
-    f32 two-tower Dot — the reference's numerics. precision "bf16" (BASELINE
+    f32 two-tower Dot — the reference's numerics. For top_k <= 8, batches of
+    >= 8 users and two-tower widths 32/64/128 the exact path is the pruned one
+    (hrec_hybrid_exact_*: both models bounded on the bf16 matrix cores, the
+    exact chains only for the item groups the bounds cannot rule out; no
+    score matrix in HBM); pruned=False keeps the score matrices
+    (als_score + tt_score + rows_minmax + fuse_rows_topk) — the same bits.
+    precision "bf16" (BASELINE
     config c5: rank-256 factors and d = 256 towers stored in bf16): both
     models' scores on the bf16 matrix cores (f32 accumulation) from bf16
     copies of the factors / item vectors made once here; pass V_local (the
@@ -87,6 +101,13 @@ class ShardedRecommender:
         if precision not in ("exact", "bf16"):
             raise ValueError(f"precision must be 'exact' or 'bf16', got {precision!r}")
         self.precision = precision
+        self.pruned_exact = False
+        if precision == "exact":
+            self.pruned_exact = (bool(pruned) and hasattr(self.ops, "hybrid_exact")
+                                 and _hrec.exact_dk(self.k, int(item_vecs_local.shape[1])) is not None)
+            self.exact_items = None
+            if self.pruned_exact and self.n_local > 0:
+                self.exact_items = self.ops.hybrid_exact_items(Vt_local, self.n_local, self.k, item_vecs_local)
         if precision == "bf16":
             if V_local is None:
                 raise ValueError("precision='bf16' needs V_local (ALS item factor rows of the shard)")
@@ -146,11 +167,47 @@ class ShardedRecommender:
             return idx, val
         return merge_candidates(idx, val, top_k, self.world, self.group, o)
 
+    def _recommend_exact_pruned(self, user_rows, user_vecs, als_wins, top_k):
+        """Exact path without score matrices (hrec_hybrid_exact_*): phase 1 +
+        the exact extremes, C2, the top-k; one call for one shard."""
+        o = self.ops
+        B = int(user_rows.shape[0])
+        dev = user_vecs.device
+        if self.n_local > 0:
+            cache = self.__dict__.setdefault("_hx", {})
+            hx = cache.get((B, int(top_k)))
+            if hx is None:
+                hx = cache[(B, int(top_k))] = o.hybrid_exact(self.U, user_rows, user_vecs, self.exact_items, top_k)
+            else:
+                hx.rebind(user_rows, user_vecs)
+            self.last_exact = hx
+            if self.world == 1:
+                idx, val, _, _ = hx.local(als_wins, self.offset)
+                return idx, val
+            a_mm, t_mm = hx.minmax()
+        else:
+            inf = float("inf")
+            a_mm = torch.tensor([[inf] * B, [-inf] * B], dtype=torch.float32, device=dev)
+            t_mm = a_mm.clone()
+        if self.world > 1:
+            a_mm, t_mm = global_minmax(a_mm, t_mm, self.group)
+        if self.n_local > 0:
+            idx, val = hx.topk(a_mm, t_mm, als_wins, self.offset)
+        else:
+            idx = torch.empty((B, 0), dtype=torch.int64, device=dev)
+            val = torch.empty((B, 0), dtype=torch.float64, device=dev)
+        if self.world == 1:
+            return idx, val
+        return merge_candidates(idx, val, top_k, self.world, self.group, o)
+
     def recommend(self, user_rows, user_vecs, als_wins, top_k):
         """user_rows: [B] int64 ALS rows; user_vecs: [B, d] two-tower user
         vectors. Returns (global item ids [B, k], fused scores f64 [B, k])."""
         if self.precision == "bf16" and self.pruned and 1 <= int(top_k) <= _hrec.PRUNE_MAX_K:
             return self._recommend_pruned(user_rows, user_vecs, als_wins, top_k)
+        if (self.pruned_exact and 1 <= int(top_k) <= _hrec.EXACT_MAX_K and int(user_rows.shape[0]) >= 8
+                and user_vecs.dtype == torch.float32 and user_vecs.stride(1) == 1):
+            return self._recommend_exact_pruned(user_rows, user_vecs, als_wins, top_k)
         o = self.ops
         B = int(user_rows.shape[0])
         dev = user_vecs.device

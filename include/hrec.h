@@ -41,7 +41,7 @@ extern "C" {
  * 3: hrec_hybrid_minmax / hrec_hybrid_topk removed (the pruned hybrid
  *    replaces them); hrec_dot_topk's +inf bound admits scores >= +inf.
  * 4: the RCCL exchange steps (hrec_comm_*, hrec_allgather, hrec_allreduce_minmax). */
-#define HREC_ABI_VERSION 4
+#define HREC_ABI_VERSION 5
 
 #define HREC_OK 0
 #define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
@@ -382,7 +382,14 @@ int hrec_adam_sparse_tables_phase(const hrec_sparse_table* tables, int n_tables,
  * v_mfma_f32_16x16x4_f32, k order permuted), 1 = bf16 bit patterns
  * (v_mfma_f32_16x16x32_bf16, f32 accumulation). n_items < 2^31. */
 int hrec_f32_to_bf16(const float* in, int64_t n, uint16_t* out, void* stream);
-/* out[b*ld_out + j] = <U[b], V[j]> for b < n_users, j < n_items. */
+/* out[b*ld_out + j] = <U[b], V[j]> for b < n_users, j < n_items.
+ * Summation order and batch size: f32 calls of 1-4 users run the streaming
+ * GEMV kernel (one partial per 16-B load, then a butterfly), larger batches
+ * the matrix cores (k order 16 ks + 4 g + e); a user's f32 scores can
+ * therefore differ in the last bits between a call of <= 4 users and one of
+ * more (both within the f32 error bound). bf16 calls always use the matrix
+ * cores. A chunked caller that needs the same bits for every chunk keeps
+ * chunks of >= 5 users. The same holds for hrec_dot_topk. */
 int hrec_dot_scores(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
                     int dtype, float* out, int64_t ld_out, void* stream);
 size_t hrec_dot_topk_workspace_bytes(int n_users, int64_t n_items, int top_k);
@@ -486,6 +493,69 @@ int hrec_hybrid_prune_local(const float* als_users, int64_t als_ld, const int64_
  * user (out: n_users int32, device). */
 int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_items, int dk, int top_k,
                                 int32_t* out, void* stream);
+
+/* ---------------------------------------------------------------------
+ * Exact hybrid top-k without score matrices (csrc/hybrid_exact.hip, BASELINE
+ * config c2): get_hybrid_recommendations for a batch of users over an item
+ * shard (src/hybrid_system.py:57-75, :95-116) with the reference's numerics —
+ * the JVM-exact ALS dot (Spark ALSModel.transform, src/als_model.py:75) and
+ * the f32 Keras Dot (src/two_tower_model.py:80) in hrec_dot_scores' MFMA k
+ * order — bit for bit the result of hrec_als_score + hrec_tt_score (>= 8
+ * users) + hrec_rows_minmax_f32 + hrec_fuse_rows_topk, without writing either
+ * [n_users, n_items] score matrix: both models are approximated on the bf16
+ * matrix cores with a rigorous error bound, and only the item groups the
+ * bound cannot rule out (a model's extremes; the fused top-k) are rescored
+ * with the exact chains.
+ *   als_users[als_rows[b] * als_ld + c], c < als_width (a row outside
+ *     [0, n_als_rows) is an unknown user: NaN ALS scores);
+ *   tt_users[b * tt_ld + c], c < tt_width in {32, 64, 128};
+ *   als_items / tt_items: the shard's f32 item rows (row strides multiples of
+ *     4, 16-B aligned; ALS rows readable up to als_width rounded up to 4);
+ *   prepared: hrec_hybrid_exact_prepare's bf16 operands + norm bounds of the
+ *     same item rows (hrec_hybrid_exact_items_bytes, once per shard);
+ *   dk in {64, 128} >= both widths. n_users < 65536. */
+typedef struct hrec_hybrid_batch {
+  const float* als_users;
+  const int64_t* als_rows;
+  const float* tt_users;
+  const float* als_items;
+  const float* tt_items;
+  const void* prepared;
+  int64_t als_ld;
+  int64_t n_als_rows;
+  int64_t tt_ld;
+  int64_t als_items_ld;
+  int64_t tt_items_ld;
+  int64_t n_items;
+  int32_t als_width;
+  int32_t tt_width;
+  int32_t n_users;
+  int32_t dk;
+} hrec_hybrid_batch;
+size_t hrec_hybrid_exact_items_bytes(int64_t n_items, int dk);
+int hrec_hybrid_exact_prepare(const float* als_items, int64_t als_ld, int als_width, const float* tt_items,
+                              int64_t tt_ld, int tt_width, int64_t n_items, int dk, void* out, void* stream);
+/* Workspace (the same dk) carrying phase 1 into phase 2: 16 B per user and
+ * 32-item group + the bf16 user operands — 12.8 MB for 256 users x 100k items. */
+size_t hrec_hybrid_exact_workspace_bytes(int n_users, int64_t n_items, int dk);
+/* Phase 1 + the exact extremes: als_mm / tt_mm [2, n_users] f32 (the
+ * hrec_rows_minmax_f32 layout). All-reduce them across item shards, then: */
+int hrec_hybrid_exact_minmax(const hrec_hybrid_batch* batch, float* als_mm, float* tt_mm, void* workspace,
+                             size_t workspace_bytes, void* stream);
+/* the stable top-k (ties -> smaller item; ids + idx_offset) with the (global)
+ * extremes; top_k in [1, 8]. */
+int hrec_hybrid_exact_topk(const hrec_hybrid_batch* batch, const float* als_mm, const float* tt_mm, int als_wins,
+                           int top_k, int64_t idx_offset, int64_t* out_idx, double* out_val, void* workspace,
+                           size_t workspace_bytes, void* stream);
+/* Both for ONE shard (als_mm / tt_mm are outputs): 3 launches. */
+int hrec_hybrid_exact_local(const hrec_hybrid_batch* batch, int als_wins, int top_k, int64_t idx_offset,
+                            float* als_mm, float* tt_mm, int64_t* out_idx, double* out_val, void* workspace,
+                            size_t workspace_bytes, void* stream);
+/* Diagnostics of the last call: out[b] = item groups rescored for user b's
+ * exact extremes, out[n_users + b] = for its top-k, out[2 n_users] = 1 when
+ * some user rescored every group (int32, device). */
+int hrec_hybrid_exact_counts(const void* workspace, int n_users, int64_t n_items, int dk, int32_t* out,
+                             void* stream);
 
 /* ---------------------------------------------------------------------
  * Multi-GPU exchange steps (csrc/comm.hip) for hosts without

@@ -1,0 +1,94 @@
+"""c2 hybrid probe (GPU): the bench's hybrid_top5 inputs — c2's ALS factors
+after a few epochs, random-init towers (d = 64) — through the exact pruned
+path (hrec_hybrid_exact_*) and the materialised one, checked bit for bit;
+prints per-call times (HIP events, eager and one HIP graph) and how many
+32-item groups the bounds left per user.
+
+    python scripts/hx_probe.py [--users 256] [--epochs 2] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hybrid-als-twotower-recommender_amd"))
+sys.path.insert(0, ROOT)
+
+from src import _hrec, synthetic  # noqa: E402
+from src.als_engine import DeviceALS  # noqa: E402
+from src.recommend import CapturedRecommend, ShardedRecommender  # noqa: E402
+from src.tt_engine import DeviceTwoTower  # noqa: E402
+
+
+def ev_ms(fn, reps):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--n-users", type=int, default=1_000_000)
+    ap.add_argument("--n-items", type=int, default=100_000)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    n_users, n_items, k, d = args.n_users, args.n_items, 64, 64
+    csr = synthetic.generate(n_users, n_items, 0.005, False)
+    csc = synthetic.generate(n_users, n_items, 0.005, True)
+    eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc)
+    eng.init_user_factors(synthetic.SEED_INIT)
+    eng.fit(args.epochs)
+    tt = DeviceTwoTower(n_users, n_items, 2651, 255, d, seed=1)
+    g = torch.Generator().manual_seed(5)
+    items = torch.arange(n_items, dtype=torch.int32)
+    man = torch.randint(0, 2651, (n_items,), generator=g, dtype=torch.int32)
+    cat = torch.randint(0, 255, (n_items,), generator=g, dtype=torch.int32)
+    num = torch.rand((n_items, 2), generator=g).contiguous()
+    ivec = tt.item_vectors(items.cuda(), man.cuda(), cat.cuda(), num.cuda())
+    Vt = _hrec.transpose(eng.item_factor_rows(0, n_items).contiguous())
+    B = args.users
+    hu_ids = (torch.arange(B, dtype=torch.int64) * (n_users // B)).cuda()
+    hu = eng.user_rows(hu_ids)
+    uvec = tt.user_vectors(hu_ids.to(torch.int32))
+    pr = ShardedRecommender(eng.U, Vt, ivec, 0, k)
+    mt = ShardedRecommender(eng.U, Vt, ivec, 0, k, pruned=False)
+    out = {"users": B, "items": n_items}
+    for wins in (False, True):
+        a = pr.recommend(hu, uvec, wins, 5)
+        b = mt.recommend(hu, uvec, wins, 5)
+        same = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
+        n_ext, n_top, every = pr.last_exact.counts()
+        r = {"bit_identical": same, "every_group_rescored": every,
+             "groups_extremes": {"mean": float(n_ext.double().mean()), "max": int(n_ext.max())},
+             "groups_topk": {"mean": float(n_top.double().mean()), "max": int(n_top.max())},
+             "groups_total": -(-n_items // 32)}
+        r["pruned_eager_ms"] = ev_ms(lambda: pr.recommend(hu, uvec, wins, 5), args.reps)
+        r["materialised_eager_ms"] = ev_ms(lambda: mt.recommend(hu, uvec, wins, 5), args.reps)
+        cp = CapturedRecommend(pr, hu, uvec, wins, 5)
+        r["pruned_graph_ms"] = ev_ms(lambda: cp(), args.reps)
+        cm = CapturedRecommend(mt, hu, uvec, wins, 5)
+        r["materialised_graph_ms"] = ev_ms(lambda: cm(), args.reps)
+        out["als_wins" if wins else "tt_wins"] = r
+        print(json.dumps({("als_wins" if wins else "tt_wins"): r}), flush=True)
+    hx = pr.last_exact
+    out["stage_ms"] = {"local (3 launches)": ev_ms(lambda: hx.local(False), args.reps),
+                       "minmax (ops + stats + extremes)": ev_ms(lambda: hx.minmax(), args.reps)}
+    a_mm, t_mm = hx.minmax()
+    out["stage_ms"]["topk (given extremes)"] = ev_ms(lambda: hx.topk(a_mm, t_mm, False), args.reps)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

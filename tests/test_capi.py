@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared if not hasattr(lib, n)]
     assert not missing, missing
     lib.hrec_abi_version.restype = ctypes.c_int
-    assert lib.hrec_abi_version() == 4
+    assert lib.hrec_abi_version() == 5
 
 
 def test_python_binding_covers_the_header():
@@ -96,6 +96,35 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert b"negative n_als_rows" in lib.hrec_last_error()
     assert hs(None, 64, None, 0, 64, None, 64, 64, 0, None, None, 10, 64, None, None, 10, None, None, None, 0,
               None) == 0  # no users: nothing to do
+    # exact hybrid without score matrices: the batch description is checked first
+    from src import _hrec
+
+    ex = lib.hrec_hybrid_exact_minmax
+    ex.restype = ctypes.c_int
+    ex.argtypes = [ctypes.POINTER(_hrec.HybridBatch)] + [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_void_p]
+    assert ex(None, None, None, None, 0, None) == -1
+    assert b"null batch" in lib.hrec_last_error()
+    bt = _hrec.HybridBatch(None, None, None, None, None, None, 64, 10, 64, 64, 64, 100, 64, 64, 4, 96)
+    assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
+    assert b"dk must be 64 or 128" in lib.hrec_last_error()
+    bt.dk, bt.tt_width = 64, 48
+    assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
+    assert b"tt_width must be 32, 64 or 128" in lib.hrec_last_error()
+    bt.tt_width, bt.als_items_ld = 64, 30
+    assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
+    assert b"als_items_ld must be a multiple of 4" in lib.hrec_last_error()
+    bt.als_items_ld = 64
+    assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
+    assert b"null pointer" in lib.hrec_last_error()
+    tk = lib.hrec_hybrid_exact_topk
+    tk.restype = ctypes.c_int
+    tk.argtypes = [ctypes.POINTER(_hrec.HybridBatch), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                   ctypes.c_void_p]
+    bt.n_users = 0
+    assert tk(ctypes.byref(bt), None, None, 0, 9, 0, None, None, None, 0, None) == -1
+    assert b"top_k must be in [1, 8]" in lib.hrec_last_error()
+    assert tk(ctypes.byref(bt), None, None, 0, 5, 0, None, None, None, 0, None) == 0  # no users
 
 
 def test_product_has_no_oracle_imports():
