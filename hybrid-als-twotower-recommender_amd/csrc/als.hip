@@ -34,9 +34,6 @@
 #ifndef HREC_ALS_CH1
 #define HREC_ALS_CH1 4
 #endif
-#ifndef HREC_ALS_SPLIT
-#define HREC_ALS_SPLIT 0  // 1 = producer/consumer kernel (Gramian waves hand rows to factor/solve waves)
-#endif
 #ifndef HREC_ALS_INTCVT
 #define HREC_ALS_INTCVT 0  // 1 = Gramian operands f32 -> f64 by 32-bit integer ops (measured slower)
 #endif
@@ -157,7 +154,7 @@ __device__ __forceinline__ Vec<NT> struct_load(i4v rsrc, int vindex, int voffset
   return v;
 }
 
-#if defined(HREC_ALS_STAMPS) || defined(HREC_ALS_TRIO_STATS)
+#ifdef HREC_ALS_STAMPS
 // Diagnostic builds only: per-phase cycle sums (s_memtime) over all waves.
 __device__ unsigned long long g_als_stamps[8];
 #endif
@@ -253,8 +250,8 @@ struct NoHook {
 };
 
 // `before_lds` runs once the row's Gramian is in registers, before the first
-// LDS write (b, MODE 1 re-layout): the producer of the trio kernel waits there
-// for its hand-off slot.
+// LDS write (b, MODE 1 re-layout) — a no-op in the product kernel (the
+// producer/consumer splits that waited there measured slower).
 template <int NT, int CH, int MODE, typename Hook = NoHook, bool S64 = false>
 __device__ __forceinline__ void gram_row(int64_t beg, int64_t end, int lane, const int32_t* __restrict__ indices,
                                          const float* __restrict__ values, const float* __restrict__ src,
@@ -885,116 +882,6 @@ __device__ __forceinline__ void factor_row(int lane, d4 (&acc)[NT * (NT + 1) / 2
 }
 
 
-// factor_row with the Gramian resident in LDS (Up holds it packed upper,
-// column-packed, as the trio producers hand it off) instead of in the
-// accumulator registers: each trailing tile is read from LDS, updated by the
-// same 4 MFMAs and written back, so the factorisation needs ~110 VGPRs (the
-// trio kernel runs 3 waves per SIMD: <= 168) and gives the same bits as
-// factor_row (same operands, same MFMA order).
-template <int NT>
-__device__ __forceinline__ void factor_row_lds(int lane, double* __restrict__ Up, double* __restrict__ scratch,
-                                               const double* __restrict__ bsh, float* __restrict__ out,
-                                               double* junk) {
-  constexpr int KP = 16 * NT;
-  double* __restrict__ colbuf = scratch;    // two 64-entry row buffers (16-B aligned)
-  double* __restrict__ dsh = colbuf + 128;  // pivots d_r
-  double* __restrict__ rdsh = dsh + KP;     // 1 / d_r
-  const int sub = lane >> 4, col = lane & 15;
-#pragma unroll
-  for (int J = 0; J < NT; ++J) {
-    const int c = lane;
-    const bool own = c >= 16 * J && c < KP;
-    double a[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int q = 16 * J + m;
-      const double x = Up[tri(c) + (q <= c ? q : c)];  // in bounds for every lane
-      a[m] = (own && q <= c) ? x : 0.0;
-    }
-    double piv = bcast(a[0], 16 * J);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int pv = 16 * J + i;
-      double* cb = colbuf + 64 * (i & 1);
-      if (c < KP) cb[c] = a[i];
-      const double r0 = __builtin_amdgcn_rcp(piv);
-      const double r = fma(r0, fma(-piv, r0, 1.0), r0);
-      const double ut = a[i] * r;
-      // unconditional LDS stores (masked ones by address select: no exec
-      // masks to keep live in SGPRs); piv and r are wave-uniform
-      *((own && c > pv) ? &Up[tri(c) + pv] : junk) = ut;
-      dsh[pv] = piv;
-      rdsh[pv] = r;
-      if (i < 15) {
-        piv = bcast(fma(-a[i], ut, a[i + 1]), pv + 1);
-        wave_lds_sync();
-#pragma unroll
-        for (int m0 = (i + 1) & ~1; m0 < 16; m0 += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(cb + 16 * J + m0);
-          if (m0 > i) a[m0] = fma(-u.x, ut, a[m0]);
-          a[m0 + 1] = fma(-u.y, ut, a[m0 + 1]);
-        }
-      }
-    }
-    wave_lds_sync();
-    if (J + 1 < NT) {
-      double dq[4];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) dq[rr] = dsh[16 * J + sub + 4 * rr];
-      d4 uj[NT], yv[NT];
-#pragma unroll
-      for (int K = J + 1; K < NT; ++K) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const double x = Up[tri(16 * K + col) + 16 * J + sub + 4 * rr];
-          uj[K][rr] = x;
-          yv[K][rr] = x * dq[rr];
-        }
-      }
-#pragma unroll
-      for (int K = J + 1; K < NT; ++K) {
-#pragma unroll
-        for (int M = K; M < NT; ++M) {
-          d4 t;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int q = 16 * K + sub + 4 * rr, cc = 16 * M + col;
-            const double x = Up[tri(cc) + q];  // in bounds (q, cc < 64)
-            t[rr] = (K < M || q <= cc) ? x : 0.0;
-          }
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) t = __builtin_amdgcn_mfma_f64_16x16x4f64(-uj[K][rr], yv[M][rr], t, 0, 0, 0);
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int q = 16 * K + sub + 4 * rr, cc = 16 * M + col;
-            *((K < M || q <= cc) ? &Up[tri(cc) + q] : junk) = t[rr];
-          }
-        }
-      }
-      wave_lds_sync();
-    }
-  }
-  const int lc = lane < KP ? lane : KP - 1;
-  const double myrd = rdsh[lc];
-  double bi = lane < KP ? bsh[lane] : 0.0;
-#pragma unroll HREC_ALS_SOLVE_UNROLL
-  for (int q = 0; q < KP; ++q) {
-    const double u = Up[tri(lc) + q];
-    const double wq = bcast(bi, q);
-    if (lane > q) bi = fma(-u, wq, bi);
-  }
-  bi *= myrd;
-#pragma unroll HREC_ALS_SOLVE_UNROLL
-  for (int q = KP - 1; q >= 0; --q) {
-    const double u = Up[tri(q) + (lane < KP ? lane : 0)];
-    const double xq = bcast(bi, q);
-    if (lane < q) bi = fma(-u, xq, bi);
-  }
-  if (lane < KP) out[NT * (lane & 15) + (lane >> 4)] = (float)bi;
-  wave_lds_sync();
-}
-
-// One destination row on one wave (lane = 0..63), all scratch in `lds`.
 template <int NT, int CH, int MODE, bool S64 = false>
 __device__ __forceinline__ void als_row(int64_t row, int lane, const int64_t* __restrict__ indptr,
                                         const int32_t* __restrict__ indices, const float* __restrict__ values,
@@ -1031,266 +918,6 @@ __global__ __launch_bounds__(256) void f32_to_f64_kernel(const float* __restrict
     out[i] = (double)in[i];
 }
 
-// Producer/consumer variant: one block of 8 waves per CU. Wave p (0..3)
-// computes Gramians (matrix-core bound) and hands each row's normal equations
-// to its SIMD partner, wave p + 4, through a double-buffered LDS slot; the
-// partner factors and solves (latency-bound f64 VALU chain) while the
-// producer already accumulates the next row. Rows are claimed dynamically
-// from a device counter (zeroed by the launcher), one row ahead.
-template <int KP>
-struct SplitLds {
-  static constexpr int kUp = RowLds<KP>::kUpPad;
-  static constexpr int kSlot = kUp + KP;               // Gramian/Ut + b
-  static constexpr int kPair = 2 * kSlot + 128 + 2 * KP;  // two slots + consumer scratch
-  static constexpr int kSize = 4 * kPair;
-};
-
-template <int NT, int CH, int MODE>
-__global__ __launch_bounds__(512) void als_half_sweep_split_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
-    int k, double reg, float* __restrict__ dst, unsigned long long* __restrict__ counter) {
-  constexpr int KP = 16 * NT;
-  constexpr int NPAIR = NT * (NT + 1) / 2;
-  using L = SplitLds<KP>;
-  __shared__ __attribute__((aligned(16))) double lds[L::kSize];
-  __shared__ int state[8];      // per slot: 0 empty, 1 full
-  __shared__ int64_t slot_row[8];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pair = w & 3;
-  if (threadIdx.x < 8) state[threadIdx.x] = 0;
-  __syncthreads();
-  double* base = lds + pair * L::kPair;
-  auto slot_up = [&](int sl) { return base + sl * L::kSlot; };
-  auto slot_b = [&](int sl) { return base + sl * L::kSlot + L::kUp; };
-  int* st = state + 2 * pair;
-  int64_t* srow = slot_row + 2 * pair;
-  const int sub = lane >> 4, col = lane & 15;
-  auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
-
-  if (w < 4) {  // ---------------- producer: Gramians
-    auto fetch = [&]() -> int64_t {
-      unsigned long long v = 0;
-      if (lane == 0) v = atomicAdd(counter, 1ull);
-      return (int64_t)__builtin_amdgcn_readfirstlane((int)v) |
-             ((int64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
-    };
-    int sl = 0;
-    int64_t row = fetch();
-    while (true) {
-      const int64_t next = fetch();
-      while (__hip_atomic_load(&st[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
-        __builtin_amdgcn_s_sleep(1);
-      if (row >= n_rows) {
-        srow[sl] = -1;
-        __hip_atomic_store(&st[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        break;
-      }
-      const int64_t beg = indptr[row], end = indptr[row + 1];
-      if (end == beg) {
-        if (lane < KP) dst[row * KP + lane] = 0.f;
-        row = next;
-        continue;
-      }
-      d4 acc[NPAIR];
-      double* up = slot_up(sl);
-      gram_row<NT, CH, MODE>(beg, end, lane, indices, values, src, n_src, k, reg, acc, slot_b(sl), up);
-      // all tiles -> the slot (upper triangle, column-packed)
-#pragma unroll
-      for (int J = 0; J < NT; ++J) {
-#pragma unroll
-        for (int K = J; K < NT; ++K) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int q = 16 * J + sub + 4 * rr, c = 16 * K + col;
-            if (q <= c) up[tri(c) + q] = acc[pidx(J, K)][rr];
-          }
-        }
-      }
-      if (lane == 0) srow[sl] = row;
-      __hip_atomic_store(&st[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      sl ^= 1;
-      row = next;
-    }
-  } else {  // ---------------- consumer: factor + solve
-    double* scratch = base + 2 * L::kSlot;
-    int sl = 0;
-    while (true) {
-      while (__hip_atomic_load(&st[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 1)
-        __builtin_amdgcn_s_sleep(1);
-      const int64_t row = srow[sl];
-      if (row < 0) break;
-      double* up = slot_up(sl);
-      d4 acc[NPAIR];
-#pragma unroll
-      for (int J = 0; J < NT; ++J) {
-#pragma unroll
-        for (int K = J; K < NT; ++K) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int q = 16 * J + sub + 4 * rr, c = 16 * K + col;
-            acc[pidx(J, K)][rr] = q <= c ? up[tri(c) + q] : 0.0;
-          }
-        }
-      }
-      factor_row<NT>(lane, acc, up, scratch, slot_b(sl), dst + row * KP);
-      __hip_atomic_store(&st[sl], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      sl ^= 1;
-    }
-  }
-}
-
-// Trio variant (HREC_ALS_SPLIT=2): one 12-wave workgroup per CU, three waves
-// per SIMD — waves w, w + 4 and w + 8 share a SIMD (round-robin placement,
-// scripts/micro/hwid_probe.hip). Waves 0..7 are Gramian producers, waves
-// 8..11 one factor/solve consumer per SIMD. Two producers keep the SIMD's f64
-// matrix pipe as busy as the symmetric 2-wave kernel's Gramian phase does;
-// the consumer's LDL^T + substitutions (a latency chain whose f64 ops take
-// the pipe only ~5.5 cycles each) run beside them instead of after them.
-// Each producer owns one LDS hand-off slot (packed upper Gramian + b); it
-// waits for the slot only once its next row's Gramian sits in registers, and
-// the consumer factors in place in the slot, polling both of its producers.
-template <int KP>
-struct TrioLds {
-  static constexpr int kUp = RowLds<KP>::kUpPad;
-  static constexpr int kSlot = kUp + KP;                     // Gramian / Ut + b
-  static constexpr int kSimd = 2 * kSlot + 128 + 2 * KP + 2;  // two slots + consumer scratch + junk
-  static constexpr int kSize = 4 * kSimd;
-};
-
-template <int NT, int CH, int MODE>
-__global__ __launch_bounds__(768) void als_half_sweep_trio_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
-    int k, double reg, float* __restrict__ dst, unsigned long long* __restrict__ counter) {
-  static_assert(HREC_ALS_DIAG4 == 0, "the trio producer hands off before any DIAG4 LDS staging: build it with -DHREC_ALS_DIAG4=0");
-  constexpr int KP = 16 * NT;
-  constexpr int NPAIR = NT * (NT + 1) / 2;
-  using L = TrioLds<KP>;
-  __shared__ __attribute__((aligned(16))) double lds[L::kSize];
-  __shared__ int state[8];  // per slot: 0 empty, 1 full
-  __shared__ int64_t slot_row[8];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int simd = w & 3;
-  if (threadIdx.x < 8) state[threadIdx.x] = 0;
-  __syncthreads();
-  double* base = lds + simd * L::kSimd;
-  auto slot_up = [&](int sl) { return base + sl * L::kSlot; };
-  auto slot_b = [&](int sl) { return base + sl * L::kSlot + L::kUp; };
-  int* st = state + 2 * simd;
-  int64_t* srow = slot_row + 2 * simd;
-  double* junk = base + 2 * L::kSlot + 128 + 2 * KP;  // target of masked-off LDS stores
-  const int sub = lane >> 4, col = lane & 15;
-  auto pidx = [](int I, int K) { return I * NT - (I * (I - 1)) / 2 + (K - I); };
-  auto ld_state = [&](int sl) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(&st[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-  };
-
-  if (w < 8) {  // ---------------- producer: Gramians
-    const int sl = w >> 2;
-    auto fetch = [&]() -> int64_t {
-      unsigned long long v = 0;
-      if (lane == 0) v = atomicAdd(counter, 1ull);
-      return (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v) |
-             ((int64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
-    };
-#ifdef HREC_ALS_TRIO_STATS
-    unsigned long long t_wait = 0;
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-#endif
-    auto wait_empty = [&]() {
-#ifdef HREC_ALS_TRIO_STATS
-      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-      while (ld_state(sl) != 0) __builtin_amdgcn_s_sleep(1);
-#ifdef HREC_ALS_TRIO_STATS
-      t_wait += __builtin_amdgcn_s_memtime() - t0;
-#endif
-    };
-    int64_t row = fetch();
-    while (true) {
-      const int64_t next = fetch();
-      if (row >= n_rows) {
-        wait_empty();
-        if (lane == 0) srow[sl] = -1;
-        __hip_atomic_store(&st[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef HREC_ALS_TRIO_STATS
-        if (lane == 0) {
-          atomicAdd(&g_als_stamps[0], t_wait);
-          atomicAdd(&g_als_stamps[1], __builtin_amdgcn_s_memtime() - t_start);
-        }
-#endif
-        break;
-      }
-      const int64_t beg = indptr[row], end = indptr[row + 1];
-      if (end == beg) {
-        if (lane < KP) dst[row * KP + lane] = 0.f;
-        row = next;
-        continue;
-      }
-      d4 acc[NPAIR];
-      double* up = slot_up(sl);
-      gram_row<NT, CH, MODE>(beg, end, lane, indices, values, src, n_src, k, reg, acc, slot_b(sl), up,
-                             wait_empty);
-#pragma unroll
-      for (int J = 0; J < NT; ++J) {
-#pragma unroll
-        for (int K = J; K < NT; ++K) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int q = 16 * J + sub + 4 * rr, c = 16 * K + col;
-            if (q <= c) up[tri(c) + q] = acc[pidx(J, K)][rr];
-          }
-        }
-      }
-      if (lane == 0) srow[sl] = row;
-      __hip_atomic_store(&st[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      row = next;
-    }
-  } else {  // ---------------- consumer: factor + solve, rows of either producer
-#ifndef HREC_ALS_TRIO_PRIO
-#define HREC_ALS_TRIO_PRIO 3
-#endif
-    // the consumer's f64 chain wins the issue arbitration against the
-    // producers' MFMAs (otherwise the youngest wave waits out both streams)
-    __builtin_amdgcn_s_setprio(HREC_ALS_TRIO_PRIO);
-    double* scratch = base + 2 * L::kSlot;
-    int live = 3, sl = 0;
-#ifdef HREC_ALS_TRIO_STATS
-    unsigned long long t_busy = 0, n_solved = 0;
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-#endif
-    while (live) {
-      if (((live >> sl) & 1) && ld_state(sl) == 1) {
-        const int64_t row = srow[sl];
-        if (row < 0) {
-          live &= ~(1 << sl);
-        } else {
-#ifdef HREC_ALS_TRIO_STATS
-          const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-          factor_row_lds<NT>(lane, slot_up(sl), scratch, slot_b(sl), dst + row * KP, junk);
-#ifdef HREC_ALS_TRIO_STATS
-          t_busy += __builtin_amdgcn_s_memtime() - t0;
-          ++n_solved;
-#endif
-          __hip_atomic_store(&st[sl], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      } else {
-        __builtin_amdgcn_s_sleep(1);
-      }
-      sl ^= 1;
-    }
-#ifdef HREC_ALS_TRIO_STATS
-    if (lane == 0) {
-      atomicAdd(&g_als_stamps[2], t_busy);
-      atomicAdd(&g_als_stamps[3], __builtin_amdgcn_s_memtime() - t_start);
-      atomicAdd(&g_als_stamps[4], n_solved);
-    }
-#endif
-  }
-}
-
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int64_t rows,
                                                         int64_t cols, float* __restrict__ out, int64_t ld_out) {
   __shared__ float tile[64][65];
@@ -1311,24 +938,6 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
 }  // namespace hrec
 
 using namespace hrec;
-
-#if HREC_ALS_SPLIT
-#include <mutex>
-#include <vector>
-// One 8-byte row counter per (device, stream), allocated on first use and
-// kept for the life of the process; zeroed on the stream before each launch.
-static unsigned long long* row_counter(int dev, hipStream_t s) {
-  static std::mutex mu;
-  static std::vector<std::pair<std::pair<int, hipStream_t>, unsigned long long*>> pool;
-  std::lock_guard<std::mutex> lock(mu);
-  for (auto& e : pool)
-    if (e.first.first == dev && e.first.second == s) return e.second;
-  unsigned long long* p = nullptr;
-  if (hipMalloc(&p, sizeof(unsigned long long)) != hipSuccess) return nullptr;
-  pool.push_back({{dev, s}, p});
-  return p;
-}
-#endif
 
 extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices, const float* values,
                                    int64_t n_rows, const float* src_factors, int64_t n_src, int k,
@@ -1356,29 +965,10 @@ extern "C" int hrec_als_half_sweep(const int64_t* indptr, const int32_t* indices
                                     dst_factors, stream);
   }
   hipStream_t s = as_stream(stream);
-#if HREC_ALS_SPLIT
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  unsigned long long* counter = row_counter(dev, s);
-  HREC_REQUIRE(counter != nullptr, "als_half_sweep: cannot allocate the row counter");
-  if (hipMemsetAsync(counter, 0, sizeof(unsigned long long), s) != hipSuccess) return check_launch("als_half_sweep: counter reset");
-#if HREC_ALS_SPLIT == 2
-  const dim3 grid((unsigned)cus), block(768);
-#define HREC_SWEEP(NT, CH, M)                                                                        \
-  hipLaunchKernelGGL((als_half_sweep_trio_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
-                     n_rows, src_factors, n_src, k, reg_param, dst_factors, counter)
-#else
-  const dim3 grid((unsigned)cus), block(512);
-#define HREC_SWEEP(NT, CH, M)                                                                        \
-  hipLaunchKernelGGL((als_half_sweep_split_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
-                     n_rows, src_factors, n_src, k, reg_param, dst_factors, counter)
-#endif
-#else
   const dim3 grid((unsigned)n_rows), block(64);
 #define HREC_SWEEP(NT, CH, M)                                                                      \
   hipLaunchKernelGGL((als_half_sweep_f64_kernel<NT, CH, M>), grid, block, 0, s, indptr, indices, values, \
                      n_rows, src_factors, n_src, k, reg_param, dst_factors)
-#endif
   if (accum_mode == 0) {
     if (kp == 64) HREC_SWEEP(4, HREC_ALS_CH0, 0);
     else if (kp == 32) HREC_SWEEP(2, 8, 0);
@@ -1433,7 +1023,7 @@ extern "C" int hrec_transpose_f32(const float* in, int64_t rows, int64_t cols, f
   return check_launch("transpose_kernel");
 }
 
-#if defined(HREC_ALS_STAMPS) || defined(HREC_ALS_TRIO_STATS)
+#ifdef HREC_ALS_STAMPS
 extern "C" int hrec_debug_als_stamps(unsigned long long* host_out, int reset) {
   if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_als_stamps), sizeof(g_als_stamps)) != hipSuccess) return -2;
   if (reset) {

@@ -22,7 +22,6 @@
 //                 >= thr[b * thr_stride] (NaN admits every score, +inf the
 //                 scores >= +inf), one wave-aggregated atomic per user and
 //                 wave; cand_n[b] counts every survivor (> cap = overflow).
-#include <stdlib.h>
 
 
 #include "common.h"
@@ -263,16 +262,11 @@ static bool gemv_fits_rt(int nb, int dk, int bf16) {
 // 6.15 ms on the matrix cores (16x16x4 f32 tiles, 15 of 16 users empty) ->
 // 3.95 ms here (non-temporal loads; 4.35 cached); bf16 2.23 ms on the matrix
 // cores vs 2.29-2.59 here, so bf16 operands keep the matrix-core path.
-// HREC_DOT_GEMV=0 turns the kernel off, =2 also takes bf16 operands.
 bool dot_gemv_applies(int B, int64_t step, int dk, int bf16) {
-  static const int mode = [] {
-    const char* e = getenv("HREC_DOT_GEMV");
-    return e ? atoi(e) : 1;
-  }();
-  const bool on = mode == 2 || (mode == 1 && !bf16);
+  if (bf16) return false;  // bf16 operands keep the matrix-core path (measured faster)
   // a tile's 64 rows x step must stay within one 32-bit buffer offset
-  const int64_t tile_bytes = 64 * step * (int64_t)dk * (bf16 ? 2 : 4);
-  return on && B >= 1 && B <= kGemvMaxB && gemv_fits_rt(gemv_nb(B), dk, bf16) && tile_bytes < ((int64_t)1 << 32);
+  const int64_t tile_bytes = 64 * step * (int64_t)dk * 4;
+  return B >= 1 && B <= kGemvMaxB && gemv_fits_rt(gemv_nb(B), dk, 0) && tile_bytes < ((int64_t)1 << 32);
 }
 
 template <bool FILTER>
@@ -282,12 +276,8 @@ int dot_gemv_run(const void* U, int B, const void* V, int64_t n_rows, int64_t n_
 #define HREC_GEMV(BF, DK) \
   return gemv_launch_nb<BF, DK, FILTER>(U, B, V, n_rows, n_items, step, out, ldo, thr, thr_stride, cap, cv, ci, cn, off, s)
   if (bf16) {
-    switch (dk) {
-      case 32: HREC_GEMV(true, 32);
-      case 64: HREC_GEMV(true, 64);
-      case 128: HREC_GEMV(true, 128);
-      default: HREC_GEMV(true, 256);
-    }
+    set_error("dot_gemv_run: f32 operands only (dot_gemv_applies)");
+    return HREC_E_INVALID;
   }
   switch (dk) {
     case 32: HREC_GEMV(false, 32);

@@ -24,7 +24,6 @@
 // the 2 user-waves of its column; the user tiles of one item group run on the
 // same XCD, so the other user tiles hit that XCD's L2).
 #include <float.h>
-#include <stdlib.h>
 
 #include <type_traits>
 
@@ -629,10 +628,9 @@ __global__ __launch_bounds__(kDotThreads) void dot_res_kernel(
   }
 }
 
-// Tilings: FILTER passes keep each item fragment for 128 users (item bytes
-// through the vector cache halve vs 64 x 64 wave tiles; the user fragments
-// come from LDS, which has twice the bandwidth); HREC_DOT_TILING (0/1)
-// selects the variant for measurements.
+// Tilings of the tile kernel (f32 at dk 256): FILTER passes keep each item
+// fragment for 128 users (item bytes through the vector cache halve vs 64 x 64
+// wave tiles; the user fragments come from LDS, which has twice the bandwidth).
 typedef DotTiling<4, 4, 2> DotTileA;   // 128 users x 256 items, wave 64 x 64
 typedef DotTiling<8, 2, 1> DotTileB;   // 128 users x 256 items, wave 128 x 32
 
@@ -654,14 +652,6 @@ static unsigned dot_grid(int n_ut, int64_t n_items, int tile_items, int blocks_p
   if (m > m_max) m = m_max;
   if (m < 1) m = 1;
   return (unsigned)(8 * n_ut * m);
-}
-
-static int dot_tiling_choice() {
-  static int v = [] {
-    const char* e = getenv("HREC_DOT_TILING");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
 }
 
 template <bool FILTER, class TL>
@@ -764,22 +754,16 @@ static int dot_launch(const void* U, int B, const void* V, int64_t n_rows, int64
   if (dot_gemv_applies(B, step, dk, bf16))  // a few users: the streaming GEMV kernel (csrc/dot_gemv.hip)
     return dot_gemv_run<FILTER>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap, cv, ci, cn,
                                 off, s);
-  const int choice = dot_tiling_choice();
-  if (choice == 2 && (bf16 || dk <= 128))
+  if (bf16 || dk <= 128)  // the resident-user kernel
     return dot_launch_res<FILTER>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap, cv, ci,
                                   cn, off, s);
+  // f32 at dk 256 (the resident users would not fit the LDS): the tile kernel
   if constexpr (!FILTER) {
     return dot_launch_t<false, DotTileA>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
                                          cv, ci, cn, off, s);
   }
-  switch (choice) {
-    case 0:
-      return dot_launch_t<FILTER, DotTileA>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
-                                            cv, ci, cn, off, s);
-    default:
-      return dot_launch_t<FILTER, DotTileB>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap,
-                                            cv, ci, cn, off, s);
-  }
+  return dot_launch_t<FILTER, DotTileB>(U, B, V, n_rows, n_items, step, dk, bf16, out, ldo, thr, thr_stride, cap, cv,
+                                        ci, cn, off, s);
 }
 
 // Sample size and candidate capacity of the threshold filter: the k-th best

@@ -11,14 +11,18 @@
 // extremes before any fused score exists. So the scores of every pair are
 // first APPROXIMATED on the bf16 matrix cores, with a rigorous error bound,
 // and the exact chains run only where the bound cannot decide:
-//   phase 1 (hx_stats_kernel): both models' bf16 GEMMs
-//     (v_mfma_f32_32x32x16_bf16, f32 accumulation), no score stores: per user
-//     and 32-item group the approximate max and min of both models (16 B per
-//     user and group);
+//   phase 1 (hx_stats_kernel): both models' GEMMs on the bf16 matrix cores
+//     (v_mfma_f32_32x32x16_bf16, f32 accumulation) in split form: every
+//     operand as hi + lo bf16 (x = xh + xl + r, |r| <= 2^-16 |x|) and the
+//     score as uh.vh + uh.vl + ul.vh; no score stores: per user and 32-item
+//     group the approximate max and min of both models (16 B per user and
+//     group);
 //   phase 2 (hx_user_kernel, one block per user):
-//     a. exact extremes: |approx - exact| <= E = 2^-6 ||u|| max_j ||v_j||
-//        (bf16 rounding of both operands: 2^-7 sum |u_c v_c|, plus the f32
-//        accumulation of both forms; sum |u_c v_c| <= ||u|| ||v||), so the item
+//     a. exact extremes: |approx - exact| <= E = 2^-13 ||u|| max_j ||v_j||
+//        (the dropped terms ul.vl and the split residues: 3 2^-16 sum
+//        |u_c v_c|; the f32 accumulation of 3k products and the JVM chain's
+//        own rounding: (3k + k) 2^-24 sum |u_c v_c| at k <= 128; twice that
+//        margin; sum |u_c v_c| <= ||u|| ||v||), so the item
 //        holding a model's exact max lies in a group whose approximate max is
 //        within 2E of the approximate extreme (likewise the min). Those groups
 //        are rescored exactly: the ALS JVM chain per item, the two-tower score
@@ -53,20 +57,21 @@ union HxFrag {
 
 constexpr int kHxGrp = 32;       // items per statistics group (one 32-row MFMA tile)
 constexpr int kHxMaxK = 8;       // top_k handled here (kFuseK of the materialised path)
-constexpr double kHxRel = 0x1p-6;
+constexpr double kHxRel = 0x1p-13;
 constexpr double kHxAbs = 1e-30;  // denormal products the matrix cores may flush
 constexpr double kHxHuge = 0x1p60;  // a bound above this (or non-finite): rescore every group
 constexpr int kHxThreads1 = 256;
 constexpr int kHxThreads2 = 512;
+constexpr int kHxStatsLds = 8192;  // group records a phase-2 block keeps in LDS (128 KiB)
 
 template <int DK>
 struct HxShape {
-  static constexpr int KS = DK / 16;               // 32x32x16 k-steps
-  static constexpr int kRowB = DK * 2 + 16;        // LDS bytes per staged user row
-  static constexpr int UB = DK == 64 ? 256 : 128;  // users per tile (2 x UB rows: <= 74 KB of LDS)
-  static constexpr int NI = DK == 64 ? 2 : 1;      // 32-item tiles per wave slice (VGPR budget)
-  static constexpr int kSlice = 32 * NI;
-  static constexpr int kBlockItems = (kHxThreads1 / 64) * kSlice;
+  static constexpr int KS = DK / 16;               // 32x32x16 k-steps per operand half
+  static constexpr int kOpB = DK * 4;              // bytes per operand row: [hi | lo] bf16
+  static constexpr int kRowB = kOpB + 16;          // LDS bytes per staged user row
+  static constexpr int UB = DK == 64 ? 128 : 64;   // users per tile (2 x UB rows: <= 70 KB of LDS)
+  static constexpr int kSlices = DK == 64 ? 4 : 2;  // 32-item slices per wave
+  static constexpr int kBlockItems = (kHxThreads1 / 64) * 32 * kSlices;
 };
 
 __device__ __forceinline__ float hx_up(double x) {  // the smallest float >= x
@@ -81,9 +86,16 @@ __device__ __forceinline__ float hx_down(double x) {  // the largest float <= x
 }
 __device__ __forceinline__ float hx_u2f(uint32_t u) { return __uint_as_float(u); }
 
-// 0. bf16 user operands [2][B][DK]: the ALS rows als_users[rows[b]] (a row
-// outside [0, n_rows) reads as NaN, as hrec_als_score's unknown users), the
-// two-tower rows; columns >= width zero.
+// Split bf16 of x: hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in f32).
+__device__ __forceinline__ void hx_split(float x, uint16_t& hi, uint16_t& lo) {
+  const uint32_t h = hp_bf16(x);
+  hi = (uint16_t)h;
+  lo = (uint16_t)hp_bf16(x - __uint_as_float(h << 16));
+}
+
+// 0. Split bf16 user operands [2][B][2 DK] ([hi | lo] per row): the ALS rows
+// als_users[rows[b]] (a row outside [0, n_rows) reads as NaN, as
+// hrec_als_score's unknown users), the two-tower rows; columns >= width zero.
 __global__ __launch_bounds__(128) void hx_user_ops_kernel(const float* __restrict__ U, int64_t ldu,
                                                           const int64_t* __restrict__ rows, int64_t n_rows, int ka,
                                                           const float* __restrict__ T, int64_t ldt, int kt, int B,
@@ -97,171 +109,213 @@ __global__ __launch_bounds__(128) void hx_user_ops_kernel(const float* __restric
   }
   const float* src = m ? T + (int64_t)b * ldt : U + (bad ? 0 : r) * ldu;
   const int w = m ? kt : ka;
-  uint16_t* out = uop + ((int64_t)m * B + b) * dk;
+  uint16_t* out = uop + ((int64_t)m * B + b) * 2 * dk;
   for (int c = threadIdx.x; c < dk; c += blockDim.x) {
     float v = 0.f;
     if (c < w) v = bad ? __builtin_nanf("") : src[c];
-    out[c] = (uint16_t)hp_bf16(v);
+    hx_split(v, out[c], out[dk + c]);
   }
 }
 
-// Item-side operands (once per shard): bf16 rows [2][N][dk] (ALS, two-tower;
-// zero beyond the width) and each model's largest row 2-norm rounded up
-// (+inf when a row holds a non-finite value or the norm is huge). One wave per
-// (row, model).
+// Item-side operands (once per shard): split bf16 rows [2][N][2 dk] (ALS,
+// two-tower; [hi | lo], zero beyond the width) and each model's largest row
+// 2-norm rounded up (+inf when a row holds a non-finite value or the norm is
+// huge). One thread per (row, model); the ALS factors come transposed
+// (A[c * lda + row], hrec_als_score's layout), the two-tower rows row-major.
 __global__ __launch_bounds__(256) void hx_prepare_kernel(const float* __restrict__ A, int64_t lda, int ka,
                                                          const float* __restrict__ T, int64_t ldt, int kt,
                                                          int64_t N, int dk, uint16_t* __restrict__ out,
                                                          unsigned* __restrict__ norms) {
-  const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wid >= 2 * N) return;  // wave-uniform
-  const int m = (int)(wid & 1);
-  const int64_t row = wid >> 1;
-  const float* src = m ? T + row * ldt : A + row * lda;
-  const int w = m ? kt : ka;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int m = blockIdx.y;
   double ss = 0.0;
   bool bad = false;
-  for (int c = lane; c < dk; c += 64) {
-    const float v = c < w ? src[c] : 0.f;
-    out[((int64_t)m * N + row) * dk + c] = (uint16_t)hp_bf16(v);
-    ss += (double)v * (double)v;
-    bad = bad || !isfinite(v);
-  }
+  if (row < N) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + ((int64_t)m * N + row) * 2 * dk);
+    const int w = m ? kt : ka;
+    for (int c = 0; c < dk; c += 2) {
+      float v[2];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, kWave);
-  const bool any_bad = __ballot(bad) != 0;
-  if (lane == 0) {
-    const double nrm = sqrt(ss) * (1.0 + 1e-6);
-    const float f = (any_bad || !(nrm < kHxHuge)) ? INFINITY : hx_up(nrm);
-    atomicMax(&norms[m], __float_as_uint(f));  // non-negative floats order as their bits
+      for (int e = 0; e < 2; ++e)
+        v[e] = c + e < w ? (m ? T[row * ldt + c + e] : A[(int64_t)(c + e) * lda + row]) : 0.f;
+      uint16_t h[2], l[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        hx_split(v[e], h[e], l[e]);
+        ss += (double)v[e] * (double)v[e];
+        bad = bad || !isfinite(v[e]);
+      }
+      o[c >> 1] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      o[(dk + c) >> 1] = (uint32_t)l[0] | ((uint32_t)l[1] << 16);
+    }
   }
+  const double nrm = sqrt(ss) * (1.0 + 1e-6);
+  unsigned f = __float_as_uint((bad || !(nrm < kHxHuge)) ? INFINITY : hx_up(nrm));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned o = (unsigned)__shfl_xor((int)f, off, kWave);
+    f = o > f ? o : f;  // non-negative floats order as their bits
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(&norms[m], f);
 }
 
 // 1. Phase 1: block = (user tile of UB users, kBlockItems items); each wave
-// owns one slice of NI 32-item tiles, keeps its item fragments (both models,
-// every k-step) in registers and sweeps the tile's users in chunks of 32 from
-// LDS. MFMA roles: A = items (32 rows), B = users (32 columns), so lane (h, c)
+// walks kSlices 32-item slices, keeps a slice's item fragments (both models,
+// hi and lo, every k-step) in registers and sweeps the tile's users in chunks
+// of 32 from LDS; the last chunk refills the fragments with the next slice's.
+// MFMA roles: A = items (32 rows), B = users (32 columns), so lane (h, c)
 // holds user c and items 8 q + 4 h + r (register 4 q + r). Per (user, group):
 // [max, min] of each model's approximate scores (fmaxf / fminf: NaN-free,
 // like hrec_rows_minmax_f32), one 16-B record.
+#ifdef HREC_HX_STAMPS
+__device__ unsigned long long g_hx1_stamps[4096][4];  // per block: start, staged, wave 0 done, wave 3 done
+#define HX1_STAMP(i)                                                                         \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) g_hx1_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define HX1_STAMP(i)
+#endif
+
 template <int DK>
 __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* __restrict__ uop, int B, int n_ut,
                                                                const char* __restrict__ items, int64_t N, int G,
                                                                float* __restrict__ stats) {
   using S = HxShape<DK>;
-  constexpr int KS = S::KS, NI = S::NI, UB = S::UB, kRowB = S::kRowB;
+  constexpr int KS = S::KS, UB = S::UB, kRowB = S::kRowB, kOpB = S::kOpB;
   __shared__ __attribute__((aligned(16))) char us[2 * UB * kRowB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c = lane & 31;
   const int ut = (int)(blockIdx.x % (unsigned)n_ut);
   const int64_t i0 = (int64_t)(blockIdx.x / (unsigned)n_ut) * S::kBlockItems;
-  const int64_t jb = i0 + (int64_t)S::kSlice * w;
   const int b0 = ut * UB;
   const int ub = B - b0 < UB ? B - b0 : UB;
-  const char* ia = items;                              // ALS operand [N][DK]
-  const char* it = items + (size_t)N * (DK * 2);      // two-tower operand [N][DK]
-  const hrec_rsrc_t ra = rows_rsrc(ia, i0, DK * 2, N), rt = rows_rsrc(it, i0, DK * 2, N);
-  // the wave's item fragments first: they arrive while the users are staged
-  HxFrag fa[NI][KS], ft[NI][KS];
-  const bool work = jb < N;
-  if (work) {
+  const char* ia = items;                        // ALS operand [N][2 DK]
+  const char* it = items + (size_t)N * kOpB;     // two-tower operand [N][2 DK]
+  const hrec_rsrc_t ra = rows_rsrc(ia, i0, kOpB, N), rt = rows_rsrc(it, i0, kOpB, N);
+  HxFrag fa[2][KS], ft[2][KS];  // [hi / lo][k-step]
+  auto load = [&](int64_t jb) {
+    const int64_t j = jb + c;
+    const int vi = j < N ? (int)(j - i0) : 0x7fffffff;  // out of range: the buffer check reads zeros
 #pragma unroll
-    for (int t = 0; t < NI; ++t) {
-      const int64_t j = jb + 32 * t + c;
-      const int vi = j < N ? (int)(j - i0) : 0x7fffffff;  // out of range: the buffer check reads zeros
+    for (int p = 0; p < 2; ++p)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        fa[t][ks].f = hx_sbuf_load(ra, vi, 32 * ks + 16 * h, 0, 0);
-        ft[t][ks].f = hx_sbuf_load(rt, vi, 32 * ks + 16 * h, 0, 0);
+        fa[p][ks].f = hx_sbuf_load(ra, vi, p * (DK * 2) + 32 * ks + 16 * h, 0, 0);
+        ft[p][ks].f = hx_sbuf_load(rt, vi, p * (DK * 2) + 32 * ks + 16 * h, 0, 0);
       }
+  };
+  int64_t jb = i0 + 32 * w;
+  if (w == 0) HX1_STAMP(0);
+  if (jb < N) load(jb);  // the first slice arrives while the users are staged
+  // users -> LDS: every load of a thread in flight before its stores (one
+  // round trip, not one per 16-B chunk)
+  constexpr int CPR = kOpB / 16;  // 16-B chunks per user row
+  constexpr int kPer = 2 * UB * CPR / kHxThreads1;
+  static_assert(kPer * kHxThreads1 == 2 * UB * CPR, "whole chunks per thread");
+  {
+    int4 v[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      const int o = threadIdx.x + e * kHxThreads1;
+      const int m = o / (UB * CPR), rem = o % (UB * CPR), r = rem / CPR, q = rem % CPR;
+      v[e] = int4{0, 0, 0, 0};
+      if (r < ub) v[e] = *reinterpret_cast<const int4*>(uop + (int64_t)(m * B + b0 + r) * (2 * DK) + 8 * q);
     }
-  }
-  constexpr int CPR = DK / 8;  // 16-B chunks per user row
-  for (int o = threadIdx.x; o < 2 * UB * CPR; o += kHxThreads1) {
-    const int m = o / (UB * CPR), rem = o % (UB * CPR), r = rem / CPR, q = rem % CPR;
-    int4 v = {0, 0, 0, 0};
-    if (r < ub) v = *reinterpret_cast<const int4*>(uop + ((int64_t)(m * B + b0 + r) * DK + 8 * q));
-    *reinterpret_cast<int4*>(us + (m * UB + r) * kRowB + 16 * q) = v;
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      const int o = threadIdx.x + e * kHxThreads1;
+      const int m = o / (UB * CPR), rem = o % (UB * CPR), r = rem / CPR, q = rem % CPR;
+      *reinterpret_cast<int4*>(us + (m * UB + r) * kRowB + 16 * q) = v[e];
+    }
   }
   __syncthreads();
-  if (!work) return;  // wave-uniform; no barrier follows
-  const bool full = jb + S::kSlice <= N;
-  for (int ch = 0; 32 * ch < ub; ++ch) {
-    hx_f16 acc[2][NI];
+  if (w == 0) HX1_STAMP(1);
+  for (int sl = 0; jb < N; ++sl) {  // wave-uniform; no barrier follows
+    const bool full = jb + 32 <= N;
+    const int64_t jn = jb + 32 * (kHxThreads1 / 64);
+    const bool more = sl + 1 < S::kSlices && jn < N;
+    for (int ch = 0; 32 * ch < ub; ++ch) {
+      hx_f16 acc[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int t = 0; t < NI; ++t)
+        for (int v = 0; v < 16; ++v) acc[m][v] = 0.f;
+      const char* ura = us + (32 * ch + c) * kRowB + 16 * h;
+      const char* urt = us + (UB + 32 * ch + c) * kRowB + 16 * h;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc[m][t][v] = 0.f;
-    const char* ura = us + (32 * ch + c) * kRowB + 16 * h;
-    const char* urt = us + (UB + 32 * ch + c) * kRowB + 16 * h;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      HxFrag ua, uu;
-      ua.i = *reinterpret_cast<const int4*>(ura + 32 * ks);
-      uu.i = *reinterpret_cast<const int4*>(urt + 32 * ks);
-#pragma unroll
-      for (int t = 0; t < NI; ++t) {
-        acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(hx_bf8, fa[t][ks].i),
-                                                            __builtin_bit_cast(hx_bf8, ua.i), acc[0][t], 0, 0, 0);
-        acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(hx_bf8, ft[t][ks].i),
-                                                            __builtin_bit_cast(hx_bf8, uu.i), acc[1][t], 0, 0, 0);
+      for (int ks = 0; ks < KS; ++ks) {
+        HxFrag ah, al, th, tl;
+        ah.i = *reinterpret_cast<const int4*>(ura + 32 * ks);
+        al.i = *reinterpret_cast<const int4*>(ura + DK * 2 + 32 * ks);
+        th.i = *reinterpret_cast<const int4*>(urt + 32 * ks);
+        tl.i = *reinterpret_cast<const int4*>(urt + DK * 2 + 32 * ks);
+#define HX_MMA(ACC, X, Y) \
+  ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(hx_bf8, (X).i), __builtin_bit_cast(hx_bf8, (Y).i), ACC, 0, 0, 0)
+        HX_MMA(acc[0], fa[0][ks], ah);  // vh.uh
+        HX_MMA(acc[1], ft[0][ks], th);
+        HX_MMA(acc[0], fa[1][ks], ah);  // vl.uh
+        HX_MMA(acc[1], ft[1][ks], th);
+        HX_MMA(acc[0], fa[0][ks], al);  // vh.ul
+        HX_MMA(acc[1], ft[0][ks], tl);
+#undef HX_MMA
       }
-    }
-    float mx[2][NI], mn[2][NI];
+      if (more && 32 * (ch + 1) >= ub) load(jn);  // last chunk: the next slice's fragments
+      float mx[2], mn[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int t = 0; t < NI; ++t) {
+      for (int m = 0; m < 2; ++m) {
         float hi = -INFINITY, lo = INFINITY;
         if (full) {
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            hi = fmaxf(hi, acc[m][t][v]);
-            lo = fminf(lo, acc[m][t][v]);
+            hi = fmaxf(hi, acc[m][v]);
+            lo = fminf(lo, acc[m][v]);
           }
         } else {
 #pragma unroll
           for (int v = 0; v < 16; ++v)
-            if (jb + 32 * t + 8 * (v >> 2) + 4 * h + (v & 3) < N) {
-              hi = fmaxf(hi, acc[m][t][v]);
-              lo = fminf(lo, acc[m][t][v]);
+            if (jb + 8 * (v >> 2) + 4 * h + (v & 3) < N) {
+              hi = fmaxf(hi, acc[m][v]);
+              lo = fminf(lo, acc[m][v]);
             }
         }
-        mx[m][t] = hi;
-        mn[m][t] = lo;
+        mx[m] = hi;
+        mn[m] = lo;
       }
-    const int b = b0 + 32 * ch + c;
-    // the two lane halves hold the two halves of a group: one
-    // v_permlane32_swap per register pair folds them for two tiles / models
-    if constexpr (NI == 2) {
-      float rec[4];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const auto X = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx[m][0]), __float_as_uint(mx[m][1]), false,
-                                                        false);
-        const auto Y = __builtin_amdgcn_permlane32_swap(__float_as_uint(mn[m][0]), __float_as_uint(mn[m][1]), false,
-                                                        false);
-        rec[2 * m] = fmaxf(hx_u2f(X[0]), hx_u2f(X[1]));  // lanes < 32: tile 0, lanes >= 32: tile 1
-        rec[2 * m + 1] = fminf(hx_u2f(Y[0]), hx_u2f(Y[1]));
-      }
-      const int64_t grp = (jb >> 5) + h;
-      if (b < B && grp < G)
-        *reinterpret_cast<float4*>(stats + ((int64_t)b * G + grp) * 4) = make_float4(rec[0], rec[1], rec[2], rec[3]);
-    } else {
-      const auto X = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx[0][0]), __float_as_uint(mx[1][0]), false,
-                                                      false);
-      const auto Y = __builtin_amdgcn_permlane32_swap(__float_as_uint(mn[0][0]), __float_as_uint(mn[1][0]), false,
-                                                      false);
+      // the two lane halves hold the two halves of the group: one
+      // v_permlane32_swap per register pair folds them for both models
+      const auto X = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx[0]), __float_as_uint(mx[1]), false, false);
+      const auto Y = __builtin_amdgcn_permlane32_swap(__float_as_uint(mn[0]), __float_as_uint(mn[1]), false, false);
       const float hi = fmaxf(hx_u2f(X[0]), hx_u2f(X[1]));  // lanes < 32: ALS, lanes >= 32: two-tower
       const float lo = fminf(hx_u2f(Y[0]), hx_u2f(Y[1]));
-      const int64_t grp = jb >> 5;
-      if (b < B) *reinterpret_cast<float2*>(stats + ((int64_t)b * G + grp) * 4 + 2 * h) = make_float2(hi, lo);
+      const int b = b0 + 32 * ch + c;
+      if (b < B) *reinterpret_cast<float2*>(stats + ((int64_t)b * G + (jb >> 5)) * 4 + 2 * h) = make_float2(hi, lo);
     }
+    if (!more) break;
+    jb = jn;
   }
+  if (w == 0) HX1_STAMP(2);
+  if (w == 3) HX1_STAMP(3);
 }
+
+#ifdef HREC_HX_STAMPS
+// Diagnostic builds only: per block (thread 0) s_memtime at the phase points
+// of hx_user_kernel, plain stores.
+constexpr int kHxStampBlocks = 1024;
+__device__ unsigned long long g_hx_stamps[kHxStampBlocks][16];
+__device__ unsigned long long g_hx_wstamps[kHxStampBlocks][8][4];  // per wave: seed start, scan done, insert done, merge entry
+#define HX_WSTAMP(i)                                                           \
+  do {                                                                         \
+    if (lane == 0 && b < kHxStampBlocks) g_hx_wstamps[b][wv][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define HX_STAMP(i)                                                            \
+  do {                                                                         \
+    if (tid == 0 && b < kHxStampBlocks) g_hx_stamps[b][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define HX_STAMP(i)
+#define HX_WSTAMP(i)
+#endif
 
 struct HxArgs {
   const float* U;  // ALS user factors (rows[b] of them; width ka)
@@ -273,10 +327,12 @@ struct HxArgs {
   int64_t ldt;
   int kt;
   int B;
-  const float* Va;  // ALS item factor rows [N] (f32, row stride lda)
+  const float* Vat;  // ALS item factors transposed: item j, column c at Vat[c * lda + j]
   int64_t lda;
-  const float* Vt;  // two-tower item vectors [N] (f32, row stride ldv)
+  const float* Vt;   // two-tower item vectors [N] (row-major, row stride ldv)
   int64_t ldv;
+  const float* Vtt;  // the same transposed: Vtt[c * ldtt + j]
+  int64_t ldtt;
   const float* inorm;  // [2] the item operands' largest norms (hx_prepare_kernel)
   int64_t N;
   int G;
@@ -294,35 +350,72 @@ struct HxArgs {
 
 // 2. Phase 2, one 512-thread block per user. MODE 0: the exact extremes
 // (mm_a / mm_t out); 1: the top-k with the given (global) extremes; 2: both
-// (one shard).
-template <int DK, int MODE>
+// (one shard). FULL: ka == kt == DK (the c2 shape), no width guards.
+//
+// A wave scores two groups at a time, lane l = item l of the pair. The ALS
+// score is the JVM chain itself, read from the TRANSPOSED item factors (per
+// column c one coalesced 128-B run per group: the row-major gathers touched
+// 64 lines per instruction). The two-tower score is first bounded by an f32
+// fma chain over the transposed item vectors (within Ef of the exact
+// score); the exact two-tower score — hrec_dot_scores' MFMA chain over
+// row-major rows — is computed only for the items whose fused bound can
+// still reach the top-k (16 per MFMA round), or for every item of the few
+// groups that can hold a two-tower extreme.
+template <int DK, int MODE, bool FULL>
 __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
 #pragma clang fp contract(off)
   constexpr int KK = kHxMaxK;
   static_assert(8 * KK == 64, "one merge slot per lane of wave 0");
+  constexpr int kList = 1024;  // groups compacted per sweep window
   __shared__ __attribute__((aligned(16))) float sua[DK];
   __shared__ __attribute__((aligned(16))) float sut[DK];
   __shared__ float sred[8][4];
-  __shared__ double se[2];
+  __shared__ double se[3];
   __shared__ double rv[8 * KK];
   __shared__ int64_t ri[8 * KK];
   __shared__ double s_tau;
-  __shared__ int s_full, s_cnt;
+  __shared__ int s_full, s_cnt, s_n;
+  __shared__ int s_list[kList];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int b = blockIdx.x;
   const int64_t N = a.N;
   const int G = a.G;
-  const float4* st_row = reinterpret_cast<const float4*>(a.stats) + (int64_t)b * G;
+  const int ka = FULL ? DK : a.ka, kt = FULL ? DK : a.kt;
+  // the user's group records: staged in LDS once when they fit (every pass
+  // below reads them several times), else read from memory
+  extern __shared__ __attribute__((aligned(16))) float4 st_lds[];
+  const float4* st_glob = reinterpret_cast<const float4*>(a.stats) + (int64_t)b * G;
+  const bool st_in_lds = G <= kHxStatsLds;
+  const float4* st_row = st_in_lds ? st_lds : st_glob;
+  HX_STAMP(0);
+  if (st_in_lds) {
+    HX_STAMP(12);
+    for (int g0 = tid; g0 < G; g0 += 8 * kHxThreads2) {
+      float4 x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int g = g0 + e * kHxThreads2;
+        if (g < G) x[e] = st_glob[g];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int g = g0 + e * kHxThreads2;
+        if (g < G) st_lds[g] = x[e];
+      }
+    }
+  }
   // the user's f32 rows (the exact chains read them from LDS)
   const int64_t r = a.rows ? a.rows[b] : (int64_t)b;
   const bool rok = r >= 0 && r < a.n_rows;
   for (int c = tid; c < DK; c += kHxThreads2) {
-    sua[c] = c < a.ka ? (rok ? a.U[r * a.ldu + c] : __builtin_nanf("")) : 0.f;
-    sut[c] = c < a.kt ? a.T[(int64_t)b * a.ldt + c] : 0.f;
+    sua[c] = c < ka ? (rok ? a.U[r * a.ldu + c] : __builtin_nanf("")) : 0.f;
+    sut[c] = c < kt ? a.T[(int64_t)b * a.ldt + c] : 0.f;
   }
   if (tid == 0) s_cnt = 0;
+  HX_STAMP(13);
   __syncthreads();
-  if (wv == 0) {  // E of both models (f64 norms)
+  HX_STAMP(14);
+  if (wv == 0) {  // the bounds of both models (f64 norms)
     double sa = 0.0, sb = 0.0;
     for (int c = lane; c < DK; c += 64) {
       sa += (double)sua[c] * (double)sua[c];
@@ -336,131 +429,125 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
     if (lane == 0) {
       se[0] = kHxRel * (sqrt(sa) * (1.0 + 1e-6)) * (double)a.inorm[0] + kHxAbs;
       se[1] = kHxRel * (sqrt(sb) * (1.0 + 1e-6)) * (double)a.inorm[1] + kHxAbs;
+      // the f32 fma chain vs the MFMA chain (bitwise an fma chain): both
+      // within gamma_kt sum |u_c v_c| of the real dot
+      se[2] = (2.0 * kt + 4.0) * 0x1p-24 * (sqrt(sb) * (1.0 + 1e-6)) * (double)a.inorm[1] + kHxAbs;
     }
   }
   __syncthreads();
-  const double Ea = se[0], Et = se[1];
+  const double Ea = se[0], Et = se[1], Ef = se[2];
   const bool bad_a = !(Ea < kHxHuge), bad_t = !(Et < kHxHuge);  // NaN / inf / huge: no bound
 
-  // exact scores of two groups' 64 items (lane l: item l of the pair; gB < 0:
-  // none), wave-uniform: the ALS JVM chain per lane, the two-tower score by
-  // 4 MFMA chains of 16 items in hrec_dot_scores' k order, moved to the lanes
-  auto rescore = [&](int gA, int gB, float& s_als, float& s_tt, bool& ok, int64_t& j) {
+  // lane l's item of the pair (gA, gB): j, in range
+  auto item_of = [&](int gA, int gB, int64_t& j) {
     const int gl = lane < 32 ? gA : gB;
     j = (int64_t)gl * kHxGrp + (lane & 31);
-    ok = gl >= 0 && j < N;
-    {  // ALS: sequential rounded products and sums over c < ka (Spark's
-       // dotProduct += a(i) * b(i)); the zero-padded tail adds +-0, a no-op
-      const float* vr = a.Va + (ok ? j : 0) * a.lda;
-      float s = 0.f;
-      for (int c0 = 0; c0 < a.ka; c0 += 64) {
-        float4 v[16];
+    return gl >= 0 && j < N;
+  };
+  // the exact ALS score (sequential rounded products and sums over c < ka,
+  // Spark's dotProduct += a(i) * b(i)) and the two-tower fma chain of item j,
+  // from the transposed matrices: 16 columns of both per batch of loads
+  auto scan = [&](int64_t j, bool ok, float& s_als, float& t_fma) {
+    const int64_t jj = ok ? j : 0;
+    const float* pa = a.Vat + jj;
+    const float* pt = a.Vtt + jj;
+    const int n = ka > kt ? ka : kt;
+    float s = 0.f, t = 0.f;
+    for (int c0 = 0; c0 < n; c0 += 32) {  // 64 loads per lane in flight per batch
+      float va[32], vt[32];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int cq = c0 + 4 * q;
-          v[q] = cq < a.ka ? *reinterpret_cast<const float4*>(vr + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
-          if (cq + 4 > a.ka) {  // columns >= ka: zero (whatever the padding holds)
-            if (cq + 1 >= a.ka) v[q].y = 0.f;
-            if (cq + 2 >= a.ka) v[q].z = 0.f;
-            if (cq + 3 >= a.ka) v[q].w = 0.f;
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          if (c0 + 4 * q >= a.ka) break;
-          const float4 u = *reinterpret_cast<const float4*>(sua + c0 + 4 * q);
-          float p = u.x * v[q].x;
-          s = s + p;
-          p = u.y * v[q].y;
-          s = s + p;
-          p = u.z * v[q].z;
-          s = s + p;
-          p = u.w * v[q].w;
-          s = s + p;
-        }
+      for (int q = 0; q < 32; ++q) {
+        va[q] = (FULL || c0 + q < ka) ? pa[(int64_t)(c0 + q) * a.lda] : 0.f;
+        vt[q] = (FULL || c0 + q < kt) ? pt[(int64_t)(c0 + q) * a.ldtt] : 0.f;
       }
-      s_als = s;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 32; q += 4) {
+        const float4 u = *reinterpret_cast<const float4*>(sua + c0 + q);
+        const float4 w = *reinterpret_cast<const float4*>(sut + c0 + q);
+        float p = u.x * va[q];
+        s = s + p;
+        p = u.y * va[q + 1];
+        s = s + p;
+        p = u.z * va[q + 2];
+        s = s + p;
+        p = u.w * va[q + 3];
+        s = s + p;  // columns >= ka: 0 * 0, adds +0 (a no-op)
+        t = fmaf(w.x, vt[q], t);
+        t = fmaf(w.y, vt[q + 1], t);
+        t = fmaf(w.z, vt[q + 2], t);
+        t = fmaf(w.w, vt[q + 3], t);
+      }
     }
-    {  // two-tower
-      const int g = lane >> 4, cc = lane & 15;
-      const int KT = a.kt >> 4;
-      hp_f4 acc[4];
+    s_als = s;
+    t_fma = t;
+  };
+  // exact two-tower scores of up to 16 items, survivor cc's lane `my`
+  // (-1: none) given on lane cc (< 16): hrec_dot_scores' MFMA chain (k order
+  // 16 ks + 4 g + e, A = the item rows). Lane (g, cc < 4) gets survivor 4 g + cc.
+  auto tt_exact16 = [&](int64_t jrow, bool has) {
+    const int g4 = lane >> 4;
+    const float* row = a.Vt + (has ? jrow : 0) * a.ldv + 4 * g4;
+    const int KT = kt >> 4;
+    hp_f4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks0 = 0; ks0 < KT; ks0 += 4) {
+      HxFrag itf[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = hp_f4{0.f, 0.f, 0.f, 0.f};
-      const float* rowq[4];
+      for (int kq = 0; kq < 4; ++kq)
+        itf[kq].f = (FULL || ks0 + kq < KT) ? *reinterpret_cast<const hp_f4*>(row + 16 * (ks0 + kq))
+                                            : hp_f4{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gq = q < 2 ? gA : gB;
-        const int64_t jq = (int64_t)gq * kHxGrp + 16 * (q & 1) + cc;
-        rowq[q] = a.Vt + ((gq >= 0 && jq < N) ? jq : 0) * a.ldv + 4 * g;
-      }
-      for (int ks0 = 0; ks0 < KT; ks0 += 4) {
-        HxFrag itf[4][4], uf[4];
+      for (int kq = 0; kq < 4; ++kq) {
+        if (FULL || ks0 + kq < KT) {
+          HxFrag uf;
+          uf.f = *reinterpret_cast<const hp_f4*>(sut + 16 * (ks0 + kq) + 4 * g4);
 #pragma unroll
-        for (int kq = 0; kq < 4; ++kq) {
-          if (ks0 + kq < KT) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) itf[q][kq].f = *reinterpret_cast<const hp_f4*>(rowq[q] + 16 * (ks0 + kq));
-            uf[kq].f = *reinterpret_cast<const hp_f4*>(sut + 16 * (ks0 + kq) + 4 * g);
-          }
-        }
-#pragma unroll
-        for (int kq = 0; kq < 4; ++kq) {
-          if (ks0 + kq < KT) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(itf[q][kq].f[e], uf[kq].f[e], acc[q], 0, 0, 0);
-          }
+          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(itf[kq].f[e], uf.f[e], acc, 0, 0, 0);
         }
       }
-      // lane (g, cc) holds items 16 q + 4 g + r of chain q; publish item
-      // 16 (cc >> 2) + 4 g + (cc & 3), then lane l reads item l
-      const hp_f4& aq = (cc >> 2) == 0 ? acc[0] : ((cc >> 2) == 1 ? acc[1] : ((cc >> 2) == 2 ? acc[2] : acc[3]));
-      const float pub = hp_pick(aq, cc & 3);
-      const int src = 16 * ((lane >> 2) & 3) + 4 * (lane >> 4) + (lane & 3);
-      s_tt = __shfl(pub, src, kWave);
+    }
+    return hp_pick(acc, lane & 3);  // meaningful on lanes (g, cc < 4)
+  };
+  // every lane with `m`'s bit set in rounds of 16: fn(j, s_als, t_exact) on
+  // lane (g, cc < 4) for survivor 4 g + cc (wave-uniform)
+  auto exact_rounds = [&](uint64_t m, int64_t j, float s_als, auto fn) {
+    const int cc = lane & 15;
+    while (m) {
+      int my = -1;
+      for (int i = 0; i < 16 && m; ++i) {
+        const int bit = __builtin_ctzll(m);
+        m &= m - 1;
+        my = cc == i ? bit : my;
+      }
+      const int src = my < 0 ? 0 : my;
+      const int64_t jr = __shfl(j, src, kWave);
+      const float ar = __shfl(s_als, src, kWave);
+      const float tx = tt_exact16(jr, my >= 0);
+      const int q = 4 * (lane >> 4) + (cc & 3);
+      const int myq = __shfl(my, q, kWave);
+      const int64_t jq = __shfl(jr, q, kWave);
+      const float aq = __shfl(ar, q, kWave);
+      if (cc < 4 && myq >= 0) fn(jq, aq, tx);
     }
   };
-  // every group with pred(g) rescored, two per wave call; consume(s_als,
-  // s_tt, ok, j) per lane. Groups are dealt in batches of 64 per wave.
-  auto sweep = [&](auto pred, auto consume) {
-    int n_resc = 0;
-    int carry = -1;  // a lone group waiting for a partner
-    for (int base = 64 * wv; base < G; base += 64 * 8) {
-      const int g = base + lane;
-      const bool p = g < G && pred(g);
-      uint64_t m = __ballot(p);
-      n_resc += __popcll(m);
-      while (m) {
-        int gA = carry;
-        if (gA < 0) {
-          gA = base + __builtin_ctzll(m);
-          m &= m - 1;
-        }
-        if (!m) {
-          carry = gA;
-          break;
-        }
-        const int gB = base + __builtin_ctzll(m);
-        m &= m - 1;
-        carry = -1;
-        float sa, stt;
-        bool ok;
-        int64_t j;
-        rescore(gA, gB, sa, stt, ok, j);
-        consume(sa, stt, ok, j);
-      }
+  // every group with pred(g), in windows of kList groups: compacted into LDS
+  // (any order: the results do not depend on it), then dealt to the waves
+  // two at a time, round robin (the live groups of a user cluster; dealing
+  // them by index left one wave most of them)
+  auto sweep = [&](auto pred, auto pair) {
+    for (int w0 = 0; w0 < G; w0 += kList) {
+      const int w1e = G - w0 < kList ? G : w0 + kList;
+      if (tid == 0) s_n = 0;
+      __syncthreads();
+      for (int g = w0 + tid; g < w1e; g += kHxThreads2)
+        if (pred(g)) s_list[atomicAdd(&s_n, 1)] = g;
+      __syncthreads();
+      const int n = s_n;
+      if (tid == 0) s_cnt += n;
+      for (int p = wv; 2 * p < n; p += 8) pair(s_list[2 * p], 2 * p + 1 < n ? s_list[2 * p + 1] : -1);
+      __syncthreads();  // the list is rewritten by the next window
     }
-    if (carry >= 0) {
-      float sa, stt;
-      bool ok;
-      int64_t j;
-      rescore(carry, -1, sa, stt, ok, j);
-      consume(sa, stt, ok, j);
-    }
-    if (lane == 0) atomicAdd(&s_cnt, n_resc);
   };
   auto block_minmax = [&](float& lo_a, float& hi_a, float& lo_t, float& hi_t) {
     lo_a = fminf(lo_a, hp_dpp32<0xB1>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0xB1>(hi_a));
@@ -490,13 +577,22 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
 
   float amin = INFINITY, amax = -INFINITY, tmin = INFINITY, tmax = -INFINITY;
   if constexpr (MODE != 1) {
-    // a. approximate extremes, then the groups that can hold an exact one
+    // a. approximate extremes (the group records, 4 loads in flight per
+    // thread), then the groups that can hold an exact one
     float AMN = INFINITY, AMX = -INFINITY, TMN = INFINITY, TMX = -INFINITY;
-    for (int g = tid; g < G; g += kHxThreads2) {
-      const float4 x = st_row[g];
-      AMX = fmaxf(AMX, x.x), AMN = fminf(AMN, x.y), TMX = fmaxf(TMX, x.z), TMN = fminf(TMN, x.w);
+    for (int g0 = tid; g0 < G; g0 += 4 * kHxThreads2) {
+      float4 x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int g = g0 + e * kHxThreads2;
+        x[e] = g < G ? st_row[g] : make_float4(-INFINITY, INFINITY, -INFINITY, INFINITY);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        AMX = fmaxf(AMX, x[e].x), AMN = fminf(AMN, x[e].y), TMX = fmaxf(TMX, x[e].z), TMN = fminf(TMN, x[e].w);
     }
     block_minmax(AMN, AMX, TMN, TMX);
+    HX_STAMP(1);
     const bool all_a = rok && bad_a, all_t = bad_t;
     const bool use_a = rok && !bad_a && AMX >= AMN, use_t = !bad_t && TMX >= TMN;
     const float a_hi = use_a ? hx_down((double)AMX - 2.0 * Ea) : INFINITY;
@@ -512,31 +608,40 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
           const float4 x = st_row[g];
           return x.x >= a_hi || x.y <= a_lo || x.z >= t_hi || x.w <= t_lo;
         },
-        [&](float sa, float stt, bool ok, int64_t) {
-          if (ok) {
-            lo_a = fminf(lo_a, sa), hi_a = fmaxf(hi_a, sa);
-            lo_t = fminf(lo_t, stt), hi_t = fmaxf(hi_t, stt);
-          }
+        [&](int gA, int gB) {
+          // exact ALS scores of every item; the exact two-tower score only
+          // where the fma chain cannot rule the item out as the pair's
+          // extreme (|t_fma - t| <= Ef: the item holding the exact max has
+          // t_fma + Ef >= the pair's max of t_fma - Ef, likewise the min)
+          int64_t j;
+          const bool ok = item_of(gA, gB, j);
+          float sa, tf;
+          scan(j, ok, sa, tf);
+          if (ok) lo_a = fminf(lo_a, sa), hi_a = fmaxf(hi_a, sa);
+          float pm = ok ? tf : -INFINITY, pn = ok ? tf : INFINITY;
+          pm = fmaxf(pm, hp_dpp32<0xB1>(pm)), pn = fminf(pn, hp_dpp32<0xB1>(pn));
+          pm = fmaxf(pm, hp_dpp32<0x4E>(pm)), pn = fminf(pn, hp_dpp32<0x4E>(pn));
+          pm = fmaxf(pm, hp_dpp32<0x141>(pm)), pn = fminf(pn, hp_dpp32<0x141>(pn));
+          pm = fmaxf(pm, hp_dpp32<0x140>(pm)), pn = fminf(pn, hp_dpp32<0x140>(pn));
+          pm = fmaxf(pm, hp_xor16(pm)), pn = fminf(pn, hp_xor16(pn));
+          pm = fmaxf(pm, hp_xor32(pm)), pn = fminf(pn, hp_xor32(pn));
+          const bool cand = ok && (every || (double)tf + Ef >= (double)pm - Ef || (double)tf - Ef <= (double)pn + Ef ||
+                                   tf != tf);
+          exact_rounds(__ballot(cand), j, sa, [&](int64_t, float, float tx) {
+            lo_t = fminf(lo_t, tx), hi_t = fmaxf(hi_t, tx);
+          });
         });
     block_minmax(lo_a, hi_a, lo_t, hi_t);
+    HX_STAMP(2);
     amin = lo_a, amax = hi_a, tmin = lo_t, tmax = hi_t;
     if (tid == 0) {
       a.counts[b] = s_cnt;
       s_cnt = 0;
+      a.mm_a[b] = amin, a.mm_a[a.B + b] = amax;
+      a.mm_t[b] = tmin, a.mm_t[a.B + b] = tmax;
     }
     __syncthreads();  // s_cnt reset before the top-k sweep counts into it
-    if constexpr (MODE == 0) {
-      if (tid == 0) {
-        a.mm_a[b] = amin, a.mm_a[a.B + b] = amax;
-        a.mm_t[b] = tmin, a.mm_t[a.B + b] = tmax;
-      }
-      return;
-    } else {
-      if (tid == 0) {
-        a.mm_a[b] = amin, a.mm_a[a.B + b] = amax;
-        a.mm_t[b] = tmin, a.mm_t[a.B + b] = tmax;
-      }
-    }
+    if constexpr (MODE == 0) return;
   } else {
     amin = a.mm_a[b], amax = a.mm_a[a.B + b], tmin = a.mm_t[b], tmax = a.mm_t[a.B + b];
   }
@@ -560,10 +665,81 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
     return hp_fuse(sc, hx_up((double)x.x + Ea), hx_up((double)x.z + Et), w0, w1);
   };
   HpList<KK> L;
-  // the lanes' lists -> each wave's best kk -> wave 0's merge: s_tau = the
-  // kk-th best value, s_full = 1 when a NaN or a missing entry is among the
-  // kk; the outputs written when `write`
+  // the lanes' lists -> the block's kk best: s_tau = the kk-th best value,
+  // s_full = 1 when a NaN or a missing entry is among the kk; the outputs
+  // written when `write`. The lanes' entries (few: only exactly scored items
+  // enter) are compacted into LDS and each ranked by counting the better ones
+  // (one order key per entry); more than kMerge entries take the waves'
+  // arg-best rounds instead.
+  constexpr int kMerge = 512;
+  __shared__ uint64_t mk[kMerge];
+  __shared__ int64_t mi[kMerge];
+  __shared__ double mv[kMerge];
+  __shared__ int s_m, s_bad;
   auto merge = [&](bool write) {
+    if (tid == 0) s_m = 0, s_bad = 0;
+    __syncthreads();
+    // a wave holding more than 8 entries sends only its kk best (the
+    // block's kk best are among the waves' kk best): <= 64 entries to rank
+    int wn = 0;
+#pragma unroll
+    for (int e = 0; e < KK; ++e) wn += __popcll(__ballot(L.i[e] != INT64_MAX));
+    if (wn > 8) {  // wave-uniform
+      L.wave_top(kk, lane, rv + wv * KK, ri + wv * KK);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's LDS writes -> the wave's reads
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < kk && ri[wv * KK + lane] != INT64_MAX) {
+        const int p = atomicAdd(&s_m, 1);
+        const double v = rv[wv * KK + lane];
+        const int64_t i = ri[wv * KK + lane];
+        if (p < kMerge) mk[p] = hp_order_key(v, i), mi[p] = i, mv[p] = v;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < KK; ++e) {
+        if (L.i[e] != INT64_MAX) {
+          const int p = atomicAdd(&s_m, 1);
+          if (p < kMerge) mk[p] = hp_order_key(L.v[e], L.i[e]), mi[p] = L.i[e], mv[p] = L.v[e];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = s_m;
+    if (n <= kMerge) {  // block-uniform
+      if (tid < kk && tid >= n) {  // fewer than kk entries: the missing ranks
+        s_bad = 1;
+        if (write) {
+          a.out_idx[(int64_t)b * kk + tid] = -1;
+          a.out_val[(int64_t)b * kk + tid] = 0.0;
+        }
+      }
+      for (int q = tid; q < n; q += kHxThreads2) {
+        const uint64_t kq = mk[q];
+        const int64_t iq = mi[q];
+        int rank = 0;
+        for (int x = 0; x < n; ++x) {
+          const uint64_t kx = mk[x];
+          rank += (int)(kx > kq) | ((int)(kx == kq) & (int)(mi[x] < iq));
+        }
+        if (rank < kk) {
+          const double vq = mv[q];
+          if (vq != vq) s_bad = 1;
+          if (write) {
+            a.out_idx[(int64_t)b * kk + rank] = iq + a.idx_offset;
+            a.out_val[(int64_t)b * kk + rank] = vq;
+          }
+          if (rank == kk - 1) s_tau = vq;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        s_full = s_bad;
+        if (s_bad) s_tau = -INFINITY;
+      }
+      __syncthreads();
+      return;
+    }
     L.wave_top(kk, lane, rv + wv * KK, ri + wv * KK);
     __syncthreads();
     if (wv == 0) {
@@ -594,14 +770,29 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
     }
     __syncthreads();
   };
-  auto take = [&](float sa, float stt, bool ok, int64_t j) {
-    if (ok) L.insert(hp_fuse(sc, sa, stt, w0, w1), j);
-  };
   double tau = -INFINITY;
+  // the top-k over two groups: items whose fused bound (exact ALS score,
+  // two-tower fma chain + Ef) reaches tau (all: all_pass) take the exact
+  // two-tower chain and enter the lists
+  auto topk_pair = [&](int gA, int gB, bool all_pass) {
+    int64_t j;
+    const bool ok = item_of(gA, gB, j);
+    float sa, tf;
+    scan(j, ok, sa, tf);
+    const bool pass = ok && (all_pass || hp_fuse(sc, sa, hx_up((double)tf + Ef), w0, w1) >= tau);
+    exact_rounds(__ballot(pass), j, sa,
+                 [&](int64_t jq, float aq, float tx) { L.insert(hp_fuse(sc, aq, tx, w0, w1), jq); });
+  };
   if (!every) {
-    // seeds: each wave's two groups with the largest bounds
+    // tau from seeds: each wave's two groups with the largest bounds; a
+    // seed's fused score is bounded below by its exact ALS score and its
+    // fma chain - Ef, so the kk-th best of those bounds (distinct items) is a
+    // lower bound of the shard's kk-th best fused score — no exact two-tower
+    // chain needed
     double bu = -INFINITY;
     int64_t bg = INT64_MAX;
+    HX_STAMP(7);
+    HX_WSTAMP(0);
     for (int g = 64 * wv + lane; g < G; g += 64 * 8) {
       const double u = ub_of(g);
       if (bg == INT64_MAX || hp_better(u, g, bu, bg)) {
@@ -609,6 +800,7 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
         bg = g;
       }
     }
+    HX_STAMP(8);
     double v1 = bu;
     int64_t g1 = bg;
     hp_wave_best(v1, g1);
@@ -617,33 +809,42 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
     int64_t g2 = bg;
     hp_wave_best(v2, g2);
     L.reset();
+    HX_STAMP(9);
     if (g1 != INT64_MAX) {
-      float sa, stt;
-      bool ok;
       int64_t j;
-      rescore((int)g1, g2 == INT64_MAX ? -1 : (int)g2, sa, stt, ok, j);
-      take(sa, stt, ok, j);
+      const bool ok = item_of((int)g1, g2 == INT64_MAX ? -1 : (int)g2, j);
+      float sa, tf;
+      scan(j, ok, sa, tf);
+      HX_STAMP(10);
+      HX_WSTAMP(1);
+      if (ok) L.insert(hp_fuse(sc, sa, hx_down((double)tf - Ef), w0, w1), j);
     }
+    HX_STAMP(11);
+    HX_WSTAMP(2);
     merge(false);
+    HX_STAMP(3);
     tau = s_tau;  // -inf: fewer than kk numeric seeds (every group below qualifies)
   }
   L.reset();
-  sweep([&](int g) { return every || ub_of(g) >= tau; }, take);
+  sweep([&](int g) { return every || ub_of(g) >= tau; }, [&](int gA, int gB) { topk_pair(gA, gB, every); });
+  HX_STAMP(4);
   merge(true);
+  HX_STAMP(5);
   if (s_full && !every) {  // a NaN or a missing entry among the kk: the whole shard
     every = true;
     L.reset();
-    sweep([&](int) { return true; }, take);
+    sweep([&](int) { return true; }, [&](int gA, int gB) { topk_pair(gA, gB, true); });
     merge(true);
   }
   if (tid == 0) {
     a.counts[a.B + b] = s_cnt;
     if (every) *a.flag = 1;
   }
+  HX_STAMP(6);
 }
 
 struct HxWs {
-  uint16_t* uop;  // [2][B][dk]
+  uint16_t* uop;  // [2][B][2 dk] split bf16
   float* stats;   // [B][G][4]
   int* counts;    // [2][B]
   int* flag;
@@ -659,7 +860,7 @@ static HxWs hx_layout(char* base, int B, int64_t N, int dk) {
     return r;
   };
   const int64_t G = (N + kHxGrp - 1) / kHxGrp;
-  w.uop = (uint16_t*)take((size_t)2 * B * dk * 2);
+  w.uop = (uint16_t*)take((size_t)2 * B * dk * 4);
   w.stats = (float*)take((size_t)B * G * 16);
   w.counts = (int*)take((size_t)2 * B * 4);
   w.flag = (int*)take(4);
@@ -667,7 +868,7 @@ static HxWs hx_layout(char* base, int B, int64_t N, int dk) {
   return w;
 }
 
-static size_t hx_items_bytes(int64_t N, int dk) { return (((size_t)2 * N * dk * 2 + 255) & ~(size_t)255) + 256; }
+static size_t hx_items_bytes(int64_t N, int dk) { return (((size_t)2 * N * dk * 4 + 255) & ~(size_t)255) + 256; }
 static const float* hx_norms(const void* prepared, int64_t N, int dk) {
   return reinterpret_cast<const float*>(static_cast<const char*>(prepared) + hx_items_bytes(N, dk) - 256);
 }
@@ -687,15 +888,16 @@ static int hx_check(const hrec_hybrid_batch* x, const char* who) {
   HREC_REQUIRE(x->tt_width <= x->dk, "%s: tt_width > dk", who);
   HREC_REQUIRE(x->als_ld >= x->als_width && x->tt_ld >= x->tt_width && x->n_als_rows >= 0,
                "%s: bad user row stride / count", who);
-  const int64_t ka4 = (x->als_width + 3) / 4 * 4;
-  HREC_REQUIRE(x->als_items_ld >= ka4 && x->als_items_ld % 4 == 0, "%s: als_items_ld must be a multiple of 4 >= %lld",
-               who, (long long)ka4);
-  HREC_REQUIRE(x->tt_items_ld >= x->tt_width && x->tt_items_ld % 4 == 0,
-               "%s: tt_items_ld must be a multiple of 4 >= tt_width", who);
+  HREC_REQUIRE(x->als_items_ld >= 1 && x->tt_items_ld >= x->tt_width && x->tt_items_ld % 4 == 0 &&
+                   x->tt_items_t_ld >= 1,
+               "%s: bad item strides (tt_items_ld: a multiple of 4 >= tt_width)", who);
   if (x->n_users == 0 || x->n_items == 0) return HREC_OK;
-  HREC_REQUIRE(x->als_users && x->tt_users && x->als_items && x->tt_items && x->prepared, "%s: null pointer", who);
-  HREC_REQUIRE((((uintptr_t)x->als_items | (uintptr_t)x->tt_items | (uintptr_t)x->prepared) & 15) == 0,
-               "%s: item rows / prepared operands must be 16-B aligned", who);
+  HREC_REQUIRE(x->als_items_ld >= x->n_items && x->tt_items_t_ld >= x->n_items,
+               "%s: transposed item strides below n_items", who);
+  HREC_REQUIRE(x->als_users && x->tt_users && x->als_items_t && x->tt_items && x->tt_items_t && x->prepared,
+               "%s: null pointer", who);
+  HREC_REQUIRE((((uintptr_t)x->tt_items | (uintptr_t)x->prepared) & 15) == 0,
+               "%s: two-tower rows / prepared operands must be 16-B aligned", who);
   return HREC_OK;
 }
 
@@ -703,23 +905,23 @@ extern "C" size_t hrec_hybrid_exact_items_bytes(int64_t n_items, int dk) {
   return hx_items_bytes(n_items > 0 ? n_items : 0, dk);
 }
 
-extern "C" int hrec_hybrid_exact_prepare(const float* als_items, int64_t als_ld, int als_width, const float* tt_items,
-                                         int64_t tt_ld, int tt_width, int64_t n_items, int dk, void* out,
-                                         void* stream) {
+extern "C" int hrec_hybrid_exact_prepare(const float* als_items_t, int64_t als_ld, int als_width,
+                                         const float* tt_items, int64_t tt_ld, int tt_width, int64_t n_items, int dk,
+                                         void* out, void* stream) {
   HREC_REQUIRE(dk == 64 || dk == 128, "hybrid_exact_prepare: dk must be 64 or 128");
   HREC_REQUIRE(n_items >= 0 && n_items < 0x7fffffffll, "hybrid_exact_prepare: bad n_items");
   HREC_REQUIRE(als_width >= 1 && als_width <= dk && tt_width >= 1 && tt_width <= dk,
                "hybrid_exact_prepare: widths must be in [1, dk]");
-  HREC_REQUIRE(als_ld >= als_width && tt_ld >= tt_width, "hybrid_exact_prepare: row stride below the width");
+  HREC_REQUIRE(als_ld >= n_items && tt_ld >= tt_width,
+               "hybrid_exact_prepare: bad strides (ALS: transposed, stride >= n_items; two-tower: row stride >= width)");
   HREC_REQUIRE(out && ((uintptr_t)out & 15) == 0, "hybrid_exact_prepare: output must be 16-B aligned");
   hipStream_t s = as_stream(stream);
   float* norms = const_cast<float*>(hx_norms(out, n_items, dk));
   if (hipMemsetAsync(norms, 0, 8, s) != hipSuccess) return check_launch("hybrid_exact_prepare: memset");
   if (n_items == 0) return HREC_OK;
-  HREC_REQUIRE(als_items && tt_items, "hybrid_exact_prepare: null pointer");
-  const int64_t waves = 2 * n_items;
-  hipLaunchKernelGGL(hx_prepare_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, als_items, als_ld,
-                     als_width, tt_items, tt_ld, tt_width, n_items, dk, static_cast<uint16_t*>(out),
+  HREC_REQUIRE(als_items_t && tt_items, "hybrid_exact_prepare: null pointer");
+  hipLaunchKernelGGL(hx_prepare_kernel, dim3((unsigned)((n_items + 255) / 256), 2), dim3(256), 0, s, als_items_t,
+                     als_ld, als_width, tt_items, tt_ld, tt_width, n_items, dk, static_cast<uint16_t*>(out),
                      reinterpret_cast<unsigned*>(norms));
   return check_launch("hx_prepare_kernel");
 }
@@ -758,7 +960,8 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   HxArgs a{};
   a.U = x->als_users, a.ldu = x->als_ld, a.rows = x->als_rows, a.n_rows = x->n_als_rows, a.ka = x->als_width;
   a.T = x->tt_users, a.ldt = x->tt_ld, a.kt = x->tt_width, a.B = B;
-  a.Va = x->als_items, a.lda = x->als_items_ld, a.Vt = x->tt_items, a.ldv = x->tt_items_ld;
+  a.Vat = x->als_items_t, a.lda = x->als_items_ld, a.Vt = x->tt_items, a.ldv = x->tt_items_ld;
+  a.Vtt = x->tt_items_t, a.ldtt = x->tt_items_t_ld;
   a.inorm = hx_norms(x->prepared, N, dk);
   a.N = N, a.G = G, a.stats = w.stats;
   a.mm_a = als_mm, a.mm_t = tt_mm;
@@ -767,8 +970,18 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   a.kk = (int)(top_k < N ? top_k : N);
   a.idx_offset = idx_offset, a.out_idx = out_idx, a.out_val = out_val;
   a.counts = w.counts, a.flag = w.flag;
-#define HREC_HX_USER(DK, M) \
-  hipLaunchKernelGGL((hx_user_kernel<DK, M>), dim3((unsigned)B), dim3(kHxThreads2), 0, s, a)
+  const bool full = x->als_width == dk && x->tt_width == dk;
+  const size_t st_lds = G <= kHxStatsLds ? (size_t)G * 16 : 0;  // the user's group records in LDS
+#define HREC_HX_USER(DK, M)                                                                                      \
+  do {                                                                                                           \
+    if (full) {                                                                                                  \
+      if (!allow_max_lds(hx_user_kernel<DK, M, true>)) return check_launch("hx_user_kernel: LDS attribute");    \
+      hipLaunchKernelGGL((hx_user_kernel<DK, M, true>), dim3((unsigned)B), dim3(kHxThreads2), st_lds, s, a);     \
+    } else {                                                                                                     \
+      if (!allow_max_lds(hx_user_kernel<DK, M, false>)) return check_launch("hx_user_kernel: LDS attribute");   \
+      hipLaunchKernelGGL((hx_user_kernel<DK, M, false>), dim3((unsigned)B), dim3(kHxThreads2), st_lds, s, a);    \
+    }                                                                                                            \
+  } while (0)
   if (dk == 64) {
     if (mode == 0) HREC_HX_USER(64, 0); else if (mode == 1) HREC_HX_USER(64, 1); else HREC_HX_USER(64, 2);
   } else {
@@ -843,3 +1056,14 @@ extern "C" int hrec_hybrid_exact_counts(const void* workspace, int n_users, int6
     return check_launch("hybrid_exact_counts: copy");
   return HREC_OK;
 }
+
+#ifdef HREC_HX_STAMPS
+extern "C" int hrec_debug_hx1_stamps(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hx1_stamps), sizeof(g_hx1_stamps)) == hipSuccess ? 0 : -2;
+}
+extern "C" int hrec_debug_hx_stamps(unsigned long long* host_out) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hx_stamps), sizeof(g_hx_stamps)) != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(host_out + kHxStampBlocks * 16, HIP_SYMBOL(g_hx_wstamps), sizeof(g_hx_wstamps)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif

@@ -37,7 +37,6 @@
 // the same MFMA chain and every fused score the same arithmetic.
 #include <float.h>
 #include <math.h>
-#include <stdlib.h>
 
 #include "common.h"
 #include "hybrid_common.h"
@@ -620,16 +619,6 @@ struct HpWs {
   size_t total;
 };
 
-// HREC_HP_FILTER: 1 (default) = the per-group filter on the phase-1 GEMM
-// (hyb_scores_kernel HS_FILTER), 0 = the K8 resident-user filter.
-static int hp_filter_choice() {
-  static const int v = [] {
-    const char* e = getenv("HREC_HP_FILTER");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
 static HpWs hp_layout(char* base, int B, int64_t N, int dk, int kk) {
   HpWs w{};
   size_t off = 0;
@@ -746,16 +735,9 @@ static int hp_phase2(bool local, int n_users, const void* als_items, const void*
   // b. the heavy model's scores, survivors of the per-group bounds: one
   //    block per item group (the bound is one LDS value per user), the
   //    phase-1 GEMM's tiling and k order (the same scores)
-  if (hp_filter_choice() == 1) {
-    const HsFilter f{w.theta, hm, kHpCap, w.cv, w.ci, w.cn};
-    rc = hybrid_scores_run(2 /* HS_FILTER */, nullptr, 0, nullptr, 0, 0, nullptr, 0, 0, n_users, als_items, tt_items,
-                           n_items, dk, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, s, w.uop, &f);
-  } else {  // the K8 resident-user filter (round 3)
-    const uint16_t* uh = w.uop + (size_t)hm * n_users * dk;
-    const int64_t per = ((n_items + G - 1) / G + 15) / 16 * 16;
-    rc = dot_filter_run(uh, n_users, hm ? tt_items : als_items, n_items, dk, 1, w.theta, G, per, kHpCap, w.cv, w.ci,
-                        w.cn, s);
-  }
+  const HsFilter f{w.theta, hm, kHpCap, w.cv, w.ci, w.cn};
+  rc = hybrid_scores_run(2 /* HS_FILTER */, nullptr, 0, nullptr, 0, 0, nullptr, 0, 0, n_users, als_items, tt_items,
+                         n_items, dk, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, s, w.uop, &f);
   if (rc) return rc;
   // c. light scores + fusion of the survivors, exact top-k; the exact path in
   //    the same block for the users that need it

@@ -780,7 +780,6 @@ using namespace hrec;
 // scalar kernel below
 static int item_forward(const hrec_tt_params& p, const int32_t* item, const int32_t* man, const int32_t* cat,
                         const float* numeric, int64_t n, float* out, float* z, float* xh, float* rs, void* stream) {
-  if (getenv("HREC_TT_SCALAR_FWD")) return 1;  // A/B against the scalar kernel (scripts, tests)
   return hrec_tt_item_forward_mfma(p.d, p.item_emb, p.man_emb, p.cat_emb, p.w1, p.b1, p.w2, p.b2, p.ln_item_gamma,
                                    p.ln_item_beta, item, man, cat, numeric, n, out, z, xh, rs, stream);
 }
@@ -832,8 +831,7 @@ extern "C" int hrec_tt_score(const float* user_vec, int n_users, const float* it
   // fma chains per k-step, item fragments kept in registers across the
   // user chunks, XCD-aware tile order; csrc/dot_topk.hip) — 0.91 of the f32
   // peak at c4 against ~0.33 for the LDS-staged tile kernel below
-  if ((d == 32 || d == 64 || d == 128 || d == 256) && (((uintptr_t)user_vec | (uintptr_t)item_vec) & 15) == 0 &&
-      !getenv("HREC_TT_SCORE_TILE"))
+  if ((d == 32 || d == 64 || d == 128 || d == 256) && (((uintptr_t)user_vec | (uintptr_t)item_vec) & 15) == 0)
     return hrec_dot_scores(user_vec, n_users, item_vec, n_items, d, 0, out, n_items, stream);
   if (HREC_TT_SCORE_V2 && d % 4 == 0 && (((uintptr_t)user_vec | (uintptr_t)item_vec) & 15) == 0) {
     hipLaunchKernelGGL(tt_score_mfma2_kernel, dim3((unsigned)((n_items + 63) / 64)), dim3(256), 0,
@@ -896,11 +894,9 @@ extern "C" int hrec_tt_forward_backward(const hrec_tt_params* params, const int3
   }
   // backward with both Dense GEMMs on the matrix cores (csrc/tt_mfma.hip);
   // the scratch (B·(d + 19) floats) reuses the partials region
-  if (!getenv("HREC_TT_SCALAR_BWD")) {  // set: the scalar kernels below (A/B, tests)
-    rc = hrec_tt_backward_mfma(d, P.w2, P.gu, P.gi, y, batch, uvec, uxh, urs, ivec, ixh, irs, zs, numeric, g_user,
-                               g_item, g_man, g_cat, grad_dense, part, stream);
-    if (rc <= 0) return rc;
-  }
+  rc = hrec_tt_backward_mfma(d, P.w2, P.gu, P.gi, y, batch, uvec, uxh, urs, ivec, ixh, irs, zs, numeric, g_user,
+                             g_item, g_man, g_cat, grad_dense, part, stream);
+  if (rc <= 0) return rc;  // 1: d needs the scalar kernels below
   const size_t bsm = ((size_t)kTR * d + kTR * 16 + kTR + 8) * sizeof(float);
   hipLaunchKernelGGL(tt_backward_kernel, dim3((unsigned)nblk), dim3(kBlock), bsm, s, P, y, batch, uvec, uxh, urs,
                      ivec, ixh, irs, zs, numeric, g_user, g_item, g_man, g_cat, part);

@@ -125,10 +125,11 @@ _SIGNATURES.update({
 
 class HybridBatch(ctypes.Structure):
     """hrec_hybrid_batch (include/hrec.h)."""
-    _fields_ = [("als_users", _vp), ("als_rows", _vp), ("tt_users", _vp), ("als_items", _vp), ("tt_items", _vp),
-                ("prepared", _vp), ("als_ld", _c_i64), ("n_als_rows", _c_i64), ("tt_ld", _c_i64),
-                ("als_items_ld", _c_i64), ("tt_items_ld", _c_i64), ("n_items", _c_i64), ("als_width", _c_i32),
-                ("tt_width", _c_i32), ("n_users", _c_i32), ("dk", _c_i32)]
+    _fields_ = [("als_users", _vp), ("als_rows", _vp), ("tt_users", _vp), ("als_items_t", _vp), ("tt_items", _vp),
+                ("tt_items_t", _vp), ("prepared", _vp), ("als_ld", _c_i64), ("n_als_rows", _c_i64),
+                ("tt_ld", _c_i64), ("als_items_ld", _c_i64), ("tt_items_ld", _c_i64), ("tt_items_t_ld", _c_i64),
+                ("n_items", _c_i64), ("als_width", _c_i32), ("tt_width", _c_i32), ("n_users", _c_i32),
+                ("dk", _c_i32)]
 
 
 _HBP = ctypes.POINTER(HybridBatch)
@@ -753,28 +754,30 @@ def exact_dk(als_width, tt_width):
 
 class HybridExactItems:
     """One item shard prepared for the exact pruned hybrid
-    (hrec_hybrid_exact_prepare): the f32 rows the exact chains read (ALS item
-    factor rows [n, >= k], row stride a multiple of 4; two-tower item vectors
-    [n, d], d in 32/64/128) and their bf16 operands + norm bounds."""
+    (hrec_hybrid_exact_prepare): the ALS item factors TRANSPOSED as
+    hrec_als_score takes them (Vt [>= k, ld], ld >= n), the two-tower item
+    vectors [n, d] (d in 32/64/128, row stride a multiple of 4) and their
+    transpose, and the split-bf16 operands + norm bounds of both."""
 
-    def __init__(self, als_items, k, tt_items):
-        self.k, self.d = int(k), int(tt_items.shape[1])
+    def __init__(self, Vt, n_items, k, tt_items):
+        self.k, self.d, self.N = int(k), int(tt_items.shape[1]), int(n_items)
         self.dk = exact_dk(self.k, self.d)
         if self.dk is None:
             raise HrecError(f"hybrid_exact: widths (k={self.k}, d={self.d}) outside the exact pruned path")
-        for t, name in ((als_items, "als_items"), (tt_items, "tt_items")):
-            if t.dtype != torch.float32 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 4 \
-                    or t.data_ptr() % 16:
-                raise HrecError(f"hybrid_exact: {name} must be a 16-B aligned row-major float32 device matrix "
-                                "with a row stride that is a multiple of 4")
-        if als_items.shape[0] != tt_items.shape[0] or als_items.stride(0) < -(-self.k // 4) * 4:
-            raise HrecError("hybrid_exact: item counts differ or ALS rows narrower than k rounded up to 4")
-        self.Va, self.Vt, self.N = als_items, tt_items, int(tt_items.shape[0])
+        for t, name in ((Vt, "Vt"), (tt_items, "tt_items")):
+            if t.dtype != torch.float32 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+                raise HrecError(f"hybrid_exact: {name} must be a row-major float32 device matrix")
+        if Vt.shape[0] < self.k or Vt.stride(0) < self.N or tt_items.shape[0] != self.N:
+            raise HrecError("hybrid_exact: Vt must be [>= k, >= n_items] and tt_items [n_items, d]")
+        if tt_items.stride(0) % 4 or tt_items.data_ptr() % 16:
+            raise HrecError("hybrid_exact: tt_items rows must be 16-B aligned (row stride a multiple of 4)")
+        self.Vat, self.Vt = Vt, tt_items
+        self.Vtt = transpose(tt_items.contiguous())  # [d, ld]
         self.buf = torch.empty(int(lib().hrec_hybrid_exact_items_bytes(self.N, self.dk)), dtype=torch.uint8,
                                device=tt_items.device)
         _check("hrec_hybrid_exact_prepare", lib().hrec_hybrid_exact_prepare(
-            _vp(als_items.data_ptr()), als_items.stride(0), self.k, _vp(tt_items.data_ptr()), tt_items.stride(0),
-            self.d, self.N, self.dk, _vp(self.buf.data_ptr()), _stream()))
+            _vp(Vt.data_ptr()), Vt.stride(0), self.k, _vp(tt_items.data_ptr()), tt_items.stride(0), self.d, self.N,
+            self.dk, _vp(self.buf.data_ptr()), _stream()))
 
 
 class HybridExact:
@@ -815,9 +818,10 @@ class HybridExact:
         self.T = tt_users
         it = self.items
         self.arg = HybridBatch(_vp(self.U.data_ptr()), _vp(self.rows.data_ptr()), _vp(self.T.data_ptr()),
-                               _vp(it.Va.data_ptr()), _vp(it.Vt.data_ptr()), _vp(it.buf.data_ptr()),
-                               self.U.stride(0), self.U.shape[0], self.T.stride(0), it.Va.stride(0), it.Vt.stride(0),
-                               self.N, it.k, it.d, self.B, self.dk)
+                               _vp(it.Vat.data_ptr()), _vp(it.Vt.data_ptr()), _vp(it.Vtt.data_ptr()),
+                               _vp(it.buf.data_ptr()), self.U.stride(0), self.U.shape[0], self.T.stride(0),
+                               it.Vat.stride(0), it.Vt.stride(0), it.Vtt.stride(0), self.N, it.k, it.d, self.B,
+                               self.dk)
         return self
 
     def _mm(self):

@@ -55,10 +55,9 @@ class DeviceOps:
 
     @staticmethod
     def hybrid_exact_items(Vt_local, n_local, k, item_vecs_local):
-        """The shard's ALS item factor rows (row-major again: the exact chain
-        reads one row per item) + two-tower rows, prepared for hrec_hybrid_exact_*."""
-        rows = _hrec.transpose(Vt_local.contiguous())[:n_local]
-        return _hrec.HybridExactItems(rows, k, item_vecs_local.contiguous())
+        """The shard's items prepared for hrec_hybrid_exact_* (the transposed
+        ALS factors are the ones hrec_als_score reads)."""
+        return _hrec.HybridExactItems(Vt_local, n_local, k, item_vecs_local.contiguous())
 
     hybrid_exact = staticmethod(_hrec.HybridExact)
     dot_scores = staticmethod(_hrec.dot_scores)

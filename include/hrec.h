@@ -509,23 +509,27 @@ int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_it
  *   als_users[als_rows[b] * als_ld + c], c < als_width (a row outside
  *     [0, n_als_rows) is an unknown user: NaN ALS scores);
  *   tt_users[b * tt_ld + c], c < tt_width in {32, 64, 128};
- *   als_items / tt_items: the shard's f32 item rows (row strides multiples of
- *     4, 16-B aligned; ALS rows readable up to als_width rounded up to 4);
- *   prepared: hrec_hybrid_exact_prepare's bf16 operands + norm bounds of the
- *     same item rows (hrec_hybrid_exact_items_bytes, once per shard);
+ *   als_items_t: the shard's ALS item factors transposed (item j, column c
+ *     at als_items_t[c * als_items_ld + j]: hrec_als_score's layout);
+ *   tt_items: the shard's two-tower item vectors, row-major (row stride a
+ *     multiple of 4, 16-B aligned), tt_items_t the same transposed;
+ *   prepared: hrec_hybrid_exact_prepare's split-bf16 operands + norm bounds
+ *     of the same items (hrec_hybrid_exact_items_bytes, once per shard);
  *   dk in {64, 128} >= both widths. n_users < 65536. */
 typedef struct hrec_hybrid_batch {
   const float* als_users;
   const int64_t* als_rows;
   const float* tt_users;
-  const float* als_items;
+  const float* als_items_t;
   const float* tt_items;
+  const float* tt_items_t;
   const void* prepared;
   int64_t als_ld;
   int64_t n_als_rows;
   int64_t tt_ld;
   int64_t als_items_ld;
   int64_t tt_items_ld;
+  int64_t tt_items_t_ld;
   int64_t n_items;
   int32_t als_width;
   int32_t tt_width;
@@ -533,7 +537,7 @@ typedef struct hrec_hybrid_batch {
   int32_t dk;
 } hrec_hybrid_batch;
 size_t hrec_hybrid_exact_items_bytes(int64_t n_items, int dk);
-int hrec_hybrid_exact_prepare(const float* als_items, int64_t als_ld, int als_width, const float* tt_items,
+int hrec_hybrid_exact_prepare(const float* als_items_t, int64_t als_ld, int als_width, const float* tt_items,
                               int64_t tt_ld, int tt_width, int64_t n_items, int dk, void* out, void* stream);
 /* Workspace (the same dk) carrying phase 1 into phase 2: 16 B per user and
  * 32-item group + the bf16 user operands — 12.8 MB for 256 users x 100k items. */

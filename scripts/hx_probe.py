@@ -35,21 +35,14 @@ def ev_ms(fn, reps):
     return s.elapsed_time(e) / reps
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--users", type=int, default=256)
-    ap.add_argument("--epochs", type=int, default=2)
-    ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--n-users", type=int, default=1_000_000)
-    ap.add_argument("--n-items", type=int, default=100_000)
-    args = ap.parse_args()
-    torch.cuda.set_device(0)
-    n_users, n_items, k, d = args.n_users, args.n_items, 64, 64
+def setup(B, epochs, n_users=1_000_000, n_items=100_000, pruned=True):
+    """The bench's hybrid_top5 inputs: (recommender, user rows, user vectors)."""
+    k, d = 64, 64
     csr = synthetic.generate(n_users, n_items, 0.005, False)
     csc = synthetic.generate(n_users, n_items, 0.005, True)
     eng = DeviceALS(n_users, n_items, k, 0.1, csr, csc)
     eng.init_user_factors(synthetic.SEED_INIT)
-    eng.fit(args.epochs)
+    eng.fit(epochs)
     tt = DeviceTwoTower(n_users, n_items, 2651, 255, d, seed=1)
     g = torch.Generator().manual_seed(5)
     items = torch.arange(n_items, dtype=torch.int32)
@@ -58,12 +51,61 @@ def main():
     num = torch.rand((n_items, 2), generator=g).contiguous()
     ivec = tt.item_vectors(items.cuda(), man.cuda(), cat.cuda(), num.cuda())
     Vt = _hrec.transpose(eng.item_factor_rows(0, n_items).contiguous())
-    B = args.users
     hu_ids = (torch.arange(B, dtype=torch.int64) * (n_users // B)).cuda()
     hu = eng.user_rows(hu_ids)
     uvec = tt.user_vectors(hu_ids.to(torch.int32))
-    pr = ShardedRecommender(eng.U, Vt, ivec, 0, k)
-    mt = ShardedRecommender(eng.U, Vt, ivec, 0, k, pruned=False)
+    rec = ShardedRecommender(eng.U, Vt, ivec, 0, k, pruned=pruned)
+    rec.materialised = ShardedRecommender(eng.U, Vt, ivec, 0, k, pruned=False)
+    return rec, hu, uvec
+
+
+def analyze(pr, hu, uvec, wins=False, k=5):
+    """How many 32-item groups the bounds could leave at best: the groups
+    whose upper bound (phase-1 records + E) reaches the FINAL k-th best fused
+    score, against the groups the kernel rescored (tau from the seeds)."""
+    import numpy as np
+
+    idx, val = pr.recommend(hu, uvec, wins, k)
+    hx = pr.last_exact
+    B, N, dk = hx.B, hx.N, hx.dk
+    G = -(-N // 32)
+    off = -(-(2 * B * dk * 4) // 256) * 256
+    st = hx.ws[off: off + B * G * 16].view(torch.float32).view(B, G, 4).double().cpu().numpy()
+    a_mm, t_mm = hx.minmax()
+    a_mm, t_mm = a_mm.double().cpu().numpy(), t_mm.double().cpu().numpy()
+    U = pr.U[hu][:, :pr.k].double()
+    un = torch.linalg.vector_norm(U, dim=1).cpu().numpy()
+    tn = torch.linalg.vector_norm(uvec.double(), dim=1).cpu().numpy()
+    nrm = hx.items.buf[-256:].view(torch.float32)[:2].double().cpu().numpy()
+    Ea, Et = 2.0 ** -13 * un * nrm[0], 2.0 ** -13 * tn * nrm[1]
+    w0, w1 = (0.8, 0.2) if wins else (0.2, 0.8)
+    ar = np.maximum(a_mm[1] - a_mm[0], 1e-300)
+    trr = np.maximum(t_mm[1] - t_mm[0], 1e-30)
+    ub = (w0 * (st[:, :, 0] + Ea[:, None] - a_mm[0][:, None]) / ar[:, None]
+          + w1 * (st[:, :, 2] + Et[:, None] - t_mm[0][:, None]) / trr[:, None])
+    kth = val[:, k - 1].cpu().numpy()
+    ideal = (ub >= kth[:, None] - 1e-9).sum(1)
+    _, n_top, _ = hx.counts()
+    n_top = n_top.cpu().numpy()
+    worst = int(np.argmax(n_top))
+    return {"live_groups_mean": float(n_top.mean()), "live_groups_max": int(n_top.max()),
+            "ideal_groups_mean": float(ideal.mean()), "ideal_groups_max": int(ideal.max()),
+            "worst_user": worst, "worst_user_live": int(n_top[worst]), "worst_user_ideal": int(ideal[worst])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--n-users", type=int, default=1_000_000)
+    ap.add_argument("--n-items", type=int, default=100_000)
+    ap.add_argument("--analyze", action="store_true")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    B, n_items = args.users, args.n_items
+    pr, hu, uvec = setup(B, args.epochs, args.n_users, n_items)
+    mt = pr.materialised
     out = {"users": B, "items": n_items}
     for wins in (False, True):
         a = pr.recommend(hu, uvec, wins, 5)
@@ -83,6 +125,8 @@ def main():
         out["als_wins" if wins else "tt_wins"] = r
         print(json.dumps({("als_wins" if wins else "tt_wins"): r}), flush=True)
     hx = pr.last_exact
+    if args.analyze:
+        out["bound_analysis"] = analyze(pr, hu, uvec)
     out["stage_ms"] = {"local (3 launches)": ev_ms(lambda: hx.local(False), args.reps),
                        "minmax (ops + stats + extremes)": ev_ms(lambda: hx.minmax(), args.reps)}
     a_mm, t_mm = hx.minmax()

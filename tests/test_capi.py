@@ -104,16 +104,16 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     ex.argtypes = [ctypes.POINTER(_hrec.HybridBatch)] + [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_void_p]
     assert ex(None, None, None, None, 0, None) == -1
     assert b"null batch" in lib.hrec_last_error()
-    bt = _hrec.HybridBatch(None, None, None, None, None, None, 64, 10, 64, 64, 64, 100, 64, 64, 4, 96)
+    bt = _hrec.HybridBatch(None, None, None, None, None, None, None, 64, 10, 64, 128, 64, 128, 100, 64, 64, 4, 96)
     assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
     assert b"dk must be 64 or 128" in lib.hrec_last_error()
     bt.dk, bt.tt_width = 64, 48
     assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
     assert b"tt_width must be 32, 64 or 128" in lib.hrec_last_error()
-    bt.tt_width, bt.als_items_ld = 64, 30
+    bt.tt_width, bt.tt_items_ld = 64, 30
     assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
-    assert b"als_items_ld must be a multiple of 4" in lib.hrec_last_error()
-    bt.als_items_ld = 64
+    assert b"bad item strides" in lib.hrec_last_error()
+    bt.tt_items_ld = 64
     assert ex(ctypes.byref(bt), None, None, None, 0, None) == -1
     assert b"null pointer" in lib.hrec_last_error()
     tk = lib.hrec_hybrid_exact_topk

@@ -242,10 +242,10 @@ def test_tt_forward_backward_matches_oracle(device, d):
 
 
 @pytest.mark.parametrize("d,n", [(16, 1), (50, 77), (64, 1000), (100, 333), (128, 4099), (256, 530)])
-def test_tt_item_tower_mfma_matches_oracle(device, d, n, monkeypatch):
+def test_tt_item_tower_mfma_matches_oracle(device, d, n):
     """K4m (csrc/tt_mfma.hip, f32 matrix cores, permuted-k Dense + fused LN)
     against the f64 Keras graph at rtol 1e-5, ragged tails and padded d
-    included, and against the scalar K4 kernel it replaces."""
+    included."""
     from src import _hrec
     from src.tt_engine import DeviceTwoTower
 
@@ -258,9 +258,6 @@ def test_tt_item_tower_mfma_matches_oracle(device, d, n, monkeypatch):
     got = eng.item_vectors(T(i), T(m), T(c), T(x)).cpu().numpy()
     want = ott.forward(p, u, i, m, c, x)["ivec"]
     np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-5)
-    monkeypatch.setenv("HREC_TT_SCALAR_FWD", "1")
-    scalar = eng.item_vectors(T(i), T(m), T(c), T(x)).cpu().numpy()
-    np.testing.assert_allclose(got, scalar, rtol=1e-5, atol=2e-5)
 
 
 def test_tt_item_tower_mfma_catalogue_sample(device):
@@ -288,10 +285,11 @@ def test_tt_item_tower_mfma_catalogue_sample(device):
 
 
 @pytest.mark.parametrize("d,B", [(16, 1), (64, 256), (50, 77), (128, 300), (256, 40)])
-def test_tt_backward_mfma_matches_scalar(device, d, B, monkeypatch):
-    """K6m (dz and dW2 on the f32 matrix cores, column sums in one pass)
-    against the scalar backward kernels it replaces, at rtol 1e-5 (both are
-    f32; the summation orders differ)."""
+def test_tt_backward_mfma_shapes_match_oracle(device, d, B):
+    """K6m (dz and dW2 on the f32 matrix cores, column sums in one pass) at
+    the batch shapes of its tilings (one sample, ragged, several sample
+    stripes) against the f64 Keras graph's gradients (oracle/two_tower.py,
+    checked against finite differences) at rtol 1e-4."""
     from src import _hrec
     from src.tt_engine import DeviceTwoTower
 
@@ -299,13 +297,18 @@ def test_tt_backward_mfma_matches_scalar(device, d, B, monkeypatch):
     nu, ni, nm, nc = 40, 30, 7, 5
     p = _tt_params(rng, nu, ni, nm, nc, d)
     eng = DeviceTwoTower(nu, ni, nm, nc, d, init=p)
+    u, i, m, c, x, y = _tt_batch(rng, B, nu, ni, nm, nc)
     T = lambda a: torch.as_tensor(a, device=device)  # noqa: E731
-    batch = [T(a) for a in _tt_batch(rng, B, nu, ni, nm, nc)]
-    got = [g.cpu().numpy() for g in _hrec.tt_forward_backward(eng.params, *batch)]
-    monkeypatch.setenv("HREC_TT_SCALAR_BWD", "1")
-    ref = [g.cpu().numpy() for g in _hrec.tt_forward_backward(eng.params, *batch)]
-    for a, b in zip(got, ref):
-        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5 * (np.abs(b).max() + 1e-12))
+    gd, gu, gi, gm, gc = _hrec.tt_forward_backward(eng.params, T(u), T(i), T(m), T(c), T(x), T(y))
+    grads, rows, sq, ab = ott.backward(p, ott.forward(p, u, i, m, c, x), y)
+    gd = gd.cpu().numpy()
+    for name, (off, shape) in eng.layout.items():
+        got = gd[off: off + int(np.prod(shape))].reshape(shape)
+        scale = np.abs(grads[name]).max() + 1e-12
+        np.testing.assert_allclose(got, grads[name], rtol=1e-4, atol=1e-4 * scale, err_msg=name)
+    for name, g in (("user_emb", gu), ("item_emb", gi), ("man_emb", gm), ("cat_emb", gc)):
+        scale = np.abs(rows[name]).max() + 1e-12
+        np.testing.assert_allclose(g.cpu().numpy(), rows[name], rtol=1e-4, atol=1e-4 * scale, err_msg=name)
 
 
 def test_tt_adam_steps_match_oracle(device):
