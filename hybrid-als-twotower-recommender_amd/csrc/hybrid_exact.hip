@@ -17,7 +17,7 @@
 //     score as uh.vh + uh.vl + ul.vh; no score stores: per user and 32-item
 //     group the approximate max and min of both models (16 B per user and
 //     group);
-//   phase 2 (hx_user_kernel, one block per user):
+//   phase 2a (hx_pre_kernel, one block per user):
 //     a. exact extremes: |approx - exact| <= E = 2^-13 ||u|| max_j ||v_j||
 //        (the dropped terms ul.vl and the split residues: 3 2^-16 sum
 //        |u_c v_c|; the f32 accumulation of 3k products and the JVM chain's
@@ -29,17 +29,23 @@
 //        by hrec_dot_scores' own MFMA chain (v_mfma_f32_16x16x4_f32, k order
 //        16 ks + 4 g + e) — the same bits as the materialised scores;
 //     [with the items sharded, the caller all-reduces the extremes here (C2)]
-//     b. top-k: per group an upper bound of every fused score in it
-//        (hp_fuse of the approximate maxima + E, rounded up to f32: the
-//        fusion arithmetic is non-decreasing in both scores); tau = the kk-th
-//        best exact fused score of a few seed groups (each wave's two groups
-//        with the largest bounds); every group whose bound reaches tau is
-//        rescored exactly, and the exact stable top-k (ties -> smaller item)
-//        is taken over those items. An item outside them has a fused score
-//        below tau, under kk items already found.
-//   Users with non-finite or huge norms rescore every group (same kernel);
-//   users whose kk best include a NaN or fewer than kk items rescore every
-//   group too (the order of NaN items is by item id over the whole shard).
+//     b. per group an upper bound of every fused score in it (hp_fuse of the
+//        approximate maxima + E, rounded up to f32: the fusion arithmetic is
+//        non-decreasing in both scores); tau = the kk-th best lower bound of
+//        a few seed groups' fused scores (each wave's two groups with the
+//        largest bounds); every group whose bound reaches tau joins a global
+//        queue of group pairs;
+//   phase 2b (hx_pairs_kernel, persistent): the waves pull the queued pairs
+//     of all users from one counter (a user's live groups vary by an order
+//     of magnitude; a block per user waited on the heaviest) and score their
+//     items exactly where an item's own bound still reaches tau; those exact
+//     fused scores are the user's candidates;
+//   phase 2c (hx_final_kernel, one block per user): the stable top-k (ties ->
+//     smaller item) of the candidates. An item outside them has a fused
+//     score below tau, under kk items already found.
+//   Users with non-finite or huge norms, too many live groups or candidates,
+//   or whose kk best include a NaN or fewer than kk items, rescore every
+//   group in 2c (the order of NaN items is by item id over the whole shard).
 #include "common.h"
 #include "hybrid_common.h"
 
@@ -70,8 +76,6 @@ struct HxShape {
   static constexpr int kOpB = DK * 4;              // bytes per operand row: [hi | lo] bf16
   static constexpr int kRowB = kOpB + 16;          // LDS bytes per staged user row
   static constexpr int UB = DK == 64 ? 128 : 64;   // users per tile (2 x UB rows: <= 70 KB of LDS)
-  static constexpr int kSlices = DK == 64 ? 4 : 2;  // 32-item slices per wave
-  static constexpr int kBlockItems = (kHxThreads1 / 64) * 32 * kSlices;
 };
 
 __device__ __forceinline__ float hx_up(double x) {  // the smallest float >= x
@@ -99,7 +103,8 @@ __device__ __forceinline__ void hx_split(float x, uint16_t& hi, uint16_t& lo) {
 __global__ __launch_bounds__(128) void hx_user_ops_kernel(const float* __restrict__ U, int64_t ldu,
                                                           const int64_t* __restrict__ rows, int64_t n_rows, int ka,
                                                           const float* __restrict__ T, int64_t ldt, int kt, int B,
-                                                          int dk, uint16_t* __restrict__ uop) {
+                                                          int dk, uint16_t* __restrict__ uop, float* __restrict__ uf,
+                                                          int* __restrict__ uok) {
   const int b = blockIdx.x, m = blockIdx.y;
   int64_t r = b;
   bool bad = false;
@@ -110,11 +115,14 @@ __global__ __launch_bounds__(128) void hx_user_ops_kernel(const float* __restric
   const float* src = m ? T + (int64_t)b * ldt : U + (bad ? 0 : r) * ldu;
   const int w = m ? kt : ka;
   uint16_t* out = uop + ((int64_t)m * B + b) * 2 * dk;
+  float* of = uf + ((int64_t)m * B + b) * dk;  // the f32 row the exact chains read (phase 2)
   for (int c = threadIdx.x; c < dk; c += blockDim.x) {
     float v = 0.f;
     if (c < w) v = bad ? __builtin_nanf("") : src[c];
     hx_split(v, out[c], out[dk + c]);
+    of[c] = v;
   }
+  if (m == 0 && threadIdx.x == 0) uok[b] = bad ? 0 : 1;
 }
 
 // Item-side operands (once per shard): split bf16 rows [2][N][2 dk] (ALS,
@@ -159,8 +167,8 @@ __global__ __launch_bounds__(256) void hx_prepare_kernel(const float* __restrict
   if ((threadIdx.x & 63) == 0) atomicMax(&norms[m], f);
 }
 
-// 1. Phase 1: block = (user tile of UB users, kBlockItems items); each wave
-// walks kSlices 32-item slices, keeps a slice's item fragments (both models,
+// 1. Phase 1: block = (user tile of UB users, `per` items); each wave walks
+// every fourth 32-item slice of them, keeps a slice's item fragments (both models,
 // hi and lo, every k-step) in registers and sweeps the tile's users in chunks
 // of 32 from LDS; the last chunk refills the fragments with the next slice's.
 // MFMA roles: A = items (32 rows), B = users (32 columns), so lane (h, c)
@@ -180,14 +188,15 @@ __device__ unsigned long long g_hx1_stamps[4096][4];  // per block: start, stage
 template <int DK>
 __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* __restrict__ uop, int B, int n_ut,
                                                                const char* __restrict__ items, int64_t N, int G,
-                                                               float* __restrict__ stats) {
+                                                               int64_t per, float* __restrict__ stats) {
   using S = HxShape<DK>;
   constexpr int KS = S::KS, UB = S::UB, kRowB = S::kRowB, kOpB = S::kOpB;
   __shared__ __attribute__((aligned(16))) char us[2 * UB * kRowB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c = lane & 31;
   const int ut = (int)(blockIdx.x % (unsigned)n_ut);
-  const int64_t i0 = (int64_t)(blockIdx.x / (unsigned)n_ut) * S::kBlockItems;
+  const int64_t i0 = (int64_t)(blockIdx.x / (unsigned)n_ut) * per;  // per: a multiple of 32
+  const int64_t i1 = i0 + per < N ? i0 + per : N;
   const int b0 = ut * UB;
   const int ub = B - b0 < UB ? B - b0 : UB;
   const char* ia = items;                        // ALS operand [N][2 DK]
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
   };
   int64_t jb = i0 + 32 * w;
   if (w == 0) HX1_STAMP(0);
-  if (jb < N) load(jb);  // the first slice arrives while the users are staged
+  if (jb < i1) load(jb);  // the first slice arrives while the users are staged
   // users -> LDS: every load of a thread in flight before its stores (one
   // round trip, not one per 16-B chunk)
   constexpr int CPR = kOpB / 16;  // 16-B chunks per user row
@@ -231,10 +240,10 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
   }
   __syncthreads();
   if (w == 0) HX1_STAMP(1);
-  for (int sl = 0; jb < N; ++sl) {  // wave-uniform; no barrier follows
+  while (jb < i1) {  // wave-uniform; no barrier follows
     const bool full = jb + 32 <= N;
     const int64_t jn = jb + 32 * (kHxThreads1 / 64);
-    const bool more = sl + 1 < S::kSlices && jn < N;
+    const bool more = jn < i1;
     for (int ch = 0; 32 * ch < ub; ++ch) {
       hx_f16 acc[2];
 #pragma unroll
@@ -300,33 +309,38 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
 
 #ifdef HREC_HX_STAMPS
 // Diagnostic builds only: per block (thread 0) s_memtime at the phase points
-// of hx_user_kernel, plain stores.
+// of hx_pre_kernel, plain vector stores.
 constexpr int kHxStampBlocks = 1024;
 __device__ unsigned long long g_hx_stamps[kHxStampBlocks][16];
-__device__ unsigned long long g_hx_wstamps[kHxStampBlocks][8][4];  // per wave: seed start, scan done, insert done, merge entry
-#define HX_WSTAMP(i)                                                           \
-  do {                                                                         \
-    if (lane == 0 && b < kHxStampBlocks) g_hx_wstamps[b][wv][i] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
 #define HX_STAMP(i)                                                            \
   do {                                                                         \
     if (tid == 0 && b < kHxStampBlocks) g_hx_stamps[b][i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define HX_STAMP(i)
-#define HX_WSTAMP(i)
 #endif
 
+// Per-user state phase 2a hands to 2b / 2c.
+struct HxRec {
+  double tau;          // the bound an item's fused bound must reach to be scored exactly
+  double ascale, amin_;
+  double Ef;           // |two-tower fma chain - exact| bound
+  float tscale, tmin_;
+  int state;           // kHxQueued / kHxEvery / kHxNaN
+  int pair_base;       // the user's pairs: [pair_base, pair_base + n_pairs) of the queue
+  int n_pairs;
+  int pad;
+};
+constexpr int kHxQueued = 0;  // live pairs queued for 2b, candidates ranked in 2c
+constexpr int kHxEvery = 1;   // no usable bound: 2c scores every group
+constexpr int kHxNaN = 2;     // a model without any number: every fused score NaN
+constexpr int kHxSlots = 8;  // a pair's best exact candidates kept (>= top_k)
+// pairs a user may queue: a quarter of the shard's groups within [512, 8192]
+// (the live-group list sits in 2a's LDS); more: kHxEvery
+__host__ __device__ inline int hx_pair_cap(int G) { return G / 8 < 512 ? 512 : (G / 8 > 8192 ? 8192 : G / 8); }
+
 struct HxArgs {
-  const float* U;  // ALS user factors (rows[b] of them; width ka)
-  int64_t ldu;
-  const int64_t* rows;
-  int64_t n_rows;
-  int ka;
-  const float* T;  // two-tower user vectors [B] (width kt in {32, 64, 128})
-  int64_t ldt;
-  int kt;
-  int B;
+  int ka, kt, B;
   const float* Vat;  // ALS item factors transposed: item j, column c at Vat[c * lda + j]
   int64_t lda;
   const float* Vt;   // two-tower item vectors [N] (row-major, row stride ldv)
@@ -334,6 +348,8 @@ struct HxArgs {
   const float* Vtt;  // the same transposed: Vtt[c * ldtt + j]
   int64_t ldtt;
   const float* inorm;  // [2] the item operands' largest norms (hx_prepare_kernel)
+  const float* uf;     // [2][B][DK] the batch's f32 user rows (hx_user_ops_kernel)
+  const int* uok;      // [B] ALS row known
   int64_t N;
   int G;
   const float* stats;  // [B][G][4] phase 1
@@ -344,116 +360,48 @@ struct HxArgs {
   int64_t idx_offset;
   int64_t* out_idx;
   double* out_val;
-  int* counts;  // [2][B]: groups rescored for the extremes / for the top-k
+  int* counts;  // [2][B]: groups rescored for the extremes / queued for the top-k
   int* flag;    // set when a user rescored every group
+  HxRec* rec;   // [B]
+  int pair_cap;
+  int4* pairs;  // [B * pair_cap] (user, group A, group B)
+  int* pair_total;
+  double* cv;   // [pair][kHxSlots] a pair's best exact fused scores
+  int64_t* ci;  // [pair][kHxSlots] their items
+  int* pc;      // [pair] how many
 };
 
-// 2. Phase 2, one 512-thread block per user. MODE 0: the exact extremes
-// (mm_a / mm_t out); 1: the top-k with the given (global) extremes; 2: both
-// (one shard). FULL: ka == kt == DK (the c2 shape), no width guards.
-//
-// A wave scores two groups at a time, lane l = item l of the pair. The ALS
-// score is the JVM chain itself, read from the TRANSPOSED item factors (per
-// column c one coalesced 128-B run per group: the row-major gathers touched
-// 64 lines per instruction). The two-tower score is first bounded by an f32
-// fma chain over the transposed item vectors (within Ef of the exact
-// score); the exact two-tower score — hrec_dot_scores' MFMA chain over
-// row-major rows — is computed only for the items whose fused bound can
-// still reach the top-k (16 per MFMA round), or for every item of the few
-// groups that can hold a two-tower extreme.
-template <int DK, int MODE, bool FULL>
-__global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
-#pragma clang fp contract(off)
-  constexpr int KK = kHxMaxK;
-  static_assert(8 * KK == 64, "one merge slot per lane of wave 0");
-  constexpr int kList = 1024;  // groups compacted per sweep window
-  __shared__ __attribute__((aligned(16))) float sua[DK];
-  __shared__ __attribute__((aligned(16))) float sut[DK];
-  __shared__ float sred[8][4];
-  __shared__ double se[3];
-  __shared__ double rv[8 * KK];
-  __shared__ int64_t ri[8 * KK];
-  __shared__ double s_tau;
-  __shared__ int s_full, s_cnt, s_n;
-  __shared__ int s_list[kList];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int b = blockIdx.x;
-  const int64_t N = a.N;
-  const int G = a.G;
-  const int ka = FULL ? DK : a.ka, kt = FULL ? DK : a.kt;
-  // the user's group records: staged in LDS once when they fit (every pass
-  // below reads them several times), else read from memory
-  extern __shared__ __attribute__((aligned(16))) float4 st_lds[];
-  const float4* st_glob = reinterpret_cast<const float4*>(a.stats) + (int64_t)b * G;
-  const bool st_in_lds = G <= kHxStatsLds;
-  const float4* st_row = st_in_lds ? st_lds : st_glob;
-  HX_STAMP(0);
-  if (st_in_lds) {
-    HX_STAMP(12);
-    for (int g0 = tid; g0 < G; g0 += 8 * kHxThreads2) {
-      float4 x[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int g = g0 + e * kHxThreads2;
-        if (g < G) x[e] = st_glob[g];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int g = g0 + e * kHxThreads2;
-        if (g < G) st_lds[g] = x[e];
-      }
-    }
-  }
-  // the user's f32 rows (the exact chains read them from LDS)
-  const int64_t r = a.rows ? a.rows[b] : (int64_t)b;
-  const bool rok = r >= 0 && r < a.n_rows;
-  for (int c = tid; c < DK; c += kHxThreads2) {
-    sua[c] = c < ka ? (rok ? a.U[r * a.ldu + c] : __builtin_nanf("")) : 0.f;
-    sut[c] = c < kt ? a.T[(int64_t)b * a.ldt + c] : 0.f;
-  }
-  if (tid == 0) s_cnt = 0;
-  HX_STAMP(13);
-  __syncthreads();
-  HX_STAMP(14);
-  if (wv == 0) {  // the bounds of both models (f64 norms)
-    double sa = 0.0, sb = 0.0;
-    for (int c = lane; c < DK; c += 64) {
-      sa += (double)sua[c] * (double)sua[c];
-      sb += (double)sut[c] * (double)sut[c];
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      sa += __shfl_xor(sa, off, kWave);
-      sb += __shfl_xor(sb, off, kWave);
-    }
-    if (lane == 0) {
-      se[0] = kHxRel * (sqrt(sa) * (1.0 + 1e-6)) * (double)a.inorm[0] + kHxAbs;
-      se[1] = kHxRel * (sqrt(sb) * (1.0 + 1e-6)) * (double)a.inorm[1] + kHxAbs;
-      // the f32 fma chain vs the MFMA chain (bitwise an fma chain): both
-      // within gamma_kt sum |u_c v_c| of the real dot
-      se[2] = (2.0 * kt + 4.0) * 0x1p-24 * (sqrt(sb) * (1.0 + 1e-6)) * (double)a.inorm[1] + kHxAbs;
-    }
-  }
-  __syncthreads();
-  const double Ea = se[0], Et = se[1], Ef = se[2];
-  const bool bad_a = !(Ea < kHxHuge), bad_t = !(Et < kHxHuge);  // NaN / inf / huge: no bound
+// Shared by the phase-2 kernels (one wave, lane l = item l of a pair of
+// 32-item groups). The ALS score is the JVM chain itself, read from the
+// TRANSPOSED item factors (per column one coalesced 128-B run per group;
+// row-major gathers touched 64 lines per load instruction). The two-tower
+// score is first bounded by an f32 fma chain over the transposed item
+// vectors (within Ef of the exact score); the exact two-tower score —
+// hrec_dot_scores' MFMA chain over row-major rows — only for the items whose
+// bound can still matter, 16 per MFMA round.
+template <int DK, bool FULL>
+struct HxWave {
+  const HxArgs& a;
+  const float* sua;  // the user's f32 rows in LDS
+  const float* sut;
+  int ka, kt, lane;
 
-  // lane l's item of the pair (gA, gB): j, in range
-  auto item_of = [&](int gA, int gB, int64_t& j) {
+  __device__ __forceinline__ bool item_of(int gA, int gB, int64_t& j) const {
     const int gl = lane < 32 ? gA : gB;
     j = (int64_t)gl * kHxGrp + (lane & 31);
-    return gl >= 0 && j < N;
-  };
-  // the exact ALS score (sequential rounded products and sums over c < ka,
-  // Spark's dotProduct += a(i) * b(i)) and the two-tower fma chain of item j,
-  // from the transposed matrices: 16 columns of both per batch of loads
-  auto scan = [&](int64_t j, bool ok, float& s_als, float& t_fma) {
+    return gl >= 0 && j < a.N;
+  }
+  // exact ALS score (sequential rounded products and sums over c < ka,
+  // Spark's dotProduct += a(i) * b(i)) and the two-tower fma chain of item j:
+  // 32 columns of both per batch of loads
+  __device__ __forceinline__ void scan(int64_t j, bool ok, float& s_als, float& t_fma) const {
+#pragma clang fp contract(off)
     const int64_t jj = ok ? j : 0;
     const float* pa = a.Vat + jj;
     const float* pt = a.Vtt + jj;
     const int n = ka > kt ? ka : kt;
     float s = 0.f, t = 0.f;
-    for (int c0 = 0; c0 < n; c0 += 32) {  // 64 loads per lane in flight per batch
+    for (int c0 = 0; c0 < n; c0 += 32) {
       float va[32], vt[32];
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
@@ -481,11 +429,10 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
     }
     s_als = s;
     t_fma = t;
-  };
-  // exact two-tower scores of up to 16 items, survivor cc's lane `my`
-  // (-1: none) given on lane cc (< 16): hrec_dot_scores' MFMA chain (k order
-  // 16 ks + 4 g + e, A = the item rows). Lane (g, cc < 4) gets survivor 4 g + cc.
-  auto tt_exact16 = [&](int64_t jrow, bool has) {
+  }
+  // exact two-tower scores of up to 16 items (A = their rows, row cc = the
+  // item of lane cc; lane (g, cc < 4) gets item 4 g + cc)
+  __device__ __forceinline__ float tt_exact16(int64_t jrow, bool has) const {
     const int g4 = lane >> 4;
     const float* row = a.Vt + (has ? jrow : 0) * a.ldv + 4 * g4;
     const int KT = kt >> 4;
@@ -507,11 +454,13 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
         }
       }
     }
-    return hp_pick(acc, lane & 3);  // meaningful on lanes (g, cc < 4)
-  };
-  // every lane with `m`'s bit set in rounds of 16: fn(j, s_als, t_exact) on
-  // lane (g, cc < 4) for survivor 4 g + cc (wave-uniform)
-  auto exact_rounds = [&](uint64_t m, int64_t j, float s_als, auto fn) {
+    return hp_pick(acc, lane & 3);
+  }
+  // every lane with m's bit set, 16 per round: fn(j, s_als, t_exact, bit) on
+  // lane (g, cc < 4) for the round's item 4 g + cc, the item of lane `bit`
+  // (wave-uniform)
+  template <class F>
+  __device__ __forceinline__ void exact_rounds(uint64_t m, int64_t j, float s_als, F fn) const {
     const int cc = lane & 15;
     while (m) {
       int my = -1;
@@ -528,13 +477,201 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
       const int myq = __shfl(my, q, kWave);
       const int64_t jq = __shfl(jr, q, kWave);
       const float aq = __shfl(ar, q, kWave);
-      if (cc < 4 && myq >= 0) fn(jq, aq, tx);
+      if (cc < 4 && myq >= 0) fn(jq, aq, tx, myq);
     }
-  };
+  }
+};
+
+// fminf / fmaxf over the block (512 threads), 4 values
+__device__ __forceinline__ void hx_block_minmax(float& lo_a, float& hi_a, float& lo_t, float& hi_t,
+                                                float (*sred)[4], int lane, int wv) {
+  lo_a = fminf(lo_a, hp_dpp32<0xB1>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0xB1>(hi_a));
+  lo_t = fminf(lo_t, hp_dpp32<0xB1>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0xB1>(hi_t));
+  lo_a = fminf(lo_a, hp_dpp32<0x4E>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0x4E>(hi_a));
+  lo_t = fminf(lo_t, hp_dpp32<0x4E>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0x4E>(hi_t));
+  lo_a = fminf(lo_a, hp_dpp32<0x141>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0x141>(hi_a));
+  lo_t = fminf(lo_t, hp_dpp32<0x141>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0x141>(hi_t));
+  lo_a = fminf(lo_a, hp_dpp32<0x140>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0x140>(hi_a));
+  lo_t = fminf(lo_t, hp_dpp32<0x140>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0x140>(hi_t));
+  lo_a = fminf(lo_a, hp_xor16(lo_a)), hi_a = fmaxf(hi_a, hp_xor16(hi_a));
+  lo_t = fminf(lo_t, hp_xor16(lo_t)), hi_t = fmaxf(hi_t, hp_xor16(hi_t));
+  lo_a = fminf(lo_a, hp_xor32(lo_a)), hi_a = fmaxf(hi_a, hp_xor32(hi_a));
+  lo_t = fminf(lo_t, hp_xor32(lo_t)), hi_t = fmaxf(hi_t, hp_xor32(hi_t));
+  __syncthreads();  // sred's previous readers are done
+  if (lane == 0) sred[wv][0] = lo_a, sred[wv][1] = hi_a, sred[wv][2] = lo_t, sred[wv][3] = hi_t;
+  __syncthreads();
+  lo_a = sred[0][0], hi_a = sred[0][1], lo_t = sred[0][2], hi_t = sred[0][3];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) {
+    lo_a = fminf(lo_a, sred[q][0]), hi_a = fmaxf(hi_a, sred[q][1]);
+    lo_t = fminf(lo_t, sred[q][2]), hi_t = fmaxf(hi_t, sred[q][3]);
+  }
+}
+
+// The block's kk best of the given entries (each lane's HpList, or n LDS
+// entries) by ranking in LDS. Returns 1 (block-uniform) when a NaN or a
+// missing entry is among the kk; writes the outputs when out_idx != nullptr
+// and the kk-th value to *tau.
+struct HxMergeLds {
+  uint64_t mk[512];
+  int64_t mi[512];
+  double mv[512];
+  int n, bad;
+  double tau;
+};
+template <int KK>
+__device__ int hx_merge(HpList<KK>& L, bool from_lists, HxMergeLds& M, double* rv, int64_t* ri, int kk, int lane,
+                        int wv, int tid, int64_t b, int64_t idx_offset, int64_t* out_idx, double* out_val) {
+  if (from_lists) {
+    if (tid == 0) M.n = 0;
+    __syncthreads();
+    // a wave holding more than 8 entries sends only its kk best (the
+    // block's kk best are among the waves' kk best): <= 64 entries to rank
+    int wn = 0;
+#pragma unroll
+    for (int e = 0; e < KK; ++e) wn += __popcll(__ballot(L.i[e] != INT64_MAX));
+    if (wn > 8) {  // wave-uniform
+      L.wave_top(kk, lane, rv + wv * KK, ri + wv * KK);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's LDS writes -> the wave's reads
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < kk && ri[wv * KK + lane] != INT64_MAX) {
+        const int p = atomicAdd(&M.n, 1);
+        const double v = rv[wv * KK + lane];
+        const int64_t i = ri[wv * KK + lane];
+        M.mk[p] = hp_order_key(v, i), M.mi[p] = i, M.mv[p] = v;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < KK; ++e) {
+        if (L.i[e] != INT64_MAX) {
+          const int p = atomicAdd(&M.n, 1);
+          M.mk[p] = hp_order_key(L.v[e], L.i[e]), M.mi[p] = L.i[e], M.mv[p] = L.v[e];
+        }
+      }
+    }
+  }
+  if (tid == 0) M.bad = 0, M.tau = -INFINITY;
+  __syncthreads();
+  const int n = M.n;
+  if (tid < kk && tid >= n) {  // fewer than kk entries: the missing ranks
+    M.bad = 1;
+    if (out_idx) {
+      out_idx[b * kk + tid] = -1;
+      out_val[b * kk + tid] = 0.0;
+    }
+  }
+  for (int q = tid; q < n; q += kHxThreads2) {
+    const uint64_t kq = M.mk[q];
+    const int64_t iq = M.mi[q];
+    int rank = 0;
+    for (int x = 0; x < n; ++x) {
+      const uint64_t kx = M.mk[x];
+      rank += (int)(kx > kq) | ((int)(kx == kq) & (int)(M.mi[x] < iq));
+    }
+    if (rank < kk) {
+      const double vq = M.mv[q];
+      if (vq != vq) M.bad = 1;
+      if (out_idx) {
+        out_idx[b * kk + rank] = iq + idx_offset;
+        out_val[b * kk + rank] = vq;
+      }
+      if (rank == kk - 1) M.tau = vq;
+    }
+  }
+  __syncthreads();
+  return M.bad;
+}
+
+// 2a. One 512-thread block per user. MODE 0: the exact extremes only
+// (mm_a / mm_t out); 1: with the given (global) extremes, the top-k
+// prologue; 2: both (one shard). Prologue: tau from seed groups, then every
+// live pair (group bound >= tau) into the global queue for 2b.
+template <int DK, int MODE, bool FULL>
+__global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
+#pragma clang fp contract(off)
+  constexpr int KK = kHxMaxK;
+  static_assert(8 * KK == 64, "one merge slot per lane of wave 0");
+  constexpr int kList = 1024;  // groups compacted per sweep window
+  __shared__ __attribute__((aligned(16))) float sua[DK];
+  __shared__ __attribute__((aligned(16))) float sut[DK];
+  __shared__ float sred[8][4];
+  __shared__ double se[3];
+  __shared__ double rv[8 * KK];
+  __shared__ int64_t ri[8 * KK];
+  __shared__ int s_cnt, s_n;
+  __shared__ int s_list[kList];
+  __shared__ HxMergeLds M;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x;
+  const int G = a.G;
+  const int ka = FULL ? DK : a.ka, kt = FULL ? DK : a.kt;
+  // the user's group records: staged in LDS once when they fit (the passes
+  // below read them several times), else read from memory
+  extern __shared__ __attribute__((aligned(16))) float4 st_lds[];
+  const float4* st_glob = reinterpret_cast<const float4*>(a.stats) + (int64_t)b * G;
+  const bool st_in_lds = G <= kHxStatsLds;
+  const float4* st_row = st_in_lds ? st_lds : st_glob;
+  int* s_glist = reinterpret_cast<int*>(st_lds + (st_in_lds ? G : 0));  // [2 pair_cap] the live groups
+  HX_STAMP(0);
+  // the user rows first, then the group records (LDS when they fit) with the
+  // approximate extremes folded into the same pass
+  float ur_a = 0.f, ur_t = 0.f;
+  if (tid < DK) {
+    ur_a = a.uf[(int64_t)b * DK + tid];
+    ur_t = a.uf[((int64_t)a.B + b) * DK + tid];
+  }
+  const bool rok = a.uok[b] != 0;
+  float AMN = INFINITY, AMX = -INFINITY, TMN = INFINITY, TMX = -INFINITY;
+  for (int g0 = tid; g0 < G; g0 += 8 * kHxThreads2) {
+    float4 x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int g = g0 + e * kHxThreads2;
+      if (g < G) x[e] = st_glob[g];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int g = g0 + e * kHxThreads2;
+      if (g < G) {
+        if (st_in_lds) st_lds[g] = x[e];
+        AMX = fmaxf(AMX, x[e].x), AMN = fminf(AMN, x[e].y), TMX = fmaxf(TMX, x[e].z), TMN = fminf(TMN, x[e].w);
+      }
+    }
+  }
+  if (tid < DK) sua[tid] = ur_a, sut[tid] = ur_t;
+  if (tid == 0) s_cnt = 0, s_n = 0;
+  __syncthreads();
+  if (wv == 0) {  // the bounds of both models (f64 norms)
+    double sa = 0.0, sb = 0.0;
+    for (int c = lane; c < DK; c += 64) {
+      sa += (double)sua[c] * (double)sua[c];
+      sb += (double)sut[c] * (double)sut[c];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      sa += __shfl_xor(sa, off, kWave);
+      sb += __shfl_xor(sb, off, kWave);
+    }
+    if (lane == 0) {
+      se[0] = kHxRel * (sqrt(sa) * (1.0 + 1e-6)) * (double)a.inorm[0] + kHxAbs;
+      se[1] = kHxRel * (sqrt(sb) * (1.0 + 1e-6)) * (double)a.inorm[1] + kHxAbs;
+      // the f32 fma chain vs the MFMA chain (bitwise an fma chain): both
+      // within gamma_kt sum |u_c v_c| of the real dot
+      se[2] = (2.0 * kt + 4.0) * 0x1p-24 * (sqrt(sb) * (1.0 + 1e-6)) * (double)a.inorm[1] + kHxAbs;
+    }
+  }
+  if constexpr (MODE != 1) hx_block_minmax(AMN, AMX, TMN, TMX, sred, lane, wv);  // its barriers publish se
+  else __syncthreads();
+  HX_STAMP(1);
+  const double Ea = se[0], Et = se[1], Ef = se[2];
+  const bool bad_a = !(Ea < kHxHuge), bad_t = !(Et < kHxHuge);  // NaN / inf / huge: no bound
+  const HxWave<DK, FULL> W{a, sua, sut, ka, kt, lane};
+  const double w0 = a.w0, w1 = a.w1;
+  const int cap2 = 2 * a.pair_cap;
   // every group with pred(g), in windows of kList groups: compacted into LDS
   // (any order: the results do not depend on it), then dealt to the waves
-  // two at a time, round robin (the live groups of a user cluster; dealing
-  // them by index left one wave most of them)
+  // two at a time, round robin (the fallback when the list overflows)
   auto sweep = [&](auto pred, auto pair) {
     for (int w0 = 0; w0 < G; w0 += kList) {
       const int w1e = G - w0 < kList ? G : w0 + kList;
@@ -549,50 +686,42 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
       __syncthreads();  // the list is rewritten by the next window
     }
   };
-  auto block_minmax = [&](float& lo_a, float& hi_a, float& lo_t, float& hi_t) {
-    lo_a = fminf(lo_a, hp_dpp32<0xB1>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0xB1>(hi_a));
-    lo_t = fminf(lo_t, hp_dpp32<0xB1>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0xB1>(hi_t));
-    lo_a = fminf(lo_a, hp_dpp32<0x4E>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0x4E>(hi_a));
-    lo_t = fminf(lo_t, hp_dpp32<0x4E>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0x4E>(hi_t));
-    lo_a = fminf(lo_a, hp_dpp32<0x141>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0x141>(hi_a));
-    lo_t = fminf(lo_t, hp_dpp32<0x141>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0x141>(hi_t));
-    lo_a = fminf(lo_a, hp_dpp32<0x140>(lo_a)), hi_a = fmaxf(hi_a, hp_dpp32<0x140>(hi_a));
-    lo_t = fminf(lo_t, hp_dpp32<0x140>(lo_t)), hi_t = fmaxf(hi_t, hp_dpp32<0x140>(hi_t));
-    lo_a = fminf(lo_a, hp_xor16(lo_a)), hi_a = fmaxf(hi_a, hp_xor16(hi_a));
-    lo_t = fminf(lo_t, hp_xor16(lo_t)), hi_t = fmaxf(hi_t, hp_xor16(hi_t));
-    lo_a = fminf(lo_a, hp_xor32(lo_a)), hi_a = fmaxf(hi_a, hp_xor32(hi_a));
-    lo_t = fminf(lo_t, hp_xor32(lo_t)), hi_t = fmaxf(hi_t, hp_xor32(hi_t));
-    __syncthreads();  // sred's previous readers are done
-    if (lane == 0) {
-      sred[wv][0] = lo_a, sred[wv][1] = hi_a, sred[wv][2] = lo_t, sred[wv][3] = hi_t;
+
+  // the seeds (top-k modes): each wave's group with the largest fused bound
+  // (mode 2: under the scaler of the APPROXIMATE extremes — any choice of
+  // seeds is sound, their exact scores bound tau from below), scanned in the
+  // same round as the extremes' groups; a seed's lower bound needs the exact
+  // scaler, after the extremes
+  constexpr int kSeedPairs = MODE == 0 ? 0 : 4;
+  __shared__ int s_seed[8];
+  HpScale sc0{};
+  if constexpr (MODE == 2) sc0 = hp_scale(AMN, AMX, TMN, TMX);
+  if constexpr (MODE == 1) sc0 = hp_scale(a.mm_a[b], a.mm_a[a.B + b], a.mm_t[b], a.mm_t[a.B + b]);
+  if constexpr (kSeedPairs > 0) {
+    double bu = -INFINITY;
+    int64_t bg = INT64_MAX;
+    for (int g = 64 * wv + lane; g < G; g += 64 * 8) {
+      const float4 x = st_row[g];
+      const double u = hp_fuse(sc0, hx_up((double)x.x + Ea), hx_up((double)x.z + Et), w0, w1);
+      if (bg == INT64_MAX || hp_better(u, g, bu, bg)) {
+        bu = u;
+        bg = g;
+      }
     }
-    __syncthreads();
-    lo_a = sred[0][0], hi_a = sred[0][1], lo_t = sred[0][2], hi_t = sred[0][3];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) {
-      lo_a = fminf(lo_a, sred[q][0]), hi_a = fmaxf(hi_a, sred[q][1]);
-      lo_t = fminf(lo_t, sred[q][2]), hi_t = fmaxf(hi_t, sred[q][3]);
-    }
+    hp_wave_best(bu, bg);
+    if (lane == 0) s_seed[wv] = bg == INT64_MAX ? -1 : (int)bg;
+  }
+  float s_sa = 0.f, s_tf = 0.f;  // the seed pair of waves 0-3: exact ALS score, fma chain
+  int64_t s_j = 0;
+  bool s_ok = false;
+  auto seed_scan = [&](int q) {
+    s_ok = W.item_of(s_seed[2 * q], s_seed[2 * q + 1], s_j);
+    W.scan(s_j, s_ok, s_sa, s_tf);
   };
 
   float amin = INFINITY, amax = -INFINITY, tmin = INFINITY, tmax = -INFINITY;
   if constexpr (MODE != 1) {
-    // a. approximate extremes (the group records, 4 loads in flight per
-    // thread), then the groups that can hold an exact one
-    float AMN = INFINITY, AMX = -INFINITY, TMN = INFINITY, TMX = -INFINITY;
-    for (int g0 = tid; g0 < G; g0 += 4 * kHxThreads2) {
-      float4 x[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int g = g0 + e * kHxThreads2;
-        x[e] = g < G ? st_row[g] : make_float4(-INFINITY, INFINITY, -INFINITY, INFINITY);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        AMX = fmaxf(AMX, x[e].x), AMN = fminf(AMN, x[e].y), TMX = fmaxf(TMX, x[e].z), TMN = fminf(TMN, x[e].w);
-    }
-    block_minmax(AMN, AMX, TMN, TMX);
-    HX_STAMP(1);
+    // a. the groups that can hold an exact extreme
     const bool all_a = rok && bad_a, all_t = bad_t;
     const bool use_a = rok && !bad_a && AMX >= AMN, use_t = !bad_t && TMX >= TMN;
     const float a_hi = use_a ? hx_down((double)AMX - 2.0 * Ea) : INFINITY;
@@ -601,253 +730,294 @@ __global__ __launch_bounds__(kHxThreads2) void hx_user_kernel(HxArgs a) {
     const float t_lo = use_t ? hx_up((double)TMN + 2.0 * Et) : -INFINITY;
     const bool every = all_a || all_t;
     if (every && tid == 0) *a.flag = 1;
+    auto pred = [&](int g) {
+      if (every) return true;
+      const float4 x = st_row[g];
+      return x.x >= a_hi || x.y <= a_lo || x.z >= t_hi || x.w <= t_lo;
+    };
     float lo_a = INFINITY, hi_a = -INFINITY, lo_t = INFINITY, hi_t = -INFINITY;
-    sweep(
-        [&](int g) {
-          if (every) return true;
-          const float4 x = st_row[g];
-          return x.x >= a_hi || x.y <= a_lo || x.z >= t_hi || x.w <= t_lo;
-        },
-        [&](int gA, int gB) {
-          // exact ALS scores of every item; the exact two-tower score only
-          // where the fma chain cannot rule the item out as the pair's
-          // extreme (|t_fma - t| <= Ef: the item holding the exact max has
-          // t_fma + Ef >= the pair's max of t_fma - Ef, likewise the min)
-          int64_t j;
-          const bool ok = item_of(gA, gB, j);
-          float sa, tf;
-          scan(j, ok, sa, tf);
-          if (ok) lo_a = fminf(lo_a, sa), hi_a = fmaxf(hi_a, sa);
-          float pm = ok ? tf : -INFINITY, pn = ok ? tf : INFINITY;
-          pm = fmaxf(pm, hp_dpp32<0xB1>(pm)), pn = fminf(pn, hp_dpp32<0xB1>(pn));
-          pm = fmaxf(pm, hp_dpp32<0x4E>(pm)), pn = fminf(pn, hp_dpp32<0x4E>(pn));
-          pm = fmaxf(pm, hp_dpp32<0x141>(pm)), pn = fminf(pn, hp_dpp32<0x141>(pn));
-          pm = fmaxf(pm, hp_dpp32<0x140>(pm)), pn = fminf(pn, hp_dpp32<0x140>(pn));
-          pm = fmaxf(pm, hp_xor16(pm)), pn = fminf(pn, hp_xor16(pn));
-          pm = fmaxf(pm, hp_xor32(pm)), pn = fminf(pn, hp_xor32(pn));
-          const bool cand = ok && (every || (double)tf + Ef >= (double)pm - Ef || (double)tf - Ef <= (double)pn + Ef ||
-                                   tf != tf);
-          exact_rounds(__ballot(cand), j, sa, [&](int64_t, float, float tx) {
-            lo_t = fminf(lo_t, tx), hi_t = fmaxf(hi_t, tx);
-          });
-        });
-    block_minmax(lo_a, hi_a, lo_t, hi_t);
+    auto pair = [&](int gA, int gB) {
+      // exact ALS scores of every item; the exact two-tower score only
+      // where the fma chain cannot rule the item out as the pair's
+      // extreme (|t_fma - t| <= Ef: the item holding the exact max has
+      // t_fma + Ef >= the pair's max of t_fma - Ef, likewise the min)
+      int64_t j;
+      const bool ok = W.item_of(gA, gB, j);
+      float sa, tf;
+      W.scan(j, ok, sa, tf);
+      if (ok) lo_a = fminf(lo_a, sa), hi_a = fmaxf(hi_a, sa);
+      float pm = ok ? tf : -INFINITY, pn = ok ? tf : INFINITY;
+      pm = fmaxf(pm, hp_dpp32<0xB1>(pm)), pn = fminf(pn, hp_dpp32<0xB1>(pn));
+      pm = fmaxf(pm, hp_dpp32<0x4E>(pm)), pn = fminf(pn, hp_dpp32<0x4E>(pn));
+      pm = fmaxf(pm, hp_dpp32<0x141>(pm)), pn = fminf(pn, hp_dpp32<0x141>(pn));
+      pm = fmaxf(pm, hp_dpp32<0x140>(pm)), pn = fminf(pn, hp_dpp32<0x140>(pn));
+      pm = fmaxf(pm, hp_xor16(pm)), pn = fminf(pn, hp_xor16(pn));
+      pm = fmaxf(pm, hp_xor32(pm)), pn = fminf(pn, hp_xor32(pn));
+      const bool cand = ok && (every || (double)tf + Ef >= (double)pm - Ef || (double)tf - Ef <= (double)pn + Ef ||
+                               tf != tf);
+      W.exact_rounds(__ballot(cand), j, sa, [&](int64_t, float, float tx, int) {
+        lo_t = fminf(lo_t, tx), hi_t = fmaxf(hi_t, tx);
+      });
+    };
+    // one pass into the LDS list (the windowed sweep when it overflows)
+    for (int g = tid; g < G; g += kHxThreads2) {
+      if (pred(g)) {
+        const int q = atomicAdd(&s_n, 1);
+        if (q < cap2) s_glist[q] = g;
+      }
+    }
+    __syncthreads();
+    const int n = s_n;
+    if (n <= cap2) {
+      // work items: the seed pairs (waves 0-3), then the extremes' pairs
+      const int n_items = kSeedPairs + (n + 1) / 2;
+      for (int it = wv; it < n_items; it += 8) {
+        if (it < kSeedPairs) {
+          seed_scan(it);
+        } else {
+          const int q = it - kSeedPairs;
+          pair(s_glist[2 * q], 2 * q + 1 < n ? s_glist[2 * q + 1] : -1);
+        }
+      }
+      if (tid == 0) s_cnt = n;
+    } else {
+      sweep(pred, pair);
+      if (wv < kSeedPairs) seed_scan(wv);
+    }
+    hx_block_minmax(lo_a, hi_a, lo_t, hi_t, sred, lane, wv);
     HX_STAMP(2);
     amin = lo_a, amax = hi_a, tmin = lo_t, tmax = hi_t;
     if (tid == 0) {
       a.counts[b] = s_cnt;
-      s_cnt = 0;
       a.mm_a[b] = amin, a.mm_a[a.B + b] = amax;
       a.mm_t[b] = tmin, a.mm_t[a.B + b] = tmax;
     }
-    __syncthreads();  // s_cnt reset before the top-k sweep counts into it
     if constexpr (MODE == 0) return;
   } else {
     amin = a.mm_a[b], amax = a.mm_a[a.B + b], tmin = a.mm_t[b], tmax = a.mm_t[a.B + b];
+    __syncthreads();  // s_seed
+    if (wv < kSeedPairs) seed_scan(wv);
   }
-  // b. the top-k
-  const int kk = a.kk;
-  if (!(amin <= amax) || !(tmin <= tmax)) {
-    // one model has no number at all: every fused score is NaN, and NaN
-    // orders by item id
-    if (tid < kk) {
-      a.out_idx[(int64_t)b * kk + tid] = tid < N ? tid + a.idx_offset : -1;
-      a.out_val[(int64_t)b * kk + tid] = tid < N ? __builtin_nan("") : 0.0;
+  // b. the top-k prologue
+  HxRec r{};
+  r.Ef = Ef;
+  if (!(amin <= amax) || !(tmin <= tmax)) {  // every fused score NaN
+    if (tid == 0) {
+      r.state = kHxNaN;
+      a.rec[b] = r;
+      a.counts[a.B + b] = 0;
     }
-    if (tid == 0) a.counts[a.B + b] = 0;
     return;
   }
   const HpScale sc = hp_scale(amin, amax, tmin, tmax);
-  const double w0 = a.w0, w1 = a.w1;
-  bool every = bad_a || bad_t || !(isfinite(amin) && isfinite(amax) && isfinite(tmin) && isfinite(tmax));
+  r.ascale = sc.ascale, r.amin_ = sc.amin_, r.tscale = sc.tscale, r.tmin_ = sc.tmin_;
+  const int kk = a.kk;
+  if (bad_a || bad_t || !(isfinite(amin) && isfinite(amax) && isfinite(tmin) && isfinite(tmax))) {
+    if (tid == 0) {  // no usable bound: 2c scores every group
+      r.state = kHxEvery;
+      r.tau = -INFINITY;
+      a.rec[b] = r;
+      a.counts[a.B + b] = G;
+      *a.flag = 1;
+    }
+    return;
+  }
   auto ub_of = [&](int g) {
     const float4 x = st_row[g];
     return hp_fuse(sc, hx_up((double)x.x + Ea), hx_up((double)x.z + Et), w0, w1);
   };
+  // tau: a seed's fused score is bounded below by its exact ALS score and its
+  // fma chain - Ef, so the kk-th best of those bounds (distinct items) is a
+  // lower bound of the shard's kk-th best fused score
   HpList<KK> L;
-  // the lanes' lists -> the block's kk best: s_tau = the kk-th best value,
-  // s_full = 1 when a NaN or a missing entry is among the kk; the outputs
-  // written when `write`. The lanes' entries (few: only exactly scored items
-  // enter) are compacted into LDS and each ranked by counting the better ones
-  // (one order key per entry); more than kMerge entries take the waves'
-  // arg-best rounds instead.
-  constexpr int kMerge = 512;
-  __shared__ uint64_t mk[kMerge];
-  __shared__ int64_t mi[kMerge];
-  __shared__ double mv[kMerge];
-  __shared__ int s_m, s_bad;
-  auto merge = [&](bool write) {
-    if (tid == 0) s_m = 0, s_bad = 0;
-    __syncthreads();
-    // a wave holding more than 8 entries sends only its kk best (the
-    // block's kk best are among the waves' kk best): <= 64 entries to rank
-    int wn = 0;
-#pragma unroll
-    for (int e = 0; e < KK; ++e) wn += __popcll(__ballot(L.i[e] != INT64_MAX));
-    if (wn > 8) {  // wave-uniform
-      L.wave_top(kk, lane, rv + wv * KK, ri + wv * KK);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's LDS writes -> the wave's reads
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (lane < kk && ri[wv * KK + lane] != INT64_MAX) {
-        const int p = atomicAdd(&s_m, 1);
-        const double v = rv[wv * KK + lane];
-        const int64_t i = ri[wv * KK + lane];
-        if (p < kMerge) mk[p] = hp_order_key(v, i), mi[p] = i, mv[p] = v;
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < KK; ++e) {
-        if (L.i[e] != INT64_MAX) {
-          const int p = atomicAdd(&s_m, 1);
-          if (p < kMerge) mk[p] = hp_order_key(L.v[e], L.i[e]), mi[p] = L.i[e], mv[p] = L.v[e];
-        }
-      }
-    }
-    __syncthreads();
-    const int n = s_m;
-    if (n <= kMerge) {  // block-uniform
-      if (tid < kk && tid >= n) {  // fewer than kk entries: the missing ranks
-        s_bad = 1;
-        if (write) {
-          a.out_idx[(int64_t)b * kk + tid] = -1;
-          a.out_val[(int64_t)b * kk + tid] = 0.0;
-        }
-      }
-      for (int q = tid; q < n; q += kHxThreads2) {
-        const uint64_t kq = mk[q];
-        const int64_t iq = mi[q];
-        int rank = 0;
-        for (int x = 0; x < n; ++x) {
-          const uint64_t kx = mk[x];
-          rank += (int)(kx > kq) | ((int)(kx == kq) & (int)(mi[x] < iq));
-        }
-        if (rank < kk) {
-          const double vq = mv[q];
-          if (vq != vq) s_bad = 1;
-          if (write) {
-            a.out_idx[(int64_t)b * kk + rank] = iq + a.idx_offset;
-            a.out_val[(int64_t)b * kk + rank] = vq;
-          }
-          if (rank == kk - 1) s_tau = vq;
-        }
-      }
-      __syncthreads();
-      if (tid == 0) {
-        s_full = s_bad;
-        if (s_bad) s_tau = -INFINITY;
-      }
-      __syncthreads();
-      return;
-    }
-    L.wave_top(kk, lane, rv + wv * KK, ri + wv * KK);
-    __syncthreads();
-    if (wv == 0) {
-      double v0 = 0.0;
-      int64_t i0 = INT64_MAX;
-      if ((lane % KK) < kk) {
-        v0 = rv[lane];
-        i0 = ri[lane];
-      }
-      bool bad = false;
-      double last = -INFINITY;
-      for (int q = 0; q < kk; ++q) {
-        double bv = v0;
-        int64_t bi = i0;
-        hp_wave_best(bv, bi);
-        if (bi == INT64_MAX || bv != bv) bad = true;
-        if (write && lane == 0) {
-          a.out_idx[(int64_t)b * kk + q] = bi == INT64_MAX ? -1 : bi + a.idx_offset;
-          a.out_val[(int64_t)b * kk + q] = bi == INT64_MAX ? 0.0 : bv;
-        }
-        if (bi != INT64_MAX && i0 == bi) i0 = INT64_MAX;  // the owner pops its entry
-        last = bv;
-      }
-      if (lane == 0) {
-        s_full = bad ? 1 : 0;
-        s_tau = bad ? -INFINITY : last;
-      }
-    }
-    __syncthreads();
-  };
-  double tau = -INFINITY;
-  // the top-k over two groups: items whose fused bound (exact ALS score,
-  // two-tower fma chain + Ef) reaches tau (all: all_pass) take the exact
-  // two-tower chain and enter the lists
-  auto topk_pair = [&](int gA, int gB, bool all_pass) {
-    int64_t j;
-    const bool ok = item_of(gA, gB, j);
-    float sa, tf;
-    scan(j, ok, sa, tf);
-    const bool pass = ok && (all_pass || hp_fuse(sc, sa, hx_up((double)tf + Ef), w0, w1) >= tau);
-    exact_rounds(__ballot(pass), j, sa,
-                 [&](int64_t jq, float aq, float tx) { L.insert(hp_fuse(sc, aq, tx, w0, w1), jq); });
-  };
-  if (!every) {
-    // tau from seeds: each wave's two groups with the largest bounds; a
-    // seed's fused score is bounded below by its exact ALS score and its
-    // fma chain - Ef, so the kk-th best of those bounds (distinct items) is a
-    // lower bound of the shard's kk-th best fused score — no exact two-tower
-    // chain needed
-    double bu = -INFINITY;
-    int64_t bg = INT64_MAX;
-    HX_STAMP(7);
-    HX_WSTAMP(0);
-    for (int g = 64 * wv + lane; g < G; g += 64 * 8) {
-      const double u = ub_of(g);
-      if (bg == INT64_MAX || hp_better(u, g, bu, bg)) {
-        bu = u;
-        bg = g;
-      }
-    }
-    HX_STAMP(8);
-    double v1 = bu;
-    int64_t g1 = bg;
-    hp_wave_best(v1, g1);
-    if (g1 != INT64_MAX && bg == g1) bg = INT64_MAX;  // the owner drops it
-    double v2 = bu;
-    int64_t g2 = bg;
-    hp_wave_best(v2, g2);
-    L.reset();
-    HX_STAMP(9);
-    if (g1 != INT64_MAX) {
-      int64_t j;
-      const bool ok = item_of((int)g1, g2 == INT64_MAX ? -1 : (int)g2, j);
-      float sa, tf;
-      scan(j, ok, sa, tf);
-      HX_STAMP(10);
-      HX_WSTAMP(1);
-      if (ok) L.insert(hp_fuse(sc, sa, hx_down((double)tf - Ef), w0, w1), j);
-    }
-    HX_STAMP(11);
-    HX_WSTAMP(2);
-    merge(false);
-    HX_STAMP(3);
-    tau = s_tau;  // -inf: fewer than kk numeric seeds (every group below qualifies)
-  }
   L.reset();
-  sweep([&](int g) { return every || ub_of(g) >= tau; }, [&](int gA, int gB) { topk_pair(gA, gB, every); });
-  HX_STAMP(4);
-  merge(true);
-  HX_STAMP(5);
-  if (s_full && !every) {  // a NaN or a missing entry among the kk: the whole shard
-    every = true;
-    L.reset();
-    sweep([&](int) { return true; }, [&](int gA, int gB) { topk_pair(gA, gB, true); });
-    merge(true);
+  if (s_ok) L.insert(hp_fuse(sc, s_sa, hx_down((double)s_tf - Ef), w0, w1), s_j);
+  const int seed_bad = hx_merge<KK>(L, true, M, rv, ri, kk, lane, wv, tid, b, 0, nullptr, nullptr);
+  const double tau = seed_bad ? -INFINITY : M.tau;  // -inf: fewer than kk numeric seeds (every group qualifies)
+  HX_STAMP(3);
+  // the live groups into LDS, then their pairs into the queue for 2b (one
+  // reservation per user: its pairs are contiguous)
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  for (int g = tid; g < G; g += kHxThreads2) {
+    if (ub_of(g) >= tau) {
+      const int q = atomicAdd(&s_n, 1);
+      if (q < cap2) s_glist[q] = g;
+    }
   }
+  __syncthreads();
+  const int n_live = s_n;
+  if (n_live > cap2) {  // too many: 2c scores every group
+    if (tid == 0) {
+      r.state = kHxEvery;
+      r.tau = -INFINITY;
+      a.rec[b] = r;
+      a.counts[a.B + b] = G;
+    }
+    return;
+  }
+  const int np = (n_live + 1) / 2;
+  __shared__ int s_base;
+  if (tid == 0) s_base = np ? atomicAdd(a.pair_total, np) : 0;
+  __syncthreads();
+  const int base = s_base;
+  for (int q = tid; q < np; q += kHxThreads2)
+    a.pairs[base + q] = make_int4(b, s_glist[2 * q], 2 * q + 1 < n_live ? s_glist[2 * q + 1] : -1, 0);
   if (tid == 0) {
-    a.counts[a.B + b] = s_cnt;
-    if (every) *a.flag = 1;
+    r.state = kHxQueued;
+    r.tau = tau;
+    r.pair_base = base;
+    r.n_pairs = np;
+    a.rec[b] = r;
+    a.counts[a.B + b] = n_live;
   }
-  HX_STAMP(6);
+  HX_STAMP(4);
+}
+
+#ifdef HREC_HX_STAMPS
+constexpr int kHxPStampWaves = 8192;
+__device__ unsigned long long g_hx_pstamps[kHxPStampWaves][4];  // start, end, pairs, exact items
+#endif
+
+// 2b. The queued pairs of every user, dealt round robin to the waves of a
+// persistent grid (a user's live groups vary by an order of magnitude: a
+// block per user waited on the heaviest; a pair costs about the same
+// whoever's it is). Per pair: both scans, each item's fused bound against
+// its user's tau, the exact two-tower chain for the items that reach it;
+// the pair's best kHxSlots exact fused scores go to its own slots (no
+// atomics: device-scope atomics on one counter serialised 8k pulls into
+// 130 us). The user rows are read from memory (uniform loads).
+template <int DK, bool FULL>
+__global__ __launch_bounds__(256) void hx_pairs_kernel(HxArgs a) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int ka = FULL ? DK : a.ka, kt = FULL ? DK : a.kt;
+  const int total = *(volatile const int*)a.pair_total;  // final: 2a has completed
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), n_waves = gridDim.x * 4;
+#ifdef HREC_HX_STAMPS
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  int n_pairs = 0, n_exact = 0;
+#endif
+  for (int p = gw; p < total; p += n_waves) {
+    const int4 e = a.pairs[p];
+    const int b = e.x;
+    const HxRec r = a.rec[b];
+    const HxWave<DK, FULL> W{a, a.uf + (int64_t)b * DK, a.uf + ((int64_t)a.B + b) * DK, ka, kt, lane};
+    HpScale sc;
+    sc.ascale = r.ascale, sc.amin_ = r.amin_, sc.tscale = r.tscale, sc.tmin_ = r.tmin_;
+    int64_t j;
+    const bool ok = W.item_of(e.y, e.z, j);
+    float sa, tf;
+    W.scan(j, ok, sa, tf);
+    const bool pass = ok && hp_fuse(sc, sa, hx_up((double)tf + r.Ef), a.w0, a.w1) >= r.tau;
+    const uint64_t m = __ballot(pass);
+    const int n = __popcll(m);
+    double* pv = a.cv + (int64_t)p * kHxSlots;
+    int64_t* pi = a.ci + (int64_t)p * kHxSlots;
+    if (n <= kHxSlots) {  // every passing item keeps a slot: its rank among the passing lanes
+      W.exact_rounds(m, j, sa, [&](int64_t jq, float aq, float tx, int bit) {
+        const int q = __popcll(m & ((1ull << bit) - 1));
+        pv[q] = hp_fuse(sc, aq, tx, a.w0, a.w1);
+        pi[q] = jq;
+      });
+    } else {  // the pair's best kHxSlots (the user's kk best are among the pairs' best kk)
+      HpList<kHxSlots> L;
+      L.reset();
+      W.exact_rounds(m, j, sa, [&](int64_t jq, float aq, float tx, int) { L.insert(hp_fuse(sc, aq, tx, a.w0, a.w1), jq); });
+      L.wave_top(kHxSlots, lane, pv, pi);
+    }
+    if (lane == 0) a.pc[p] = n < kHxSlots ? n : kHxSlots;
+#ifdef HREC_HX_STAMPS
+    ++n_pairs;
+    n_exact += n;
+#endif
+  }
+#ifdef HREC_HX_STAMPS
+  if (lane == 0 && gw < kHxPStampWaves) {
+    g_hx_pstamps[gw][0] = t0;
+    g_hx_pstamps[gw][1] = __builtin_amdgcn_s_memtime();
+    g_hx_pstamps[gw][2] = n_pairs;
+    g_hx_pstamps[gw][3] = n_exact;
+  }
+#endif
+}
+
+// 2c. One 512-thread block per user: the stable top-k of its candidates
+// (ranked in LDS), or — no bound, too many live groups or candidates, a NaN
+// or a missing entry among the kk — every group of the shard scored exactly.
+template <int DK, bool FULL>
+__global__ __launch_bounds__(kHxThreads2) void hx_final_kernel(HxArgs a) {
+#pragma clang fp contract(off)
+  constexpr int KK = kHxMaxK;
+  __shared__ __attribute__((aligned(16))) float sua[DK];
+  __shared__ __attribute__((aligned(16))) float sut[DK];
+  __shared__ double rv[8 * KK];
+  __shared__ int64_t ri[8 * KK];
+  __shared__ HxMergeLds M;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x;
+  const int kk = a.kk;
+  const HxRec r = a.rec[b];
+  if (r.state == kHxNaN) {  // NaN orders by item id: the first kk items
+    if (tid < kk) {
+      a.out_idx[(int64_t)b * kk + tid] = tid < a.N ? tid + a.idx_offset : -1;
+      a.out_val[(int64_t)b * kk + tid] = tid < a.N ? __builtin_nan("") : 0.0;
+    }
+    return;
+  }
+  HpList<KK> L;
+  L.reset();
+  if (r.state == kHxQueued) {
+    for (int q = r.pair_base + tid; q < r.pair_base + r.n_pairs; q += kHxThreads2) {
+      const int c = a.pc[q];
+      for (int e = 0; e < c; ++e) L.insert(a.cv[(int64_t)q * kHxSlots + e], a.ci[(int64_t)q * kHxSlots + e]);
+    }
+    if (!hx_merge<KK>(L, true, M, rv, ri, kk, lane, wv, tid, b, a.idx_offset, a.out_idx, a.out_val)) return;
+  }
+  // every group of the shard, exactly
+  if (tid == 0) *a.flag = 1;
+  const int ka = FULL ? DK : a.ka, kt = FULL ? DK : a.kt;
+  for (int c = tid; c < DK; c += kHxThreads2) {
+    sua[c] = a.uf[(int64_t)b * DK + c];
+    sut[c] = a.uf[((int64_t)a.B + b) * DK + c];
+  }
+  __syncthreads();
+  HpScale sc;
+  sc.ascale = r.ascale, sc.amin_ = r.amin_, sc.tscale = r.tscale, sc.tmin_ = r.tmin_;
+  const HxWave<DK, FULL> W{a, sua, sut, ka, kt, lane};
+  L.reset();
+  const int G = a.G;
+  for (int p = wv; 2 * p < G; p += 8) {
+    int64_t j;
+    const bool ok = W.item_of(2 * p, 2 * p + 1 < G ? 2 * p + 1 : -1, j);
+    float sa, tf;
+    W.scan(j, ok, sa, tf);
+    W.exact_rounds(__ballot(ok), j, sa,
+                   [&](int64_t jq, float aq, float tx, int) { L.insert(hp_fuse(sc, aq, tx, a.w0, a.w1), jq); });
+  }
+  hx_merge<KK>(L, true, M, rv, ri, kk, lane, wv, tid, b, a.idx_offset, a.out_idx, a.out_val);
+}
+
+// The per-call counters: flag (modes 0 / 2: a minmax call starts the batch)
+// and the pair queue's length. A kernel, not a memset: captured in a HIP
+// graph, the memset node left the counters of the previous replay in place.
+__global__ void hx_reset_kernel(int* flag, int n, int keep_flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && (i > 0 || !keep_flag)) flag[i] = 0;
 }
 
 struct HxWs {
   uint16_t* uop;  // [2][B][2 dk] split bf16
+  float* uf;      // [2][B][dk] f32 user rows (NaN: an unknown ALS row)
+  int* uok;       // [B] ALS row known
   float* stats;   // [B][G][4]
   int* counts;    // [2][B]
-  int* flag;
+  int* flag;      // [0] flag, [1] pair_total
+  HxRec* rec;
+  int4* pairs;
+  double* cv;
+  int64_t* ci;
+  int* pc;
   size_t total;
 };
 
@@ -861,9 +1031,17 @@ static HxWs hx_layout(char* base, int B, int64_t N, int dk) {
   };
   const int64_t G = (N + kHxGrp - 1) / kHxGrp;
   w.uop = (uint16_t*)take((size_t)2 * B * dk * 4);
+  w.uf = (float*)take((size_t)2 * B * dk * 4);
+  w.uok = (int*)take((size_t)B * 4);
   w.stats = (float*)take((size_t)B * G * 16);
   w.counts = (int*)take((size_t)2 * B * 4);
-  w.flag = (int*)take(4);
+  w.flag = (int*)take(16);  // flag, pair_total
+  w.rec = (HxRec*)take((size_t)B * sizeof(HxRec));
+  const size_t n_pairs = (size_t)B * hx_pair_cap((int)G);
+  w.pairs = (int4*)take(n_pairs * 16);
+  w.cv = (double*)take(n_pairs * kHxSlots * 8);
+  w.ci = (int64_t*)take(n_pairs * kHxSlots * 8);
+  w.pc = (int*)take(n_pairs * 4);
   w.total = off + 256;
   return w;
 }
@@ -930,6 +1108,15 @@ extern "C" size_t hrec_hybrid_exact_workspace_bytes(int n_users, int64_t n_items
   return hx_layout(nullptr, n_users > 0 ? n_users : 0, n_items > 0 ? n_items : 0, dk).total;
 }
 
+static int hx_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
 // Launches up to phase 2 (mode 0 / 2) or phase 2 alone (mode 1).
 static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt_mm, int als_wins, int top_k,
                   int64_t idx_offset, int64_t* out_idx, double* out_val, void* workspace, hipStream_t s) {
@@ -938,19 +1125,27 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   const HxWs w = hx_layout((char*)workspace, B, N, dk);
   const int G = (int)((N + kHxGrp - 1) / kHxGrp);
   const char* items = static_cast<const char*>(x->prepared);
+  {
+    hipLaunchKernelGGL(hx_reset_kernel, dim3(1), dim3(64), 0, s, w.flag, 2, mode == 1);
+    const int rc = check_launch("hx_reset_kernel");
+    if (rc) return rc;
+  }
   if (mode != 1) {
-    if (hipMemsetAsync(w.flag, 0, 4, s) != hipSuccess) return check_launch("hybrid_exact: memset");
     hipLaunchKernelGGL(hx_user_ops_kernel, dim3((unsigned)B, 2), dim3(128), 0, s, x->als_users, x->als_ld,
-                       x->als_rows, x->n_als_rows, x->als_width, x->tt_users, x->tt_ld, x->tt_width, B, dk, w.uop);
+                       x->als_rows, x->n_als_rows, x->als_width, x->tt_users, x->tt_ld, x->tt_width, B, dk, w.uop,
+                       w.uf, w.uok);
     int rc = check_launch("hx_user_ops_kernel");
     if (rc) return rc;
 #define HREC_HX_STATS(DK)                                                                                        \
   do {                                                                                                           \
     using S = HxShape<DK>;                                                                                       \
     const int n_ut = (B + S::UB - 1) / S::UB;                                                                    \
-    const int64_t n_rng = (N + S::kBlockItems - 1) / S::kBlockItems;                                             \
+    /* two blocks per CU (the LDS holds two user tiles): item ranges of whole 32-item slices */                  \
+    int64_t n_rng = (2 * hx_cus() + n_ut - 1) / n_ut;                                                            \
+    int64_t per = ((N + n_rng - 1) / n_rng + 31) / 32 * 32;                                                      \
+    n_rng = (N + per - 1) / per;                                                                                 \
     hipLaunchKernelGGL(hx_stats_kernel<DK>, dim3((unsigned)(n_ut * n_rng)), dim3(kHxThreads1), 0, s, w.uop, B,     \
-                       n_ut, items, N, G, w.stats);                                                              \
+                       n_ut, items, N, G, per, w.stats);                                                         \
   } while (0)
     if (dk == 64) HREC_HX_STATS(64); else HREC_HX_STATS(128);
 #undef HREC_HX_STATS
@@ -958,11 +1153,11 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
     if (rc) return rc;
   }
   HxArgs a{};
-  a.U = x->als_users, a.ldu = x->als_ld, a.rows = x->als_rows, a.n_rows = x->n_als_rows, a.ka = x->als_width;
-  a.T = x->tt_users, a.ldt = x->tt_ld, a.kt = x->tt_width, a.B = B;
+  a.ka = x->als_width, a.kt = x->tt_width, a.B = B;
   a.Vat = x->als_items_t, a.lda = x->als_items_ld, a.Vt = x->tt_items, a.ldv = x->tt_items_ld;
   a.Vtt = x->tt_items_t, a.ldtt = x->tt_items_t_ld;
   a.inorm = hx_norms(x->prepared, N, dk);
+  a.uf = w.uf, a.uok = w.uok;
   a.N = N, a.G = G, a.stats = w.stats;
   a.mm_a = als_mm, a.mm_t = tt_mm;
   // src/hybrid_system.py:69 — strict '>' picks (0.8, 0.2), else (0.2, 0.8)
@@ -970,25 +1165,38 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   a.kk = (int)(top_k < N ? top_k : N);
   a.idx_offset = idx_offset, a.out_idx = out_idx, a.out_val = out_val;
   a.counts = w.counts, a.flag = w.flag;
+  a.pair_cap = hx_pair_cap(G);
+  a.rec = w.rec, a.pairs = w.pairs, a.pair_total = w.flag + 1;
+  a.cv = w.cv, a.ci = w.ci, a.pc = w.pc;
   const bool full = x->als_width == dk && x->tt_width == dk;
-  const size_t st_lds = G <= kHxStatsLds ? (size_t)G * 16 : 0;  // the user's group records in LDS
-#define HREC_HX_USER(DK, M)                                                                                      \
+  // 2a's dynamic LDS: the user's group records (when they fit), the live groups
+  const size_t st_lds = (G <= kHxStatsLds ? (size_t)G * 16 : 0) + (size_t)a.pair_cap * 8;
+  // 2b: a persistent grid, 4 waves per block, four blocks per CU (<= 128 VGPRs)
+  const unsigned n_pairs_blocks = (unsigned)(4 * hx_cus());
+#define HREC_HX_2(DK, M, F)                                                                                      \
   do {                                                                                                           \
-    if (full) {                                                                                                  \
-      if (!allow_max_lds(hx_user_kernel<DK, M, true>)) return check_launch("hx_user_kernel: LDS attribute");    \
-      hipLaunchKernelGGL((hx_user_kernel<DK, M, true>), dim3((unsigned)B), dim3(kHxThreads2), st_lds, s, a);     \
-    } else {                                                                                                     \
-      if (!allow_max_lds(hx_user_kernel<DK, M, false>)) return check_launch("hx_user_kernel: LDS attribute");   \
-      hipLaunchKernelGGL((hx_user_kernel<DK, M, false>), dim3((unsigned)B), dim3(kHxThreads2), st_lds, s, a);    \
-    }                                                                                                            \
+    if (!allow_max_lds(hx_pre_kernel<DK, M, F>)) return check_launch("hx_pre_kernel: LDS attribute");          \
+    hipLaunchKernelGGL((hx_pre_kernel<DK, M, F>), dim3((unsigned)B), dim3(kHxThreads2), st_lds, s, a);          \
+    int rc2 = check_launch("hx_pre_kernel");                                                                     \
+    if (rc2 || M == 0) return rc2;                                                                               \
+    hipLaunchKernelGGL((hx_pairs_kernel<DK, F>), dim3(n_pairs_blocks), dim3(256), 0, s, a);                    \
+    rc2 = check_launch("hx_pairs_kernel");                                                                       \
+    if (rc2) return rc2;                                                                                         \
+    hipLaunchKernelGGL((hx_final_kernel<DK, F>), dim3((unsigned)B), dim3(kHxThreads2), 0, s, a);                \
+    return check_launch("hx_final_kernel");                                                                      \
+  } while (0)
+#define HREC_HX_M(DK, M)                 \
+  do {                                   \
+    if (full) HREC_HX_2(DK, M, true);    \
+    else HREC_HX_2(DK, M, false);        \
   } while (0)
   if (dk == 64) {
-    if (mode == 0) HREC_HX_USER(64, 0); else if (mode == 1) HREC_HX_USER(64, 1); else HREC_HX_USER(64, 2);
+    if (mode == 0) HREC_HX_M(64, 0); else if (mode == 1) HREC_HX_M(64, 1); else HREC_HX_M(64, 2);
   } else {
-    if (mode == 0) HREC_HX_USER(128, 0); else if (mode == 1) HREC_HX_USER(128, 1); else HREC_HX_USER(128, 2);
+    if (mode == 0) HREC_HX_M(128, 0); else if (mode == 1) HREC_HX_M(128, 1); else HREC_HX_M(128, 2);
   }
-#undef HREC_HX_USER
-  return check_launch("hx_user_kernel");
+#undef HREC_HX_M
+#undef HREC_HX_2
 }
 
 extern "C" int hrec_hybrid_exact_minmax(const hrec_hybrid_batch* x, float* als_mm, float* tt_mm, void* workspace,
@@ -1061,9 +1269,10 @@ extern "C" int hrec_hybrid_exact_counts(const void* workspace, int n_users, int6
 extern "C" int hrec_debug_hx1_stamps(unsigned long long* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hx1_stamps), sizeof(g_hx1_stamps)) == hipSuccess ? 0 : -2;
 }
+extern "C" int hrec_debug_hx_pstamps(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hx_pstamps), sizeof(g_hx_pstamps)) == hipSuccess ? 0 : -2;
+}
 extern "C" int hrec_debug_hx_stamps(unsigned long long* host_out) {
-  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hx_stamps), sizeof(g_hx_stamps)) != hipSuccess) return -2;
-  return hipMemcpyFromSymbol(host_out + kHxStampBlocks * 16, HIP_SYMBOL(g_hx_wstamps), sizeof(g_hx_wstamps)) ==
-                 hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hx_stamps), sizeof(g_hx_stamps)) == hipSuccess ? 0 : -2;
 }
 #endif

@@ -31,7 +31,8 @@ import numpy as np
 import torch
 
 from . import _hrec
-from .als_engine import DeviceALS, RowLayout, padded_k, process_group, shard_for_layout
+from .als_engine import DeviceALS, padded_k, process_group
+from .als_ingest import check_same_frame, frame_fingerprint, sharded_ingest
 from .data_preprocessing import get_item_features
 from .synthetic import DeviceCSR
 
@@ -222,6 +223,7 @@ class ALSModel:
         self.item_features = None
         self.seed = seed
         self._feat_cache = None
+        self.ingest_peak_bytes = None  # device bytes the last train's ingest peaked at (cuda only)
 
     # -------------------------------------------------------- engine handle
     def initialize_spark(self):
@@ -244,26 +246,38 @@ class ALSModel:
         dev = self.spark.device
         users_h = _int_ids(data["userId"], "userId")
         items_h = _int_ids(data["itemId"], "itemId")
-        users, items = torch.as_tensor(users_h).to(dev), torch.as_tensor(items_h).to(dev)
-        ratings = torch.as_tensor(np.asarray(data["average_review_rating"], dtype=np.float32)).to(dev)
-        # ingest on the device (§8(f) row 1): dense codes + CSR (users) / CSC (items)
-        rng = (lambda a: (int(a.min()), int(a.max())) if a.size else None)
-        user_ids_t, urow = _hrec.encode_ids(users, rng(users_h))
-        item_ids_t, irow = _hrec.encode_ids(items, rng(items_h))
-        user_ids, item_ids = user_ids_t.cpu().numpy(), item_ids_t.cpu().numpy()
+        ratings_h = np.asarray(data["average_review_rating"], dtype=np.float32)
         k = int(self.rank)
-        n_u, n_i = len(user_ids), len(item_ids)
-        csr = build_csr(urow, irow, ratings, n_u, n_i)
-        csc = build_csr(irow, urow, ratings, n_i, n_u)
-        del urow, irow, ratings, users, items
         world, rank, group = process_group()
+        track = dev.type == "cuda"
+        if track:  # the ingest's peak device memory (tests: W = 2 holds about half of W = 1)
+            torch.cuda.synchronize(dev)
+            base = torch.cuda.memory_allocated(dev)
+            torch.cuda.reset_peak_memory_stats(dev)
         if world > 1:
-            # nnz-balanced contiguous row shards (users in
-            # CHUNKS per rank: each chunk's all-gather overlaps the next
-            # chunk's sweep), this rank's parts cut out of the whole CSR/CSC
-            ulay = RowLayout.balanced((csr.indptr[1:] - csr.indptr[:-1]).cpu().numpy(), world, self.CHUNKS)
-            ilay = RowLayout.balanced((csc.indptr[1:] - csc.indptr[:-1]).cpu().numpy(), world, 1)
-            csr, csc = shard_for_layout(csr, ulay, rank), shard_for_layout(csc, ilay, rank)
+            # this rank's slice of the frame only; ids encoded
+            # over the whole frame, this rank's nnz-balanced row parts built
+            # from the ratings exchanged to it (src/als_ingest.py)
+            check_same_frame(frame_fingerprint(users_h, items_h, ratings_h), dev, group)
+            user_ids, item_ids, csr, csc, ulay, ilay = sharded_ingest(users_h, items_h, ratings_h, world, rank, group,
+                                                                      self.CHUNKS, dev)
+            n_u, n_i = len(user_ids), len(item_ids)
+        else:
+            users, items = torch.as_tensor(users_h).to(dev), torch.as_tensor(items_h).to(dev)
+            ratings = torch.as_tensor(ratings_h).to(dev)
+            # ingest on the device (§8(f) row 1): dense codes + CSR (users) / CSC (items)
+            rng = (lambda a: (int(a.min()), int(a.max())) if a.size else None)
+            user_ids_t, urow = _hrec.encode_ids(users, rng(users_h))
+            item_ids_t, irow = _hrec.encode_ids(items, rng(items_h))
+            user_ids, item_ids = user_ids_t.cpu().numpy(), item_ids_t.cpu().numpy()
+            n_u, n_i = len(user_ids), len(item_ids)
+            csr = build_csr(urow, irow, ratings, n_u, n_i)
+            csc = build_csr(irow, urow, ratings, n_i, n_u)
+            del urow, irow, ratings, users, items, user_ids_t, item_ids_t
+        if track:
+            torch.cuda.synchronize(dev)
+            self.ingest_peak_bytes = int(torch.cuda.max_memory_allocated(dev) - base)
+        if world > 1:
             eng = DeviceALS(n_u, n_i, k, float(self.reg_param), csr, csc, world=world, rank=rank, group=group,
                             chunks=self.CHUNKS, item_chunks=1, user_layout=ulay, item_layout=ilay)
         else:

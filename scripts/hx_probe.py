@@ -69,7 +69,8 @@ def analyze(pr, hu, uvec, wins=False, k=5):
     hx = pr.last_exact
     B, N, dk = hx.B, hx.N, hx.dk
     G = -(-N // 32)
-    off = -(-(2 * B * dk * 4) // 256) * 256
+    r256 = lambda n: -(-n // 256) * 256  # noqa: E731  (hx_layout: uop, uf, uok, then the records)
+    off = r256(2 * B * 2 * dk * 2) + r256(2 * B * dk * 4) + r256(B * 4)
     st = hx.ws[off: off + B * G * 16].view(torch.float32).view(B, G, 4).double().cpu().numpy()
     a_mm, t_mm = hx.minmax()
     a_mm, t_mm = a_mm.double().cpu().numpy(), t_mm.double().cpu().numpy()
@@ -122,6 +123,9 @@ def main():
         r["pruned_graph_ms"] = ev_ms(lambda: cp(), args.reps)
         cm = CapturedRecommend(mt, hu, uvec, wins, 5)
         r["materialised_graph_ms"] = ev_ms(lambda: cm(), args.reps)
+        cp()
+        n_ext, n_top, every = pr.last_exact.counts()
+        r["after_graph"] = {"every": every, "groups_topk_max": int(n_top.max())}
         out["als_wins" if wins else "tt_wins"] = r
         print(json.dumps({("als_wins" if wins else "tt_wins"): r}), flush=True)
     hx = pr.last_exact

@@ -451,3 +451,116 @@ def test_sharded_dot_topk_matches_single(world):
     for _, (gi, gv) in res:
         np.testing.assert_array_equal(gi, ref_i)
         np.testing.assert_array_equal(gv, ref_v)
+
+
+# ------------------------------------------- sharded ingest (ALSModel.train, W > 1)
+class _NumpyIngestOps:
+    """numpy stand-ins for hrec_encode_ids / hrec_coo_to_csr (numpy.unique;
+    a stable sort by row): the device kernels' parity is pinned by the gpu
+    tests, these pin the orchestration."""
+
+    @staticmethod
+    def encode_ids(ids, id_range):
+        u, inv = np.unique(ids.numpy(), return_inverse=True)
+        return torch.from_numpy(u.astype(np.int64)), torch.from_numpy(inv.astype(np.int32).reshape(-1))
+
+    @staticmethod
+    def coo_to_csr(rows, cols, vals, n_rows):
+        r = rows.numpy()
+        order = np.argsort(r, kind="stable")
+        indptr = np.zeros(n_rows + 1, np.int64)
+        indptr[1:] = np.cumsum(np.bincount(r, minlength=n_rows))
+        return (torch.from_numpy(indptr), torch.from_numpy(cols.numpy()[order].copy()),
+                torch.from_numpy(vals.numpy()[order].copy()))
+
+
+def _ingest_frame():
+    """Skewed degrees, duplicates, non-contiguous raw ids (some only in one
+    rank's slice), negative ids."""
+    rng = np.random.default_rng(11)
+    n_u, n_i, nnz = 700, 300, 9001
+    pu = 1 / (np.arange(n_u) + 1.0) ** 0.7
+    pi = 1 / (np.arange(n_i) + 1.0) ** 0.7
+    u = rng.choice(n_u, nnz, p=pu / pu.sum()) * 5 - 1000
+    i = rng.choice(n_i, nnz, p=pi / pi.sum()) * 3 + 7
+    r = rng.integers(0, 19, nnz).astype(np.float32) * 0.25
+    return u.astype(np.int64), i.astype(np.int64), r
+
+
+def _ingest_worker(rank, world, port, q, chunks, tamper):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.als_ingest import check_same_frame, frame_fingerprint, sharded_ingest
+
+        u, i, r = _ingest_frame()
+        if tamper and rank == world - 1:
+            r = r.copy()
+            r[17] += 1.0
+        try:
+            check_same_frame(frame_fingerprint(u, i, r), torch.device("cpu"), dist.group.WORLD)
+        except ValueError as e:
+            q.put((rank, "refused: " + str(e)))
+            return
+        uid, iid, csr, csc, ulay, ilay = sharded_ingest(u, i, r, world, rank, dist.group.WORLD, chunks,
+                                                        torch.device("cpu"), ops=_NumpyIngestOps)
+        q.put((rank, (uid, iid, ulay.bounds, ilay.bounds,
+                      [(c.indptr.numpy(), c.indices.numpy(), c.values.numpy(), c.row_begin, c.n_rows, c.n_cols)
+                       for c in (csr, csc)])))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_ingest(world, chunks, tamper=False):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ingest_worker, args=(r, world, port, q, chunks, tamper)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=90) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 4), (3, 1), (3, 4)])
+def test_sharded_ingest_matches_whole_build(world, chunks):
+    """each rank uploads its 1/W slice of the frame, encodes
+    ids globally (range all-reduce + all-gathered distinct ids), balances
+    rows on the all-reduced degrees and receives its rows' ratings by
+    all_to_all — its CSR / CSC parts equal the whole matrix's cut by
+    shard_for_layout (ids, layouts, indptr, in-row order, values) exactly."""
+    from src.als_engine import RowLayout
+
+    res = _run_ingest(world, chunks)
+    u, i, r = _ingest_frame()
+    uid, cu = np.unique(u, return_inverse=True)
+    iid, ci = np.unique(i, return_inverse=True)
+    ops = _NumpyIngestOps
+    whole = [ops.coo_to_csr(torch.from_numpy(cu.astype(np.int32)), torch.from_numpy(ci.astype(np.int32)),
+                            torch.from_numpy(r), len(uid)),
+             ops.coo_to_csr(torch.from_numpy(ci.astype(np.int32)), torch.from_numpy(cu.astype(np.int32)),
+                            torch.from_numpy(r), len(iid))]
+    lays = [RowLayout.balanced(np.diff(whole[0][0].numpy()), world, chunks),
+            RowLayout.balanced(np.diff(whole[1][0].numpy()), world, 1)]
+    for rank in range(world):
+        g_uid, g_iid, ub, ib, sides = res[rank]
+        np.testing.assert_array_equal(g_uid, uid)
+        np.testing.assert_array_equal(g_iid, iid)
+        assert ub == lays[0].bounds and ib == lays[1].bounds
+        for s, (ip, ix, v, row0, n_rows, n_cols) in enumerate(sides):
+            want = _layout_shard(tuple(t.numpy() for t in whole[s]), lays[s], rank, (len(iid), len(uid))[s])
+            np.testing.assert_array_equal(ip, want.indptr.numpy())
+            np.testing.assert_array_equal(ix, want.indices.numpy())
+            np.testing.assert_array_equal(v, want.values.numpy())
+            assert (row0, n_rows, n_cols) == (want.row_begin, want.n_rows, want.n_cols)
+
+
+def test_sharded_ingest_refuses_different_frames():
+    """the ranks' frames are fingerprinted (length, id and rating
+    bit sums) and compared by one all-reduce before any slice is taken."""
+    res = _run_ingest(2, 1, tamper=True)
+    for rank in range(2):
+        assert isinstance(res[rank], str) and res[rank].startswith("refused"), res[rank]

@@ -160,7 +160,7 @@ def _als_worker(rank, world, port, q):
         m = ALSModel(rank=24, max_iter=4, reg_param=0.1, seed=9)
         assert m.train(_als_frame()) is True
         s = m.predict_for_user(int(m.model.user_ids[5]), [int(x) for x in m.model.item_ids[:50]])
-        q.put((rank, (m.model.U.cpu().numpy(), m.model.V.cpu().numpy(), [v for _, v in s])))
+        q.put((rank, (m.model.U.cpu().numpy(), m.model.V.cpu().numpy(), [v for _, v in s], m.ingest_peak_bytes)))
         dist.barrier()
     except BaseException as e:
         q.put((rank, repr(e)))
@@ -170,12 +170,14 @@ def _als_worker(rank, world, port, q):
 
 
 def test_als_model_train_two_ranks_matches_one(device):
-    """ALSModel.train under an initialised 2-rank world (the
-    reference's caller under torchrun, src/als_model.py:43-66) shards users
-    and items (nnz-balanced parts, 4 user chunks per rank, chunked
-    all-gathers through the HIP half-sweeps) and every rank ends with the
-    factors of the one-rank fit, bit for bit; predict_for_user serves the
-    same scores on every rank."""
+    """ALSModel.train under an initialised 2-rank world
+    (the reference's caller under torchrun, src/als_model.py:43-66) ingests
+    its slice of the frame only (src/als_ingest.py: global id encoding, rows
+    exchanged to their owners), shards users and items (nnz-balanced parts,
+    4 user chunks per rank, chunked all-gathers through the HIP
+    half-sweeps) and every rank ends with the factors of the one-rank fit,
+    bit for bit; predict_for_user serves the same scores on every rank; the
+    ingest's device peak per rank is at most 0.6 of the one-rank ingest's."""
     import torch.multiprocessing as mp
 
     from src.als_model import ALSModel
@@ -183,6 +185,7 @@ def test_als_model_train_two_ranks_matches_one(device):
     m = ALSModel(rank=24, max_iter=4, reg_param=0.1, seed=9)
     assert m.train(_als_frame()) is True
     U1, V1 = m.model.U.cpu().numpy(), m.model.V.cpu().numpy()
+    peak1 = m.ingest_peak_bytes
     s1 = [v for _, v in m.predict_for_user(int(m.model.user_ids[5]), [int(x) for x in m.model.item_ids[:50]])]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -198,7 +201,10 @@ def test_als_model_train_two_ranks_matches_one(device):
     for r in range(2):
         assert not isinstance(res[r], str), res[r]
         assert procs[r].exitcode == 0
-        U, V, sc = res[r]
+        U, V, sc, peak = res[r]
         np.testing.assert_array_equal(U, U1)
         np.testing.assert_array_equal(V, V1)
         assert sc == s1
+        # the sharded ingest holds about half the device memory
+        # of the one-rank ingest (its slice, exchange buffers and own rows)
+        assert peak <= 0.6 * peak1, (r, peak, peak1)
