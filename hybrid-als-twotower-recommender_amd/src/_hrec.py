@@ -85,6 +85,9 @@ _SIGNATURES.update({
     "hrec_tt_user_forward": (_c_i32, [_PP, _vp, _c_i64, _vp, _vp]),
     "hrec_tt_score": (_c_i32, [_vp, _c_i32, _vp, _c_i64, _c_i32, _vp, _vp]),
     "hrec_tt_pair_score": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _vp, _vp]),
+    "hrec_tt_item_inputs_workspace_bytes": (_c_sz, [_c_i64]),
+    "hrec_tt_item_inputs": (_c_i32, [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_tt_train_workspace_bytes": (_c_sz, [_c_i32, _c_i64]),
     "hrec_tt_grad_len": (_c_sz, [_c_i32]),
     "hrec_tt_forward_backward": (_c_i32, [_PP, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp,
@@ -900,6 +903,36 @@ def tt_pair_score(user_vec, item_vec):
         _dev(user_vec, torch.float32, "user_vec"), _dev(item_vec, torch.float32, "item_vec"), n, d,
         _dev(out, torch.float32, "out"), _stream()))
     return out
+
+
+TT_INPUTS_IDS, TT_INPUTS_INF, TT_INPUTS_DUP = 1, 2, 4
+
+
+def tt_item_inputs(item, man, cat, price, rating, tables, scale, min_, ws=None):
+    """hrec_tt_item_inputs: device int64 id columns + f64 numeric columns ->
+    (item, man, cat int32 [n], numeric f32 [n, 2], flags int32 [1] device).
+    tables = (n_item, n_man, n_cat); scale / min_: the scaler's 2 doubles.
+    flags != 0: an id outside its table (or >= 2^24), an infinite numeric
+    value or a repeated item id — the outputs are then not the model's
+    inputs. ws: a reusable uint8 workspace of
+    hrec_tt_item_inputs_workspace_bytes(n_item) bytes."""
+    n = item.numel()
+    dev = item.device
+    need = int(lib().hrec_tt_item_inputs_workspace_bytes(int(tables[0])))
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(3)]
+    num = torch.empty((n, 2), dtype=torch.float32, device=dev)
+    flags = torch.empty(1, dtype=torch.int32, device=dev)
+    sc = (ctypes.c_double * 2)(float(scale[0]), float(scale[1]))
+    mn = (ctypes.c_double * 2)(float(min_[0]), float(min_[1]))
+    _check("hrec_tt_item_inputs", lib().hrec_tt_item_inputs(
+        _dev(item, torch.int64, "item"), _dev(man, torch.int64, "man"), _dev(cat, torch.int64, "cat"),
+        _dev(price, torch.float64, "price"), _dev(rating, torch.float64, "rating"), n, int(tables[0]),
+        int(tables[1]), int(tables[2]), ctypes.cast(sc, _vp), ctypes.cast(mn, _vp), _vp(outs[0].data_ptr()),
+        _vp(outs[1].data_ptr()), _vp(outs[2].data_ptr()), _vp(num.data_ptr()), _vp(flags.data_ptr()),
+        _vp(ws.data_ptr()), ws.numel(), _stream()))
+    return outs[0], outs[1], outs[2], num, flags, ws
 
 
 def tt_grad_len(d):

@@ -104,6 +104,7 @@ class HybridRecommendationSystem:
         self.als_f1_score = 0.0
         self.twotower_f1_score = 0.0
         self.models_loaded = False
+        self._flags_bad = False
 
     def load_models(self, als_model_path, twotower_model_path):
         try:
@@ -176,10 +177,29 @@ class HybridRecommendationSystem:
             # below only if the list path runs); other model objects are used
             # through their predict_for_user as the reference does
             als_preds = _scored(self.als_model, ALSModel, user_id, all_items)
-            tt_preds = _scored(self.twotower_model, TwoTowerModel, user_id, all_items)
+            tt_fast = None
+            if (not save_predictions and not actual_ratings
+                    and type(self.twotower_model).predict_for_user is TwoTowerModel.predict_for_user):
+                # the candidate frame's item inputs built on the device (ids,
+                # scaler, uniqueness checked there; read back with the top-k)
+                tt_fast = self.twotower_model._predict_device_fast(user_id, all_items)
+            if tt_fast is not None:
+                self._flags_bad = False
+                try:
+                    top = self._top_on_device(als_preds, tt_fast[:2], top_k, flags=tt_fast[2])
+                except Exception:
+                    top, self._flags_bad = None, True
+                if top is not None:
+                    return top
+                # ties or NaN scores: the list path on the same scores; bad
+                # inputs: the host path (raises where the reference raises)
+                tt_preds = tt_fast[:2] if not self._flags_bad else _scored(self.twotower_model, TwoTowerModel,
+                                                                           user_id, all_items)
+            else:
+                tt_preds = _scored(self.twotower_model, TwoTowerModel, user_id, all_items)
             if actual_ratings:
                 self.evaluate_individual_models(user_id, actual_ratings, all_items)
-            if not save_predictions:
+            if not save_predictions and tt_fast is None:
                 try:
                     top = self._top_on_device(als_preds, tt_preds, top_k)
                 except Exception:  # the list path below meets the same error and reports it as the reference does
@@ -207,7 +227,7 @@ class HybridRecommendationSystem:
             print(f"Error generating recommendations: {str(e)}")
             return []
 
-    def _top_on_device(self, als_side, tt_side, top_k):
+    def _top_on_device(self, als_side, tt_side, top_k, flags=None):
         """get_hybrid_recommendations without the Python lists: when both
         sides cover the same unique candidate ids (or the ALS side is empty,
         the reference's DataFrame wiring, SURVEY D9) the union is those ids;
@@ -217,13 +237,18 @@ class HybridRecommendationSystem:
         the items in, so it is returned; otherwise (ties, NaN/inf scores,
         duplicate or mismatched ids) None sends the call down the list path,
         which reproduces the set order exactly. The scalers are fitted as
-        fit_transform leaves them either way (min/max are order-free)."""
+        fit_transform leaves them either way (min/max are order-free).
+        flags: the device input flags of TwoTowerModel._predict_device_fast
+        (its device check replaces the host uniqueness pass); read back with
+        the top-k; non-zero sets self._flags_bad and returns None."""
         if not isinstance(tt_side, tuple) or not isinstance(top_k, (int, np.integer)) or top_k < 0:
             return None
         frame, t = tt_side
         col = frame["itemId"]
         vals = col.values
-        if not isinstance(vals, np.ndarray) or vals.dtype.kind not in "iu" or not _unique(vals, col):
+        if not isinstance(vals, np.ndarray) or vals.dtype.kind not in "iu":
+            return None
+        if flags is None and not _unique(vals, col):
             return None
         n = t.numel()
         if isinstance(als_side, tuple):
@@ -243,9 +268,13 @@ class HybridRecommendationSystem:
         idx, sc, _ = _hrec.fuse_topk(a, t, self.als_f1_score > self.twotower_f1_score, k1, want_fused=False,
                                      minmax=mm)
         bad = (~torch.isfinite(a).all() | ~torch.isfinite(t).all()).double().view(1)
-        host = torch.cat([sc, idx.double(), mm, bad]).cpu().numpy()
+        parts = [sc, idx.double(), mm, bad] + ([flags.double()] if flags is not None else [])
+        host = torch.cat(parts).cpu().numpy()
         sc_h, idx_h, m = host[:k1], host[k1:2 * k1].astype(np.int64), host[2 * k1: 2 * k1 + 4]
-        if host[-1] != 0 or not np.all(sc_h[:-1] > sc_h[1:]):
+        if flags is not None and host[2 * k1 + 5] != 0:
+            self._flags_bad = True
+            return None
+        if host[2 * k1 + 4] != 0 or not np.all(sc_h[:-1] > sc_h[1:]):
             return None
         _set_fitted(self.als_scaler, m[0], m[1], n, np.float64)
         _set_fitted(self.twotower_scaler, m[2], m[3], n, np.float32)

@@ -82,6 +82,7 @@ class TwoTowerModel:
         self.scaler = MinMaxScaler()
         self.is_trained = False
         self.seed = seed
+        self._inputs_ws = None  # hrec_tt_item_inputs' presence bitmap, reused across calls
 
     def _build_item_tower(self):
         """(:38-66) -> (inputs, item_vec) as the reference returns them: the
@@ -229,6 +230,53 @@ class TwoTowerModel:
         if len(item_features) == 0:
             return []
         return item_features, self._score_device(inputs)
+
+    _FAST_ID_COLS = ("itemId", "manufacturer_id", "category_id")
+    _FAST_NUM_COLS = ("price", "average_review_rating")
+
+    def _predict_device_fast(self, user_id, item_features):
+        """_predict_device for a plain candidate frame with the item-side
+        input work on the device (hrec_tt_item_inputs: id casts and range
+        checks, the MinMaxScaler transform, the candidates' uniqueness):
+        (item_features, f32 device scores [n], device flags int32 [1]), or
+        None when the frame or scaler is outside that path. Non-zero flags
+        mean the inputs are NOT the model's (an id out of range, an infinite
+        value, a repeated item id): the caller redoes the call through
+        _predict_device, which raises where predict_for_user raises. The user
+        id is checked here, on the host, first — as _device_inputs does."""
+        sc = self.scaler
+        if (self.model is None or not isinstance(item_features, pd.DataFrame) or type(sc) is not MinMaxScaler
+                or sc.clip or not hasattr(sc, "scale_") or getattr(sc, "n_features_in_", None) != 2):
+            return None
+        names = getattr(sc, "feature_names_in_", None)
+        if names is not None and list(names) != list(self._FAST_NUM_COLS):
+            return None
+        if len(item_features) == 0 or not item_features.columns.is_unique:
+            return None
+        cols = []
+        for c in self._FAST_ID_COLS + self._FAST_NUM_COLS:
+            if c not in item_features.columns:
+                return None
+            a = item_features[c].to_numpy()
+            if not isinstance(a, np.ndarray) or a.ndim != 1:
+                return None
+            if c in self._FAST_ID_COLS:
+                if a.dtype.kind not in "iu" or a.dtype == np.uint64:
+                    return None
+                a = a.astype(np.int64, copy=False)
+            else:  # to_numpy(dtype=float64) of _minmax_transform: floats as they are, ints converted
+                if not (a.dtype == np.float64 or (a.dtype.kind in "iu" and a.dtype != np.bool_)):
+                    return None
+                a = a.astype(np.float64, copy=False)
+            cols.append(np.ascontiguousarray(a))
+        dev, sz = self.model.device, self.model.sizes
+        u = torch.as_tensor(_ids(np.full(1, user_id), sz["user_emb"], "user_in"), device=dev)
+        t = [torch.from_numpy(a).to(dev) for a in cols]
+        item, man, cat, num, flags, self._inputs_ws = _hrec.tt_item_inputs(
+            *t, (sz["item_emb"], sz["man_emb"], sz["cat_emb"]), sc.scale_, sc.min_, self._inputs_ws)
+        uvec = self.model.user_vectors(u)
+        ivec = self.model.item_vectors(item, man, cat, num)
+        return item_features, _hrec.tt_score(uvec, ivec).reshape(-1), flags
 
     # --------------------------------------------------------- persistence
     def save_model(self, model_path="models/twotower.keras"):

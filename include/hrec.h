@@ -297,6 +297,25 @@ int hrec_tt_user_forward(const hrec_tt_params* params, const int32_t* user, int6
 int hrec_tt_score(const float* user_vec, int n_users, const float* item_vec,
                   int64_t n_items, int d, float* out, void* stream);
 
+/* The item tower's inputs of one predict_for_user call from the candidate
+ * frame's raw columns (src/two_tower_model.py:136-146): item / manufacturer /
+ * category ids (int64) -> int32 (each in [0, its table) and below 2^24, where
+ * Keras' float32 Input round trip is the identity), numeric [n,2] f32 =
+ * (price, rating) * scale + min in f64 (MinMaxScaler.transform), rounded once.
+ * scale / min_: HOST arrays of 2 doubles (the fitted scaler's scale_ / min_).
+ * *flags (device int32, written by the call): bit 1 an id outside those
+ * bounds, bit 2 an infinite numeric input, bit 4 a repeated item id — the
+ * outputs are then unusable and the caller takes the host path (which raises
+ * the reference's error where it raises). Replaces the host-side _ids casts,
+ * scaler.transform and the candidate-uniqueness pass of the hybrid's array
+ * path (src/hybrid_system.py:95-116). */
+size_t hrec_tt_item_inputs_workspace_bytes(int64_t n_item_table);
+int hrec_tt_item_inputs(const int64_t* item, const int64_t* manufacturer, const int64_t* category,
+                        const double* price, const double* rating, int64_t n, int64_t n_item_table,
+                        int64_t n_man_table, int64_t n_cat_table, const double* scale, const double* min_,
+                        int32_t* item_out, int32_t* man_out, int32_t* cat_out, float* numeric_out,
+                        int32_t* flags, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Row-wise dot: out[r] = <user_vec[r], item_vec[r]> (n rows of d). */
 int hrec_tt_pair_score(const float* user_vec, const float* item_vec, int64_t n, int d,
                        float* out, void* stream);

@@ -74,4 +74,8 @@ timed("ALS fromiter", lambda: np.fromiter(ids, np.int64, len(ids)))
 timed("ALS _predict_device", lambda: als._predict_device(3, both))
 timed("TT _minmax_transform", lambda: _minmax_transform(tt.scaler, items, ["price", "average_review_rating"]))
 timed("TT _predict_device", lambda: tt._predict_device(3, items))
+timed("TT _predict_device_fast", lambda: tt._predict_device_fast(3, items))
+cols = [torch.from_numpy(items[c].to_numpy()) for c in ("itemId", "manufacturer_id", "category_id", "price",
+                                                         "average_review_rating")]
+timed("TT H2D of the 5 columns", lambda: [c.to(dev) for c in cols])
 timed("_top_on_device", lambda: h._top_on_device(a_side, t_side, 5))

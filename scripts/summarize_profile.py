@@ -145,10 +145,19 @@ def main(base):
             out[k] = e
         return out
 
-    c5 = per_kernel(["hp_user_ops_kernel", "hyb_scores_kernel<256, 4, 1>", "hyb_mm_reduce_kernel",
-                     "hp_bound_kernel<256>", "dot_res_kernel<true, 256, true, 2>", "hp_cand_topk_kernel<256>"],
-                    "prof_fetch_c5", "prof_write_c5")
-    tot = sum(e.get("hbm_bytes_avg_per_launch_corrected", 0.0) for e in c5.values())
+    # every instantiation of the batch's kernels (matched by base name: the
+    # r04 keys named one template each and missed hyb_scores_kernel<256, 4, 2>
+    # and hp_bound_kernel<256, true>); batch bytes = sum over kernels of the
+    # average bytes per launch x launches per batch (hp_user_ops_kernel runs
+    # once per batch)
+    bases = ["hp_user_ops_kernel", "hyb_scores_kernel<", "hyb_mm_reduce_kernel", "hp_bound_kernel<",
+             "dot_res_kernel<true, 256", "hp_cand_topk_kernel<"]
+    names = sorted({r["Kernel_Name"].split("(")[0].replace("void ", "").replace("hrec::", "") for r in trace
+                    if any(b in r["Kernel_Name"] for b in bases)})
+    c5 = per_kernel(names, "prof_fetch_c5", "prof_write_c5")
+    n_batches = max(next((e["launches"] for k, e in c5.items() if k.startswith("hp_user_ops_kernel")), 1), 1)
+    tot = sum(e.get("hbm_bytes_avg_per_launch_corrected", 0.0) * e["launches"] for e in c5.values()) / n_batches
+    c5["batches_in_profile"] = n_batches
     c5["batch_hbm_bytes_corrected"] = tot
     c5["no_store_bytes"] = 102.4e6
     c5["traffic_over_no_store"] = tot / 102.4e6

@@ -696,7 +696,11 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
     (predict_for_user lists + _union + fuse_device) returns, and leaves the
     scalers fitted the same: frame wiring (ALS -> []), ids on both sides,
     cold-start rows (NaN -> fallback), duplicate ids, ties, top_k >= n and
-    top_k = 0, both F1 orders."""
+    top_k = 0, both F1 orders. The array path builds the two-tower item
+    inputs on the device (hrec_tt_item_inputs); the list runs build them on
+    the host (_predict_device), so the cases with ids outside the table,
+    infinite / NaN prices, an int rating column and a float32 price column
+    pin the device inputs and their fallbacks to the host path's outcome."""
     from src.als_model import ALSModel
     from src.hybrid_system import HybridRecommendationSystem
     from src.two_tower_model import TwoTowerModel
@@ -718,12 +722,19 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
     als_half = ALSModel(rank=8, max_iter=2, seed=3)
     assert als_half.train(df.head(60))
     assert len(set(items["itemId"]) - set(df["itemId"].head(60))) > 0
-    cases = [("frame", items), ("ids", _IdsFrame(items)), ("dup", _IdsFrame(dup)), ("frame_dup", dup)]
+    bad_id, inf, nan, int_r, f32_p = (items.copy() for _ in range(5))
+    bad_id.loc[3, "itemId"] = 10 ** 6        # outside the item table: IndexError -> []
+    inf.loc[2, "price"] = np.inf              # sklearn's finiteness error -> []
+    nan.loc[4, "price"] = np.nan              # NaN scores -> the list path
+    int_r["average_review_rating"] = int_r["average_review_rating"].round().astype(np.int64)
+    f32_p["price"] = f32_p["price"].astype(np.float32)  # outside the device input path
+    cases = [("frame", items), ("ids", _IdsFrame(items)), ("dup", _IdsFrame(dup)), ("frame_dup", dup),
+             ("bad_id", bad_id), ("inf", inf), ("nan", nan), ("int_rating", int_r), ("f32_price", f32_p)]
     calls = {"fast": 0}
     orig = HybridRecommendationSystem._top_on_device
 
-    def counting(self, *a):
-        r = orig(self, *a)
+    def counting(self, *a, **kw):
+        r = orig(self, *a, **kw)
         calls["fast"] += r is not None
         return r
 
@@ -733,7 +744,9 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
         h.als_f1_score, h.twotower_f1_score = f1
         with monkeypatch.context() as m:
             m.setattr(HybridRecommendationSystem, "_top_on_device",
-                      (lambda self, *a: None) if list_path else counting)
+                      (lambda self, *a, **kw: None) if list_path else counting)
+            if list_path:  # the host-built two-tower inputs (_predict_device) as well
+                m.setattr(TwoTowerModel, "_predict_device_fast", lambda self, *a: None)
             top = h.get_hybrid_recommendations(uid, cand, top_k=k)
         return top, h
 

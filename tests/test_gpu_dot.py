@@ -102,6 +102,36 @@ def test_few_user_scores_and_topk(device, dtype, B, d):
         np.testing.assert_array_equal(gv.cpu().numpy(), ev)
 
 
+def test_dot_topk_batch_of_four_vs_five(device):
+    """f32 batches of 1-4 users take the GEMV (another summation
+    order than the matrix-core tiles of >= 5 users; include/hrec.h states the
+    batch-size dependence). Away from ties the same users get the same top-k
+    ids from a batch of 4 and from a batch of 5, and scores that agree within
+    the f32 dot bound (1e-6 sum |u_c v_c|); near ties only the bound holds."""
+    h = _h()
+    N, d, k = 50_000, 64, 10
+    U = _vecs(5, d, 71)
+    V = _vecs(N, d, 72)
+    Ud = h.dot_operand(torch.from_numpy(U).to(device), torch.float32)
+    Vd = h.dot_operand(torch.from_numpy(V).to(device), torch.float32)
+    i4, v4 = h.dot_topk(Ud[:4].contiguous(), Vd, k)
+    i5, v5 = h.dot_topk(Ud, Vd, k)
+    i4, v4, i5, v5 = i4.cpu().numpy(), v4.cpu().numpy(), i5.cpu().numpy()[:4], v5.cpu().numpy()[:4]
+    ref = U[:4].astype(np.float64) @ V.astype(np.float64).T
+    bound = 1e-6 * (np.abs(U[:4]).astype(np.float64) @ np.abs(V).astype(np.float64).T) + 1e-30
+    checked = 0
+    for b in range(4):
+        order = np.argsort(-ref[b], kind="stable")[: k + 1]
+        gaps = -np.diff(ref[b][order])
+        if np.all(gaps > 2 * bound[b][order[:-1]]):  # no near-tie in the top k + 1
+            np.testing.assert_array_equal(i4[b], i5[b])
+            np.testing.assert_array_equal(i4[b], order[:k])
+            checked += 1
+        rb = bound[b][i5[b]]
+        assert np.all(np.abs(v4[b].astype(np.float64) - v5[b]) <= 2 * rb)
+    assert checked >= 3
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,N,d,k", [(7, 5000, 64, 5), (130, 40000, 128, 5), (3, 100003, 64, 10),
                                      (1, 20000, 256, 1), (200, 17000, 32, 64), (2, 3, 64, 5)])
