@@ -141,6 +141,52 @@ def hybrid_stages(rec, hu, uvec, top_k, reps, stream):
     roofline. Same calls recommend() makes, in the same order."""
     o = rec.ops
     B, N = int(hu.shape[0]), rec.n_local
+    if (rec.precision == "exact" and getattr(rec, "pruned_exact", False) and top_k <= _hrec.EXACT_MAX_K
+            and B >= 8):
+        # exact path without score matrices (csrc/hybrid_exact.hip): phase 1
+        # (split-bf16 bound GEMMs of both models, no stores) + the exact
+        # extremes; then the group bounds, seeds and the live groups rescored
+        # by the exact chains, stable top-k
+        hx = o.hybrid_exact(rec.U, hu, uvec, rec.exact_items, top_k)
+        a_mm, t_mm = hx.minmax()
+        d, dk = int(rec.iv.shape[1]), hx.dk
+        G = -(-N // 32)
+        op_b = 2.0 * 2 * 2.0 * dk * N  # both models' split operands (hi + lo bf16) read once
+        st = [("hybrid_exact_minmax (split-bf16 bound GEMMs of both models, dk %d, no score stores; exact extremes "
+               "of the candidate groups)" % dk, hx.minmax,
+               dict(bound="hbm", work=op_b, peak=HBM_PEAK_GBS, unit="GB/s", mfma_flops=2 * 3 * 2.0 * dk * B * N))]
+        hx.topk(a_mm, t_mm, False, rec.offset)
+        n_ext, n_top, every = hx.counts()
+        live = float(n_top.double().sum())
+        # phase 2's bytes: every user's group records + the f32 item rows of
+        # both models of its live groups (the exact chains' inputs)
+        p2_b = 16.0 * B * G + live * 32 * 4.0 * (rec.k + d)
+        st.append(("hybrid_exact_topk (group bounds, seeds, live groups rescored by the exact chains, stable "
+                   "top-k)", lambda: hx.topk(a_mm, t_mm, False, rec.offset),
+                   dict(bound="hbm", work=p2_b, peak=HBM_PEAK_GBS, unit="GB/s")))
+        out = []
+        for name, fn, rf in st:
+            fn()
+            ms = ev_time(fn, reps, stream)
+            r = roofline(rf["bound"], rf["work"], ms, rf["peak"], rf["unit"], name)
+            if "mfma_flops" in rf:
+                tf = rf["mfma_flops"] / (ms * 1e-3) / 1e12
+                r["mfma_view"] = {"achieved": tf, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": tf / BF16_MFMA_PEAK_TFLOPS}
+            out.append(r)
+        local_ms = ev_time(lambda: hx.local(False, rec.offset), reps, stream)
+        n_ext, n_top, every = hx.counts()
+        tot = sum(r["avg_launch_ms"] for r in out)
+        item_b = 4.0 * (rec.k + d) * N  # the reference's inputs: both models' f32 item rows, once
+        dom = max(out, key=lambda r: r["avg_launch_ms"])
+        return dict(dom, stages=out, one_shard_call_ms=local_ms, every_group_rescored=bool(every),
+                    groups_per_user={"total": G, "extremes_mean": float(n_ext.double().mean()),
+                                     "topk_mean": float(n_top.double().mean()), "topk_max": int(n_top.max())},
+                    batch_view={"ms": tot, "algorithmic_bytes": item_b,
+                                "note": "both models' f32 item rows once (the materialised path's inputs) / both "
+                                        "phases' time",
+                                "achieved": item_b / (tot * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": item_b / (tot * 1e-3) / 1e9 / HBM_PEAK_GBS})
     if rec.precision == "exact":
         als = o.als_scores(rec.U, hu, rec.Vt, N, rec.k)
         tt = o.tt_scores(uvec, rec.iv)
@@ -776,7 +822,11 @@ def main():
                   "eager_ms_per_batch": (hs_eager if hs_eager else hs_g) * 1e3,
                   "graph_ms_per_batch": hs_g * 1e3 if hs_eager else None, "launch": how,
                   "top_k": 5, "d": d, "items_sharded_over": world,
-                  "steps": "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5"}
+                  "steps": ("exact pruned hybrid (hrec_hybrid_exact_*: split-bf16 bound GEMMs of both models, "
+                            "no score matrices; the candidate groups rescored by the JVM-exact ALS chain and the f32 "
+                            "MFMA Dot; min-max fusion f64 + stable top-5, bit for bit the materialised path)"
+                            if getattr(rec, "pruned_exact", False) else
+                            "ALS JVM-exact f32 + two-tower f32 MFMA Dot + min-max fusion f64 + stable top-5")}
         if world == 1:
             hybrid["roofline"] = hybrid_stages(rec, hu, uvec, 5, 10, stream)
         if WANT_CPU(args, rank, world):

@@ -50,6 +50,9 @@
 #ifndef HREC_WIDE_WR_WIDE
 #define HREC_WIDE_WR_WIDE 32  // ratings per window at kp >= 192 (16: 641 ms, 32: 638 ms per rank-256 epoch) (multiple of 4; LDS: two windows of WR x (kp + 16) doubles)
 #endif
+#ifndef HREC_WIDE_LOOKAHEAD
+#define HREC_WIDE_LOOKAHEAD 0  // 1 = block row J + 1 factored beside J's trailing update (A/B)
+#endif
 #ifndef HREC_WIDE_CUT
 #define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
 #endif
@@ -391,10 +394,9 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
 
   WSTAMP(0);
   // ---------------------------------------------------------------- phase 2
-#pragma unroll 1
-  for (int J = 0; J < NT; ++J) {
+  // (a) owners of block row J -> panel rows 0..15
+  auto write_panel = [&](int J) {
     double* P = buf[J & 1];
-    // (a) owners of block row J -> panel rows 0..15
 #pragma unroll
     for (int s = 0; s < S::SLOTS; ++s) {
       if (pij[s] >= 0) {
@@ -405,10 +407,11 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         }
       }
     }
-    __syncthreads();
-    WSTAMP(1);
-    // (b) panel: wave w < n_act takes the diagonal block (lanes 0..15,
-    //     redundantly) and 48 columns beyond it (lanes 16..63)
+  };
+  // (b) panel: wave w < n_act takes the diagonal block (lanes 0..15,
+  //     redundantly) and 48 columns beyond it (lanes 16..63)
+  auto panel = [&](int J) {
+    double* P = buf[J & 1];
     const int rest = KP - 16 * (J + 1);
     const int n_act = rest > 0 ? (rest + 47) / 48 : 1;
     if (HREC_WIDE_CUT != 3 && w < n_act) {
@@ -471,10 +474,11 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
         }
       }
     }
-    __syncthreads();
-    WSTAMP(2);
-    // b_K -= U_JK^T w_J for every later column, one thread per column (the
-    // panel still holds U_J); runs beside the trailing MFMAs below
+  };
+  // b_K -= U_JK^T w_J for every later column, one thread per column (the
+  // panel still holds U_J)
+  auto rhs_upd = [&](int J) {
+    const double* P = buf[J & 1];
     if (tid < KP - 16 * (J + 1)) {
       const int cc = 16 * (J + 1) + tid;
       double part = 0.0;
@@ -482,56 +486,99 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       for (int q = 0; q < 16; ++q) part = fma(P[q * LD + cc], xsh[16 * J + q], part);
       bsh[cc] -= part;
     }
-    // (c) trailing update A_KM -= U_JK^T D_J U_JM; owners of row J take U_JK.
-    // Slot rows K grow with the slot index, so the tiles still to update
-    // (K > J) are a suffix of the slots: walk it from the end, reading the
-    // next slot's panel operands before this slot's four MFMAs.
-    if (HREC_WIDE_CUT != 4) {
-      const double* dj = dsh + 16 * J;
-      auto opnd = [&](int s, double (&ua)[4], double (&ub)[4]) {
-        const int q0 = pij[s] < 0 ? 0 : pij[s];
-        const int K = q0 & 255, M = q0 >> 8;
+  };
+  // (c) trailing update A_KM -= U_JK^T D_J U_JM of the tiles with kstop < K
+  // <= kmax. Slot rows K grow with the slot index, so they are a suffix of
+  // the slots (minus rows above kmax): walk it from the end, reading the next
+  // slot's panel operands before this slot's four MFMAs.
+  auto trail = [&](int J, int kstop, int kmax) {
+    if (HREC_WIDE_CUT == 4) return;
+    const double* P = buf[J & 1];
+    const double* dj = dsh + 16 * J;
+    auto opnd = [&](int s, double (&ua)[4], double (&ub)[4]) {
+      const int q0 = pij[s] < 0 ? 0 : pij[s];
+      const int K = q0 & 255, M = q0 >> 8;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int q = 4 * kk + sub;
-          ua[kk] = -P[q * LD + 16 * K + col] * dj[q];
-          ub[kk] = P[q * LD + 16 * M + col];
-        }
-      };
-      double ua[4], ub[4];
-      opnd(S::SLOTS - 1, ua, ub);
-#pragma unroll
-      for (int s = S::SLOTS - 1; s >= 0; --s) {
-        const int K = pij[s] & 255;
-        if (pij[s] >= 0 && K <= J) break;  // wave-uniform
-        double ca[4], cbv[4];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          ca[kk] = ua[kk];
-          cbv[kk] = ub[kk];
-        }
-        if (s > 0) opnd(s - 1, ua, ub);
-        if (pij[s] >= 0) {
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[kk], cbv[kk], acc[s], 0, 0, 0);
-        }
+      for (int kk = 0; kk < 4; ++kk) {
+        const int q = 4 * kk + sub;
+        ua[kk] = -P[q * LD + 16 * K + col] * dj[q];
+        ub[kk] = P[q * LD + 16 * M + col];
       }
+    };
+    double ua[4], ub[4];
+    opnd(S::SLOTS - 1, ua, ub);
 #pragma unroll
-      for (int s = 0; s < S::SLOTS; ++s) {
-        if (pij[s] >= 0 && (pij[s] & 255) == J) {
-          const int M = pij[s] >> 8;
-          if (M == J) {
+    for (int s = S::SLOTS - 1; s >= 0; --s) {
+      const int K = pij[s] & 255;
+      if (pij[s] >= 0 && K <= kstop) break;  // wave-uniform
+      double ca[4], cbv[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[s][r] = udg[(sub + 4 * r) * 17 + col];
-          } else {
+      for (int kk = 0; kk < 4; ++kk) {
+        ca[kk] = ua[kk];
+        cbv[kk] = ub[kk];
+      }
+      if (s > 0) opnd(s - 1, ua, ub);
+      if (pij[s] >= 0 && K <= kmax) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[s][r] = P[(sub + 4 * r) * LD + 16 * M + col];
-          }
+        for (int kk = 0; kk < 4; ++kk)
+          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[kk], cbv[kk], acc[s], 0, 0, 0);
+      }
+    }
+  };
+  // owners of row J take U_JK (the panel) / U_JJ (udg)
+  auto take_u = [&](int J) {
+    if (HREC_WIDE_CUT == 4) return;
+    const double* P = buf[J & 1];
+#pragma unroll
+    for (int s = 0; s < S::SLOTS; ++s) {
+      if (pij[s] >= 0 && (pij[s] & 255) == J) {
+        const int M = pij[s] >> 8;
+        if (M == J) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s][r] = udg[(sub + 4 * r) * 17 + col];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s][r] = P[(sub + 4 * r) * LD + 16 * M + col];
         }
       }
     }
+  };
+#if HREC_WIDE_LOOKAHEAD
+  // Lookahead: block row J + 1 is updated first and factored by the panel
+  // waves while the other waves apply J's update to the rows below it (the
+  // panel's latency chain beside their MFMAs). Every tile still receives
+  // its updates in the order J = 0, 1, ...: bit-identical to the plain order.
+  write_panel(0);
+  __syncthreads();
+  panel(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int J = 0; J < NT; ++J) {
+    rhs_upd(J);
+    trail(J, J, J + 1);  // row J + 1
+    if (J + 1 < NT) write_panel(J + 1);
+    take_u(J);
+    __syncthreads();
+    WSTAMP(1);
+    if (J + 1 < NT) panel(J + 1);
+    trail(J, J + 1, NT);  // rows below J + 1
+    __syncthreads();
+    WSTAMP(2);
   }
+#else
+#pragma unroll 1
+  for (int J = 0; J < NT; ++J) {
+    write_panel(J);
+    __syncthreads();
+    WSTAMP(1);
+    panel(J);
+    __syncthreads();
+    WSTAMP(2);
+    rhs_upd(J);  // beside the trailing MFMAs below
+    trail(J, J, NT);
+    take_u(J);
+  }
+#endif
   __syncthreads();
 
 #if HREC_WIDE_CUT == 2 || HREC_WIDE_CUT == 3 || HREC_WIDE_CUT == 4

@@ -687,17 +687,20 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
     }
   };
 
-  // the seeds (top-k modes): each wave's group with the largest fused bound
-  // (mode 2: under the scaler of the APPROXIMATE extremes — any choice of
-  // seeds is sound, their exact scores bound tau from below), scanned in the
-  // same round as the extremes' groups; a seed's lower bound needs the exact
-  // scaler, after the extremes
-  constexpr int kSeedPairs = MODE == 0 ? 0 : 4;
-  __shared__ int s_seed[8];
+  // the seeds (top-k modes): each wave's two groups with the largest fused
+  // bounds (mode 2: under the scaler of the APPROXIMATE extremes — any choice
+  // of seeds is sound, their exact scores bound tau from below); the best
+  // 2 nsp of those 16 are scanned in the same round as the extremes' groups
+  // (nsp pairs beside them, 4..8, so that no wave scans twice when the
+  // extremes need few pairs); a seed's lower bound needs the exact scaler,
+  // after the extremes
+  constexpr bool kSeeds = MODE != 0;
+  __shared__ double s_sv[16];
+  __shared__ int s_sg[16];
   HpScale sc0{};
   if constexpr (MODE == 2) sc0 = hp_scale(AMN, AMX, TMN, TMX);
   if constexpr (MODE == 1) sc0 = hp_scale(a.mm_a[b], a.mm_a[a.B + b], a.mm_t[b], a.mm_t[a.B + b]);
-  if constexpr (kSeedPairs > 0) {
+  if constexpr (kSeeds) {
     double bu = -INFINITY;
     int64_t bg = INT64_MAX;
     for (int g = 64 * wv + lane; g < G; g += 64 * 8) {
@@ -708,14 +711,40 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
         bg = g;
       }
     }
-    hp_wave_best(bu, bg);
-    if (lane == 0) s_seed[wv] = bg == INT64_MAX ? -1 : (int)bg;
+    double v1 = bu;
+    int64_t g1 = bg;
+    hp_wave_best(v1, g1);
+    if (g1 != INT64_MAX && bg == g1) bg = INT64_MAX;  // the owner drops it
+    double v2 = bu;
+    int64_t g2 = bg;
+    hp_wave_best(v2, g2);
+    if (lane == 0) {
+      s_sv[2 * wv] = v1, s_sg[2 * wv] = g1 == INT64_MAX ? -1 : (int)g1;
+      s_sv[2 * wv + 1] = v2, s_sg[2 * wv + 1] = g2 == INT64_MAX ? -1 : (int)g2;
+    }
   }
-  float s_sa = 0.f, s_tf = 0.f;  // the seed pair of waves 0-3: exact ALS score, fma chain
+  float s_sa = 0.f, s_tf = 0.f;  // this wave's seed pair: exact ALS score, fma chain
   int64_t s_j = 0;
   bool s_ok = false;
+  // seed pair q: the entries ranked 2q, 2q + 1 of the 16 (lanes 0..15 rank
+  // one entry each; better bound first, ties -> the smaller group)
   auto seed_scan = [&](int q) {
-    s_ok = W.item_of(s_seed[2 * q], s_seed[2 * q + 1], s_j);
+    int rank = 99, gl = -1;
+    if (lane < 16) {
+      gl = s_sg[lane];
+      const double v = s_sv[lane];
+      int r = 0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int ge = s_sg[e];
+        r += ge >= 0 && ge != gl && hp_better(s_sv[e], ge, v, gl);
+      }
+      rank = gl >= 0 ? r : 99;
+    }
+    const uint64_t mA = __ballot(rank == 2 * q), mB = __ballot(rank == 2 * q + 1);
+    const int gA = mA ? __shfl(gl, __builtin_ctzll(mA), kWave) : -1;
+    const int gB = mB ? __shfl(gl, __builtin_ctzll(mB), kWave) : -1;
+    s_ok = W.item_of(gA, gB, s_j);
     W.scan(s_j, s_ok, s_sa, s_tf);
   };
 
@@ -769,20 +798,21 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
     __syncthreads();
     const int n = s_n;
     if (n <= cap2) {
-      // work items: the seed pairs (waves 0-3), then the extremes' pairs
-      const int n_items = kSeedPairs + (n + 1) / 2;
-      for (int it = wv; it < n_items; it += 8) {
-        if (it < kSeedPairs) {
+      // work items: the seed pairs (waves 0..nsp-1), then the extremes' pairs
+      const int n_ext = (n + 1) / 2;
+      const int nsp = kSeeds ? (n_ext >= 4 ? 4 : 8 - n_ext) : 0;
+      for (int it = wv; it < nsp + n_ext; it += 8) {
+        if (it < nsp) {
           seed_scan(it);
         } else {
-          const int q = it - kSeedPairs;
+          const int q = it - nsp;
           pair(s_glist[2 * q], 2 * q + 1 < n ? s_glist[2 * q + 1] : -1);
         }
       }
       if (tid == 0) s_cnt = n;
     } else {
       sweep(pred, pair);
-      if (wv < kSeedPairs) seed_scan(wv);
+      if (kSeeds) seed_scan(wv);
     }
     hx_block_minmax(lo_a, hi_a, lo_t, hi_t, sred, lane, wv);
     HX_STAMP(2);
@@ -795,8 +825,8 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
     if constexpr (MODE == 0) return;
   } else {
     amin = a.mm_a[b], amax = a.mm_a[a.B + b], tmin = a.mm_t[b], tmax = a.mm_t[a.B + b];
-    __syncthreads();  // s_seed
-    if (wv < kSeedPairs) seed_scan(wv);
+    __syncthreads();  // the seed candidates
+    seed_scan(wv);
   }
   // b. the top-k prologue
   HxRec r{};

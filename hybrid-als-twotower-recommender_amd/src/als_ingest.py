@@ -16,8 +16,8 @@ only its own CSR (user) and CSC (item) rows:
   3. degrees: per-code rating counts, all-reduced (SUM) -> the nnz-balanced
      RowLayouts DeviceALS uses (the same bounds a one-process build gives);
   4. exchange: each rating goes to the rank owning its user row (CSR) and to
-     the one owning its item row (CSC) — one all_to_all_single per side,
-     (row code, column code, rating bits) as int32 triples, stably grouped by
+     the one owning its item row (CSC) — all_to_all_single of the row codes,
+     column codes and rating bits (int32 columns), stably grouped by
      destination, so a destination receives the ratings in frame order;
   5. each rank builds its rows with hrec_coo_to_csr (a row's entries in input
      order) at the layout's local slots (parts in chunk order, each padded to
@@ -76,43 +76,55 @@ def _global_codes(ids, id_range, world, group, ops):
     allq = _all_gather_varlen(uq, world, group)
     guq, _ = ops.encode_ids(allq, id_range)
     pos = torch.searchsorted(guq, uq).to(torch.int32)
-    return guq, pos[codes.long()] if codes.numel() else codes
+    return guq, torch.index_select(pos, 0, codes) if codes.numel() else codes
 
 
-def _owner(codes, layout, world):
-    """(destination rank, local row) of every code under `layout`."""
-    bounds = torch.as_tensor(layout.bounds, dtype=torch.int64, device=codes.device)
-    c64 = codes.long()
-    p = torch.searchsorted(bounds, c64, right=True) - 1  # part c·W + r holds [bounds[p], bounds[p+1])
-    # empty parts share a bound with the next: searchsorted(right) lands on the last part starting there
-    dest = p % world
-    local = (p // world) * layout.cs + (c64 - bounds[p])
-    return dest, local
+def _part(codes, layout):
+    """int32 part index of every code: part c·W + r holds [bounds[p],
+    bounds[p+1]); empty parts share a bound with the next, and
+    searchsorted(right) lands on the last part starting there."""
+    bounds = torch.as_tensor(layout.bounds, dtype=torch.int32, device=codes.device)
+    return torch.searchsorted(bounds, codes, right=True, out_int32=True) - 1
 
 
-def _exchange(rows, cols, vals, dest, world, group):
-    """all_to_all_single of (rows, cols, vals) to `dest`, stable: the result
-    is in source-rank order, each source's entries in their input order."""
-    dev = rows.device
-    order = torch.sort(dest, stable=True).indices
-    send = torch.stack([rows.to(torch.int32), cols.to(torch.int32), vals.view(torch.int32)], 1)[order].contiguous()
-    counts = torch.bincount(dest, minlength=world).to(torch.int64)
+def _local_rows(codes, layout, world):
+    """This rank's local row of each of its codes (int32): chunk c of the
+    rank at rows [c·cs, (c+1)·cs)."""
+    p = _part(codes, layout)
+    bounds = torch.as_tensor(layout.bounds, dtype=torch.int32, device=codes.device)
+    return torch.div(p, world, rounding_mode="floor") * layout.cs + (codes - torch.index_select(bounds, 0, p))
+
+
+def _exchange(cols_in, dest, world, group):
+    """all_to_all_single of each int32 column to `dest`, stable: the result is
+    in source-rank order, each source's entries in their input order. One
+    boolean mask per destination (masked_select keeps order): no int64 index
+    arrays beside the ratings."""
+    dev = dest.device
+    masks = [dest == d for d in range(world)]
+    counts = torch.stack([m.sum() for m in masks]).to(torch.int64)
     rc = torch.empty_like(_to_comm(counts, group))
     dist.all_to_all_single(rc, _to_comm(counts, group), group=group)
     s_split, r_split = counts.cpu().tolist(), rc.cpu().tolist()
-    recv = torch.empty((sum(r_split), 3), dtype=torch.int32, device=dev)
-    r = _to_comm(recv, group)
-    dist.all_to_all_single(r, _to_comm(send, group), r_split, s_split, group=group)
-    recv = r.to(dev)
-    del send, order
-    return recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous().view(torch.float32)
+    out = []
+    for c in cols_in:
+        send = torch.cat([torch.masked_select(c, m) for m in masks])
+        recv = torch.empty(sum(r_split), dtype=torch.int32, device=dev)
+        r = _to_comm(recv, group)
+        dist.all_to_all_single(r, _to_comm(send, group), r_split, s_split, group=group)
+        del send
+        out.append(r.to(dev))
+    return out
 
 
 def _side(rows_g, cols_g, vals, layout, n_cols, world, rank, group, ops):
     """This rank's rows (parts in chunk order, padded to cs) of one side."""
-    dest, _ = _owner(rows_g, layout, world)
-    r_rows, r_cols, r_vals = _exchange(rows_g, cols_g, vals, dest, world, group)
-    _, local = _owner(r_rows, layout, world)
+    dest = _part(rows_g, layout) % world
+    r_rows, r_cols, r_vals = _exchange([rows_g, cols_g, vals.view(torch.int32)], dest, world, group)
+    del dest
+    local = _local_rows(r_rows, layout, world)
+    del r_rows
+    r_vals = r_vals.view(torch.float32)
     n_rows = layout.cs * layout.chunks
     indptr, indices, values = ops.coo_to_csr(local.to(torch.int32), r_cols, r_vals, n_rows)
     return DeviceCSR(indptr, indices, values, layout.part_rows(rank)[0][0], n_rows, int(n_cols))
