@@ -768,7 +768,11 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
                         assert [type(i) for i, _ in a] == [type(i) for i, _ in b]
                         assert all(type(s) is np.float64 for _, s in a)
                         for x, y in ((ha.als_scaler, hb.als_scaler), (ha.twotower_scaler, hb.twotower_scaler)):
-                            assert hasattr(x, "scale_") == hasattr(y, "scale_") and hasattr(x, "scale_")
+                            assert hasattr(x, "scale_") == hasattr(y, "scale_")
+                            if name in ("bad_id", "inf"):  # both paths raised before fitting: []
+                                assert a == [] and not hasattr(x, "scale_")
+                                continue
+                            assert hasattr(x, "scale_")
                             for attr in ("data_min_", "data_max_", "data_range_", "scale_", "min_"):
                                 assert getattr(x, attr).dtype == getattr(y, attr).dtype
                                 assert np.array_equal(getattr(x, attr), getattr(y, attr)), (name, attr)
