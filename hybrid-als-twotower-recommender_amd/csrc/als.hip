@@ -909,16 +909,6 @@ __global__ __launch_bounds__(64, HREC_ALS_WAVES) void als_half_sweep_f64_kernel(
     const float* __restrict__ values, int64_t n_rows, const float* __restrict__ src, int64_t n_src,
     int k, double reg, float* __restrict__ dst) {
   __shared__ __attribute__((aligned(16))) double lds[RowLds<16 * NT>::kSize];
-#ifdef HREC_ALS_STAGGER
-  // A/B: the first generation's odd wave slot of each SIMD
-  // starts HREC_ALS_STAGGER x 8k cycles late, so the partners' solves fall in
-  // each other's Gramian phases (equal-degree rows keep the offset)
-  if (blockIdx.x < 2 * 1024 * HREC_ALS_WAVES) {
-    const unsigned hw = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4);  // HW_ID.WAVE_ID
-    if (hw & 1)
-      for (int i = 0; i < HREC_ALS_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   als_row<NT, CH, MODE, S64>(blockIdx.x, threadIdx.x, indptr, indices, values, src, n_src, k, reg, dst, lds);
 }
 

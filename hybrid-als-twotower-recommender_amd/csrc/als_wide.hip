@@ -50,9 +50,6 @@
 #ifndef HREC_WIDE_WR_WIDE
 #define HREC_WIDE_WR_WIDE 32  // ratings per window at kp >= 192 (16: 641 ms, 32: 638 ms per rank-256 epoch) (multiple of 4; LDS: two windows of WR x (kp + 16) doubles)
 #endif
-#ifndef HREC_WIDE_LOOKAHEAD
-#define HREC_WIDE_LOOKAHEAD 0  // 1 = block row J + 1 factored beside J's trailing update (A/B)
-#endif
 #ifndef HREC_WIDE_CUT
 #define HREC_WIDE_CUT 0  // timing/diagnostic builds only: 1 = Gramian only, 2 = no substitutions
 #endif
@@ -543,29 +540,6 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
       }
     }
   };
-#if HREC_WIDE_LOOKAHEAD
-  // Lookahead: block row J + 1 is updated first and factored by the panel
-  // waves while the other waves apply J's update to the rows below it (the
-  // panel's latency chain beside their MFMAs). Every tile still receives
-  // its updates in the order J = 0, 1, ...: bit-identical to the plain order.
-  write_panel(0);
-  __syncthreads();
-  panel(0);
-  __syncthreads();
-#pragma unroll 1
-  for (int J = 0; J < NT; ++J) {
-    rhs_upd(J);
-    trail(J, J, J + 1);  // row J + 1
-    if (J + 1 < NT) write_panel(J + 1);
-    take_u(J);
-    __syncthreads();
-    WSTAMP(1);
-    if (J + 1 < NT) panel(J + 1);
-    trail(J, J + 1, NT);  // rows below J + 1
-    __syncthreads();
-    WSTAMP(2);
-  }
-#else
 #pragma unroll 1
   for (int J = 0; J < NT; ++J) {
     write_panel(J);
@@ -578,7 +552,6 @@ __global__ __launch_bounds__(WideShape<NT>::THREADS) void als_half_sweep_wide_ke
     trail(J, J, NT);
     take_u(J);
   }
-#endif
   __syncthreads();
 
 #if HREC_WIDE_CUT == 2 || HREC_WIDE_CUT == 3 || HREC_WIDE_CUT == 4
