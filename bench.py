@@ -341,13 +341,21 @@ def api_line(eng, n_users, n_items, k, reps, want_cpu):
     uids = [int(u) for u in rng.integers(0, n_users, reps + 1)]
     sink = io.StringIO()
 
-    def timed(fn):
+    per_call = {}
+
+    def timed(fn, key=None):
         fn(uids[0])
         torch.cuda.synchronize()
+        ts = []
         t0 = time.perf_counter()
         for u in uids[1:]:
-            fn(u)
+            c0 = time.perf_counter()
+            fn(u)  # each call ends on the device -> host copy of its top-k (synchronous)
+            ts.append(time.perf_counter() - c0)
         torch.cuda.synchronize()
+        if key:
+            per_call[key] = {"median_ms": float(np.median(ts)) * 1e3, "min_ms": float(np.min(ts)) * 1e3,
+                             "max_ms": float(np.max(ts)) * 1e3}
         return (time.perf_counter() - t0) / reps * 1e3
 
     class Candidates:
@@ -378,9 +386,9 @@ def api_line(eng, n_users, n_items, k, reps, want_cpu):
     arr = items["itemId"].to_numpy().view(IdArray)
     parts = {}
     with contextlib.redirect_stdout(sink):
-        ref_ms = timed(lambda u: h.get_hybrid_recommendations(u, items, top_k=5))
-        iter_ms = timed(lambda u: h.get_hybrid_recommendations(u, both, top_k=5))
-        arr_ms = timed(lambda u: h.get_hybrid_recommendations(u, arr, top_k=5))
+        ref_ms = timed(lambda u: h.get_hybrid_recommendations(u, items, top_k=5), "reference_call")
+        iter_ms = timed(lambda u: h.get_hybrid_recommendations(u, both, top_k=5), "api_call_iterable")
+        arr_ms = timed(lambda u: h.get_hybrid_recommendations(u, arr, top_k=5), "api_call")
         top_api = h.get_hybrid_recommendations(uids[0], arr, top_k=5)
         top_iter = h.get_hybrid_recommendations(uids[0], both, top_k=5)
         parts["als.predict_for_user (id list)"] = timed(lambda u: als.predict_for_user(u, ids))
@@ -419,7 +427,7 @@ def api_line(eng, n_users, n_items, k, reps, want_cpu):
     dev_ms = ev_time(device_call, reps, stream)
     item_bytes = n_items * (4.0 * k + 4.0 * d)  # each candidate's ALS factor row + tower vector, read once
     out = {"users_per_s": 1e3 / arr_ms, "pairs_per_s": n_items * 1e3 / arr_ms, "api_call_ms": arr_ms,
-           "api_call_iterable_ms": iter_ms, "reference_call_ms": ref_ms, "list_path_ms": work,
+           "api_call_iterable_ms": iter_ms, "reference_call_ms": ref_ms, "per_call": per_call, "list_path_ms": work,
            "list_parts_ms": parts, "items": n_items, "top_k": 5, "reps": reps,
            "top5_nonempty": len(top_api) == 5,
            "api_top5_equals_list_path": [i for i, _ in top_api] == [i for i, _ in top] == [i for i, _ in top_iter],
@@ -697,7 +705,7 @@ def main():
     ap.add_argument("--c3-epochs", type=int, default=None,
                     help="timed epochs of the c3 sub-line (BASELINE configs[2]: 10M x 1M, 1 %%, rank 64, "
                          "8 GPUs), run after the c2 lines when 8 or more ranks are present; default 2")
-    ap.add_argument("--api-reps", type=int, default=20,
+    ap.add_argument("--api-reps", type=int, default=50,
                     help="users timed through HybridRecommendationSystem.get_hybrid_recommendations (0 = skip)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="W > 1: user-side ALS row chunks per rank (per-chunk all-gathers overlap the next chunk)")

@@ -258,7 +258,7 @@ class HybridRecommendationSystem:
             a = a.double()
             def item(i): return items[i]      # the union keeps the ALS side's key objects
         elif not als_side:
-            a = torch.zeros(n, dtype=torch.float64, device=t.device)
+            a = torch.zeros(n, dtype=torch.float64, device=t.device)  # finite: only t is checked below
             def item(i): return vals.item(i)  # iterating the Series yields .item() scalars
         else:
             return None
@@ -267,7 +267,10 @@ class HybridRecommendationSystem:
         mm = torch.empty(4, dtype=torch.float64, device=t.device)
         idx, sc, _ = _hrec.fuse_topk(a, t, self.als_f1_score > self.twotower_f1_score, k1, want_fused=False,
                                      minmax=mm)
-        bad = (~torch.isfinite(a).all() | ~torch.isfinite(t).all()).double().view(1)
+        fin = torch.isfinite(t).all()
+        if isinstance(als_side, tuple):
+            fin = fin & torch.isfinite(a).all()
+        bad = fin.logical_not().double().view(1)
         parts = [sc, idx.double(), mm, bad] + ([flags.double()] if flags is not None else [])
         host = torch.cat(parts).cpu().numpy()
         sc_h, idx_h, m = host[:k1], host[k1:2 * k1].astype(np.int64), host[2 * k1: 2 * k1 + 4]
