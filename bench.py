@@ -957,7 +957,7 @@ def main():
         def run_ingest():
             _, urow = _hrec.encode_ids(uid, (u0, u0 + u_per - 1))
             iu, irow = _hrec.encode_ids(iid, (0, n_items - 1))
-            a = _hrec.coo_to_csr(urow, irow, vals, u_per)
+            a = _hrec.coo_to_csr(urow, irow, vals, u_per, alias=True)  # grouped by user: the codes are the CSR
             b = _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()))
             return a, b
 
@@ -969,15 +969,18 @@ def main():
         gs = time.perf_counter() - g0
         ok = bool(torch.equal(out[0][0], csr.indptr) and torch.equal(out[0][1], csr.indices))
         ingest = {"ratings_per_s": csr.nnz / gs, "ms": gs * 1e3, "ratings": csr.nnz,
-                  "steps": ("encode user ids + encode item ids (radix sort on the id range + scan) + CSR + CSC "
-                            "(stable radix sort)"),
+                  "steps": ("encode user ids + encode item ids (presence bitmap + rank) + CSR (rows grouped by "
+                            "user: the item codes and ratings ARE the CSR, indptr from the row codes) + CSC "
+                            "(2-pass stable radix sort, each row's start by atomicMin in the last pass)"),
                   "csr_matches_generator": ok,
                   # algorithmic bytes per rating: read user id, item id (int64) + rating (f32) = 20 B; write
-                  # both id codes (2 x int32) + CSR and CSC column/value arrays (2 x (int32 + f32)) = 24 B
-                  "roofline": roofline("hbm", 44.0 * csr.nnz, gs * 1e3, HBM_PEAK_GBS, "GB/s",
+                  # both id codes (2 x int32) + the CSC column/value arrays (int32 + f32) = 16 B (the CSR's
+                  # arrays are the item codes and the ratings themselves)
+                  "roofline": roofline("hbm", 36.0 * csr.nnz, gs * 1e3, HBM_PEAK_GBS, "GB/s",
                                        "ingest (4 launches' sequence: encode_ids x2 + coo_to_csr x2, wall clock)",
-                                       note=("several radix-sort passes per step: the bytes moved are a multiple "
-                                             "of the algorithmic 44 B per rating"))}
+                                       note=("two radix passes for the CSC: the bytes moved are a multiple "
+                                             "of the algorithmic 36 B per rating (44 B before round 5 counted "
+                                             "the CSR copy)"))}
         if WANT_CPU(args, rank, world):
             import numpy as np
 

@@ -283,6 +283,39 @@ __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* 
   }
 }
 
+// indptr[r] = min(first[r], first[r + 1], ...) from the end: rows without
+// entries take the next row's start (first[] holds each present key's first
+// position, nnz elsewhere; indptr[n_rows] = nnz). One block: chunks of the
+// rows per thread, a block min-scan of the chunk minima, then each chunk.
+__global__ __launch_bounds__(1024) void indptr_suffix_min_kernel(unsigned long long* __restrict__ first,
+                                                                 int64_t n_rows) {
+  __shared__ unsigned long long cm[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n_rows + 1 + 1023) / 1024;
+  const int64_t r0 = t * per, r1 = r0 + per < n_rows + 1 ? r0 + per : n_rows + 1;
+  unsigned long long m = ~0ull;
+  for (int64_t r = r1 - 1; r >= r0; --r) m = first[r] < m ? first[r] : m;
+  cm[t] = m;
+  __syncthreads();
+  // inclusive suffix min over the chunk minima (Hillis-Steele)
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned long long o = t + off < 1024 ? cm[t + off] : ~0ull;
+    __syncthreads();
+    cm[t] = o < cm[t] ? o : cm[t];
+    __syncthreads();
+  }
+  unsigned long long run = t + 1 < 1024 ? cm[t + 1] : ~0ull;  // the rows after this chunk
+  for (int64_t r = r1 - 1; r >= r0; --r) {
+    run = first[r] < run ? first[r] : run;
+    first[r] = run;
+  }
+}
+
+__global__ __launch_bounds__(256) void fill_u64_kernel(unsigned long long* __restrict__ x, int64_t n,
+                                                       unsigned long long v) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) x[i] = v;
+}
+
 // ---------------------------------------------------------------- CSR build
 // Stable LSD radix sort of the row codes carrying (col, rating), written for
 // this shape: dense codes < n_rows, so ceil(bits / 10) passes of <= 10-bit
@@ -389,12 +422,18 @@ __global__ __launch_bounds__(512) void sort_colscan_apply_kernel(uint32_t* __res
   }
 }
 
+// LAST with imin != nullptr (the CSR build): the sorted keys are not written;
+// each key's first position goes to imin[key] by atomicMin (the first entry of
+// every distinct key of a tile's digit run — runs are sorted by the whole key,
+// earlier passes sorted the low digits), and indptr_suffix_min_kernel fills
+// the empty rows: no keys written, no indptr pass re-reading them.
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
     const int32_t* __restrict__ keys_in, const int32_t* __restrict__ cols_in, const float* __restrict__ vals_in,
     const uint64_t* __restrict__ pay_in, int64_t n, int shift, int bits, int64_t n_tiles,
     const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out, uint64_t* __restrict__ pay_out,
-    int32_t* __restrict__ idx_out, float* __restrict__ val_out) {
+    int32_t* __restrict__ idx_out, float* __restrict__ val_out, unsigned long long* __restrict__ imin,
+    int64_t imin_n) {
   constexpr int R_MAX = 1 << kSortMaxBits, NW = kSortThreads / 64, PW = kSortTile / NW;  // entries per wave
   __shared__ int32_t sk[kSortTile];                 // the tile, sorted by digit (stable)
   __shared__ uint64_t sp[kSortTile];
@@ -532,7 +571,11 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
       const uint32_t dg = ((uint32_t)k >> shift) & dmask;
       const uint32_t pos = goff[dg] + ((uint32_t)q - wh[0][dg]);
       const uint64_t pv = sp[q];
-      keys_out[pos] = k;
+      if (!LAST || imin == nullptr) {
+        keys_out[pos] = k;
+      } else if (((uint32_t)q == wh[0][dg] || sk[q - 1] != k) && (uint32_t)k < (uint64_t)imin_n) {
+        atomicMin(&imin[(uint32_t)k], (unsigned long long)pos);  // the run's first entry of key k
+      }
       if constexpr (LAST) {
         idx_out[pos] = (int32_t)(uint32_t)pv;
         val_out[pos] = __uint_as_float((uint32_t)(pv >> 32));
@@ -665,7 +708,8 @@ struct EncodeWs {
 // keys: ceil(bits / 10) LSD passes. idx_out / val_out get the cols / vals in
 // key order; *sorted_keys points at the sorted keys (inside ws).
 int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, int64_t nnz, int bits, void* ws,
-                 int32_t* idx_out, float* val_out, const int32_t** sorted_keys, hipStream_t s) {
+                 int32_t* idx_out, float* val_out, const int32_t** sorted_keys, hipStream_t s,
+                 unsigned long long* imin = nullptr, int64_t imin_n = 0) {
   const CsrWs L(nnz, bits);
   char* w = static_cast<char*>(ws);
   int32_t* kbuf[2] = {reinterpret_cast<int32_t*>(w + L.ka), reinterpret_cast<int32_t*>(w + L.kb)};
@@ -693,7 +737,7 @@ int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, in
     uint64_t* pout = pbuf[p & 1];
 #define HREC_DOWN(F, LST)                                                                                        \
   hipLaunchKernelGGL((sort_downsweep_kernel<F, LST>), dim3(nd), dim3(kSortThreads), 0, s, kin, cols, vals, pin, nnz, \
-                     shift, db, L.n_tiles, cnt, kout, pout, idx_out, val_out)
+                     shift, db, L.n_tiles, cnt, kout, pout, idx_out, val_out, imin, imin_n)
     if (first && last) HREC_DOWN(true, true);
     else if (first) HREC_DOWN(true, false);
     else if (last) HREC_DOWN(false, true);
@@ -837,11 +881,15 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   const int bits = bits_for(n_rows);
   const CsrWs L(nnz, bits);
   HREC_REQUIRE(ws_bytes >= L.total, "coo_to_csr: workspace %zu < %zu bytes", ws_bytes, L.total);
+  // indptr: every row's first position (atomicMin in the last pass, nnz for
+  // rows without entries), then a suffix min fills the empty rows
+  unsigned long long* first = reinterpret_cast<unsigned long long*>(indptr);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(grid_for(n_rows + 1)), dim3(256), 0, s, first, n_rows + 1,
+                     (unsigned long long)nnz);
   const int32_t* kin = nullptr;
-  int rc = csr_sort_run(rows, cols, vals, nnz, bits, ws, indices, values, &kin, s);
+  int rc = csr_sort_run(rows, cols, vals, nnz, bits, ws, indices, values, &kin, s, first, n_rows);
   if (rc) return rc;
-  hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz / 4 + 1)), dim3(256), 0, s, kin, nnz, n_rows,
-                     indptr);
+  hipLaunchKernelGGL(indptr_suffix_min_kernel, dim3(1), dim3(1024), 0, s, first, n_rows);
   return check_launch("coo_to_csr");
 }
 
@@ -868,7 +916,9 @@ extern "C" int hrec_coo_to_csr_sorted(const int32_t* rows, const int32_t* cols, 
     return HREC_OK;
   }
   HREC_REQUIRE(n_rows > 0 && rows && cols && vals && indices && values, "coo_to_csr_sorted: null pointer");
-  hipLaunchKernelGGL(copy_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, cols, vals, nnz, indices, values);
+  HREC_REQUIRE((indices == cols) == (values == vals), "coo_to_csr_sorted: alias both outputs or neither");
+  if (indices != cols)  // indices == cols, values == vals: the CSR is the input columns themselves
+    hipLaunchKernelGGL(copy_entries_kernel, dim3(grid_for(nnz)), dim3(256), 0, s, cols, vals, nnz, indices, values);
   hipLaunchKernelGGL(indptr_from_sorted_kernel, dim3(grid_for(nnz / 4 + 1)), dim3(256), 0, s, rows, nnz, n_rows,
                      indptr);
   return check_launch("coo_to_csr_sorted");

@@ -265,21 +265,27 @@ def encode_ids(ids, id_range=None):
     return uniq[: int(n_uniq.item())], codes
 
 
-def coo_to_csr(rows, cols, vals, n_rows):
+def coo_to_csr(rows, cols, vals, n_rows, alias=False):
     """(indptr int64[n_rows+1], indices int32[nnz], values f32[nnz]) of the COO
-    (rows, cols, vals), rows ascending, a row's entries in input order."""
+    (rows, cols, vals), rows ascending, a row's entries in input order.
+    alias=True: when rows are already in order the returned indices / values
+    ARE cols / vals (no copy) — for callers that do not modify either after."""
     nnz = rows.numel()
     dev = rows.device
     if cols.numel() != nnz or vals.numel() != nnz:
         raise HrecError("coo_to_csr: rows, cols and vals must have the same length")
     indptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
-    indices = torch.empty(nnz, dtype=torch.int32, device=dev)
-    values = torch.empty(nnz, dtype=torch.float32, device=dev)
     # rows already in order (e.g. ratings grouped by user): no sort needed
     flag = torch.empty(1, dtype=torch.int32, device=dev)
     _check("hrec_rows_descending_pairs", lib().hrec_rows_descending_pairs(
         _dev(rows, torch.int32, "rows"), nnz, _dev(flag, torch.int32, "out"), _stream()))
-    if int(flag.item()) == 0:
+    in_order = int(flag.item()) == 0
+    if in_order and alias:
+        indices, values = cols, vals
+    else:
+        indices = torch.empty(nnz, dtype=torch.int32, device=dev)
+        values = torch.empty(nnz, dtype=torch.float32, device=dev)
+    if in_order:
         _check("hrec_coo_to_csr_sorted", lib().hrec_coo_to_csr_sorted(
             _dev(rows, torch.int32, "rows"), _dev(cols, torch.int32, "cols"), _dev(vals, torch.float32, "vals"),
             nnz, n_rows, _dev(indptr, torch.int64, "indptr"), _dev(indices, torch.int32, "indices"),

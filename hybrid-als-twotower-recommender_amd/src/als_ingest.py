@@ -47,7 +47,7 @@ class _HrecIngestOps:
     def coo_to_csr(rows, cols, vals, n_rows):
         from . import _hrec
 
-        return _hrec.coo_to_csr(rows, cols, vals, int(n_rows))
+        return _hrec.coo_to_csr(rows, cols, vals, int(n_rows), alias=True)  # the exchanged columns are private
 
 
 def _to_comm(t, group):

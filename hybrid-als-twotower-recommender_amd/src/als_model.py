@@ -184,11 +184,12 @@ def _int_ids(col, name):
     return a
 
 
-def build_csr(rows, cols, vals, n_rows, n_cols):
+def build_csr(rows, cols, vals, n_rows, n_cols, alias=False):
     """Device CSR of COO ratings (hrec_coo_to_csr): rows ascending, a row's
     entries in input order; duplicate (u, i) ratings stay separate terms, as
-    in Spark. rows/cols int32, vals f32, all device tensors."""
-    indptr, indices, values = _hrec.coo_to_csr(rows, cols, vals, int(n_rows))
+    in Spark. rows/cols int32, vals f32, all device tensors. alias: rows
+    already in order hand back cols / vals themselves (no copy)."""
+    indptr, indices, values = _hrec.coo_to_csr(rows, cols, vals, int(n_rows), alias=alias)
     return DeviceCSR(indptr, indices, values, 0, int(n_rows), int(n_cols))
 
 
@@ -271,7 +272,7 @@ class ALSModel:
             item_ids_t, irow = _hrec.encode_ids(items, rng(items_h))
             user_ids, item_ids = user_ids_t.cpu().numpy(), item_ids_t.cpu().numpy()
             n_u, n_i = len(user_ids), len(item_ids)
-            csr = build_csr(urow, irow, ratings, n_u, n_i)
+            csr = build_csr(urow, irow, ratings, n_u, n_i, alias=True)  # ratings grouped by user: no copy
             csc = build_csr(irow, urow, ratings, n_i, n_u)
             del urow, irow, ratings, users, items, user_ids_t, item_ids_t
         if track:

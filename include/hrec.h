@@ -110,6 +110,8 @@ int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const float* vals,
                     void* stream);
 /* The same CSR when rows[] is already non-decreasing (then input order is the
  * stable order): entries copied, indptr from the rows, no sort or workspace.
+ * indices == cols and values == vals (both or neither) skip the copy: the
+ * CSR's column and value arrays are then the input columns themselves.
  * hrec_rows_descending_pairs writes *out (device int32) = 1 if some
  * rows[i] > rows[i+1], else 0 — the caller's choice between the two. */
 int hrec_rows_descending_pairs(const int32_t* rows, int64_t n, int32_t* out, void* stream);

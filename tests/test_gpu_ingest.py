@@ -90,11 +90,18 @@ def test_coo_to_csr_matches_stable_argsort(device, nnz, n_rows, n_cols, presorte
     np.testing.assert_array_equal(ip.cpu().numpy(), e_ip)
     np.testing.assert_array_equal(ix.cpu().numpy(), e_ix)
     np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), e_v.view(np.uint32))
+    # alias=True: rows in order hand back the input columns themselves (no
+    # copy); otherwise the same sorted arrays as above
+    tc, tv = torch.as_tensor(cols, device=device), torch.as_tensor(vals, device=device)
+    ip2, ix2, v2 = h.coo_to_csr(torch.as_tensor(rows, device=device), tc, tv, n_rows, alias=True)
+    assert torch.equal(ip2, ip) and torch.equal(ix2, ix) and torch.equal(v2.view(torch.int32), v.view(torch.int32))
+    assert (ix2.data_ptr() == tc.data_ptr() and v2.data_ptr() == tv.data_ptr()) == presorted
 
 
 def test_coo_to_csr_empty_rows_and_duplicates(device):
-    """Leading, interior and trailing empty rows; repeated (row, col) pairs
-    stay separate entries in input order."""
+    """Leading, interior and trailing empty rows (the sorted path's row
+    starts come from an atomicMin per present row + a suffix min); repeated
+    (row, col) pairs stay separate entries in input order."""
     h = _hrec()
     rows = np.array([2, 2, 5, 2, 5, 2], np.int32)
     cols = np.array([1, 1, 0, 3, 0, 1], np.int32)
