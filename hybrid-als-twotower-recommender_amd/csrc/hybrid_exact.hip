@@ -186,7 +186,7 @@ __device__ unsigned long long g_hx1_stamps[4096][4];  // per block: start, stage
 #endif
 
 template <int DK>
-__global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* __restrict__ uop, int B, int n_ut,
+__global__ __launch_bounds__(kHxThreads1, DK == 64 ? 2 : 1) void hx_stats_kernel(const uint16_t* __restrict__ uop, int B, int n_ut,
                                                                const char* __restrict__ items, int64_t N, int G,
                                                                int64_t per, float* __restrict__ stats) {
   using S = HxShape<DK>;
@@ -202,8 +202,15 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
   const char* ia = items;                        // ALS operand [N][2 DK]
   const char* it = items + (size_t)N * kOpB;     // two-tower operand [N][2 DK]
   const hrec_rsrc_t ra = rows_rsrc(ia, i0, kOpB, N), rt = rows_rsrc(it, i0, kOpB, N);
-  HxFrag fa[2][KS], ft[2][KS];  // [hi / lo][k-step]
-  auto load = [&](int64_t jb) {
+  // DK 64: two fragment sets (double buffer): the next slice's item
+  // fragments load at the start of this slice, so their latency hides behind
+  // its 4 user chunks (loading them at the last chunk left one HBM round trip
+  // per slice exposed: 42k loop ticks per wave for 20k of MFMA work per SIMD);
+  // 244 VGPRs keep 2 waves per SIMD. DK 128 (its fragments twice the size):
+  // one set, refilled after the last chunk.
+  constexpr bool kDB = DK == 64;
+  HxFrag fa0[2][KS], ft0[2][KS], fa1[2][KS], ft1[2][KS];  // [hi / lo][k-step]
+  auto load = [&](int64_t jb, HxFrag (&fa)[2][KS], HxFrag (&ft)[2][KS]) {
     const int64_t j = jb + c;
     const int vi = j < N ? (int)(j - i0) : 0x7fffffff;  // out of range: the buffer check reads zeros
 #pragma unroll
@@ -216,7 +223,7 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
   };
   int64_t jb = i0 + 32 * w;
   if (w == 0) HX1_STAMP(0);
-  if (jb < i1) load(jb);  // the first slice arrives while the users are staged
+  if (jb < i1) load(jb, fa0, ft0);  // the first slice arrives while the users are staged
   // users -> LDS: every load of a thread in flight before its stores (one
   // round trip, not one per 16-B chunk)
   constexpr int CPR = kOpB / 16;  // 16-B chunks per user row
@@ -240,10 +247,13 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
   }
   __syncthreads();
   if (w == 0) HX1_STAMP(1);
-  while (jb < i1) {  // wave-uniform; no barrier follows
+  // one 32-item slice with the fragments in (fa, ft); the next slice's
+  // fragments go to (na, nt) first. Returns false after the range's last slice.
+  auto slice = [&](HxFrag (&fa)[2][KS], HxFrag (&ft)[2][KS], HxFrag (&na)[2][KS], HxFrag (&nt)[2][KS]) {
     const bool full = jb + 32 <= N;
     const int64_t jn = jb + 32 * (kHxThreads1 / 64);
     const bool more = jn < i1;
+    if (kDB && more) load(jn, na, nt);
     for (int ch = 0; 32 * ch < ub; ++ch) {
       hx_f16 acc[2];
 #pragma unroll
@@ -269,7 +279,6 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
         HX_MMA(acc[1], ft[0][ks], tl);
 #undef HX_MMA
       }
-      if (more && 32 * (ch + 1) >= ub) load(jn);  // last chunk: the next slice's fragments
       float mx[2], mn[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
@@ -298,10 +307,20 @@ __global__ __launch_bounds__(kHxThreads1) void hx_stats_kernel(const uint16_t* _
       const float hi = fmaxf(hx_u2f(X[0]), hx_u2f(X[1]));  // lanes < 32: ALS, lanes >= 32: two-tower
       const float lo = fminf(hx_u2f(Y[0]), hx_u2f(Y[1]));
       const int b = b0 + 32 * ch + c;
+      if (!kDB && more && 32 * (ch + 1) >= ub) load(jn, na, nt);  // last chunk: the next slice's fragments
       if (b < B) *reinterpret_cast<float2*>(stats + ((int64_t)b * G + (jb >> 5)) * 4 + 2 * h) = make_float2(hi, lo);
     }
-    if (!more) break;
     jb = jn;
+    return more;
+  };
+  if (jb < i1) {  // wave-uniform; no barrier follows
+    if constexpr (kDB) {
+      while (slice(fa0, ft0, fa1, ft1) && slice(fa1, ft1, fa0, ft0)) {
+      }
+    } else {
+      while (slice(fa0, ft0, fa0, ft0)) {
+      }
+    }
   }
   if (w == 0) HX1_STAMP(2);
   if (w == 3) HX1_STAMP(3);

@@ -162,6 +162,10 @@ def main(base):
     c5["no_store_bytes"] = 102.4e6
     c5["traffic_over_no_store"] = tot / 102.4e6
     res["c5_pruned_hybrid"] = c5
+    # c2 exact pruned hybrid (csrc/hybrid_exact.hip): every hx_ kernel
+    hx_names = sorted({r["Kernel_Name"].split("(")[0].replace("void ", "").replace("hrec::", "") for r in trace
+                       if "hx_" in r["Kernel_Name"]})
+    res["c2_exact_hybrid"] = per_kernel(hx_names, "prof_fetch_hx", "prof_write_hx")
     res["ingest"] = per_kernel(["mark_present_kernel", "codes_from_rank_kernel", "mark_bits_kernel",
                                 "codes_bits_kernel", "descent_kernel", "copy_entries_kernel",
                                 "indptr_from_sorted_kernel", "sort_upsweep_kernel",
