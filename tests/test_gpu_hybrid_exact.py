@@ -58,7 +58,9 @@ def _same(x, y):
 
 @pytest.mark.parametrize("B,N,ka,kt,k", [(256, 100_003, 64, 64, 5), (70, 20_000, 50, 32, 8), (130, 40_001, 100, 128, 1),
                                          (33, 5_000, 10, 64, 3), (300, 777, 64, 64, 5), (8, 9, 64, 64, 8),
-                                         (8, 1, 64, 64, 5), (40, 33, 16, 32, 4)])
+                                         (8, 1, 64, 64, 5), (40, 33, 16, 32, 4),
+                                         # G > 8192 groups (records read from memory, not LDS)
+                                         (16, 300_007, 64, 64, 5)])
 def test_hybrid_exact_equals_materialised(device, B, N, ka, kt, k):
     """K9x == the materialised exact path bit for bit — ids, fused scores and
     both min / max rows — for both weight orders, through the two-phase calls
