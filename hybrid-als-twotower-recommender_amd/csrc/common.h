@@ -154,6 +154,12 @@ size_t scan_ws_bytes(int64_t n);
 template <typename T>
 int scan_run(const T* in, T* out, int64_t n, bool exclusive, void* ws, hipStream_t s);
 int minmax_i64_run(const int64_t* x, int64_t n, int64_t* out, hipStream_t s);
+// csrc/ingest.hip: the in-tree stable LSD radix sort of 32-bit keys (the low
+// `bits` bits) carrying two 32-bit payload words, n < 2^31; workspace
+// radix_pairs_ws_bytes(n) at any key width. *keys_sorted points into ws.
+size_t radix_pairs_ws_bytes(int64_t n);
+int radix_pairs_sort(const uint32_t* keys, const uint32_t* p0, const uint32_t* p1, int64_t n, int bits, void* ws,
+                     uint32_t* p0_out, uint32_t* p1_out, const uint32_t** keys_sorted, hipStream_t s);
 // csrc/score.hip: hrec_fuse_rows_topk's exact segment path, gated on *gate.
 size_t fuse_rows_exact_ws_bytes(int64_t n_rows, int64_t n, int kk);
 int fuse_rows_exact(const float* als, const float* tt, int64_t n_rows, int64_t n, int64_t ld, const float* als_mm,

@@ -15,7 +15,6 @@
 // encode_ids: a marked table + scan for dense id ranges (hipCUB radix sort of
 // (id, position) otherwise); coo_to_csr: a hand-written stable LSD radix sort
 // of the dense row codes (below); plus O(n) integer passes. HBM-bound.
-#include <hipcub/hipcub.hpp>
 
 #include "common.h"
 
@@ -681,18 +680,16 @@ inline size_t csr_ws_max(int64_t n) {
 // Workspace layout of hrec_encode_ids (all 256-B aligned): the shifted
 // 32-bit keys (or, for id spans past 2^32, the sorted 64-bit keys), the
 // position columns, the distinct flags and their scan, and a temp region for
-// the key sort (the in-tree radix sort's workspace; hipCUB's 64-bit sort
-// only for spans past 2^32) or the scan.
+// the in-tree radix sort (its workspace, then four 32-bit columns for the
+// two-word sort of spans past 2^32) or the scan.
 struct EncodeWs {
   size_t keys, pos, pos2, flag, incl, temp, total;
   explicit EncodeWs(int64_t n) {
-    size_t sort64_tmp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort64_tmp, (const int64_t*)nullptr, (int64_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
     // the in-tree sort's workspace (its sorted keys stay there), the sort's
     // value output, then the scan's workspace (must not overlap the keys)
     size_t tmp = csr_ws_max(n) + align256(4 * (size_t)n) + align256(scan_ws_bytes(n));
-    if (sort64_tmp > tmp) tmp = sort64_tmp;
+    const size_t wide = csr_ws_max(n) + 4 * align256(4 * (size_t)n);
+    if (wide > tmp) tmp = wide;
     if (scan_ws_bytes(n) > tmp) tmp = scan_ws_bytes(n);
     keys = 0;
     pos = keys + align256(8 * (size_t)n);
@@ -753,6 +750,35 @@ int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, in
   return HREC_OK;
 }
 
+size_t radix_pairs_ws_bytes(int64_t n) { return csr_ws_max(n); }
+
+int radix_pairs_sort(const uint32_t* keys, const uint32_t* p0, const uint32_t* p1, int64_t n, int bits, void* ws,
+                     uint32_t* p0_out, uint32_t* p1_out, const uint32_t** keys_sorted, hipStream_t s) {
+  const int32_t* ks = nullptr;
+  const int rc = csr_sort_run(reinterpret_cast<const int32_t*>(keys), reinterpret_cast<const int32_t*>(p0),
+                              reinterpret_cast<const float*>(p1), n, bits, ws, reinterpret_cast<int32_t*>(p0_out),
+                              reinterpret_cast<float*>(p1_out), &ks, s);
+  *keys_sorted = reinterpret_cast<const uint32_t*>(ks);
+  return rc;
+}
+
+// ids spanning more than 2^32: (id - lo) split into 32-bit words ...
+__global__ __launch_bounds__(256) void split_u64_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
+                                                        uint32_t* __restrict__ w_lo, uint32_t* __restrict__ w_hi) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t d = (uint64_t)ids[i] - (uint64_t)lo;
+    w_lo[i] = (uint32_t)d;
+    w_hi[i] = (uint32_t)(d >> 32);
+  }
+}
+// ... and joined back after the two sorts (the sorted ids themselves)
+__global__ __launch_bounds__(256) void join_u64_kernel(const uint32_t* __restrict__ w_lo,
+                                                       const uint32_t* __restrict__ w_hi, int64_t n, int64_t lo,
+                                                       int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = (int64_t)((uint64_t)lo + (((uint64_t)w_hi[i] << 32) | w_lo[i]));
+}
+
 }  // namespace hrec
 
 using namespace hrec;
@@ -781,7 +807,6 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
   int32_t* flag = reinterpret_cast<int32_t*>(w + L.flag);
   int32_t* incl = reinterpret_cast<int32_t*>(w + L.incl);
   void* temp = w + L.temp;
-  size_t temp_bytes = L.total - L.temp;
   const unsigned g = grid_for(n);
   // A narrow id range sorts (id - lo) on only the bits it spans.
   const bool narrow = (uint64_t)id_hi - (uint64_t)id_lo < 0x7fffffffull;
@@ -835,12 +860,31 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
                        codes, uniq, n_uniq);
   } else {
     // ids spanning more than 2^32 (only through the C-ABI: the drop-in API's
-    // ids are Spark Ints): hipCUB's 64-bit key sort
+    // ids are Spark Ints): (id - lo) as two 32-bit words, the in-tree stable
+    // sort by the low word carrying (high word, position), then by the high
+    // word carrying (low word, position) — LSD over 64 bits
+    char* t4 = static_cast<char*>(temp) + csr_ws_max(n);
+    const size_t c4 = align256(4 * (size_t)n);
+    uint32_t* A = reinterpret_cast<uint32_t*>(t4);
+    uint32_t* Bw = reinterpret_cast<uint32_t*>(t4 + c4);
+    uint32_t* C = reinterpret_cast<uint32_t*>(t4 + 2 * c4);
+    uint32_t* D = reinterpret_cast<uint32_t*>(t4 + 3 * c4);
+    hipLaunchKernelGGL(split_u64_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, A, Bw);
+    const uint32_t* ks = nullptr;
+    int rc = radix_pairs_sort(A, Bw, reinterpret_cast<const uint32_t*>(pos), n, 32, temp, C,
+                              reinterpret_cast<uint32_t*>(pos2), &ks, s);  // C: high words, pos2: positions
+    if (rc) return rc;
+    if (hipMemcpyAsync(D, ks, 4 * (size_t)n, hipMemcpyDeviceToDevice, s) != hipSuccess)  // the low words, sorted
+      return check_launch("encode_ids: copy");
+    const uint64_t hi_span = ((uint64_t)id_hi - (uint64_t)id_lo) >> 32;
+    rc = radix_pairs_sort(C, D, reinterpret_cast<const uint32_t*>(pos2), n, bits_for((int64_t)hi_span + 1), temp, A,
+                          reinterpret_cast<uint32_t*>(pos), &ks, s);  // A: low words, pos: positions
+    if (rc) return rc;
     int64_t* keys = reinterpret_cast<int64_t*>(w + L.keys);
-    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, ids, keys, pos, pos2, (int)n, 0, 64, s) != hipSuccess)
-      return check_launch("encode_ids: radix sort");
+    hipLaunchKernelGGL(join_u64_kernel, dim3(g), dim3(256), 0, s, A, ks, n, id_lo, keys);
+    pos2 = pos;
     hipLaunchKernelGGL(distinct_flags_kernel<int64_t>, dim3(g), dim3(256), 0, s, keys, n, flag);
-    const int rc = scan_run<int32_t>(flag, incl, n, false, temp, s);
+    rc = scan_run<int32_t>(flag, incl, n, false, temp, s);
     if (rc) return rc;
     hipLaunchKernelGGL(scatter_codes_kernel<int64_t>, dim3(g), dim3(256), 0, s, keys, (int64_t)0, pos2, flag, incl,
                        n, codes, uniq, n_uniq);
