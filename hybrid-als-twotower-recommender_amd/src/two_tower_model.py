@@ -245,20 +245,20 @@ class TwoTowerModel:
         _predict_device, which raises where predict_for_user raises. The user
         id is checked here, on the host, first — as _device_inputs does."""
         sc = self.scaler
-        if (self.model is None or not isinstance(item_features, pd.DataFrame) or type(sc) is not MinMaxScaler
+        if (self.model is None or type(sc) is not MinMaxScaler
                 or sc.clip or not hasattr(sc, "scale_") or getattr(sc, "n_features_in_", None) != 2):
             return None
         names = getattr(sc, "feature_names_in_", None)
         if names is not None and list(names) != list(self._FAST_NUM_COLS):
             return None
-        if len(item_features) == 0 or not item_features.columns.is_unique:
+        series = self._fast_columns(item_features)
+        if series is None:
             return None
+        n = len(item_features)
         cols = []
-        for c in self._FAST_ID_COLS + self._FAST_NUM_COLS:
-            if c not in item_features.columns:
-                return None
-            a = item_features[c].to_numpy()
-            if not isinstance(a, np.ndarray) or a.ndim != 1:
+        for c, s in zip(self._FAST_ID_COLS + self._FAST_NUM_COLS, series):
+            a = s.to_numpy()
+            if not isinstance(a, np.ndarray) or a.ndim != 1 or len(a) != n:
                 return None
             if c in self._FAST_ID_COLS:
                 if a.dtype.kind not in "iu" or a.dtype == np.uint64:
@@ -277,6 +277,30 @@ class TwoTowerModel:
         uvec = self.model.user_vectors(u)
         ivec = self.model.item_vectors(item, man, cat, num)
         return item_features, _hrec.tt_score(uvec, ivec).reshape(-1), flags
+
+    def _fast_columns(self, item_features):
+        """The five Series _predict_device reads, through the same lookups
+        (frame["col"] for the ids, frame[[price, rating]] for the scaler), or
+        None: an empty candidate set, a missing or repeated column, or a
+        lookup that is not a plain Series. Besides a DataFrame this takes any
+        candidates object answering those lookups from a frame (e.g. an item
+        id array whose ["col"] comes from the item frame, bench.py)."""
+        try:
+            if len(item_features) == 0:
+                return None
+            if isinstance(item_features, pd.DataFrame):
+                if not item_features.columns.is_unique or not all(
+                        c in item_features.columns for c in self._FAST_ID_COLS + self._FAST_NUM_COLS):
+                    return None
+                return [item_features[c] for c in self._FAST_ID_COLS + self._FAST_NUM_COLS]
+            ids = [item_features[c] for c in self._FAST_ID_COLS]
+            sub = item_features[list(self._FAST_NUM_COLS)]
+        except Exception:  # the host path makes the same lookups and reports the error
+            return None
+        if (not isinstance(sub, pd.DataFrame) or list(sub.columns) != list(self._FAST_NUM_COLS)
+                or not all(type(s) is pd.Series for s in ids)):
+            return None
+        return ids + [sub[c] for c in self._FAST_NUM_COLS]
 
     # --------------------------------------------------------- persistence
     def save_model(self, model_path="models/twotower.keras"):

@@ -53,6 +53,17 @@ class Candidates:
 both = Candidates()
 
 
+class IdArray(np.ndarray):
+    def __getitem__(self, key):
+        if isinstance(key, (str, list)):
+            return items[key]
+        return super().__getitem__(key)
+
+
+arr = items["itemId"].to_numpy().view(IdArray)
+keys = np.asarray(arr)
+
+
 def timed(name, fn):
     fn()
     torch.cuda.synchronize()
@@ -68,6 +79,23 @@ t_side = tt._predict_device(3, items)
 with contextlib.redirect_stdout(io.StringIO()):
     timed("api call (both sides)", lambda: h.get_hybrid_recommendations(3, both, top_k=5))
     timed("api call (reference wiring)", lambda: h.get_hybrid_recommendations(3, items, top_k=5))
+    timed("api call (id array)", lambda: h.get_hybrid_recommendations(3, arr, top_k=5))
+timed("ALS _predict_device (id array)", lambda: als._predict_device(3, arr))
+timed("ALS keys H2D", lambda: torch.as_tensor(keys, device=dev))
+timed("ALS _lookup_device", lambda: als.model._lookup_device(keys))
+irows = als.model._lookup_device(keys)
+urow = torch.as_tensor(als.model._lookup(als.model.user_ids, [3]), device=dev)
+from src import _hrec  # noqa: E402
+timed("ALS als_score", lambda: _hrec.als_score(als.model.U, urow, als.model.Vt, irows, n_items, k))
+timed("ALS model.score", lambda: als.model.score([3], keys))
+timed("array_equal(keys, vals)", lambda: np.array_equal(keys, items["itemId"].values))
+timed("frame[[price, rating]]", lambda: items[["price", "average_review_rating"]])
+timed("TT _fast_columns (frame)", lambda: tt._fast_columns(items))
+timed("TT _fast_columns (id array)", lambda: tt._fast_columns(arr))
+timed("TT _predict_device_fast (id array)", lambda: tt._predict_device_fast(3, arr))
+a_arr = als._predict_device(3, arr)
+t_arr = tt._predict_device_fast(3, arr)
+timed("_top_on_device (id array, flags)", lambda: h._top_on_device(a_arr, t_arr[:2], 5, flags=t_arr[2]))
 timed("ALS list(all_items)", lambda: list(both))
 timed("ALS _check_int_ids", lambda: ALSModel._check_int_ids(ids))
 timed("ALS fromiter", lambda: np.fromiter(ids, np.int64, len(ids)))
@@ -79,3 +107,15 @@ cols = [torch.from_numpy(items[c].to_numpy()) for c in ("itemId", "manufacturer_
                                                          "average_review_rating")]
 timed("TT H2D of the 5 columns", lambda: [c.to(dev) for c in cols])
 timed("_top_on_device", lambda: h._top_on_device(a_side, t_side, 5))
+
+if os.environ.get("API_PROFILE"):
+    import cProfile
+    import pstats
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(reps):
+            h.get_hybrid_recommendations(3, arr, top_k=5)
+        pr.disable()
+    pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(30)

@@ -690,6 +690,23 @@ class _IdsFrame:
         return self.df[key]
 
 
+class _IdArray(np.ndarray):
+    """An integer item id array (the ALS side iterates it) whose column
+    lookups come from the item frame (the two-tower side): bench.py's
+    api_call candidates."""
+
+    def __getitem__(self, key):
+        if isinstance(key, (str, list)):
+            return self._df[key]
+        return super().__getitem__(key)
+
+
+def _id_array(df):
+    a = df["itemId"].to_numpy().view(_IdArray)
+    a._df = df
+    return a
+
+
 def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
     """get_hybrid_recommendations' array path (_top_on_device: fusion on the
     device scores, no Python lists) returns exactly what the list path
@@ -729,9 +746,17 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
     int_r["average_review_rating"] = int_r["average_review_rating"].round().astype(np.int64)
     f32_p["price"] = f32_p["price"].astype(np.float32)  # outside the device input path
     cases = [("frame", items), ("ids", _IdsFrame(items)), ("dup", _IdsFrame(dup)), ("frame_dup", dup),
+             ("id_array", _id_array(items)), ("id_array_dup", _id_array(dup)),
              ("bad_id", bad_id), ("inf", inf), ("nan", nan), ("int_rating", int_r), ("f32_price", f32_p)]
-    calls = {"fast": 0}
+    calls = {"fast": 0, "tt_fast": set()}
     orig = HybridRecommendationSystem._top_on_device
+    orig_tt = TwoTowerModel._predict_device_fast
+
+    def counting_tt(self, uid, cand):
+        r = orig_tt(self, uid, cand)
+        if r is not None:
+            calls["tt_fast"].add(type(cand).__name__)
+        return r
 
     def counting(self, *a, **kw):
         r = orig(self, *a, **kw)
@@ -747,6 +772,8 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
                       (lambda self, *a, **kw: None) if list_path else counting)
             if list_path:  # the host-built two-tower inputs (_predict_device) as well
                 m.setattr(TwoTowerModel, "_predict_device_fast", lambda self, *a: None)
+            else:
+                m.setattr(TwoTowerModel, "_predict_device_fast", counting_tt)
             top = h.get_hybrid_recommendations(uid, cand, top_k=k)
         return top, h
 
@@ -781,6 +808,8 @@ def test_hybrid_device_path_matches_list_path(device, monkeypatch, capsys):
         tt.model.tensors["item_emb"].copy_(saved)
     # the array path served the unique-id cases; the tie case fell back
     assert calls["fast"] > 0
+    # the device-built item inputs served frames, ids frames and id arrays
+    assert calls["tt_fast"] == {"DataFrame", "_IdsFrame", "_IdArray"}
     capsys.readouterr()
 
 

@@ -104,3 +104,41 @@ def test_hybrid_list_path_keeps_als_error_contract(capsys):
     out = m._predictions_guarded([7, 8], torch.tensor([1.5, float("nan")]))
     assert out == []
     assert "Prediction error:" in capsys.readouterr().out
+
+
+def test_fast_columns_lookup_rules():
+    """TwoTowerModel._fast_columns (the device input path's column source):
+    the same lookups as _predict_device for a frame, an ids-frame object and
+    an id array whose lookups come from the frame; None for anything the
+    host path must handle (missing / repeated columns, empty candidates,
+    lookups that are not plain Series)."""
+    from src.two_tower_model import TwoTowerModel
+
+    tt = TwoTowerModel(10, 10, 3, 3, embedding_size=4)
+    df = pd.DataFrame({"itemId": [3, 1, 2], "manufacturer_id": [0, 1, 2], "category_id": [2, 2, 0],
+                       "price": [1.0, 2.5, 3.0], "average_review_rating": [4.0, 3.5, 1.0]})
+    want = [df[c].to_numpy() for c in TwoTowerModel._FAST_ID_COLS + TwoTowerModel._FAST_NUM_COLS]
+
+    class Lookup:
+        def __init__(self, f):
+            self.f = f
+
+        def __len__(self):
+            return len(self.f)
+
+        def __getitem__(self, key):
+            return self.f[key]
+
+    class Arr(np.ndarray):
+        def __getitem__(self, key):
+            return df[key] if isinstance(key, (str, list)) else super().__getitem__(key)
+
+    for cand in (df, Lookup(df), df["itemId"].to_numpy().view(Arr)):
+        got = tt._fast_columns(cand)
+        assert got is not None and all(np.array_equal(g.to_numpy(), w) for g, w in zip(got, want))
+    assert tt._fast_columns(df.iloc[:0]) is None
+    assert tt._fast_columns(df.drop(columns="price")) is None
+    assert tt._fast_columns(Lookup(df.drop(columns="category_id"))) is None
+    assert tt._fast_columns(pd.concat([df, df[["price"]]], axis=1)) is None
+    assert tt._fast_columns(df["itemId"].to_numpy()) is None   # a plain id array: no column lookups
+    assert tt._fast_columns({"itemId": df["itemId"]}) is None
