@@ -94,10 +94,11 @@ constexpr size_t kHsMaxLds = 160 * 1024 - 256;  // the stamp build's static per-
 constexpr size_t kHsMaxLds = 160 * 1024;
 #endif
 
-// HS_FILTER: LDS bytes before the staged survivors (users, bounds, counts,
-// overflow marks, the staging counter), 16-B aligned
+// HS_FILTER: LDS bytes before the staged survivors (live users' rows, their
+// bounds, per-user counts and overflow marks, the staging and live counters,
+// the slot -> user map), 16-B aligned
 __host__ __device__ inline size_t hs_filter_head(int UB, int row_b) {
-  return ((size_t)UB * row_b + (size_t)UB * 12 + 4 + 15) & ~(size_t)15;
+  return ((size_t)UB * row_b + (size_t)UB * 16 + 8 + 15) & ~(size_t)15;
 }
 
 // f32 -> bf16 bits, round to nearest even (NaN stays NaN): hrec_f32_to_bf16.
@@ -185,14 +186,19 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
   uint32_t* mmk = reinterpret_cast<uint32_t*>(dsm + (size_t)a.UB * kRowB);  // [UB][2]: ~key(min), key(max)
   // HS_PRUNE: [UB] key(max) << 32 | ~slice (ds_max_u64: the larger max, then the earlier slice)
   unsigned long long* amk = reinterpret_cast<unsigned long long*>(dsm + (size_t)a.UB * kRowB + (size_t)a.UB * 8);
-  // HS_FILTER (in place of the two above): [UB] bounds, [UB] survivor counts
-  // (then list bases), [UB] overflow marks, the staging counter, then the
+  // HS_FILTER (in place of the two above): [UB] bounds per slot, [UB]
+  // survivor counts per user (then list bases), [UB] overflow marks per user,
+  // the staging counter, the live-user counter, [UB] slot -> user, then the
   // staged survivors (meta = user << 24 | item offset in the group, score,
-  // rank among the user's survivors of the block)
+  // rank among the user's survivors of the block). Only the users whose
+  // bound for this group is live are staged, packed into the first slots, so
+  // the MFMA chunks cover ceil(live / CU) chunks instead of the whole tile.
   float* ths = reinterpret_cast<float*>(dsm + (size_t)a.UB * kRowB);
   int* cnt_l = reinterpret_cast<int*>(ths + a.UB);
   int* ovf_l = cnt_l + a.UB;
   int* bn = ovf_l + a.UB;
+  int* n_live_l = bn + 1;
+  int* smap = bn + 2;
   uint32_t* sb_meta = reinterpret_cast<uint32_t*>(dsm + hs_filter_head(a.UB, kRowB));
   float* sb_val = reinterpret_cast<float*>(sb_meta + a.sbuf);
   int* sb_rank = reinterpret_cast<int*>(sb_val + a.sbuf);
@@ -243,6 +249,36 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       for (int t = 0; t < NI; ++t) it_f[ks][t].f = hs_sbuf_load(rsrc, vnext[t], voff + 64 * ks, 0, 0);
   }
 
+  // HS_FILTER: the tile's live users (bound finite, or NaN = admit all) get
+  // the first slots; rows staged and MFMA chunks run for those alone
+  int n_st = ub;  // rows staged (slots)
+  if constexpr (MODE == HS_FILTER) {
+    if (threadIdx.x == 0) *n_live_l = 0;
+    __syncthreads();
+    float t = __builtin_nanf("");
+    int slot = -1;
+    if ((int)threadIdx.x < ub) {
+      t = a.theta[(int64_t)(b0 + threadIdx.x) * a.G + grp];
+      // +inf: a dead (user, group) — nothing passes; NaN admits every score
+      t = t == t ? (t == __builtin_inff() ? __builtin_nanf("") : t) : -__builtin_inff();
+      if (t == t) slot = atomicAdd(n_live_l, 1);
+    }
+    __syncthreads();
+    n_st = *n_live_l;
+    if (slot >= 0) {
+      ths[slot] = t;
+      smap[slot] = (int)threadIdx.x;
+    }
+    for (int o = threadIdx.x; o < a.UB; o += kHsThreads) {
+      if (o >= n_st) ths[o] = __builtin_nanf("");  // padding slots: nothing passes
+      cnt_l[o] = 0;
+      ovf_l[o] = 0;
+    }
+    if (threadIdx.x == 0) *bn = 0;
+    __syncthreads();
+  }
+  auto src_row = [&](int r) { return MODE == HS_FILTER ? smap[r] : r; };
+
   // users of the tile -> LDS as bf16 (zero rows / columns beyond the batch /
   // width). Batches of chunks (8 floats each) per thread: all loads are
   // issued before the first conversion (16-B loads when the row allows).
@@ -252,7 +288,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
     // by all 32 CUs at once), and the whole tile is in flight at once at d >= 128
     const char* src = reinterpret_cast<const char*>(a.uop) + ((int64_t)model * a.B + b0) * (DK * 2);
     constexpr int kBatch = HREC_HS_STAGE_BATCH;
-    const int n_chunks = a.UB * S::kChunks;
+    const int n_chunks = (MODE == HS_FILTER ? n_st : a.UB) * S::kChunks;
     const int rot = HREC_HS_STAGE_ROT ? (int)((blockIdx.x >> 3) & 15) * (n_chunks >> 4) : 0;
     for (int o0 = threadIdx.x; o0 < n_chunks; o0 += kBatch * kHsThreads) {
       int4 v[kBatch];
@@ -262,8 +298,8 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         o = o >= n_chunks ? o - n_chunks : o;
         const int r = o / S::kChunks, q = o % S::kChunks;
         v[j] = int4{0, 0, 0, 0};
-        if (o0 + j * kHsThreads < n_chunks && r < ub)
-          v[j] = *reinterpret_cast<const int4*>(src + (int64_t)r * (DK * 2) + 16 * q);
+        if (o0 + j * kHsThreads < n_chunks && r < n_st)
+          v[j] = *reinterpret_cast<const int4*>(src + (int64_t)src_row(r) * (DK * 2) + 16 * q);
       }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
@@ -290,8 +326,8 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
         const int r = o / S::kChunks, q = o % S::kChunks;
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[j][e] = 0.f;
-        if (o < n_chunks && r < ub && 8 * q < wd) {
-          const int64_t row = rws ? rws[b0 + r] : (int64_t)(b0 + r);
+        if (o < n_chunks && r < n_st && 8 * q < wd) {
+          const int64_t row = rws ? rws[b0 + src_row(r)] : (int64_t)(b0 + src_row(r));
           const float* p = src + row * ld + 8 * q;
           if (row < 0 || row >= a.n_rows[model]) {  // unknown / stale row: NaN scores (as hrec_als_score's -1)
 #pragma unroll
@@ -323,20 +359,7 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       }
     }
   }
-  if constexpr (MODE == HS_FILTER) {
-    for (int o = threadIdx.x; o < a.UB; o += kHsThreads) {
-      float t = __builtin_nanf("");  // absent user: nothing passes
-      if (o < ub) {
-        t = a.theta[(int64_t)(b0 + o) * a.G + grp];
-        // +inf: a dead (user, group) — nothing passes; NaN admits every score
-        t = t == t ? (t == __builtin_inff() ? __builtin_nanf("") : t) : -__builtin_inff();
-      }
-      ths[o] = t;
-      cnt_l[o] = 0;
-      ovf_l[o] = 0;
-    }
-    if (threadIdx.x == 0) *bn = 0;
-  } else {
+  if constexpr (MODE != HS_FILTER) {
     for (int o = threadIdx.x; o < 2 * a.UB; o += kHsThreads) mmk[o] = 0u;
     if (MODE == HS_PRUNE)
       for (int o = threadIdx.x; o < a.UB; o += kHsThreads) amk[o] = 0ull;
@@ -357,7 +380,9 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       lo[ch][u] = __builtin_inff(), hi[ch][u] = -__builtin_inff();
       if constexpr (MODE == HS_PRUNE) hp[ch][u] = -1;
     }
-  if (work) {
+  // HS_FILTER: MFMA chunks over the live slots only
+  const int nch = MODE == HS_FILTER ? (n_st + CU - 1) / CU : NCH;
+  if (work && nch > 0) {
     HsFrag ua[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
@@ -376,7 +401,8 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
       };
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        const bool last = ch == NCH - 1;
+        if (MODE == HS_FILTER && ch >= nch) break;
+        const bool last = ch == nch - 1;
         const int ch_next = last ? 0 : ch + 1;
         hs_f4 acc[NU][NI];
 #pragma unroll
@@ -452,14 +478,15 @@ __global__ __launch_bounds__(kHsThreads) void hyb_scores_kernel(HybScoresArgs a)
                 for (int r = 0; r < 4; ++r) {
                   const int64_t j = jb + 16 * t + 4 * g + r;
                   if ((full || j < i1) && acc[u][t][r] >= th) {
+                    const int ul = smap[bl];  // slot -> the user's place in the tile
                     const int e = atomicAdd(bn, 1);
-                    const int rk = atomicAdd(&cnt_l[bl], 1);
+                    const int rk = atomicAdd(&cnt_l[ul], 1);
                     if (e < a.sbuf) {
-                      sb_meta[e] = ((uint32_t)bl << 24) | (uint32_t)(j - i0);
+                      sb_meta[e] = ((uint32_t)ul << 24) | (uint32_t)(j - i0);
                       sb_val[e] = acc[u][t][r];
                       sb_rank[e] = rk;
                     } else {
-                      ovf_l[bl] = 1;  // staging full: the user's list is marked overflowing at the flush
+                      ovf_l[ul] = 1;  // staging full: the user's list is marked overflowing at the flush
                     }
                   }
                 }

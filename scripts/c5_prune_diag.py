@@ -75,6 +75,19 @@ def main():
     lb = anp.repeat_interleave(gs, 1)[:, :n_items]
     grp = (0.8 * tn + 0.2 * lb >= f5).sum(1).double()
     print("exact tau + per-group(%d) light max: mean %.1f max %.0f" % (G, grp.mean(), grp.max()))
+    # the bound kernel's theta [B][G] (workspace after part / argpos / uop,
+    # each rounded to 256 B: csrc/hybrid_prune.hip hp_layout)
+    Gk = min(max((n_items + 255) // 256, 1), 128)
+    r256 = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    off = r256(2 * Gk * 2 * B * 4) + r256(2 * Gk * B * 4) + r256(2 * B * rec.V_op.shape[1] * 2)
+    th = hp.ws[off: off + B * Gk * 4].view(torch.float32).view(B, Gk)
+    live = torch.isfinite(th)
+    print("theta live (user, group) pairs %d of %d (%.2f%%); live groups/user mean %.1f max %d" % (
+        live.sum(), B * Gk, 100.0 * live.float().mean(), live.sum(1).float().mean(), live.sum(1).max()))
+    ch = live.view(-1, 64, Gk).any(1) if B % 64 == 0 else None
+    if ch is not None:
+        print("live (64-user chunk, group) tiles %d of %d" % (ch.sum(), ch.numel()))
+    print("groups live for any user %d of %d" % (live.any(0).sum(), Gk))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(20):
