@@ -137,6 +137,9 @@ int hs_slice_tiles(int dk);  // item tiles of 16 per wave slice (a slice = 16 * 
 // the list-overflow flag (cn[b] > cap -> *flag = 1).
 int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, const float* thr,
                    int thr_stride, int64_t thr_per, int cap, float* cv, int64_t* ci, int* cn, hipStream_t s);
+// the resident-user scores with at most ub_cap users per block (more blocks)
+int dot_scores_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, float* out, int64_t ldo,
+                   hipStream_t s, int ub_cap = 0);
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s);
 // csrc/dot_gemv.hip: the few-user (B <= 4) streaming scoring kernel, same
 // contract as the matrix-core launch of csrc/dot_topk.hip (FILTER: the

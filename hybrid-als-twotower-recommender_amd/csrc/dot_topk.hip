@@ -696,11 +696,13 @@ template <bool FILTER>
 static int dot_launch_res(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk,
                           int bf16, float* out, int64_t ldo, const float* thr, int thr_stride, int cap, float* cv,
                           int64_t* ci, int* cn, int64_t off, hipStream_t s, int64_t thr_per = 0,
-                          int inf_none = 0) {
+                          int inf_none = 0, int ub_cap = 0) {
   const int row_b = dk * (bf16 ? 2 : 4);
   const int row_lds = row_b >= 256 ? row_b : row_b + 16;
   int ub_max = kResUserBytes / row_lds;
+  if (ub_cap > 0 && ub_max > ub_cap) ub_max = ub_cap;  // more user tiles: more blocks for a short item range
   ub_max = ub_max / (16 * kResNU) * (16 * kResNU);
+  if (ub_max < 16 * kResNU) ub_max = 16 * kResNU;
   const int n_ut = (B + ub_max - 1) / ub_max;
   int UB = (B + n_ut - 1) / n_ut;
   UB = (UB + 16 * kResNU - 1) / (16 * kResNU) * (16 * kResNU);
@@ -791,6 +793,19 @@ int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk,
   }
   return dot_launch_res<true>(U, B, V, n_items, n_items, 1, dk, bf16, nullptr, 0, thr, thr_stride, cap, cv, ci, cn, 0,
                               s, thr_per, 1);
+}
+
+// Scores of the resident-user kernel with at most ub_cap users per block
+// (the pruned ALS top-k's sample: 8192 items are too few tiles to fill the
+// chip with the full 128 KiB of resident users).
+int dot_scores_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, float* out, int64_t ldo,
+                   hipStream_t s, int ub_cap) {
+  if (!bf16 && dk > 128) {
+    set_error("dot_scores_run: f32 operands need dk <= 128");
+    return HREC_E_INVALID;
+  }
+  return dot_launch_res<false>(U, B, V, n_items, n_items, 1, dk, bf16, out, ldo, nullptr, 0, 0, nullptr, nullptr,
+                               nullptr, 0, s, 0, 0, ub_cap);
 }
 
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s) {

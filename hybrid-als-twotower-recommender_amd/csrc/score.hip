@@ -1310,6 +1310,359 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
   return topk_rows<float>(cv, n_users, kCap, kCap, kk, out_idx, out_val, fws, (size_t)1 << 62, s, ci, cn);
 }
 
+// ---------------------------------------------------- K2p: pruned ALS top-k
+// hrec_als_score_topk's result (the stable top-k of the JVM-exact scores)
+// without the exact chain over every pair: the scores are first bounded on
+// the bf16 matrix cores, and the exact chain runs only for the pairs the
+// bound cannot rule out.
+//   bf16 operands (round to nearest even: |x - bf16(x)| <= 2^-9 |x|) give
+//   s~ = sum uh_c vh_c with |s~ - u.v| <= (2^-8 + 2^-18 + k 2^-24 (1 + 2^-8))
+//   sum |u_c v_c| (the f32 accumulation of k exact products, any order), and
+//   the JVM chain is within 2k 2^-24 sum |u_c v_c| of u.v; for k <= 256 both
+//   fit in E_b = (2^-8 + 2^-13) ||u_b|| max_j ||v_j|| (+ 1e-30 for products
+//   the matrix cores may flush).
+//   1. tau_b: the kk-th best s~ over the first 8192 items (bf16 dot on the
+//      matrix cores, the fused path's lane-maxima bound) minus E_b, rounded
+//      down: kk items have chain >= s~ - E_b >= tau_b, so the kk-th best
+//      chain over all items is >= tau_b;
+//   2. the bf16 filter (K8 hrec_dot_filter's kernel) at tau_b - E_b keeps
+//      every item whose chain can reach tau_b;
+//   3. the JVM chain over the kept items; those >= tau_b are the candidates,
+//      a superset of the top kk, ranked by the same stable top-k as the
+//      fused path (ties -> smaller item).
+// Users whose bound is not finite (a non-finite factor anywhere) or whose
+// kept list overflows raise *overflow: the caller's fallback (the
+// materialised scores + hrec_topk_f32) answers the call, as for the fused
+// path's list overflow. Unknown users (row < 0) keep no candidates, as there.
+constexpr double kPruneRel = 0x1p-8 + 0x1p-13;
+constexpr double kPruneAbs = 1e-30;
+// items of the bf16 sample bound (measured: 4096 / 8192 / 16384 / 32768 items
+// -> 160 / 144 / 145 / 153 us per 1024 x 100k batch; a larger sample writes
+// more scores than its tighter bound saves in the filter)
+constexpr int kPruneSample = 8192;
+// resident users per block of the sample's dot (the full 128 KiB of users
+// leaves 16 blocks for 8192 items: 64 -> 144 us, 128 -> 148, 256 -> 154;
+// the filter over all items keeps the kernel's own tile, capping it measured
+// no faster)
+constexpr int kPruneSampleUB = 64;
+
+__device__ __forceinline__ float pr_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, INFINITY);
+  return f;
+}
+__device__ __forceinline__ float pr_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -INFINITY);
+  return f;
+}
+__device__ __forceinline__ uint16_t pr_bf16(float v) {  // round to nearest even (NaN stays NaN)
+  const uint32_t x = __float_as_uint(v);
+  if ((x & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((x >> 16) | 0x40u);
+  return (uint16_t)((x + 0x7fffu + ((x >> 16) & 1u)) >> 16);
+}
+
+// Item operand: bf16 rows [N][dk] (zero beyond k) and the largest row norm
+// rounded up (+inf for a non-finite value), one thread per row.
+__global__ __launch_bounds__(256) void als_items_bf16_kernel(const float* __restrict__ V, int64_t ldv, int64_t N,
+                                                             int k, int dk, uint16_t* __restrict__ out,
+                                                             unsigned* __restrict__ max_norm) {
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double ss = 0.0;
+  bool bad = false;
+  if (row < N) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + row * dk);
+    for (int c = 0; c < dk; c += 2) {
+      const float v0 = c < k ? V[row * ldv + c] : 0.f;
+      const float v1 = c + 1 < k ? V[row * ldv + c + 1] : 0.f;
+      ss += (double)v0 * v0 + (double)v1 * v1;
+      bad = bad || !isfinite(v0) || !isfinite(v1);
+      o[c >> 1] = (uint32_t)pr_bf16(v0) | ((uint32_t)pr_bf16(v1) << 16);
+    }
+  }
+  const double nrm = sqrt(ss) * (1.0 + 1e-6);
+  unsigned f = __float_as_uint((bad || !(nrm < 0x1p60)) ? INFINITY : pr_up(nrm));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned o = (unsigned)__shfl_xor((int)f, off, kWave);
+    f = o > f ? o : f;  // non-negative floats order as their bits
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(max_norm, f);
+}
+
+// Per user (one wave): the bf16 user operand and E_b (+inf: no usable bound,
+// NaN: unknown user).
+__global__ __launch_bounds__(256) void als_prune_user_kernel(const float* __restrict__ U, int kp,
+                                                             const int64_t* __restrict__ user_rows, int n_users,
+                                                             int k, int dk, const float* __restrict__ max_norm,
+                                                             uint16_t* __restrict__ uop, double* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= n_users) return;  // wave-uniform
+  const int64_t r = user_rows[b];
+  double ss = 0.0;
+  bool bad = false;
+  for (int c = lane; c < dk; c += 64) {
+    const float v = (r >= 0 && c < k) ? U[r * kp + c] : 0.f;
+    ss += (double)v * v;
+    bad = bad || !isfinite(v);
+    uop[(int64_t)b * dk + c] = pr_bf16(v);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    ss += __shfl_xor(ss, off, kWave);
+    bad = bad || __shfl_xor((int)bad, off, kWave);
+  }
+  if (lane == 0) {
+    const double e = kPruneRel * (sqrt(ss) * (1.0 + 1e-6)) * (double)max_norm[0] + kPruneAbs;
+    err[b] = r < 0 ? __builtin_nan("") : ((bad || !(e < 0x1p100)) ? INFINITY : e);
+  }
+}
+
+// Per user: tau_b = down(t_b - E_b) for the exact test, down(tau_b - E_b)
+// for the bf16 filter; the candidate counter zeroed.
+__global__ __launch_bounds__(256) void als_prune_thr_kernel(int n_users, const float* __restrict__ thr,
+                                                            int thr_stride, const double* __restrict__ err,
+                                                            float* __restrict__ tau, float* __restrict__ thr2,
+                                                            int* __restrict__ cn, int* __restrict__ overflow) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= n_users) return;
+  cn[b] = 0;
+  const double e = err[b];
+  float t1 = INFINITY, t2 = INFINITY;  // unknown user / no bound: nothing passes
+  if (e == e) {
+    const double t = thr[(int64_t)b * thr_stride];
+    const double lo1 = t - e;
+    const double lo2 = (double)pr_down(lo1) - e;
+    if (isfinite(t) && isfinite(e) && isfinite(lo2)) {
+      t1 = pr_down(lo1);
+      t2 = pr_down(lo2);
+      if (!isfinite(t2)) t2 = -FLT_MAX;  // below every finite f32 score
+      if (!isfinite(t1)) t1 = -FLT_MAX;
+    } else {
+      atomicOr(overflow, 1);  // no usable bound: the caller's exact fallback
+    }
+  }
+  tau[b] = t1;
+  thr2[b] = t2;
+}
+
+// The exact JVM chain for every pair the bf16 filter kept (one block per
+// user; a thread per candidate; the item's row-major factors as 16-B loads),
+// appended to the candidate lists when it reaches tau_b. Steps c in
+// [k, 4 ceil(k / 4)) add the fused kernel's zero products (its rank loop
+// runs in steps of 4). A kept list past the cap raises *overflow here.
+__global__ __launch_bounds__(256) void als_rescore_kernel(const float* __restrict__ U, int kp,
+                                                          const int64_t* __restrict__ user_rows, int n_users, int k,
+                                                          const float* __restrict__ V, int64_t ldv,
+                                                          const int64_t* __restrict__ pre_i,
+                                                          const int* __restrict__ pre_n, int cap,
+                                                          const float* __restrict__ tau,
+                                                          float* __restrict__ cand_v, int64_t* __restrict__ cand_i,
+                                                          int* __restrict__ cand_n, int* __restrict__ overflow) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) float su[kScoreKMax];
+  const int b = blockIdx.x;
+  const int64_t r = user_rows[b];
+  if (r < 0) return;  // block-uniform: no candidates were kept
+  if (threadIdx.x == 0 && pre_n[b] > cap) atomicOr(overflow, 1);
+  for (int c = threadIdx.x; c < kp; c += blockDim.x) su[c] = c < k ? U[r * kp + c] : 0.f;
+  __syncthreads();
+  const int n = pre_n[b] < cap ? pre_n[b] : cap;
+  const float t = tau[b];
+  const int kr = (k + 3) & ~3;
+  const int lane = threadIdx.x & 63;
+  const bool vec = (ldv & 3) == 0 && ((uintptr_t)V & 15) == 0;
+  for (int e0 = 0; e0 < n; e0 += blockDim.x) {  // block-uniform trip count: the ballots see whole waves
+    const int e = e0 + threadIdx.x;
+    float acc = 0.f;
+    int64_t j = -1;
+    if (e < n) {
+      j = pre_i[(int64_t)b * cap + e];
+      const float* v = V + j * ldv;
+      int c = 0;
+      if (vec) {
+        for (; c + 4 <= k; c += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(v + c);
+          acc = acc + su[c] * x.x;
+          acc = acc + su[c + 1] * x.y;
+          acc = acc + su[c + 2] * x.z;
+          acc = acc + su[c + 3] * x.w;
+        }
+      }
+      for (; c < k; ++c) acc = acc + su[c] * v[c];
+      for (; c < kr; ++c) acc = acc + 0.f * 0.f;
+    }
+    const bool pass = e < n && acc >= t;
+    const uint64_t m = __ballot(pass);
+    if (m == 0) continue;
+    int base = 0;
+    const int leader = __builtin_ctzll(m);
+    if (lane == leader) {
+      base = atomicAdd(&cand_n[b], __popcll(m));
+      if (base + __popcll(m) > cap) atomicOr(overflow, 1);
+    }
+    base = __shfl(base, leader, kWave);
+    if (pass) {
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pos < cap) {
+        cand_v[(int64_t)b * cap + pos] = acc;
+        cand_i[(int64_t)b * cap + pos] = j;
+      }
+    }
+  }
+}
+
+static int prune_dk(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : (k <= 128 ? 128 : 256)); }
+
+extern "C" size_t hrec_als_items_bf16_bytes(int64_t n_items, int k) {
+  const int64_t n = n_items > 0 ? n_items : 0;
+  return (((size_t)n * prune_dk(k) * 2 + 255) & ~(size_t)255) + 256;
+}
+
+extern "C" int hrec_als_items_bf16(const float* item_factors, int64_t ld_v, int64_t n_items, int k, void* out,
+                                   size_t out_bytes, void* stream) {
+  HREC_REQUIRE(k >= 1 && k <= kScoreKMax && n_items >= 0 && ld_v >= k, "als_items_bf16: bad shape");
+  HREC_REQUIRE(out && out_bytes >= hrec_als_items_bf16_bytes(n_items, k) && ((uintptr_t)out & 255) == 0,
+               "als_items_bf16: output must be 256-B aligned, %zu bytes", hrec_als_items_bf16_bytes(n_items, k));
+  HREC_REQUIRE(n_items == 0 || item_factors, "als_items_bf16: null factors");
+  hipStream_t s = as_stream(stream);
+  const int dk = prune_dk(k);
+  unsigned* nrm = reinterpret_cast<unsigned*>(static_cast<char*>(out) + hrec_als_items_bf16_bytes(n_items, k) - 256);
+  if (hipMemsetAsync(nrm, 0, 4, s) != hipSuccess) return check_launch("als_items_bf16: memset");
+  if (n_items == 0) return HREC_OK;
+  hipLaunchKernelGGL(als_items_bf16_kernel, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s, item_factors,
+                     ld_v, n_items, k, dk, static_cast<uint16_t*>(out), nrm);
+  return check_launch("als_items_bf16_kernel");
+}
+
+// Workspace of the pruned path, in carve order (src/_hrec.py
+// als_topk_pruned_counts reads the two counters).
+struct PruneWs {
+  float* samp;   // [B][S] bf16 sample scores
+  char* tws;     // sample top-k workspace (kk > 64)
+  float* sv;     // [B][kk] the sample's bound(s)
+  int64_t* si;   // [B][kk]
+  double* err;   // [B] E_b
+  float* tau;    // [B]
+  float* thr2;   // [B]
+  uint16_t* uop; // [B][dk]
+  float* pv;     // [B][cap] bf16 filter's kept pairs
+  int64_t* pi;
+  int* pn;       // [B]
+  float* cv;     // [B][cap] candidates (chain >= tau)
+  int64_t* ci;
+  int* cn;       // [B]
+  char* fws;     // final top-k workspace
+  size_t total;
+};
+
+static PruneWs prune_layout(char* base, int B, int64_t N, int kk, int dk) {
+  PruneWs w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* r = base ? base + off : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+    return r;
+  };
+  const int64_t S = N < kPruneSample ? N : kPruneSample;
+  w.samp = (float*)take((size_t)B * S * 4);
+  w.tws = take(topk_ws_bytes(B, S, kk, 4));
+  w.sv = (float*)take((size_t)B * kk * 4);
+  w.si = (int64_t*)take((size_t)B * kk * 8);
+  w.err = (double*)take((size_t)B * 8);
+  w.tau = (float*)take((size_t)B * 4);
+  w.thr2 = (float*)take((size_t)B * 4);
+  w.uop = (uint16_t*)take((size_t)B * dk * 2);
+  w.pv = (float*)take((size_t)B * kCap * 4);
+  w.pi = (int64_t*)take((size_t)B * kCap * 8);
+  w.pn = (int*)take((size_t)B * 4);
+  w.cv = (float*)take((size_t)B * kCap * 4);
+  w.ci = (int64_t*)take((size_t)B * kCap * 8);
+  w.cn = (int*)take((size_t)B * 4);
+  w.fws = take(topk_ws_bytes(B, kCap, kk, 4));
+  w.total = off + 256;
+  return w;
+}
+
+extern "C" size_t hrec_als_score_topk_pruned_workspace_bytes(int n_users, int64_t n_items, int top_k, int k) {
+  const int B = n_users > 0 ? n_users : 0;
+  const int64_t N = n_items > 0 ? n_items : 0;
+  int kk = (int)(top_k < N ? top_k : N);
+  kk = kk < 1 ? 1 : (kk > 1024 ? 1024 : kk);
+  const size_t fused = hrec_als_score_topk_workspace_bytes(n_users, n_items, top_k);  // the small-catalogue path
+  const size_t own = prune_layout(nullptr, B, N, kk, prune_dk(k)).total;
+  return own > fused ? own : fused;
+}
+
+extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64_t* user_rows, int n_users,
+                                          const float* item_factors_t, int64_t ld_items, const float* item_factors,
+                                          int64_t ld_v, const void* items_bf16, int64_t n_items, int k, int kp,
+                                          int top_k, int64_t* out_idx, float* out_val, int* overflow,
+                                          void* workspace, size_t workspace_bytes, void* stream) {
+  HREC_REQUIRE(hrec_factor_ld_ok(kp), "als_score_topk_pruned: kp must be 16, 32, 64, 96, 128, 192 or 256");
+  HREC_REQUIRE(k >= 1 && k <= kp, "als_score_topk_pruned: need 1 <= k <= kp");
+  HREC_REQUIRE(n_users >= 0 && n_users < 65536 && n_items >= 0, "als_score_topk_pruned: bad shape");
+  HREC_REQUIRE(ld_items >= n_items && ld_items % 4 == 0 && ld_items < ((int64_t)1 << 29),
+               "als_score_topk_pruned: ld_items must be >= n_items, %% 4 and < 2^29");
+  HREC_REQUIRE(ld_v >= k, "als_score_topk_pruned: ld_v must be >= k");
+  HREC_REQUIRE(top_k >= 1 && top_k <= 1024, "als_score_topk_pruned: top_k must be in [1, 1024]");
+  if (n_users == 0 || n_items == 0) return HREC_OK;
+  HREC_REQUIRE(user_factors && user_rows && item_factors_t && item_factors && items_bf16 && out_idx && out_val &&
+                   overflow && workspace,
+               "als_score_topk_pruned: null pointer");
+  HREC_REQUIRE(((uintptr_t)items_bf16 & 255) == 0, "als_score_topk_pruned: items_bf16 must be 256-B aligned");
+  const size_t need = hrec_als_score_topk_pruned_workspace_bytes(n_users, n_items, top_k, k);
+  HREC_REQUIRE(workspace_bytes >= need, "als_score_topk_pruned: workspace %zu < %zu", workspace_bytes, need);
+  if (n_items <= kSample)  // small: the fused path scores everything anyway
+    return hrec_als_score_topk(user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, top_k,
+                               out_idx, out_val, overflow, workspace, workspace_bytes, stream);
+  hipStream_t s = as_stream(stream);
+  const int kk = (int)(top_k < n_items ? top_k : n_items);
+  const int dk = prune_dk(k);
+  const PruneWs w = prune_layout((char*)workspace, n_users, n_items, kk, dk);
+  const int64_t S = n_items < kPruneSample ? n_items : kPruneSample;
+  const float* max_norm = reinterpret_cast<const float*>(static_cast<const char*>(items_bf16) +
+                                                         hrec_als_items_bf16_bytes(n_items, k) - 256);
+  if (hipMemsetAsync(overflow, 0, sizeof(int), s) != hipSuccess) return check_launch("score_topk_pruned memset");
+  // 1) bf16 user operands and E_b; the sample's bf16 scores; its bound
+  hipLaunchKernelGGL(als_prune_user_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, user_factors, kp,
+                     user_rows, n_users, k, dk, max_norm, w.uop, w.err);
+  int rc = check_launch("als_prune_user_kernel");
+  if (rc) return rc;
+  rc = dot_scores_run(w.uop, n_users, items_bf16, S, dk, 1, w.samp, S, s, kPruneSampleUB);
+  if (rc) return rc;
+  const float* thr = w.sv + (kk - 1);
+  int thr_stride = kk;
+  if (kk <= 64) {  // the 64 lane maxima's kk-th (kk of the sample's scores reach it); zeroes pn
+    hipLaunchKernelGGL(sample_threshold_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, w.samp,
+                       (int64_t)n_users, S, kk, w.sv, w.pn);
+    rc = check_launch("sample_threshold_kernel");
+    thr = w.sv;
+    thr_stride = 1;
+  } else {
+    rc = topk_rows<float>(w.samp, n_users, S, S, kk, w.si, w.sv, w.tws, (size_t)1 << 62, s);
+    if (rc == HREC_OK && hipMemsetAsync(w.pn, 0, (size_t)n_users * 4, s) != hipSuccess)
+      return check_launch("score_topk_pruned memset");
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(als_prune_thr_kernel, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, n_users, thr,
+                     thr_stride, w.err, w.tau, w.thr2, w.cn, overflow);
+  rc = check_launch("als_prune_thr_kernel");
+  if (rc) return rc;
+  // 2) the matrix-core filter over every item at tau_b - E_b
+  rc = dot_filter_run(w.uop, n_users, items_bf16, n_items, dk, 1, w.thr2, 1, 0, kCap, w.pv, w.pi, w.pn, s);
+  if (rc) return rc;
+  // 3) the exact chain over the kept pairs -> candidates (chain >= tau_b)
+  hipLaunchKernelGGL(als_rescore_kernel, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp, user_rows,
+                     n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, w.cv, w.ci, w.cn, overflow);
+  rc = check_launch("als_rescore_kernel");
+  if (rc) return rc;
+  // 4) the same exact stable top-k over the candidates
+  return topk_rows<float>(w.cv, n_users, kCap, kCap, kk, out_idx, out_val, w.fws, (size_t)1 << 62, s, w.ci, w.cn);
+}
+
 extern "C" int hrec_rows_minmax_f32(const float* x, int64_t n_rows, int64_t n, int64_t ld, float* out, void* stream) {
   HREC_REQUIRE(n_rows >= 0 && n >= 0 && ld >= n, "rows_minmax: bad shape");
   if (n_rows == 0) return HREC_OK;

@@ -49,6 +49,11 @@ _SIGNATURES = {
     "hrec_als_score_topk_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32]),
     "hrec_als_score_topk": (_c_i32, [_vp, _vp, _c_i32, _vp, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
                                      _vp, _c_sz, _vp]),
+    "hrec_als_items_bf16_bytes": (_c_sz, [_c_i64, _c_i32]),
+    "hrec_als_items_bf16": (_c_i32, [_vp, _c_i64, _c_i64, _c_i32, _vp, _c_sz, _vp]),
+    "hrec_als_score_topk_pruned_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32, _c_i32]),
+    "hrec_als_score_topk_pruned": (_c_i32, [_vp, _vp, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _c_i32,
+                                            _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_topk_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "hrec_topk_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_topk_f64": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
@@ -399,6 +404,72 @@ def als_score_topk(user_factors, user_rows, item_factors_t, n_items, k, top_k, c
         scores = als_score(user_factors, user_rows, item_factors_t, None, n_items, k)
         return topk(scores, kk)
     return out_i, out_v
+
+
+def als_items_bf16(item_factors, k):
+    """The pruned ALS top-k's item operand (hrec_als_items_bf16): bf16 rows
+    [N][dk] + the largest row norm, one uint8 device buffer (once per item
+    matrix; item_factors row-major f32 [N, >= k])."""
+    n = int(item_factors.shape[0])
+    need = int(lib().hrec_als_items_bf16_bytes(n, int(k)))
+    out = torch.empty(need, dtype=torch.uint8, device=item_factors.device)
+    _check("hrec_als_items_bf16", lib().hrec_als_items_bf16(
+        _dev(item_factors, torch.float32, "item_factors"), item_factors.stride(0), n, int(k),
+        _vp(out.data_ptr()), need, _stream()))
+    return out
+
+
+def als_score_topk_pruned(user_factors, user_rows, item_factors_t, item_factors, items_bf16, n_items, k, top_k,
+                          check_overflow=True, overflow_out=None, workspace=None):
+    """als_score_topk with the bf16 matrix-core bound in front of the exact
+    chain (hrec_als_score_topk_pruned): the same (ids, scores). item_factors
+    is the row-major copy of item_factors_t, items_bf16 from als_items_bf16.
+    workspace (uint8 device, optional) is reused when large enough; the
+    overflow flag falls back to the full score matrix + top-k as
+    als_score_topk does."""
+    kp = user_factors.shape[1]
+    B = user_rows.numel()
+    kk = min(int(top_k), int(n_items))
+    dev = user_factors.device
+    if item_factors.stride(1) != 1 or item_factors.shape[0] < n_items:
+        raise HrecError("als_score_topk_pruned: item_factors must be row-major with >= n_items rows")
+    out_i = torch.empty((B, kk), dtype=torch.int64, device=dev)
+    out_v = torch.empty((B, kk), dtype=torch.float32, device=dev)
+    flag = overflow_out if overflow_out is not None else torch.empty(1, dtype=torch.int32, device=dev)
+    need = int(lib().hrec_als_score_topk_pruned_workspace_bytes(B, n_items, kk, int(k)))
+    ws = workspace if workspace is not None and workspace.numel() >= need else \
+        torch.empty(need, dtype=torch.uint8, device=dev)
+    _check("hrec_als_score_topk_pruned", lib().hrec_als_score_topk_pruned(
+        _dev(user_factors, torch.float32, "user_factors"), _dev(user_rows, torch.int64, "user_rows"), B,
+        _dev(item_factors_t, torch.float32, "item_factors_t"), item_factors_t.shape[1],
+        _dev(item_factors, torch.float32, "item_factors"), item_factors.stride(0),
+        _dev(items_bf16, torch.uint8, "items_bf16"), n_items, int(k), kp, kk,
+        _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float32, "out_val"),
+        _dev(flag, torch.int32, "overflow"), _dev(ws, torch.uint8, "ws"), ws.numel(), _stream()))
+    if check_overflow and int(flag.item()) != 0:
+        scores = als_score(user_factors, user_rows, item_factors_t, None, n_items, k)
+        return topk(scores, kk)
+    return out_i, out_v
+
+
+def als_topk_pruned_counts(ws, B, n_items, top_k, k):
+    """Diagnostics of the last als_score_topk_pruned call on workspace ws:
+    (pairs the bf16 bound kept per user, candidates per user), int32 [B]
+    each (hrec_als_score_topk_pruned's workspace layout, prune_layout in
+    csrc/score.hip: 256-B aligned carves)."""
+    kk = max(1, min(int(top_k), int(n_items), 1024))
+    S, cap = min(8192, int(n_items)), 4096
+    dk = 32 if k <= 32 else (64 if k <= 64 else (128 if k <= 128 else 256))
+    tws = int(lib().hrec_topk_workspace_bytes(B, S, kk, 0))
+    sizes = [B * S * 4, tws, B * kk * 4, B * kk * 8, B * 8, B * 4, B * 4, B * dk * 2,
+             B * cap * 4, B * cap * 8, B * 4, B * cap * 4, B * cap * 8, B * 4]
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 255) // 256 * 256
+    pn = ws[offs[10]: offs[10] + B * 4].view(torch.int32)
+    cn = ws[offs[13]: offs[13] + B * 4].view(torch.int32)
+    return pn.clone(), cn.clone()
 
 
 # ------------------------------------------------------------------ top-k

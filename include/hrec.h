@@ -194,6 +194,27 @@ int hrec_als_score_topk(const float* user_factors, const int64_t* user_rows,
                         float* out_val, int* overflow, void* workspace,
                         size_t workspace_bytes, void* stream);
 
+/* Pruned form of hrec_als_score_topk (same outputs, same overflow contract):
+ * the sample bound thr_b as there, then a bf16 matrix-core filter keeps
+ * every item with approx score >= thr_b - E, E = (2^-8 + 2^-13) ||u|| max
+ * ||v|| + 1e-30 (bounds |bf16 dot - JVM chain| for k <= 256), and the JVM
+ * chain over those items alone leaves exactly the fused filter's survivors
+ * (score >= thr_b), ranked by the same stable top-k. *overflow is also set
+ * when a bound is not finite (a non-finite factor) or the bf16 filter's list
+ * overflows. items_bf16: hrec_als_items_bf16 of item_factors (row-major
+ * [n_items, ld_v], the same values as item_factors_t), 256-B aligned; it is
+ * built once per item matrix. */
+size_t hrec_als_items_bf16_bytes(int64_t n_items, int k);
+int hrec_als_items_bf16(const float* item_factors, int64_t ld_v, int64_t n_items, int k,
+                        void* out, size_t out_bytes, void* stream);
+size_t hrec_als_score_topk_pruned_workspace_bytes(int n_users, int64_t n_items, int top_k, int k);
+int hrec_als_score_topk_pruned(const float* user_factors, const int64_t* user_rows, int n_users,
+                               const float* item_factors_t, int64_t ld_items,
+                               const float* item_factors, int64_t ld_v, const void* items_bf16,
+                               int64_t n_items, int k, int kp, int top_k, int64_t* out_idx,
+                               float* out_val, int* overflow, void* workspace,
+                               size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- top-k --
  * Stable descending top-k of each of n_rows rows (row i starts at
  * vals + i*row_stride, n elements): larger value first, equal values keep

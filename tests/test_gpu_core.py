@@ -409,6 +409,63 @@ def test_als_score_topk_overflow_flag(device):
     np.testing.assert_array_equal(val.cpu().numpy(), np.take_along_axis(full, exp_i, 1))
 
 
+@pytest.mark.parametrize("n_items,k,kp,B,top_k,case", [
+    (100_003, 64, 64, 40, 5, "normal"), (100_000, 64, 64, 17, 10, "quant"), (30_000, 16, 16, 9, 1, "normal"),
+    (50_000, 100, 128, 12, 100, "normal"), (40_000, 200, 256, 8, 8, "scaled"), (3000, 64, 64, 5, 5, "normal"),
+    (60_000, 64, 64, 10, 5, "unknown"), (60_000, 64, 64, 10, 5, "nan_item"), (60_000, 64, 64, 10, 5, "const")])
+def test_als_score_topk_pruned_matches_fused(device, n_items, k, kp, B, top_k, case):
+    """hrec_als_score_topk_pruned (bf16 matrix-core bound, exact chain only
+    for the pairs it keeps) returns the fused path's (ids, scores) bit for
+    bit, and both equal the stable top-k of the full JVM-exact matrix:
+    odd n, rank 16 / 64 / 100 (kp 128) / 200 (kp 256), top_k 1 .. 100,
+    quantised factors (ties), factors scaled by 1e6, an unknown user row
+    (the fused path's empty candidate list), a NaN item (no finite bound:
+    overflow -> the exact fallback) and constant items (list overflow)."""
+    h = _hrec()
+    rng = np.random.default_rng(n_items + k)
+    U = np.zeros((B, kp), np.float32)
+    V = np.zeros((n_items, kp), np.float32)
+    U[:, :k] = rng.normal(size=(B, k))
+    V[:, :k] = rng.normal(size=(n_items, k))
+    if case == "quant":
+        U[:, :k] = np.round(U[:, :k])
+        V[:, :k] = np.round(V[:, :k] * 0.5)
+    if case == "scaled":
+        U *= np.float32(1e6)
+    if case == "nan_item":
+        V[777, 3] = np.nan
+    if case == "const":
+        V[:, :k] = 0.25
+    dU = torch.as_tensor(U, device=device)
+    dV = torch.as_tensor(V, device=device)
+    Vt = h.transpose(dV)
+    rows = np.arange(B, dtype=np.int64)
+    if case == "unknown":
+        rows[3] = -1
+    users = torch.as_tensor(rows, device=device)
+    ops = h.als_items_bf16(dV, k)
+    flag_p = torch.full((1,), 7, dtype=torch.int32, device=device)
+    flag_f = torch.full((1,), 7, dtype=torch.int32, device=device)
+    pi, pv = h.als_score_topk_pruned(dU, users, Vt, dV, ops, n_items, k, top_k, check_overflow=False,
+                                     overflow_out=flag_p)
+    fi, fv = h.als_score_topk(dU, users, Vt, n_items, k, top_k, check_overflow=False, overflow_out=flag_f)
+    fp, ff = int(flag_p.item()), int(flag_f.item())
+    if case in ("nan_item", "const"):
+        assert fp == 1
+    else:
+        assert fp == ff == 0, (fp, ff)
+        np.testing.assert_array_equal(pi.cpu().numpy(), fi.cpu().numpy())
+        np.testing.assert_array_equal(pv.cpu().numpy().view(np.int32), fv.cpu().numpy().view(np.int32))
+    # with the fallback resolved, both equal the full matrix's stable top-k
+    pi, pv = h.als_score_topk_pruned(dU, users, Vt, dV, ops, n_items, k, top_k)
+    known = rows >= 0
+    full = oals.score_matrix(U[known, :k], V[:, :k])
+    exp_i = _np_stable_topk(full, min(top_k, n_items))
+    got_i, got_v = pi.cpu().numpy()[known], pv.cpu().numpy()[known]
+    np.testing.assert_array_equal(got_i, exp_i)
+    np.testing.assert_array_equal(got_v.view(np.int32), np.take_along_axis(full, exp_i, 1).view(np.int32))
+
+
 # ------------------------------------------------ multi-rank on one device
 def _chunked_worker(rank, world, port, chunks, q, balanced=False):
     import os
