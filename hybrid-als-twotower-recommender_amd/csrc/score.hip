@@ -1325,7 +1325,7 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
 //      matrix cores, the fused path's lane-maxima bound) minus E_b, rounded
 //      down: kk items have chain >= s~ - E_b >= tau_b, so the kk-th best
 //      chain over all items is >= tau_b;
-//   2. the bf16 filter (K8 hrec_dot_filter's kernel) at tau_b - E_b keeps
+//   2. the bf16 filter (als_bound_filter_kernel) at tau_b - E_b keeps
 //      every item whose chain can reach tau_b;
 //   3. the JVM chain over the kept items; those >= tau_b are the candidates,
 //      a superset of the top kk, ranked by the same stable top-k as the
@@ -1514,6 +1514,152 @@ __global__ __launch_bounds__(256) void als_rescore_kernel(const float* __restric
   }
 }
 
+// 2. The bf16 bound filter: block = (UBK users staged in LDS, 64 NI items),
+// wave = 16 NI items held in registers for the whole block, swept over the
+// users in chunks of 64 (v_mfma_f32_16x16x32_bf16: A = items, B = users, so
+// lane (g, c) holds user c and items 4 g + r). A pair passes when its s~
+// reaches the user's bound; survivors are rare (~0.1 %): they are staged in
+// LDS (LDS atomics) and leave at the block's end with one list reservation
+// per user (a returning global atomic per survivor in the loop serialised the
+// waves on its round trip: 84 us against 24 us of GEMM). Measured per
+// 1024 x 100k call (whole call): 2 blocks per CU and 2048 staged survivors
+// 130 us; 3 per CU / 1024 staged 138; 4 per CU 132; 1 per CU 161; the next
+// tile's fragments prefetched (186 VGPRs) 175.
+typedef __bf16 pr_bf8 __attribute__((ext_vector_type(8)));
+__host__ __device__ constexpr int prune_filter_users(int dk) { return dk <= 64 ? 256 : (dk == 128 ? 128 : 64); }
+typedef float pr_f4 __attribute__((ext_vector_type(4)));
+
+template <int DK>
+__global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* __restrict__ uop, int n_users,
+                                                               const uint16_t* __restrict__ items, int64_t N,
+                                                               const float* __restrict__ thr2, int cap,
+                                                               int64_t* __restrict__ pre_i, int* __restrict__ pre_n) {
+  constexpr int KS = DK / 32;
+  constexpr int NI = DK <= 64 ? 4 : (DK == 128 ? 2 : 1);
+  constexpr int UBK = prune_filter_users(DK);  // <= 36 KiB of users per block
+  constexpr int RB = DK * 2 + 16;  // padded LDS rows: the 16 lanes of a row group hit different banks
+  constexpr int CPR = DK / 8;      // 16-B chunks per user row
+  constexpr int kPer = UBK * CPR / 256;
+  static_assert(kPer * 256 == UBK * CPR, "whole chunks per thread");
+  constexpr int kSB = 2048;  // survivors a block stages (then one list reservation per user)
+  __shared__ __attribute__((aligned(16))) char us[UBK * RB];
+  __shared__ float sth[UBK];
+  __shared__ int s_cnt[UBK];
+  __shared__ int s_n;
+  __shared__ uint32_t s_item[kSB];
+  __shared__ int s_rank[kSB];
+  __shared__ uint16_t s_user[kSB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int n_ut = (n_users + UBK - 1) / UBK;
+  const int ut = (int)(blockIdx.x % (unsigned)n_ut);
+  const int64_t it0 = blockIdx.x / (unsigned)n_ut, it_step = gridDim.x / (unsigned)n_ut;
+  const int64_t n_it = (N + 64 * NI - 1) / (64 * NI);
+  const int b0 = ut * UBK;
+  const int ub = n_users - b0 < UBK ? n_users - b0 : UBK;
+  int4 fa[KS][NI];  // this item tile's fragments
+  auto load_items = [&](int64_t it, int4 (&fi)[KS][NI]) {
+    const int64_t j0 = it * (64 * NI) + 16 * NI * w;
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int64_t j = j0 + 16 * t + c;
+      const int64_t jr = j < N ? j : N - 1;  // rows past the end: a valid row, masked at the test
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        fi[ks][t] = *reinterpret_cast<const int4*>(items + jr * DK + 32 * ks + 8 * g);
+    }
+  };
+  if (it0 < n_it) load_items(it0, fa);  // in flight while the users are staged
+  {  // users -> LDS: every load of a thread in flight before its stores
+    int4 v[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      const int o = threadIdx.x + 256 * e, r = o / CPR, q = o % CPR;
+      v[e] = r < ub ? *reinterpret_cast<const int4*>(uop + (int64_t)(b0 + r) * DK + 8 * q) : int4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      const int o = threadIdx.x + 256 * e, r = o / CPR, q = o % CPR;
+      *reinterpret_cast<int4*>(us + r * RB + 16 * q) = v[e];
+    }
+  }
+  for (int o = threadIdx.x; o < UBK; o += 256) {
+    sth[o] = o < ub ? thr2[b0 + o] : __builtin_nanf("");
+    s_cnt[o] = 0;
+  }
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const int nch = (ub + 63) / 64;
+  auto tile = [&](int64_t it, int4 (&fi)[KS][NI]) {
+    if (it != it0) load_items(it, fi);
+    const int64_t j0 = it * (64 * NI) + 16 * NI * w;
+    for (int ch = 0; ch < nch; ++ch) {
+      pr_f4 acc[4][NI];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int t = 0; t < NI; ++t) acc[u][t] = pr_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        int4 uf[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          uf[u] = *reinterpret_cast<const int4*>(us + (64 * ch + 16 * u + c) * RB + 64 * ks + 16 * g);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int t = 0; t < NI; ++t)
+            acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pr_bf8, fi[ks][t]),
+                                                                __builtin_bit_cast(pr_bf8, uf[u]), acc[u][t], 0, 0,
+                                                                0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ul = 64 * ch + 16 * u + c;
+        const float th = sth[ul];  // NaN (absent user): nothing passes
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < NI; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (j0 + 16 * t + 4 * g + r < N) mx = fmaxf(mx, acc[u][t][r]);
+        if (__ballot(mx >= th) == 0) continue;
+#pragma unroll
+        for (int t = 0; t < NI; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t j = j0 + 16 * t + 4 * g + r;
+            if (j < N && acc[u][t][r] >= th) {
+              const int e = atomicAdd(&s_n, 1);  // LDS
+              if (e < kSB) {
+                s_item[e] = (uint32_t)j;
+                s_user[e] = (uint16_t)ul;
+                s_rank[e] = atomicAdd(&s_cnt[ul], 1);
+              } else {  // staging full: straight to the user's list
+                const int64_t b = b0 + ul;
+                const int p = atomicAdd(&pre_n[b], 1);
+                if (p < cap) pre_i[b * cap + p] = j;
+              }
+            }
+          }
+      }
+    }
+  };
+  for (int64_t it = it0; it < n_it; it += it_step) tile(it, fa);
+  // flush: one list reservation per user with staged survivors, then the entries
+  __syncthreads();
+  for (int o = threadIdx.x; o < ub; o += 256) {
+    const int k = s_cnt[o];
+    s_cnt[o] = k ? atomicAdd(&pre_n[b0 + o], k) : 0;
+  }
+  __syncthreads();
+  const int ne = s_n < kSB ? s_n : kSB;
+  for (int e = threadIdx.x; e < ne; e += 256) {
+    const int ul = s_user[e];
+    const int p = s_cnt[ul] + s_rank[e];
+    if (p < cap) pre_i[(int64_t)(b0 + ul) * cap + p] = (int64_t)s_item[e];
+  }
+}
+
 static int prune_dk(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : (k <= 128 ? 128 : 256)); }
 
 extern "C" size_t hrec_als_items_bf16_bytes(int64_t n_items, int k) {
@@ -1548,8 +1694,7 @@ struct PruneWs {
   float* tau;    // [B]
   float* thr2;   // [B]
   uint16_t* uop; // [B][dk]
-  float* pv;     // [B][cap] bf16 filter's kept pairs
-  int64_t* pi;
+  int64_t* pi;   // [B][cap] the bf16 filter's kept items
   int* pn;       // [B]
   float* cv;     // [B][cap] candidates (chain >= tau)
   int64_t* ci;
@@ -1575,7 +1720,6 @@ static PruneWs prune_layout(char* base, int B, int64_t N, int kk, int dk) {
   w.tau = (float*)take((size_t)B * 4);
   w.thr2 = (float*)take((size_t)B * 4);
   w.uop = (uint16_t*)take((size_t)B * dk * 2);
-  w.pv = (float*)take((size_t)B * kCap * 4);
   w.pi = (int64_t*)take((size_t)B * kCap * 8);
   w.pn = (int*)take((size_t)B * 4);
   w.cv = (float*)take((size_t)B * kCap * 4);
@@ -1652,8 +1796,29 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
   rc = check_launch("als_prune_thr_kernel");
   if (rc) return rc;
   // 2) the matrix-core filter over every item at tau_b - E_b
-  rc = dot_filter_run(w.uop, n_users, items_bf16, n_items, dk, 1, w.thr2, 1, 0, kCap, w.pv, w.pi, w.pn, s);
-  if (rc) return rc;
+  {
+    const unsigned n_ut = (unsigned)((n_users + prune_filter_users(dk) - 1) / prune_filter_users(dk));
+    const int per = dk <= 64 ? 256 : (dk == 128 ? 128 : 64);  // items per block round
+    // two blocks per CU; each block walks its user tile over
+    // every (grid / n_ut)-th item tile (the staged users serve several tiles)
+    const int64_t n_it = (n_items + per - 1) / per;
+    int64_t per_ut = (512 + (int64_t)n_ut - 1) / (int64_t)n_ut;
+    if (per_ut > n_it) per_ut = n_it;
+    const dim3 grid((unsigned)(n_ut * per_ut));
+    const uint16_t* io = static_cast<const uint16_t*>(items_bf16);
+    switch (dk) {
+      case 32: hipLaunchKernelGGL(als_bound_filter_kernel<32>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
+                                  w.thr2, kCap, w.pi, w.pn); break;
+      case 64: hipLaunchKernelGGL(als_bound_filter_kernel<64>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
+                                  w.thr2, kCap, w.pi, w.pn); break;
+      case 128: hipLaunchKernelGGL(als_bound_filter_kernel<128>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
+                                   w.thr2, kCap, w.pi, w.pn); break;
+      default: hipLaunchKernelGGL(als_bound_filter_kernel<256>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
+                                  w.thr2, kCap, w.pi, w.pn); break;
+    }
+    rc = check_launch("als_bound_filter_kernel");
+    if (rc) return rc;
+  }
   // 3) the exact chain over the kept pairs -> candidates (chain >= tau_b)
   hipLaunchKernelGGL(als_rescore_kernel, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp, user_rows,
                      n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, w.cv, w.ci, w.cn, overflow);

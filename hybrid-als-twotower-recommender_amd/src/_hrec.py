@@ -462,13 +462,13 @@ def als_topk_pruned_counts(ws, B, n_items, top_k, k):
     dk = 32 if k <= 32 else (64 if k <= 64 else (128 if k <= 128 else 256))
     tws = int(lib().hrec_topk_workspace_bytes(B, S, kk, 0))
     sizes = [B * S * 4, tws, B * kk * 4, B * kk * 8, B * 8, B * 4, B * 4, B * dk * 2,
-             B * cap * 4, B * cap * 8, B * 4, B * cap * 4, B * cap * 8, B * 4]
+             B * cap * 8, B * 4, B * cap * 4, B * cap * 8, B * 4]
     offs, o = [], 0
     for n in sizes:
         offs.append(o)
         o += (n + 255) // 256 * 256
-    pn = ws[offs[10]: offs[10] + B * 4].view(torch.int32)
-    cn = ws[offs[13]: offs[13] + B * 4].view(torch.int32)
+    pn = ws[offs[9]: offs[9] + B * 4].view(torch.int32)
+    cn = ws[offs[12]: offs[12] + B * 4].view(torch.int32)
     return pn.clone(), cn.clone()
 
 
