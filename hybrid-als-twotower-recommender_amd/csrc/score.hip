@@ -1521,7 +1521,10 @@ __global__ __launch_bounds__(256) void als_rescore_kernel(const float* __restric
 // reaches the user's bound; survivors are rare (~0.1 %): they are staged in
 // LDS (LDS atomics) and leave at the block's end with one list reservation
 // per user (a returning global atomic per survivor in the loop serialised the
-// waves on its round trip: 84 us against 24 us of GEMM). Measured per
+// waves on its round trip: 84 us against 24 us of GEMM); a lane's passing
+// pairs take one LDS reservation (a mask, then the entries), their per-user
+// ranks are counted at the flush (LDS atomics per survivor in the loop: 56 us
+// per launch against 46; the same launch without the survivor test: 16). Measured per
 // 1024 x 100k call (whole call): 2 blocks per CU and 2048 staged survivors
 // 130 us; 3 per CU / 1024 staged 138; 4 per CU 132; 1 per CU 161; the next
 // tile's fragments prefetched (186 VGPRs) 175.
@@ -1612,41 +1615,61 @@ __global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* _
                                                                 __builtin_bit_cast(pr_bf8, uf[u]), acc[u][t], 0, 0,
                                                                 0);
       }
+      const bool full = j0 + 16 * NI <= N;  // wave-uniform: every item of the wave in range
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int ul = 64 * ch + 16 * u + c;
         const float th = sth[ul];  // NaN (absent user): nothing passes
         float mx = -INFINITY;
+        if (full) {
 #pragma unroll
-        for (int t = 0; t < NI; ++t)
+          for (int t = 0; t < NI; ++t)
+            mx = fmaxf(mx, fmaxf(fmaxf(acc[u][t][0], acc[u][t][1]), fmaxf(acc[u][t][2], acc[u][t][3])));
+        } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (j0 + 16 * t + 4 * g + r < N) mx = fmaxf(mx, acc[u][t][r]);
+          for (int t = 0; t < NI; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (j0 + 16 * t + 4 * g + r < N) mx = fmaxf(mx, acc[u][t][r]);
+        }
         if (__ballot(mx >= th) == 0) continue;
+        {
+          // the lane's passing (t, r) as a mask; one LDS reservation per lane
+          uint32_t m = 0;
 #pragma unroll
-        for (int t = 0; t < NI; ++t)
+          for (int t = 0; t < NI; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int64_t j = j0 + 16 * t + 4 * g + r;
-            if (j < N && acc[u][t][r] >= th) {
-              const int e = atomicAdd(&s_n, 1);  // LDS
+            for (int r = 0; r < 4; ++r)
+              if (j0 + 16 * t + 4 * g + r < N && acc[u][t][r] >= th) m |= 1u << (4 * t + r);
+          if (m) {
+            int e = atomicAdd(&s_n, __popc(m));  // LDS
+            while (m) {
+              const int q = __builtin_ctz(m);
+              m &= m - 1;
+              const int64_t j = j0 + 16 * (q >> 2) + 4 * g + (q & 3);
               if (e < kSB) {
                 s_item[e] = (uint32_t)j;
                 s_user[e] = (uint16_t)ul;
-                s_rank[e] = atomicAdd(&s_cnt[ul], 1);
               } else {  // staging full: straight to the user's list
                 const int64_t b = b0 + ul;
                 const int p = atomicAdd(&pre_n[b], 1);
                 if (p < cap) pre_i[b * cap + p] = j;
               }
+              ++e;
             }
           }
+        }
       }
     }
   };
   for (int64_t it = it0; it < n_it; it += it_step) tile(it, fa);
   // flush: one list reservation per user with staged survivors, then the entries
   __syncthreads();
+  {  // ranks per user (LDS atomics, off the MFMA loop)
+    const int ne0 = s_n < kSB ? s_n : kSB;
+    for (int e = threadIdx.x; e < ne0; e += 256) s_rank[e] = atomicAdd(&s_cnt[s_user[e]], 1);
+    __syncthreads();
+  }
   for (int o = threadIdx.x; o < ub; o += 256) {
     const int k = s_cnt[o];
     s_cnt[o] = k ? atomicAdd(&pre_n[b0 + o], k) : 0;
