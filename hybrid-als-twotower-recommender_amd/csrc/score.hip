@@ -1683,6 +1683,113 @@ __global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* _
   }
 }
 
+// 3+4 fused for kk <= 8: the candidates stay in LDS and wave 0 ranks them
+// exactly as topk_wave_kernel does (per-lane sorted lists of KK, then kk
+// rounds of wave arg-best; absent entries -> (0, -1)), so the call skips the
+// list round trip and the top-k launch. cand_n[b] still counts the
+// candidates (the bench's diagnostics; > cap raises *overflow).
+template <int KK>
+__global__ __launch_bounds__(256) void als_rescore_topk_kernel(const float* __restrict__ U, int kp,
+                                                               const int64_t* __restrict__ user_rows, int n_users,
+                                                               int k, const float* __restrict__ V, int64_t ldv,
+                                                               const int64_t* __restrict__ pre_i,
+                                                               const int* __restrict__ pre_n, int cap,
+                                                               const float* __restrict__ tau, int kk,
+                                                               int64_t* __restrict__ out_idx,
+                                                               float* __restrict__ out_val, int* __restrict__ cand_n,
+                                                               int* __restrict__ overflow) {
+#pragma clang fp contract(off)
+  constexpr int kL = 2048;  // candidates kept in LDS (more: *overflow, the caller's fallback)
+  __shared__ __attribute__((aligned(16))) float su[kScoreKMax];
+  __shared__ float s_v[kL];
+  __shared__ int s_j[kL];
+  __shared__ int s_n;
+  const int b = blockIdx.x;
+  const int64_t r = user_rows[b];
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) s_n = 0;
+  if (r >= 0) {
+    if (threadIdx.x == 0 && pre_n[b] > cap) atomicOr(overflow, 1);
+    for (int c = threadIdx.x; c < kp; c += blockDim.x) su[c] = c < k ? U[r * kp + c] : 0.f;
+  }
+  __syncthreads();
+  if (r >= 0) {
+    const int n = pre_n[b] < cap ? pre_n[b] : cap;
+    const float t = tau[b];
+    const int kr = (k + 3) & ~3;
+    const bool vec = (ldv & 3) == 0 && ((uintptr_t)V & 15) == 0;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int64_t j = pre_i[(int64_t)b * cap + e];
+      const float* v = V + j * ldv;
+      float acc = 0.f;
+      int c = 0;
+      if (vec) {
+        for (; c + 4 <= k; c += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(v + c);
+          acc = acc + su[c] * x.x;
+          acc = acc + su[c + 1] * x.y;
+          acc = acc + su[c + 2] * x.z;
+          acc = acc + su[c + 3] * x.w;
+        }
+      }
+      for (; c < k; ++c) acc = acc + su[c] * v[c];
+      for (; c < kr; ++c) acc = acc + 0.f * 0.f;
+      if (acc >= t) {
+        const int p = atomicAdd(&s_n, 1);  // LDS
+        if (p < kL) {
+          s_v[p] = acc;
+          s_j[p] = (int)j;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int m = s_n;
+  if (threadIdx.x == 0) {
+    cand_n[b] = m;
+    if (m > kL || m > cap) atomicOr(overflow, 1);
+  }
+  if (threadIdx.x >= 64) return;  // wave 0 ranks
+  const int mm = m < kL ? m : kL;
+  float lv[KK];
+  int64_t li[KK];
+#pragma unroll
+  for (int q = 0; q < KK; ++q) {
+    lv[q] = 0.f;
+    li[q] = INT64_MAX;
+  }
+  for (int p = lane; p < mm; p += 64) {
+    float xv = s_v[p];
+    int64_t xi = s_j[p];
+#pragma unroll
+    for (int q = 0; q < KK; ++q) {
+      const bool sw = li[q] == INT64_MAX || better(xv, xi, lv[q], li[q]);
+      const float tv = lv[q];
+      const int64_t ti = li[q];
+      lv[q] = sw ? xv : tv;
+      li[q] = sw ? xi : ti;
+      xv = sw ? tv : xv;
+      xi = sw ? ti : xi;
+      if (xi == INT64_MAX) break;
+    }
+  }
+  for (int q = 0; q < kk; ++q) {
+    const KV<float> w = wave_best(KV<float>{lv[0], li[0]});
+    if (lane == 0) {
+      out_val[(int64_t)b * kk + q] = w.i == INT64_MAX ? 0.f : w.v;
+      out_idx[(int64_t)b * kk + q] = w.i == INT64_MAX ? -1 : w.i;
+    }
+    if (w.i != INT64_MAX && li[0] == w.i) {
+#pragma unroll
+      for (int x = 0; x + 1 < KK; ++x) {
+        lv[x] = lv[x + 1];
+        li[x] = li[x + 1];
+      }
+      li[KK - 1] = INT64_MAX;
+    }
+  }
+}
+
 static int prune_dk(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : (k <= 128 ? 128 : 256)); }
 
 extern "C" size_t hrec_als_items_bf16_bytes(int64_t n_items, int k) {
@@ -1842,7 +1949,19 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
     rc = check_launch("als_bound_filter_kernel");
     if (rc) return rc;
   }
-  // 3) the exact chain over the kept pairs -> candidates (chain >= tau_b)
+  // 3) the exact chain over the kept pairs -> candidates (chain >= tau_b);
+  //    kk <= 8: ranked in the same block
+  if (kk <= 8) {
+#define HREC_RTK(KK)                                                                                          \
+  hipLaunchKernelGGL(als_rescore_topk_kernel<KK>, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp,      \
+                     user_rows, n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, kk, out_idx, out_val, w.cn, \
+                     overflow)
+    if (kk <= 2) HREC_RTK(2);
+    else if (kk <= 4) HREC_RTK(4);
+    else HREC_RTK(8);
+#undef HREC_RTK
+    return check_launch("als_rescore_topk_kernel");
+  }
   hipLaunchKernelGGL(als_rescore_kernel, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp, user_rows,
                      n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, w.cv, w.ci, w.cn, overflow);
   rc = check_launch("als_rescore_kernel");
