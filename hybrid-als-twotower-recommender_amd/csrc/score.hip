@@ -1336,9 +1336,13 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
 // path's list overflow. Unknown users (row < 0) keep no candidates, as there.
 constexpr double kPruneRel = 0x1p-8 + 0x1p-13;
 constexpr double kPruneAbs = 1e-30;
-// items of the bf16 sample bound (measured: 4096 / 8192 / 16384 / 32768 items
-// -> 160 / 144 / 145 / 153 us per 1024 x 100k batch; a larger sample writes
-// more scores than its tighter bound saves in the filter)
+// items of the bf16 sample bound: kk <= 64 takes the first 32768 items'
+// wave-tile maxima (no score matrix; 8192 / 16384 / 32768 items -> 105 /
+// 96 / 94 us per 1024 x 100k call: a larger sample leaves fewer pairs to the
+// filter), kk > 64 the exact kk-th of the first 8192 items' scores (a
+// materialised [B][8192] sample: 4096 / 8192 / 16384 / 32768 items measured
+// 160 / 144 / 145 / 153 us before the maxima form)
+constexpr int kPruneSampleMax = 32768;
 constexpr int kPruneSample = 8192;
 // resident users per block of the sample's dot (the full 128 KiB of users
 // leaves 16 blocks for 8192 items: 64 -> 144 us, 128 -> 148, 256 -> 154;
@@ -1532,11 +1536,15 @@ typedef __bf16 pr_bf8 __attribute__((ext_vector_type(8)));
 __host__ __device__ constexpr int prune_filter_users(int dk) { return dk <= 64 ? 256 : (dk == 128 ? 128 : 64); }
 typedef float pr_f4 __attribute__((ext_vector_type(4)));
 
-template <int DK>
+// MAXONLY (the sample bound, step 1): no test; per (user, wave tile of 16 NI
+// items) the largest s~ goes to wmax[b * n_wt + tile] — disjoint item sets,
+// so the kk-th largest of those maxima is reached by kk distinct items.
+template <int DK, bool MAXONLY>
 __global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* __restrict__ uop, int n_users,
                                                                const uint16_t* __restrict__ items, int64_t N,
                                                                const float* __restrict__ thr2, int cap,
-                                                               int64_t* __restrict__ pre_i, int* __restrict__ pre_n) {
+                                                               int64_t* __restrict__ pre_i, int* __restrict__ pre_n,
+                                                               float* __restrict__ wmax) {
   constexpr int KS = DK / 32;
   constexpr int NI = DK <= 64 ? 4 : (DK == 128 ? 2 : 1);
   constexpr int UBK = prune_filter_users(DK);  // <= 36 KiB of users per block
@@ -1586,7 +1594,7 @@ __global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* _
     }
   }
   for (int o = threadIdx.x; o < UBK; o += 256) {
-    sth[o] = o < ub ? thr2[b0 + o] : __builtin_nanf("");
+    sth[o] = (!MAXONLY && o < ub) ? thr2[b0 + o] : __builtin_nanf("");  // MAXONLY: no bounds (thr2 null)
     s_cnt[o] = 0;
   }
   if (threadIdx.x == 0) s_n = 0;
@@ -1616,6 +1624,23 @@ __global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* _
                                                                 0);
       }
       const bool full = j0 + 16 * NI <= N;  // wave-uniform: every item of the wave in range
+      if constexpr (MAXONLY) {
+        const int64_t n_wt = (N + 16 * NI - 1) / (16 * NI);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float mx = -INFINITY;
+#pragma unroll
+          for (int t = 0; t < NI; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (full || j0 + 16 * t + 4 * g + r < N) mx = fmaxf(mx, acc[u][t][r]);
+          mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+          mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+          const int ul = 64 * ch + 16 * u + c;
+          if (g == 0 && ul < ub && j0 < N) wmax[(int64_t)(b0 + ul) * n_wt + j0 / (16 * NI)] = mx;
+        }
+        continue;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int ul = 64 * ch + 16 * u + c;
@@ -1663,6 +1688,7 @@ __global__ __launch_bounds__(256) void als_bound_filter_kernel(const uint16_t* _
     }
   };
   for (int64_t it = it0; it < n_it; it += it_step) tile(it, fa);
+  if constexpr (MAXONLY) return;
   // flush: one list reservation per user with staged survivors, then the entries
   __syncthreads();
   {  // ranks per user (LDS atomics, off the MFMA loop)
@@ -1790,6 +1816,34 @@ __global__ __launch_bounds__(256) void als_rescore_topk_kernel(const float* __re
   }
 }
 
+template <bool MAXONLY>
+static int bound_filter_launch(int dk, dim3 grid, hipStream_t s, const uint16_t* uop, int n_users,
+                               const uint16_t* items, int64_t N, const float* thr2, int cap, int64_t* pre_i,
+                               int* pre_n, float* wmax) {
+  switch (dk) {
+    case 32: hipLaunchKernelGGL((als_bound_filter_kernel<32, MAXONLY>), grid, dim3(256), 0, s, uop, n_users, items, N,
+                                thr2, cap, pre_i, pre_n, wmax); break;
+    case 64: hipLaunchKernelGGL((als_bound_filter_kernel<64, MAXONLY>), grid, dim3(256), 0, s, uop, n_users, items, N,
+                                thr2, cap, pre_i, pre_n, wmax); break;
+    case 128: hipLaunchKernelGGL((als_bound_filter_kernel<128, MAXONLY>), grid, dim3(256), 0, s, uop, n_users, items,
+                                 N, thr2, cap, pre_i, pre_n, wmax); break;
+    default: hipLaunchKernelGGL((als_bound_filter_kernel<256, MAXONLY>), grid, dim3(256), 0, s, uop, n_users, items,
+                                N, thr2, cap, pre_i, pre_n, wmax); break;
+  }
+  return check_launch("als_bound_filter_kernel");
+}
+
+// blocks of the bound filter over n items: two per CU, each walking its user
+// tile over every (grid / n_ut)-th item tile (the staged users serve several)
+static dim3 bound_filter_grid(int dk, int n_users, int64_t n) {
+  const int64_t n_ut = (n_users + prune_filter_users(dk) - 1) / prune_filter_users(dk);
+  const int per = dk <= 64 ? 256 : (dk == 128 ? 128 : 64);  // items per block round
+  const int64_t n_it = (n + per - 1) / per;
+  int64_t per_ut = (512 + n_ut - 1) / n_ut;
+  if (per_ut > n_it) per_ut = n_it;
+  return dim3((unsigned)(n_ut * per_ut));
+}
+
 static int prune_dk(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : (k <= 128 ? 128 : 256)); }
 
 extern "C" size_t hrec_als_items_bf16_bytes(int64_t n_items, int k) {
@@ -1905,17 +1959,26 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
                      user_rows, n_users, k, dk, max_norm, w.uop, w.err);
   int rc = check_launch("als_prune_user_kernel");
   if (rc) return rc;
-  rc = dot_scores_run(w.uop, n_users, items_bf16, S, dk, 1, w.samp, S, s, kPruneSampleUB);
-  if (rc) return rc;
   const float* thr = w.sv + (kk - 1);
   int thr_stride = kk;
-  if (kk <= 64) {  // the 64 lane maxima's kk-th (kk of the sample's scores reach it); zeroes pn
+  if (kk <= 64) {
+    // per (user, 16 NI-item wave tile) maxima of the sample (no score
+    // matrix), then the kk-th of their 64 lane maxima: kk distinct items of
+    // the sample reach it; zeroes pn
+    const int ni = dk <= 64 ? 4 : (dk == 128 ? 2 : 1);
+    const int64_t SM = n_items < kPruneSampleMax ? n_items : kPruneSampleMax;
+    const int64_t n_wt = (SM + 16 * ni - 1) / (16 * ni);  // <= min(n_items, 8192) = the samp row length
+    rc = bound_filter_launch<true>(dk, bound_filter_grid(dk, n_users, SM), s, w.uop, n_users,
+                                   static_cast<const uint16_t*>(items_bf16), SM, nullptr, 0, nullptr, nullptr, w.samp);
+    if (rc) return rc;
     hipLaunchKernelGGL(sample_threshold_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, w.samp,
-                       (int64_t)n_users, S, kk, w.sv, w.pn);
+                       (int64_t)n_users, n_wt, kk, w.sv, w.pn);
     rc = check_launch("sample_threshold_kernel");
     thr = w.sv;
     thr_stride = 1;
   } else {
+    rc = dot_scores_run(w.uop, n_users, items_bf16, S, dk, 1, w.samp, S, s, kPruneSampleUB);
+    if (rc) return rc;
     rc = topk_rows<float>(w.samp, n_users, S, S, kk, w.si, w.sv, w.tws, (size_t)1 << 62, s);
     if (rc == HREC_OK && hipMemsetAsync(w.pn, 0, (size_t)n_users * 4, s) != hipSuccess)
       return check_launch("score_topk_pruned memset");
@@ -1927,26 +1990,9 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
   if (rc) return rc;
   // 2) the matrix-core filter over every item at tau_b - E_b
   {
-    const unsigned n_ut = (unsigned)((n_users + prune_filter_users(dk) - 1) / prune_filter_users(dk));
-    const int per = dk <= 64 ? 256 : (dk == 128 ? 128 : 64);  // items per block round
-    // two blocks per CU; each block walks its user tile over
-    // every (grid / n_ut)-th item tile (the staged users serve several tiles)
-    const int64_t n_it = (n_items + per - 1) / per;
-    int64_t per_ut = (512 + (int64_t)n_ut - 1) / (int64_t)n_ut;
-    if (per_ut > n_it) per_ut = n_it;
-    const dim3 grid((unsigned)(n_ut * per_ut));
-    const uint16_t* io = static_cast<const uint16_t*>(items_bf16);
-    switch (dk) {
-      case 32: hipLaunchKernelGGL(als_bound_filter_kernel<32>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
-                                  w.thr2, kCap, w.pi, w.pn); break;
-      case 64: hipLaunchKernelGGL(als_bound_filter_kernel<64>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
-                                  w.thr2, kCap, w.pi, w.pn); break;
-      case 128: hipLaunchKernelGGL(als_bound_filter_kernel<128>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
-                                   w.thr2, kCap, w.pi, w.pn); break;
-      default: hipLaunchKernelGGL(als_bound_filter_kernel<256>, grid, dim3(256), 0, s, w.uop, n_users, io, n_items,
-                                  w.thr2, kCap, w.pi, w.pn); break;
-    }
-    rc = check_launch("als_bound_filter_kernel");
+    const dim3 grid = bound_filter_grid(dk, n_users, n_items);
+    rc = bound_filter_launch<false>(dk, grid, s, w.uop, n_users, static_cast<const uint16_t*>(items_bf16), n_items,
+                                    w.thr2, kCap, w.pi, w.pn, nullptr);
     if (rc) return rc;
   }
   // 3) the exact chain over the kept pairs -> candidates (chain >= tau_b);
