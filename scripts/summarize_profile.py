@@ -107,8 +107,8 @@ def main(base):
         res["als_score_filter"] = {"launches": len(sd), "avg_ms": sum(sd) / len(sd)}
     # the pruned ALS top-k (K2p, the bench's scoring line): trace averages per kernel
     pk = {}
-    for key in ("als_prune_user_kernel", "dot_res_kernel<true, 64, false, 4>", "sample_threshold_kernel",
-                "als_prune_thr_kernel", "als_bound_filter_kernel<64>", "als_rescore_kernel"):
+    for key in ("als_prune_user_kernel", "als_bound_filter_kernel<64, true>", "sample_threshold_kernel",
+                "als_prune_thr_kernel", "als_bound_filter_kernel<64, false>", "als_rescore_topk_kernel<8>"):
         dd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace if key in r["Kernel_Name"]]
         if dd:
             pk[key] = {"launches": len(dd), "avg_ms": sum(dd) / len(dd)}
