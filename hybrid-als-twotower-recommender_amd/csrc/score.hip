@@ -1425,17 +1425,13 @@ __global__ __launch_bounds__(256) void als_prune_user_kernel(const float* __rest
 
 // Per user: tau_b = down(t_b - E_b) for the exact test, down(tau_b - E_b)
 // for the bf16 filter; the candidate counter zeroed.
-__global__ __launch_bounds__(256) void als_prune_thr_kernel(int n_users, const float* __restrict__ thr,
-                                                            int thr_stride, const double* __restrict__ err,
-                                                            float* __restrict__ tau, float* __restrict__ thr2,
-                                                            int* __restrict__ cn, int* __restrict__ overflow) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= n_users) return;
+__device__ __forceinline__ void pr_bounds(int b, double t, const double* __restrict__ err, float* __restrict__ tau,
+                                          float* __restrict__ thr2, int* __restrict__ cn,
+                                          int* __restrict__ overflow) {
   cn[b] = 0;
   const double e = err[b];
   float t1 = INFINITY, t2 = INFINITY;  // unknown user / no bound: nothing passes
   if (e == e) {
-    const double t = thr[(int64_t)b * thr_stride];
     const double lo1 = t - e;
     const double lo2 = (double)pr_down(lo1) - e;
     if (isfinite(t) && isfinite(e) && isfinite(lo2)) {
@@ -1449,6 +1445,44 @@ __global__ __launch_bounds__(256) void als_prune_thr_kernel(int n_users, const f
   }
   tau[b] = t1;
   thr2[b] = t2;
+}
+
+__global__ __launch_bounds__(256) void als_prune_thr_kernel(int n_users, const float* __restrict__ thr,
+                                                            int thr_stride, const double* __restrict__ err,
+                                                            float* __restrict__ tau, float* __restrict__ thr2,
+                                                            int* __restrict__ cn, int* __restrict__ overflow) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= n_users) return;
+  pr_bounds(b, thr[(int64_t)b * thr_stride], err, tau, thr2, cn, overflow);
+}
+
+// kk <= 64: sample_threshold_kernel's lane-maxima bound over the wave-tile
+// maxima and the bounds above in one launch (one wave per user; zeroes the
+// filter's counter too).
+__global__ __launch_bounds__(256) void als_prune_sample_thr_kernel(const float* __restrict__ vals, int n_users,
+                                                                   int64_t n, int kk, const double* __restrict__ err,
+                                                                   float* __restrict__ tau, float* __restrict__ thr2,
+                                                                   int* __restrict__ cn, int* __restrict__ pn,
+                                                                   int* __restrict__ overflow) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= n_users) return;  // wave-uniform
+  const float* __restrict__ rv = vals + (int64_t)b * n;
+  float m = -INFINITY;
+  for (int64_t p = lane; p < n; p += 64) m = fmaxf(m, rv[p]);
+  float t = -INFINITY;
+  for (int r = 0; r < kk; ++r) {
+    float w = m;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) w = fmaxf(w, __shfl_xor(w, off, kWave));
+    t = w;
+    const uint64_t hold = __ballot(m == w);  // retire one lane holding the maximum (the lowest such lane)
+    if (hold && lane == __builtin_ctzll(hold)) m = -INFINITY;
+  }
+  if (lane == 0) {
+    pn[b] = 0;
+    pr_bounds(b, t, err, tau, thr2, cn, overflow);
+  }
 }
 
 // The exact JVM chain for every pair the bf16 filter kept (one block per
@@ -1959,8 +1993,6 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
                      user_rows, n_users, k, dk, max_norm, w.uop, w.err);
   int rc = check_launch("als_prune_user_kernel");
   if (rc) return rc;
-  const float* thr = w.sv + (kk - 1);
-  int thr_stride = kk;
   if (kk <= 64) {
     // per (user, 16 NI-item wave tile) maxima of the sample (no score
     // matrix), then the kk-th of their 64 lane maxima: kk distinct items of
@@ -1971,23 +2003,22 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
     rc = bound_filter_launch<true>(dk, bound_filter_grid(dk, n_users, SM), s, w.uop, n_users,
                                    static_cast<const uint16_t*>(items_bf16), SM, nullptr, 0, nullptr, nullptr, w.samp);
     if (rc) return rc;
-    hipLaunchKernelGGL(sample_threshold_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, w.samp,
-                       (int64_t)n_users, n_wt, kk, w.sv, w.pn);
-    rc = check_launch("sample_threshold_kernel");
-    thr = w.sv;
-    thr_stride = 1;
+    hipLaunchKernelGGL(als_prune_sample_thr_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, w.samp,
+                       n_users, n_wt, kk, w.err, w.tau, w.thr2, w.cn, w.pn, overflow);
+    rc = check_launch("als_prune_sample_thr_kernel");
+    if (rc) return rc;
   } else {
     rc = dot_scores_run(w.uop, n_users, items_bf16, S, dk, 1, w.samp, S, s, kPruneSampleUB);
     if (rc) return rc;
     rc = topk_rows<float>(w.samp, n_users, S, S, kk, w.si, w.sv, w.tws, (size_t)1 << 62, s);
     if (rc == HREC_OK && hipMemsetAsync(w.pn, 0, (size_t)n_users * 4, s) != hipSuccess)
       return check_launch("score_topk_pruned memset");
+    if (rc) return rc;
+    hipLaunchKernelGGL(als_prune_thr_kernel, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, n_users,
+                       w.sv + (kk - 1), kk, w.err, w.tau, w.thr2, w.cn, overflow);
+    rc = check_launch("als_prune_thr_kernel");
+    if (rc) return rc;
   }
-  if (rc) return rc;
-  hipLaunchKernelGGL(als_prune_thr_kernel, dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s, n_users, thr,
-                     thr_stride, w.err, w.tau, w.thr2, w.cn, overflow);
-  rc = check_launch("als_prune_thr_kernel");
-  if (rc) return rc;
   // 2) the matrix-core filter over every item at tau_b - E_b
   {
     const dim3 grid = bound_filter_grid(dk, n_users, n_items);
