@@ -327,14 +327,24 @@ def api_line(eng, n_users, n_items, k, reps, want_cpu):
     als = ALSModel(rank=k)
     als.spark = DeviceSession()
     als.model = DeviceALSFactors(np.arange(n_users), np.arange(n_items), eng.U[:n_users], eng.V[:n_items], k)
-    als.item_features = {}
-    tt = TwoTowerModel(n_users, n_items, 2651, 255, embedding_size=d, seed=4)
+    # the two-tower user table also holds the cold users below (ids the ALS model never saw)
+    tt = TwoTowerModel(n_users + 2048, n_items, 2651, 255, embedding_size=d, seed=4)
     tt.build_model()
     rng = np.random.default_rng(9)
     items = pd.DataFrame({"itemId": np.arange(n_items), "manufacturer_id": rng.integers(0, 2651, n_items),
                           "category_id": rng.integers(0, 255, n_items), "price": rng.random(n_items) * 100,
                           "average_review_rating": rng.integers(0, 19, n_items).astype(np.float64)})
     tt.scaler = MinMaxScaler().fit(items[["price", "average_review_rating"]])
+    # the cold-start fallback's inputs (src/als_model.py:48,86): per-item content features + mean rating
+    from src.data_preprocessing import get_item_features
+
+    als.item_features = get_item_features(items)
+    als.global_mean = items["average_review_rating"].mean()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    als._fallback()  # hrec_cold_fallback over every item (once per model)
+    torch.cuda.synchronize()
+    precompute_ms = (time.perf_counter() - t0) * 1e3
     h = HybridRecommendationSystem()
     h.als_model, h.twotower_model, h.models_loaded = als, tt, True
     ids = [int(i) for i in items["itemId"]]
@@ -403,6 +413,17 @@ def api_line(eng, n_users, n_items, k, reps, want_cpu):
 
         parts["_union + fuse_device top-5"] = timed(fuse)
         top = fuse(0)
+        # cold users (the reference protocol's test users): ids the ALS model does not
+        # know -> every ALS row takes the precomputed fallback, gathered on the device
+        cold_uids = [n_users + 1000 + i for i in range(min(reps + 1, 1000))]
+        cold_ms = timed(lambda u: h.get_hybrid_recommendations(cold_uids[u % len(cold_uids)], arr, top_k=5),
+                        "cold_user_call")
+        cu = cold_uids[0]
+        top_cold = h.get_hybrid_recommendations(cu, arr, top_k=5)
+        ca, ct = als.predict_for_user(cu, ids), tt.predict_for_user(cu, items)
+        its, sa, st = h._union(ca, ct)
+        _, cidx, csc = fuse_device(sa, st, h.als_f1_score > h.twotower_f1_score, 5)
+        top_cold_list = [(its[i], np.float64(x)) for i, x in zip(cidx, csc)]
     work = sum(parts.values())
 
     # device share of one call: the same kernels on device-resident inputs
@@ -449,10 +470,26 @@ def api_line(eng, n_users, n_items, k, reps, want_cpu):
                     "(ALS side -> [] by SURVEY D9). All run the array path (device scores -> device fusion + "
                     "top-6 -> tie check); list_path = the per-model predict_for_user lists + _union + "
                     "fuse_device (still taken on ties / duplicate ids / cold-start rows)")}
+    cold_bytes = n_items * (4.0 * d + 8.0)  # each candidate's tower vector + its f64 fallback value, read once
+    out["cold_user_call_ms"] = cold_ms
+    out["cold_user"] = {
+        "call_ms": cold_ms, "users_per_s": 1e3 / cold_ms, "fallback_precompute_ms": precompute_ms,
+        "top5_nonempty": len(top_cold) == 5,
+        "top5_equals_list_path": top_cold == top_cold_list,
+        "roofline": {"kernel": "one cold call (fallback gather + tt towers + hrec_tt_score + hrec_fuse_topk), "
+                               "whole API call", "bound": "hbm",
+                     "achieved": cold_bytes / (cold_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": cold_bytes / (cold_ms / 1e3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": cold_bytes},
+        "note": ("get_hybrid_recommendations(uid, id array) for user ids the ALS model does not know: every ALS "
+                 "row is the precomputed cold-start fallback (hrec_cold_fallback once per model, "
+                 "fallback_precompute_ms, over all items; src/als_model.py:78-86,93-104), gathered for the "
+                 "candidates on the device; top5_equals_list_path compares with predict_for_user lists + "
+                 "_union + fuse_device")}
     if want_cpu:
         from oracle import cpu_baseline as cb
 
         out["cpu_baseline"] = cb.api_call(n_items, k, d, 5)
+        out["cold_user"]["cpu_baseline"] = cb.cold_call(n_items)
     return out
 
 

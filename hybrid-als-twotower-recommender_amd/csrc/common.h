@@ -141,9 +141,9 @@ int dot_filter_run(const void* U, int B, const void* V, int64_t n_items, int dk,
 int dot_scores_run(const void* U, int B, const void* V, int64_t n_items, int dk, int bf16, float* out, int64_t ldo,
                    hipStream_t s, int ub_cap = 0);
 int count_overflow(const int* cn, int n_users, int cap, int* flag, hipStream_t s);
-// csrc/dot_gemv.hip: the few-user (B <= 4) streaming scoring kernel, same
-// contract as the matrix-core launch of csrc/dot_topk.hip (FILTER: the
-// per-user survivor filter, thr_per == 0) — HREC_DOT_GEMV=0 turns it off.
+// csrc/dot_gemv.hip: the few-user (B <= 4, f32) streaming scoring kernel, same
+// contract and same score bits as the matrix-core launch of csrc/dot_topk.hip
+// (FILTER: the per-user survivor filter, thr_per == 0).
 bool dot_gemv_applies(int B, int64_t step, int dk, int bf16);
 template <bool FILTER>
 int dot_gemv_run(const void* U, int B, const void* V, int64_t n_rows, int64_t n_items, int64_t step, int dk, int bf16,

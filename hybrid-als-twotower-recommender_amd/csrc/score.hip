@@ -1315,12 +1315,14 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
 // without the exact chain over every pair: the scores are first bounded on
 // the bf16 matrix cores, and the exact chain runs only for the pairs the
 // bound cannot rule out.
-//   bf16 operands (round to nearest even: |x - bf16(x)| <= 2^-9 |x|) give
-//   s~ = sum uh_c vh_c with |s~ - u.v| <= (2^-8 + 2^-18 + k 2^-24 (1 + 2^-8))
-//   sum |u_c v_c| (the f32 accumulation of k exact products, any order), and
-//   the JVM chain is within 2k 2^-24 sum |u_c v_c| of u.v; for k <= 256 both
-//   fit in E_b = (2^-8 + 2^-13) ||u_b|| max_j ||v_j|| (+ 1e-30 for products
-//   the matrix cores may flush).
+//   bf16 operands (8 significant bits, round to nearest even: |x - bf16(x)|
+//   <= 2^-8 |x|; e.g. 1 + 2^-8 + 2^-20 -> 1 + 2^-7) give products within
+//   (2^-7 + 2^-16) |u_c v_c| of the exact ones, so s~ = sum uh_c vh_c has
+//   |s~ - u.v| <= (2^-7 + 2^-16 + k 2^-24 (1 + 2^-6)) sum |u_c v_c| (the f32
+//   accumulation of k exact bf16 products, any order), and the JVM chain is
+//   within 2k 2^-24 sum |u_c v_c| of u.v; for k <= 256 both fit in
+//   E_b = (2^-7 + 2^-13) ||u_b|| max_j ||v_j|| (2^-16 + 3 * 256 * 2^-24 <
+//   2^-13; + 1e-30 for products the matrix cores may flush).
 //   1. tau_b: the kk-th best s~ over the first 8192 items (bf16 dot on the
 //      matrix cores, the fused path's lane-maxima bound) minus E_b, rounded
 //      down: kk items have chain >= s~ - E_b >= tau_b, so the kk-th best
@@ -1334,7 +1336,7 @@ extern "C" int hrec_als_score_topk(const float* user_factors, const int64_t* use
 // kept list overflows raise *overflow: the caller's fallback (the
 // materialised scores + hrec_topk_f32) answers the call, as for the fused
 // path's list overflow. Unknown users (row < 0) keep no candidates, as there.
-constexpr double kPruneRel = 0x1p-8 + 0x1p-13;
+constexpr double kPruneRel = 0x1p-7 + 0x1p-13;
 constexpr double kPruneAbs = 1e-30;
 // items of the bf16 sample bound: kk <= 64 takes the first 32768 items'
 // wave-tile maxima (no score matrix; 8192 / 16384 / 32768 items -> 105 /
@@ -1495,7 +1497,7 @@ __global__ __launch_bounds__(256) void als_rescore_kernel(const float* __restric
                                                           const float* __restrict__ V, int64_t ldv,
                                                           const int64_t* __restrict__ pre_i,
                                                           const int* __restrict__ pre_n, int cap,
-                                                          const float* __restrict__ tau,
+                                                          const float* __restrict__ tau, int kk,
                                                           float* __restrict__ cand_v, int64_t* __restrict__ cand_i,
                                                           int* __restrict__ cand_n, int* __restrict__ overflow) {
 #pragma clang fp contract(off)
@@ -1550,6 +1552,10 @@ __global__ __launch_bounds__(256) void als_rescore_kernel(const float* __restric
       }
     }
   }
+  // fewer than kk candidates: tau_b was above the kk-th best chain (a bound
+  // slip) -> the caller's exact fallback instead of (0, -1) padding
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(&cand_n[b], 0) < kk) atomicOr(overflow, 1);
 }
 
 // 2. The bf16 bound filter: block = (UBK users staged in LDS, 64 NI items),
@@ -1807,7 +1813,9 @@ __global__ __launch_bounds__(256) void als_rescore_topk_kernel(const float* __re
   const int m = s_n;
   if (threadIdx.x == 0) {
     cand_n[b] = m;
-    if (m > kL || m > cap) atomicOr(overflow, 1);
+    // fewer than kk candidates for a known user: tau_b was above the kk-th
+    // best chain (a bound slip) -> the caller's exact fallback, never short ids
+    if (m > kL || m > cap || (r >= 0 && m < kk)) atomicOr(overflow, 1);
   }
   if (threadIdx.x >= 64) return;  // wave 0 ranks
   const int mm = m < kL ? m : kL;
@@ -1901,8 +1909,8 @@ extern "C" int hrec_als_items_bf16(const float* item_factors, int64_t ld_v, int6
   return check_launch("als_items_bf16_kernel");
 }
 
-// Workspace of the pruned path, in carve order (src/_hrec.py
-// als_topk_pruned_counts reads the two counters).
+// Workspace of the pruned path, in carve order
+// (hrec_als_score_topk_pruned_counts reads the two counters).
 struct PruneWs {
   float* samp;   // [B][S] bf16 sample scores
   char* tws;     // sample top-k workspace (kk > 64)
@@ -1956,6 +1964,26 @@ extern "C" size_t hrec_als_score_topk_pruned_workspace_bytes(int n_users, int64_
   const size_t fused = hrec_als_score_topk_workspace_bytes(n_users, n_items, top_k);  // the small-catalogue path
   const size_t own = prune_layout(nullptr, B, N, kk, prune_dk(k)).total;
   return own > fused ? own : fused;
+}
+
+extern "C" int hrec_als_score_topk_pruned_counts(const void* workspace, int n_users, int64_t n_items, int top_k,
+                                                 int k, int32_t* out, void* stream) {
+  HREC_REQUIRE(workspace && out && n_users >= 0 && n_items >= 0 && k >= 1 && k <= kScoreKMax && top_k >= 1,
+               "als_score_topk_pruned_counts: bad argument");
+  if (n_users == 0) return HREC_OK;
+  hipStream_t s = as_stream(stream);
+  if (n_items <= kSample) {  // the fused path ran: no bf16 filter
+    if (hipMemsetAsync(out, 0, (size_t)2 * n_users * 4, s) != hipSuccess)
+      return check_launch("als_score_topk_pruned_counts: memset");
+    return HREC_OK;
+  }
+  int kk = (int)(top_k < n_items ? top_k : n_items);
+  kk = kk > 1024 ? 1024 : kk;
+  const PruneWs w = prune_layout((char*)workspace, n_users, n_items, kk, prune_dk(k));
+  if (hipMemcpyAsync(out, w.pn, (size_t)n_users * 4, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(out + n_users, w.cn, (size_t)n_users * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return check_launch("als_score_topk_pruned_counts: copy");
+  return HREC_OK;
 }
 
 extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64_t* user_rows, int n_users,
@@ -2040,7 +2068,7 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
     return check_launch("als_rescore_topk_kernel");
   }
   hipLaunchKernelGGL(als_rescore_kernel, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp, user_rows,
-                     n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, w.cv, w.ci, w.cn, overflow);
+                     n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, kk, w.cv, w.ci, w.cn, overflow);
   rc = check_launch("als_rescore_kernel");
   if (rc) return rc;
   // 4) the same exact stable top-k over the candidates

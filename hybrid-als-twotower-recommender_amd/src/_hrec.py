@@ -54,10 +54,13 @@ _SIGNATURES = {
     "hrec_als_score_topk_pruned_workspace_bytes": (_c_sz, [_c_i32, _c_i64, _c_i32, _c_i32]),
     "hrec_als_score_topk_pruned": (_c_i32, [_vp, _vp, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _c_i32,
                                             _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_als_score_topk_pruned_counts": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _c_i32, _vp, _vp]),
     "hrec_topk_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "hrec_topk_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_topk_f64": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_cosine_sim": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp]),
+    "hrec_cold_fallback_workspace_bytes": (_c_sz, [_c_i64, _c_i32]),
+    "hrec_cold_fallback": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_rows_minmax_f32": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp]),
     "hrec_fuse_rows_workspace_bytes": (_c_sz, [_c_i64, _c_i64, _c_i32]),
     "hrec_fuse_rows_topk": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp,
@@ -151,7 +154,7 @@ _SIGNATURES.update({
     "hrec_hybrid_exact_counts": (_c_i32, [_vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
 })
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _LIB = None
 
 
@@ -455,21 +458,12 @@ def als_score_topk_pruned(user_factors, user_rows, item_factors_t, item_factors,
 def als_topk_pruned_counts(ws, B, n_items, top_k, k):
     """Diagnostics of the last als_score_topk_pruned call on workspace ws:
     (pairs the bf16 bound kept per user, candidates per user), int32 [B]
-    each (hrec_als_score_topk_pruned's workspace layout, prune_layout in
-    csrc/score.hip: 256-B aligned carves)."""
-    kk = max(1, min(int(top_k), int(n_items), 1024))
-    S, cap = min(8192, int(n_items)), 4096
-    dk = 32 if k <= 32 else (64 if k <= 64 else (128 if k <= 128 else 256))
-    tws = int(lib().hrec_topk_workspace_bytes(B, S, kk, 0))
-    sizes = [B * S * 4, tws, B * kk * 4, B * kk * 8, B * 8, B * 4, B * 4, B * dk * 2,
-             B * cap * 8, B * 4, B * cap * 4, B * cap * 8, B * 4]
-    offs, o = [], 0
-    for n in sizes:
-        offs.append(o)
-        o += (n + 255) // 256 * 256
-    pn = ws[offs[9]: offs[9] + B * 4].view(torch.int32)
-    cn = ws[offs[12]: offs[12] + B * 4].view(torch.int32)
-    return pn.clone(), cn.clone()
+    each (hrec_als_score_topk_pruned_counts)."""
+    out = torch.zeros(2 * B, dtype=torch.int32, device=ws.device)
+    _check("hrec_als_score_topk_pruned_counts", lib().hrec_als_score_topk_pruned_counts(
+        _dev(ws, torch.uint8, "ws"), int(B), int(n_items), int(top_k), int(k), _dev(out, torch.int32, "out"),
+        _stream()))
+    return out[:B].clone(), out[B:].clone()
 
 
 # ------------------------------------------------------------------ top-k
@@ -524,6 +518,31 @@ def cosine_sim(feats, query_rows):
         _dev(feats, torch.float64, "feats"), n_items, dim, _dev(query_rows, torch.int64, "query_rows"),
         query_rows.numel(), _dev(out, torch.float64, "out"), _stream()))
     return out
+
+
+COLD_MAX_DIM = 16  # hrec_cold_fallback's feature width limit
+
+
+def cold_fallback(feats, ratings, want_idx=False):
+    """The cold-start fallback of every item at once (hrec_cold_fallback,
+    src/als_model.py:78-86,93-104): feats [n, dim] f64 (dim <= 16), ratings
+    [n] f64 (the items' 'rating'), both device. Returns (mean f64 [n]: the
+    mean rating of the <= 3 most similar other items with cosine > 0.5, 0
+    where there is none; count int32 [n]; idx int32 [n, 3] of those items'
+    rows, -1 padded, when want_idx)."""
+    n, dim = feats.shape
+    dev = feats.device
+    mean = torch.empty(n, dtype=torch.float64, device=dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    idx = torch.empty((n, 3), dtype=torch.int32, device=dev) if want_idx else None
+    need = int(lib().hrec_cold_fallback_workspace_bytes(n, dim))
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _check("hrec_cold_fallback", lib().hrec_cold_fallback(
+        _dev(feats, torch.float64, "feats"), _dev(ratings, torch.float64, "ratings"), n, dim,
+        _dev(mean, torch.float64, "out_mean"), _dev(cnt, torch.int32, "out_count"),
+        _dev(idx, torch.int32, "out_idx") if idx is not None else None, _dev(ws, torch.uint8, "ws"), need,
+        _stream()))
+    return mean, cnt, idx
 
 
 # -------------------------------------------------------------- two-tower

@@ -90,7 +90,10 @@ class DeviceALSFactors:
     def score(self, user_ids, item_list):
         """f32 [len(user_ids), len(item_list)]; NaN where either id is unknown."""
         dev = self.U.device
-        urows = torch.as_tensor(self._lookup(self.user_ids, user_ids), device=dev)
+        urows_h = self._lookup(self.user_ids, user_ids)
+        if urows_h.size and (urows_h < 0).all():  # unknown users only: NaN everywhere, no transform to run
+            return torch.full((urows_h.size, len(item_list)), float("nan"), dtype=torch.float32, device=dev)
+        urows = torch.as_tensor(urows_h, device=dev)
         if isinstance(item_list, np.ndarray) and item_list.dtype == np.int64 and item_list.size > 4096:
             irows = self._lookup_device(item_list)
         else:
@@ -223,8 +226,20 @@ class ALSModel:
         self.global_mean = 3.0
         self.item_features = None
         self.seed = seed
-        self._feat_cache = None
         self.ingest_peak_bytes = None  # device bytes the last train's ingest peaked at (cuda only)
+
+    @property
+    def item_features(self):
+        return self._item_features
+
+    @item_features.setter
+    def item_features(self, value):
+        """Assigning the features (train, load_model, a caller) drops what was
+        derived from them: the feature matrix and the cold-start fallback."""
+        self._item_features = value
+        self._feat_cache = None
+        self._fb_cache = None
+        self._fb_keys = None
 
     # -------------------------------------------------------- engine handle
     def initialize_spark(self):
@@ -309,7 +324,6 @@ class ALSModel:
             if not self.initialize_spark():
                 return False
             self.item_features = get_item_features(data)
-            self._feat_cache = None
             self.global_mean = data["average_review_rating"].mean()
             self.model = self._fit(data, initial_user_factors)
             return True
@@ -370,12 +384,18 @@ class ALSModel:
     def _predict_device(self, user_id, all_items):
         """For HybridRecommendationSystem's array path: (items, keys, f32
         device scores), else the predict_for_user list itself (same prints,
-        same []). Cold-start rows stay NaN here (no host sync to look for
-        them): the array path sends any non-finite score to the list path,
-        which applies the fallback through _predictions."""
+        same []). A user the model does not know (every row NaN: the
+        reference protocol's test users) gets the fallback vector
+        gathered for the candidates (f64, _cold_scores) when it applies; other
+        NaN rows (unknown items) stay NaN, and the array path sends them to
+        the list path, which applies the fallback through _predictions."""
         try:
             items, keys, scores = self._score_device(user_id, all_items)
             if scores is not None:
+                if self.model._lookup(self.model.user_ids, [user_id])[0] < 0:
+                    cold = self._cold_scores(keys)
+                    if cold is not None:
+                        scores = cold
                 return items, keys, scores
             return self._predictions(items, scores)
         except Exception as e:
@@ -403,28 +423,122 @@ class ALSModel:
 
     def _predictions(self, items, scores):
         """The (item, prediction) list of :84 with the cold-start fallback
-        (:78-86) for rows the transform left NaN."""
+        (:78-86) for rows the transform left NaN: the per-item values of the
+        precomputed fallback vector (_fallback), or — for features the kernel
+        does not take — the per-call similarity search."""
         scores = scores.cpu().numpy() if scores is not None else np.zeros(0, np.float32)
         out = list(zip(items, scores.tolist()))  # (item, float(prediction)) as :84
         missing = np.flatnonzero(np.isnan(scores)).tolist()
-        if missing:  # cold-start fallback (:78-86): mean rating of <= 3 similar items, else the global mean
-            sims = self._similar_batch([items[n] for n in missing])
-            for n, sim in zip(missing, sims):
-                out[n] = (items[n], np.mean([self.item_features[s]["rating"] for s in sim]) if sim
-                          else self.global_mean)
+        if not missing:
+            return out
+        # cold-start fallback (:78-86): mean rating of <= 3 similar items, else the global mean
+        if self.item_features is not None:
+            self._check_finite_features([items[n] for n in missing])
+        fb = self._fallback() if self.item_features is not None else None
+        if fb is not None:
+            pos, mean, cnt = fb["pos"], fb["mean_h"], fb["cnt_h"]
+            for n in missing:
+                p = pos.get(items[n])  # the reference's item_features[item] (KeyError -> [] -> global mean)
+                out[n] = (items[n], mean[p] if p is not None and cnt[p] > 0 else self.global_mean)
+            return out
+        sims = self._similar_batch([items[n] for n in missing])
+        for n, sim in zip(missing, sims):
+            out[n] = (items[n], np.mean([self.item_features[s]["rating"] for s in sim]) if sim
+                      else self.global_mean)
         return out
 
+    def _check_finite_features(self, query_items):
+        """sklearn's cosine_similarity (:100) validates both arrays: a NaN or
+        infinite feature vector anywhere in item_features raises ValueError
+        from the reference's loop as soon as an item with features needs the
+        fallback (and has another item to compare with)."""
+        ids, pos, mat = self._feature_matrix()
+        bad = self._feat_cache[4]
+        if bad is None or len(ids) < 2 or not any(it in pos for it in query_items):
+            return
+        raise ValueError(bad)
+
+    def _features_key(self):
+        f = self.item_features
+        return id(f), (len(f) if f is not None else -1)
+
     def _feature_matrix(self):
-        if self._feat_cache is None:
+        key = self._features_key()
+        if self._feat_cache is None or self._feat_cache[0] != key:
             feats = self.item_features or {}
             ids = list(feats.keys())
+            bad = None
             if ids:
                 mat = np.stack([np.asarray(feats[i]["features"], dtype=np.float64).ravel() for i in ids])
                 dev_mat = torch.as_tensor(mat, device=self.spark.device if self.spark else "cuda")
+                if not np.isfinite(mat).all():  # sklearn check_array's messages
+                    bad = ("Input contains NaN." if np.isnan(mat).any() else
+                           "Input contains infinity or a value too large for dtype('float64').")
             else:
                 dev_mat = None
-            self._feat_cache = (ids, {i: n for n, i in enumerate(ids)}, dev_mat)
-        return self._feat_cache
+            self._feat_cache = (key, ids, {i: n for n, i in enumerate(ids)}, dev_mat, bad)
+        return self._feat_cache[1:4]
+
+    def _fallback(self):
+        """The cold-start fallback of every item with features, computed once
+        per item_features on the device (hrec_cold_fallback: the <= 3 most
+        similar other items with cosine > 0.5 of :93-104 and np.mean of their
+        ratings — the value of :84-85 for any user). A dict with "pos" (item
+        -> row), "mean_h" (np.float64 per row), "cnt_h" (similar items kept)
+        and their device copies; None when the features are outside the
+        kernel (wider than 16, or ratings that are not Python / numpy f64
+        floats, whose np.mean would run in another dtype), or absent."""
+        key = self._features_key()
+        if self._fb_cache is not None and self._fb_cache[0] == key:
+            return self._fb_cache[1]
+        ids, pos, mat = self._feature_matrix()
+        fb = None
+        feats = self.item_features
+        if mat is not None and mat.shape[1] <= _hrec.COLD_MAX_DIM:
+            r = [feats[i]["rating"] for i in ids]
+            # np.mean converts ints (not bools) to f64 the same way; float32 etc. would sum in their dtype
+            if all(type(x) in (float, int, np.float64, np.int64) for x in r):
+                ratings = torch.as_tensor(np.asarray(r, np.float64), device=mat.device)
+                mean, cnt, _ = _hrec.cold_fallback(mat, ratings)
+                fb = {"ids": ids, "pos": pos, "mean": mean, "cnt": cnt, "mean_h": mean.cpu().numpy(),
+                      "cnt_h": cnt.cpu().numpy()}
+        self._fb_cache = (key, fb)
+        self._fb_keys = None
+        return fb
+
+    def _cold_scores(self, keys):
+        """For a cold user on the hybrid's array path: f64 device [n], the
+        fallback value of each candidate key (global mean where the item has
+        no features or no similar item), or None when _fallback is None, the
+        features are not finite or the feature ids are not integers. Cached
+        for the last candidate set."""
+        if self.item_features is None:
+            return None
+        fb = self._fallback()
+        if fb is None or self._feat_cache[4] is not None:  # non-finite features: the list path raises
+            return None
+        c = self._fb_keys
+        if c is not None and c[0] is fb and c[1].shape == keys.shape and np.array_equal(c[1], keys):
+            return c[2]
+        if "sorted" not in fb:
+            arr = np.asarray(fb["ids"])
+            fb["sorted"] = None
+            if arr.dtype.kind in "iu" and arr.dtype != np.uint64:
+                order = np.argsort(arr, kind="stable")
+                dev = fb["mean"].device
+                fb["sorted"] = (torch.as_tensor(arr[order].astype(np.int64), device=dev),
+                                torch.as_tensor(order.astype(np.int64), device=dev))
+        if fb["sorted"] is None:
+            return None
+        sid, order = fb["sorted"]
+        k = torch.as_tensor(np.asarray(keys, np.int64), device=sid.device)
+        p = torch.searchsorted(sid, k).clamp_(max=sid.numel() - 1)
+        row = order[p]
+        hit = (sid[p] == k) & (fb["cnt"][row] > 0)
+        gm = torch.full_like(fb["mean"][:1], float(self.global_mean))
+        vals = torch.where(hit, fb["mean"][row], gm)
+        self._fb_keys = (fb, np.array(keys, np.int64, copy=True), vals)
+        return vals
 
     def _similar_batch(self, query_items, k=3):
         """_find_similar_items for many items at once on the device: cosine
@@ -486,7 +600,6 @@ class ALSModel:
                 self.reg_param = metadata["reg_param"]
                 self.global_mean = metadata["global_mean"]
                 self.item_features = metadata["item_features"]
-                self._feat_cache = None
             return self
         except Exception as e:
             print(f"Loading error: {str(e)}")

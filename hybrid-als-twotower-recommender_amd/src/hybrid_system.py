@@ -231,8 +231,9 @@ class HybridRecommendationSystem:
         """get_hybrid_recommendations without the Python lists: when both
         sides cover the same unique candidate ids (or the ALS side is empty,
         the reference's DataFrame wiring, SURVEY D9) the union is those ids;
-        the fusion runs on the device scores and the top_k + 1 fused scores
-        come back. If they are finite and strictly decreasing, the stable
+        the fusion runs on the device scores (a cold ALS user's rows already
+        hold the model's fallback vector, ALSModel._predict_device) and the
+        top_k + 1 fused scores come back. If they are finite and strictly decreasing, the stable
         top_k is the same whatever order the reference's set(...) union put
         the items in, so it is returned; otherwise (ties, NaN/inf scores,
         duplicate or mismatched ids) None sends the call down the list path,

@@ -40,8 +40,10 @@ extern "C" {
 /* 2: hrec_fuse_topk gained out_minmax; hrec_hybrid_scores gained n_als_rows.
  * 3: hrec_hybrid_minmax / hrec_hybrid_topk removed (the pruned hybrid
  *    replaces them); hrec_dot_topk's +inf bound admits scores >= +inf.
- * 4: the RCCL exchange steps (hrec_comm_*, hrec_allgather, hrec_allreduce_minmax). */
-#define HREC_ABI_VERSION 5
+ * 4: the RCCL exchange steps (hrec_comm_*, hrec_allgather, hrec_allreduce_minmax).
+ * 6: hrec_als_score_topk_pruned_counts, hrec_cold_fallback*; the pruned ALS
+ *    bound is 2^-7 + 2^-13. */
+#define HREC_ABI_VERSION 6
 
 #define HREC_OK 0
 #define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
@@ -196,14 +198,20 @@ int hrec_als_score_topk(const float* user_factors, const int64_t* user_rows,
 
 /* Pruned form of hrec_als_score_topk (same outputs, same overflow contract):
  * the sample bound thr_b as there, then a bf16 matrix-core filter keeps
- * every item with approx score >= thr_b - E, E = (2^-8 + 2^-13) ||u|| max
- * ||v|| + 1e-30 (bounds |bf16 dot - JVM chain| for k <= 256), and the JVM
- * chain over those items alone leaves exactly the fused filter's survivors
- * (score >= thr_b), ranked by the same stable top-k. *overflow is also set
- * when a bound is not finite (a non-finite factor) or the bf16 filter's list
- * overflows. items_bf16: hrec_als_items_bf16 of item_factors (row-major
- * [n_items, ld_v], the same values as item_factors_t), 256-B aligned; it is
- * built once per item matrix. */
+ * every item with approx score >= thr_b - E, E = (2^-7 + 2^-13) ||u|| max
+ * ||v|| + 1e-30 (bounds |bf16 dot - JVM chain| for k <= 256: 2^-8 relative
+ * rounding per bf16 operand), and the JVM chain over those items alone
+ * leaves exactly the fused filter's survivors (score >= thr_b), ranked by the
+ * same stable top-k. *overflow is also set when a bound is not finite (a
+ * non-finite factor), when the bf16 filter's list overflows, or when a known
+ * user ends with fewer than min(top_k, n_items) candidates (a bound slip:
+ * never short or padded ids). items_bf16: hrec_als_items_bf16 of
+ * item_factors (row-major [n_items, ld_v], the same values as
+ * item_factors_t), 256-B aligned; it is built once per item matrix.
+ * hrec_als_score_topk_pruned_counts copies the last call's diagnostics from
+ * its workspace: out[0 .. n) = pairs the bf16 bound kept per user,
+ * out[n .. 2n) = candidates per user (int32, device); zeros when the call
+ * took the small-catalogue (fused) path. */
 size_t hrec_als_items_bf16_bytes(int64_t n_items, int k);
 int hrec_als_items_bf16(const float* item_factors, int64_t ld_v, int64_t n_items, int k,
                         void* out, size_t out_bytes, void* stream);
@@ -214,6 +222,8 @@ int hrec_als_score_topk_pruned(const float* user_factors, const int64_t* user_ro
                                int64_t n_items, int k, int kp, int top_k, int64_t* out_idx,
                                float* out_val, int* overflow, void* workspace,
                                size_t workspace_bytes, void* stream);
+int hrec_als_score_topk_pruned_counts(const void* workspace, int n_users, int64_t n_items, int top_k, int k,
+                                      int32_t* out, void* stream);
 
 /* ---------------------------------------------------------------- top-k --
  * Stable descending top-k of each of n_rows rows (row i starts at
@@ -282,6 +292,21 @@ int hrec_cosine_sim(const double* feats, int64_t n_items, int dim,
                     const int64_t* query_rows, int64_t n_query, double* out,
                     void* stream);
 
+/* The cold-start fallback of EVERY item, once per model (src/als_model.py
+ * :78-86 + _find_similar_items :93-104; the value depends on the item only):
+ * out_mean[i] = the mean 'rating' (ratings[j], f64) of the <= 3 items j != i
+ * most similar to i (hrec_cosine_sim's values, ranked larger first, ties ->
+ * smaller j) with similarity > 0.5, as np.mean sums them ((r0 + r1) + r2) /
+ * count; out_count[i] = how many (0: the caller's global mean; out_mean 0);
+ * out_idx (optional, [n_items][3] int32, -1 padded) = those j in rank order.
+ * feats [n_items][dim] f64 row-major, dim <= 16, n_items < 2^31. One pass of
+ * n_items^2 similarities, no similarity matrix in memory.
+ * Workspace: hrec_cold_fallback_workspace_bytes(n_items, dim). */
+size_t hrec_cold_fallback_workspace_bytes(int64_t n_items, int dim);
+int hrec_cold_fallback(const double* feats, const double* ratings, int64_t n_items, int dim,
+                       double* out_mean, int32_t* out_count, int32_t* out_idx, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------ two-tower --
  * Keras graph of src/two_tower_model.py:38-89 (embedding_size d):
  *   user_vec = LN_u(E_user[u]);  h = relu(numeric @ W1 + b1)  [Dense(16)]
@@ -316,7 +341,12 @@ int hrec_tt_item_forward(const hrec_tt_params* params, const int32_t* item,
 int hrec_tt_user_forward(const hrec_tt_params* params, const int32_t* user, int64_t n,
                          float* user_vec /* [n,d] */, void* stream);
 /* Dot(axes=1) of every user row with every item row: out[b*n_items + j]
- * (f32; on the matrix cores for n_users >= 8). */
+ * (f32). Every two-tower score in libhrec (this call at any n_users,
+ * hrec_tt_pair_score, hrec_dot_scores / hrec_dot_topk on f32 operands, the
+ * exact hybrid) is one fmaf chain from zero in one k order, so a score's bits
+ * do not depend on the batch: d in {32, 64, 128, 256}: steps of 16, inside a
+ * step k = 16 s + 4 g + e with g fastest (the v_mfma_f32_16x16x4_f32 tiles);
+ * any other d: k = 0 .. d-1. */
 int hrec_tt_score(const float* user_vec, int n_users, const float* item_vec,
                   int64_t n_items, int d, float* out, void* stream);
 
@@ -339,7 +369,8 @@ int hrec_tt_item_inputs(const int64_t* item, const int64_t* manufacturer, const 
                         int32_t* item_out, int32_t* man_out, int32_t* cat_out, float* numeric_out,
                         int32_t* flags, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Row-wise dot: out[r] = <user_vec[r], item_vec[r]> (n rows of d). */
+/* Row-wise dot: out[r] = <user_vec[r], item_vec[r]> (n rows of d), in
+ * hrec_tt_score's order (the same bits for the same pair). */
 int hrec_tt_pair_score(const float* user_vec, const float* item_vec, int64_t n, int d,
                        float* out, void* stream);
 
@@ -426,12 +457,10 @@ int hrec_adam_sparse_tables_phase(const hrec_sparse_table* tables, int n_tables,
 int hrec_f32_to_bf16(const float* in, int64_t n, uint16_t* out, void* stream);
 /* out[b*ld_out + j] = <U[b], V[j]> for b < n_users, j < n_items.
  * Summation order and batch size: f32 calls of 1-4 users run the streaming
- * GEMV kernel (one partial per 16-B load, then a butterfly), larger batches
- * the matrix cores (k order 16 ks + 4 g + e); a user's f32 scores can
- * therefore differ in the last bits between a call of <= 4 users and one of
- * more (both within the f32 error bound). bf16 calls always use the matrix
- * cores. A chunked caller that needs the same bits for every chunk keeps
- * chunks of >= 5 users. The same holds for hrec_dot_topk. */
+ * GEMV kernel, larger batches the matrix-core tiles; both issue the same
+ * v_mfma_f32_16x16x4_f32 sequence per score (k order 16 ks + 4 g + e), so a
+ * user's scores have the same bits at every batch size. bf16 calls always use
+ * the matrix-core tiles. The same holds for hrec_dot_topk. */
 int hrec_dot_scores(const void* user_vec, int n_users, const void* item_vec, int64_t n_items, int dk,
                     int dtype, float* out, int64_t ld_out, void* stream);
 size_t hrec_dot_topk_workspace_bytes(int n_users, int64_t n_items, int top_k);
@@ -542,8 +571,8 @@ int hrec_hybrid_prune_survivors(const void* workspace, int n_users, int64_t n_it
  * shard (src/hybrid_system.py:57-75, :95-116) with the reference's numerics —
  * the JVM-exact ALS dot (Spark ALSModel.transform, src/als_model.py:75) and
  * the f32 Keras Dot (src/two_tower_model.py:80) in hrec_dot_scores' MFMA k
- * order — bit for bit the result of hrec_als_score + hrec_tt_score (>= 8
- * users) + hrec_rows_minmax_f32 + hrec_fuse_rows_topk, without writing either
+ * order — bit for bit the result of hrec_als_score + hrec_tt_score (any
+ * n_users >= 1) + hrec_rows_minmax_f32 + hrec_fuse_rows_topk, without writing either
  * [n_users, n_items] score matrix: both models are approximated on the bf16
  * matrix cores with a rigorous error bound, and only the item groups the
  * bound cannot rule out (a model's extremes; the fused top-k) are rescored

@@ -289,3 +289,41 @@ def api_call(n_items, k, d, top_k, users=8, seed=0):
         f"one user per call over {n_items} candidates: JVM-exact f32 ALS transform (rank {k}, numpy, "
         f"oracle/als.py score_matrix) + Keras item/user towers and Dot (d = {d}, torch-CPU f32) + f64 min-max "
         f"fusion + stable top-{top_k}; {users} users, {dt * 1e3:.1f} ms each"), cores)
+
+
+def cold_call(n_items, dim=3, sample=64, seed=0):
+    """The reference's cold-start fallback on the CPU (src/als_model.py:78-86,
+    93-104) for a user the model does not know: EVERY candidate
+    runs _find_similar_items — a cosine against every other item, the stable
+    sorted()[:3], sim > 0.5 — and np.mean of the kept ratings. Restated with
+    numpy vectorised over the other items (one normalised-row dot per pair,
+    the per-pair arithmetic of oracle/fusion.py cosine); `sample` candidates
+    are timed and scaled to the n_items of one call (the reference recomputes
+    this per candidate per call)."""
+    cores = _setup()
+    rng = np.random.default_rng(seed)
+    feats = rng.random((n_items, dim))
+    ratings = rng.integers(0, 19, n_items).astype(np.float64)
+    nrm = np.sqrt((feats * feats).sum(1))
+    nrm[nrm == 0] = 1.0
+    xn = feats / nrm[:, None]
+    gm = float(ratings.mean())
+
+    def one(q):
+        sims = xn @ xn[q]
+        sims[q] = -np.inf
+        top = np.argsort(-sims, kind="stable")[:3]
+        keep = [j for j in top if sims[j] > 0.5]
+        return np.mean(ratings[keep]) if keep else gm
+
+    one(0)
+    qs = rng.choice(n_items, sample, replace=False)
+    t0 = time.perf_counter()
+    for q in qs:
+        one(int(q))
+    per_item = (time.perf_counter() - t0) / sample
+    per_call = per_item * n_items
+    return _line(1.0 / per_call, "users/s", "port", (
+        f"cold user over {n_items} candidates: every candidate's fallback (cosine vs every other item, "
+        f"stable top-3, sim > 0.5, mean rating; numpy, dim {dim}); {sample} candidates timed "
+        f"({per_item * 1e3:.2f} ms each), scaled to one call = {per_call:.1f} s"), cores)

@@ -847,6 +847,65 @@ def test_batched_hybrid_matches_per_user_fusion(device):
     np.testing.assert_allclose(_hrec.tt_score(uvec, ivec).cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("d", [32, 50, 64])
+def test_single_user_hybrid_equals_batched_recommender(device, monkeypatch, d):
+    """get_hybrid_recommendations for ONE user (the array path:
+    ALS transform, hrec_tt_score at B = 1, hrec_fuse_topk) and
+    ShardedRecommender.recommend over a batch of 9 users holding that user
+    (B >= 8: the exact hybrid K9x at d = 32 / 64, the materialised tiles
+    otherwise; and the materialised path at every d) serve the same item ids
+    and the same fused f64 scores, bit for bit — the two-tower score bits do
+    not depend on the batch size."""
+    from src import _hrec
+    from src.als_model import ALSModel
+    from src.hybrid_system import HybridRecommendationSystem
+    from src.recommend import ShardedRecommender
+    from src.two_tower_model import TwoTowerModel
+
+    rng = np.random.default_rng(31 + d)
+    df = _tt_frame(rng, 4000, 90, 700, 5, 4)
+    als = ALSModel(rank=16, max_iter=3, seed=4)
+    assert als.train(df)
+    tt = TwoTowerModel(90, 700, 5, 4, embedding_size=d)
+    tt.train(df, batch_size=256, epochs=1)
+    m = als.model
+    items = df[["itemId", "manufacturer_id", "category_id", "price", "average_review_rating"]].drop_duplicates(
+        "itemId").reset_index(drop=True)
+    items = items[np.isin(items["itemId"].to_numpy(), m.item_ids)].reset_index(drop=True)  # no cold rows
+    cand = _id_array(items)
+    h = HybridRecommendationSystem()
+    h.als_model, h.twotower_model, h.models_loaded = als, tt, True
+    seen = {}
+    orig = _hrec.tt_score
+
+    def capture(uvec, ivec):
+        seen["u"], seen["i"] = uvec.clone(), ivec.clone()
+        return orig(uvec, ivec)
+
+    monkeypatch.setattr(_hrec, "tt_score", capture)
+    users = [int(u) for u in np.random.default_rng(5).choice(m.user_ids, 9, replace=False)]
+    for f1 in ((0.5, 0.1), (0.1, 0.5)):
+        h.als_f1_score, h.twotower_f1_score = f1
+        single, uvecs = [], []
+        for uid in users:
+            top = h.get_hybrid_recommendations(uid, cand, top_k=5)
+            assert len(top) == 5
+            single.append(top)
+            uvecs.append(seen["u"])
+        ivec = seen["i"]
+        rows = torch.as_tensor(np.searchsorted(m.user_ids, users), device=device)
+        irows = torch.as_tensor(np.searchsorted(m.item_ids, items["itemId"].to_numpy()), device=device)
+        Vt = _hrec.transpose(m.V.index_select(0, irows).contiguous())
+        U = torch.cat(uvecs).contiguous()
+        for pruned in (True, False):
+            rec = ShardedRecommender(m.U, Vt, ivec, 0, m.k, pruned=pruned)
+            idx, val = rec.recommend(rows, U, f1[0] > f1[1], 5)
+            ids = items["itemId"].to_numpy()[idx.cpu().numpy()]
+            for b, top in enumerate(single):
+                assert [int(i) for i, _ in top] == ids[b].tolist(), (pruned, b)
+                assert np.array_equal(np.array([s for _, s in top], np.float64), val[b].cpu().numpy()), (pruned, b)
+
+
 def test_twotower_resume_after_load_matches_continued_training(device, tmp_path):
     """save_model keeps the Adam slots (Keras include_optimizer=True), so
     training resumed from a loaded model equals uninterrupted training."""

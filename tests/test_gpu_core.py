@@ -412,7 +412,8 @@ def test_als_score_topk_overflow_flag(device):
 @pytest.mark.parametrize("n_items,k,kp,B,top_k,case", [
     (100_003, 64, 64, 40, 5, "normal"), (100_000, 64, 64, 17, 10, "quant"), (30_000, 16, 16, 9, 1, "normal"),
     (50_000, 100, 128, 12, 100, "normal"), (40_000, 200, 256, 8, 8, "scaled"), (3000, 64, 64, 5, 5, "normal"),
-    (60_000, 64, 64, 10, 5, "unknown"), (60_000, 64, 64, 10, 5, "nan_item"), (60_000, 64, 64, 10, 5, "const")])
+    (60_000, 64, 64, 10, 5, "unknown"), (60_000, 64, 64, 10, 5, "nan_item"), (60_000, 64, 64, 10, 5, "const"),
+    (3000, 16, 16, 4, 1, "round_up"), (40_000, 16, 16, 4, 1, "round_up"), (40_000, 64, 64, 6, 3, "round_up")])
 def test_als_score_topk_pruned_matches_fused(device, n_items, k, kp, B, top_k, case):
     """hrec_als_score_topk_pruned (bf16 matrix-core bound, exact chain only
     for the pairs it keeps) returns the fused path's (ids, scores) bit for
@@ -420,7 +421,9 @@ def test_als_score_topk_pruned_matches_fused(device, n_items, k, kp, B, top_k, c
     odd n, rank 16 / 64 / 100 (kp 128) / 200 (kp 256), top_k 1 .. 100,
     quantised factors (ties), factors scaled by 1e6, an unknown user row
     (the fused path's empty candidate list), a NaN item (no finite bound:
-    overflow -> the exact fallback) and constant items (list overflow)."""
+    overflow -> the exact fallback), constant items (list overflow) and
+    components whose bf16 roundings all go the same way (the bound's worst
+    case: 2^-8 relative per operand)."""
     h = _hrec()
     rng = np.random.default_rng(n_items + k)
     U = np.zeros((B, kp), np.float32)
@@ -436,6 +439,14 @@ def test_als_score_topk_pruned_matches_fused(device, n_items, k, kp, B, top_k, c
         V[777, 3] = np.nan
     if case == "const":
         V[:, :k] = 0.25
+    if case == "round_up":  # every bf16 rounding error aligned: 1 + 2^-8 + 2^-20 -> 1 + 2^-7,
+        # so s~ of the best items overshoots their chain by ~2^-7 ||u|| ||v|| (the sample bound then sits
+        # right at the kk-th chain); four tied best items in distinct sample tiles (the last past the
+        # 32768-item sample), the rest far below
+        x = np.float32(1 + 2.0 ** -8 + 2.0 ** -20)
+        U[:, :k] = x
+        V[:, :k] = 0.5
+        V[[0, 100, 200, min(33_000, n_items - 1)], :k] = x
     dU = torch.as_tensor(U, device=device)
     dV = torch.as_tensor(V, device=device)
     Vt = h.transpose(dV)

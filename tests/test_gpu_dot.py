@@ -40,14 +40,9 @@ def _bf16_round(x):
 
 
 def _mfma_scores(h, U, V):
-    """hrec_dot_scores on the matrix cores whatever the batch size: B <= 4
-    users take the streaming GEMV (another f32 summation order), so the batch
-    is padded to 5 rows and the extra rows dropped."""
-    B = U.shape[0]
-    if B > 4:
-        return h.dot_scores(U, V)
-    pad = torch.zeros((5 - B, U.shape[1]), dtype=U.dtype, device=U.device)
-    return h.dot_scores(torch.cat([U, pad]).contiguous(), V)[:B].contiguous()
+    """hrec_dot_scores (every batch size issues the same MFMA sequence per
+    score: the GEMV of B <= 4 users included)."""
+    return h.dot_scores(U, V)
 
 
 def _stable_topk(scores, k):
@@ -103,33 +98,80 @@ def test_few_user_scores_and_topk(device, dtype, B, d):
 
 
 def test_dot_topk_batch_of_four_vs_five(device):
-    """f32 batches of 1-4 users take the GEMV (another summation
-    order than the matrix-core tiles of >= 5 users; include/hrec.h states the
-    batch-size dependence). Away from ties the same users get the same top-k
-    ids from a batch of 4 and from a batch of 5, and scores that agree within
-    the f32 dot bound (1e-6 sum |u_c v_c|); near ties only the bound holds."""
+    """f32 batches of 1-4 users take the GEMV and >= 5 users
+    the matrix-core tiles; both issue the same MFMA sequence per score, so a
+    user's top-k ids AND score bits are the same from a batch of 4 and from a
+    batch of 5 — on quantised vectors with many exact ties too."""
     h = _h()
     N, d, k = 50_000, 64, 10
-    U = _vecs(5, d, 71)
-    V = _vecs(N, d, 72)
-    Ud = h.dot_operand(torch.from_numpy(U).to(device), torch.float32)
-    Vd = h.dot_operand(torch.from_numpy(V).to(device), torch.float32)
-    i4, v4 = h.dot_topk(Ud[:4].contiguous(), Vd, k)
-    i5, v5 = h.dot_topk(Ud, Vd, k)
-    i4, v4, i5, v5 = i4.cpu().numpy(), v4.cpu().numpy(), i5.cpu().numpy()[:4], v5.cpu().numpy()[:4]
-    ref = U[:4].astype(np.float64) @ V.astype(np.float64).T
-    bound = 1e-6 * (np.abs(U[:4]).astype(np.float64) @ np.abs(V).astype(np.float64).T) + 1e-30
-    checked = 0
-    for b in range(4):
-        order = np.argsort(-ref[b], kind="stable")[: k + 1]
-        gaps = -np.diff(ref[b][order])
-        if np.all(gaps > 2 * bound[b][order[:-1]]):  # no near-tie in the top k + 1
-            np.testing.assert_array_equal(i4[b], i5[b])
-            np.testing.assert_array_equal(i4[b], order[:k])
-            checked += 1
-        rb = bound[b][i5[b]]
-        assert np.all(np.abs(v4[b].astype(np.float64) - v5[b]) <= 2 * rb)
-    assert checked >= 3
+    for quant in (False, True):
+        U = _vecs(5, d, 71)
+        V = _vecs(N, d, 72)
+        if quant:  # few distinct score values: ties at the k-th place
+            U, V = np.round(U), np.round(V * 0.5)
+        Ud = h.dot_operand(torch.from_numpy(U).to(device), torch.float32)
+        Vd = h.dot_operand(torch.from_numpy(V).to(device), torch.float32)
+        for kk in (k, 64):
+            i4, v4 = h.dot_topk(Ud[:4].contiguous(), Vd, kk)
+            i5, v5 = h.dot_topk(Ud, Vd, kk)
+            np.testing.assert_array_equal(i4.cpu().numpy(), i5.cpu().numpy()[:4])
+            np.testing.assert_array_equal(v4.cpu().numpy().view(np.int32), v5.cpu().numpy()[:4].view(np.int32))
+        full = h.dot_scores(Ud, Vd).cpu().numpy()
+        ei, ev = _stable_topk(full, k)
+        np.testing.assert_array_equal(i5.cpu().numpy()[:, :k], ei)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+def test_dot_scores_bits_independent_of_batch(device, d):
+    """hrec_dot_scores (f32): the rows of a batch of 9 users, bit for bit,
+    from calls of 1 .. 9 users (GEMV for <= 4, resident / tile kernels above)
+    on a ragged catalogue (not a multiple of any kernel's item tile)."""
+    h = _h()
+    N = 20_011
+    U = torch.from_numpy(_vecs(9, d, 80 + d)).to(device)
+    V = torch.from_numpy(_vecs(N, d, 81 + d)).to(device)
+    ref = h.dot_scores(U, V).cpu().numpy().view(np.int32)
+    for B in range(1, 9):
+        got = h.dot_scores(U[:B].contiguous(), V).cpu().numpy().view(np.int32)
+        np.testing.assert_array_equal(got, ref[:B], err_msg=f"B={B}")
+        got = h.dot_scores(U[9 - B:].contiguous(), V).cpu().numpy().view(np.int32)
+        np.testing.assert_array_equal(got, ref[9 - B:], err_msg=f"last B={B}")
+
+
+@pytest.mark.parametrize("d", [16, 32, 50, 64, 100, 128, 256])
+def test_tt_score_bits_independent_of_batch(device, d):
+    """hrec_tt_score (the Keras Dot of every two-tower ranking): a user's
+    scores have the same bits at every batch size (1, 2, 3, 4, 5, 7, 8, 9, 16
+    users), from 16-B-misaligned operands (the scalar kernel's fmaf chain in
+    the same k order: the MFMA == fmaf-chain identity) and from
+    hrec_tt_pair_score on the same (user, item) pairs; within the f32 bound
+    of the f64 dot."""
+    h = _h()
+    N = 9_001
+    Un = _vecs(16, d, 90 + d)
+    Vn = _vecs(N, d, 91 + d)
+    U = torch.from_numpy(Un).to(device)
+    V = torch.from_numpy(Vn).to(device)
+    ref = h.tt_score(U, V).cpu().numpy()
+    f64 = Un.astype(np.float64) @ Vn.astype(np.float64).T
+    bound = 1e-6 * (np.abs(Un).astype(np.float64) @ np.abs(Vn).astype(np.float64).T) + 1e-30
+    assert np.all(np.abs(ref - f64) <= bound)
+    for B in (1, 2, 3, 4, 5, 7, 8, 9):
+        got = h.tt_score(U[:B].contiguous(), V).cpu().numpy()
+        np.testing.assert_array_equal(got.view(np.int32), ref[:B].view(np.int32), err_msg=f"B={B}")
+    # misaligned copies (one float in): the scalar kernel, same k order
+    for B in (1, 9, 16):
+        ub = torch.empty(B * d + 1, dtype=torch.float32, device=device)
+        ub[1:].copy_(U[:B].reshape(-1))
+        vb = torch.empty(N * d + 1, dtype=torch.float32, device=device)
+        vb[1:].copy_(V.reshape(-1))
+        got = h.tt_score(ub[1:].view(B, d), vb[1:].view(N, d)).cpu().numpy()
+        np.testing.assert_array_equal(got.view(np.int32), ref[:B].view(np.int32), err_msg=f"misaligned B={B}")
+    # pair scores: user b against item j
+    j = torch.arange(N, device=device) % 997
+    b = torch.arange(N, device=device) % 16
+    pair = h.tt_pair_score(U[b].contiguous(), V[j].contiguous()).cpu().numpy()
+    np.testing.assert_array_equal(pair.view(np.int32), ref[b.cpu().numpy(), j.cpu().numpy()].view(np.int32))
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

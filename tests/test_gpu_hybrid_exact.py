@@ -60,7 +60,10 @@ def _same(x, y):
                                          (33, 5_000, 10, 64, 3), (300, 777, 64, 64, 5), (8, 9, 64, 64, 8),
                                          (8, 1, 64, 64, 5), (40, 33, 16, 32, 4),
                                          # G > 8192 groups (records read from memory, not LDS)
-                                         (16, 300_007, 64, 64, 5)])
+                                         (16, 300_007, 64, 64, 5),
+                                         # batches of < 8 users (hrec_tt_score's GEMV: the same bits)
+                                         (3, 50_000, 32, 32, 2), (1, 30_000, 64, 64, 5), (2, 20_000, 16, 32, 1),
+                                         (4, 40_000, 64, 128, 3), (7, 25_000, 100, 64, 8)])
 def test_hybrid_exact_equals_materialised(device, B, N, ka, kt, k):
     """K9x == the materialised exact path bit for bit — ids, fused scores and
     both min / max rows — for both weight orders, through the two-phase calls
