@@ -70,12 +70,21 @@ constexpr int kHxThreads1 = 256;
 constexpr int kHxThreads2 = 512;
 constexpr int kHxStatsLds = 8192;  // group records a phase-2 block keeps in LDS (128 KiB)
 
+#ifndef HREC_HX_UB64
+// phase-1 users per tile at DK 64: 256 = one 512-thread block per CU (139 KB
+// of LDS, 2 waves per SIMD), every item fragment read once per 256-user
+// batch (half the item operand reads of 128-user tiles); measured c2 batch
+// 0.1022 -> 0.1002 ms
+#define HREC_HX_UB64 256
+#endif
 template <int DK>
 struct HxShape {
   static constexpr int KS = DK / 16;               // 32x32x16 k-steps per operand half
   static constexpr int kOpB = DK * 4;              // bytes per operand row: [hi | lo] bf16
   static constexpr int kRowB = kOpB + 16;          // LDS bytes per staged user row
-  static constexpr int UB = DK == 64 ? 128 : 64;   // users per tile (2 x UB rows: <= 70 KB of LDS)
+  static constexpr int UB = DK == 64 ? HREC_HX_UB64 : 64;  // users per tile (2 x UB rows of LDS)
+  static constexpr int kThreads = UB == 256 ? 512 : kHxThreads1;  // phase-1 block
+  static constexpr int kBlocksPerCU = UB == 256 ? 1 : 2;
 };
 
 __device__ __forceinline__ float hx_up(double x) {  // the smallest float >= x
@@ -186,11 +195,11 @@ __device__ unsigned long long g_hx1_stamps[4096][4];  // per block: start, stage
 #endif
 
 template <int DK>
-__global__ __launch_bounds__(kHxThreads1, DK == 64 ? 2 : 1) void hx_stats_kernel(const uint16_t* __restrict__ uop, int B, int n_ut,
+__global__ __launch_bounds__(HxShape<DK>::kThreads, DK == 64 ? HxShape<DK>::kBlocksPerCU : 1) void hx_stats_kernel(const uint16_t* __restrict__ uop, int B, int n_ut,
                                                                const char* __restrict__ items, int64_t N, int G,
                                                                int64_t per, float* __restrict__ stats) {
   using S = HxShape<DK>;
-  constexpr int KS = S::KS, UB = S::UB, kRowB = S::kRowB, kOpB = S::kOpB;
+  constexpr int KS = S::KS, UB = S::UB, kRowB = S::kRowB, kOpB = S::kOpB, T1 = S::kThreads;
   __shared__ __attribute__((aligned(16))) char us[2 * UB * kRowB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c = lane & 31;
@@ -227,20 +236,20 @@ __global__ __launch_bounds__(kHxThreads1, DK == 64 ? 2 : 1) void hx_stats_kernel
   // users -> LDS: every load of a thread in flight before its stores (one
   // round trip, not one per 16-B chunk)
   constexpr int CPR = kOpB / 16;  // 16-B chunks per user row
-  constexpr int kPer = 2 * UB * CPR / kHxThreads1;
-  static_assert(kPer * kHxThreads1 == 2 * UB * CPR, "whole chunks per thread");
+  constexpr int kPer = 2 * UB * CPR / T1;
+  static_assert(kPer * T1 == 2 * UB * CPR, "whole chunks per thread");
   {
     int4 v[kPer];
 #pragma unroll
     for (int e = 0; e < kPer; ++e) {
-      const int o = threadIdx.x + e * kHxThreads1;
+      const int o = threadIdx.x + e * T1;
       const int m = o / (UB * CPR), rem = o % (UB * CPR), r = rem / CPR, q = rem % CPR;
       v[e] = int4{0, 0, 0, 0};
       if (r < ub) v[e] = *reinterpret_cast<const int4*>(uop + (int64_t)(m * B + b0 + r) * (2 * DK) + 8 * q);
     }
 #pragma unroll
     for (int e = 0; e < kPer; ++e) {
-      const int o = threadIdx.x + e * kHxThreads1;
+      const int o = threadIdx.x + e * T1;
       const int m = o / (UB * CPR), rem = o % (UB * CPR), r = rem / CPR, q = rem % CPR;
       *reinterpret_cast<int4*>(us + (m * UB + r) * kRowB + 16 * q) = v[e];
     }
@@ -251,7 +260,7 @@ __global__ __launch_bounds__(kHxThreads1, DK == 64 ? 2 : 1) void hx_stats_kernel
   // fragments go to (na, nt) first. Returns false after the range's last slice.
   auto slice = [&](HxFrag (&fa)[2][KS], HxFrag (&ft)[2][KS], HxFrag (&na)[2][KS], HxFrag (&nt)[2][KS]) {
     const bool full = jb + 32 <= N;
-    const int64_t jn = jb + 32 * (kHxThreads1 / 64);
+    const int64_t jn = jb + 32 * (T1 / 64);
     const bool more = jn < i1;
     if (kDB && more) load(jn, na, nt);
     for (int ch = 0; 32 * ch < ub; ++ch) {
@@ -1189,11 +1198,11 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   do {                                                                                                           \
     using S = HxShape<DK>;                                                                                       \
     const int n_ut = (B + S::UB - 1) / S::UB;                                                                    \
-    /* two blocks per CU (the LDS holds two user tiles): item ranges of whole 32-item slices */                  \
-    int64_t n_rng = (2 * hx_cus() + n_ut - 1) / n_ut;                                                            \
+    /* the blocks a CU holds (the LDS holds two user tiles): item ranges of whole 32-item slices */          \
+    int64_t n_rng = (S::kBlocksPerCU * hx_cus() + n_ut - 1) / n_ut;                                              \
     int64_t per = ((N + n_rng - 1) / n_rng + 31) / 32 * 32;                                                      \
     n_rng = (N + per - 1) / per;                                                                                 \
-    hipLaunchKernelGGL(hx_stats_kernel<DK>, dim3((unsigned)(n_ut * n_rng)), dim3(kHxThreads1), 0, s, w.uop, B,     \
+    hipLaunchKernelGGL(hx_stats_kernel<DK>, dim3((unsigned)(n_ut * n_rng)), dim3(S::kThreads), 0, s, w.uop, B,     \
                        n_ut, items, N, G, per, w.stats);                                                         \
   } while (0)
     if (dk == 64) HREC_HX_STATS(64); else HREC_HX_STATS(128);

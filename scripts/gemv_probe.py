@@ -1,6 +1,6 @@
-"""c4 B = 1 (the reference's one-user call): hrec_dot_topk of one user over
-50M x 128 items, f32 and bf16, HIP-event time per call and the HBM rate of
-the item operand read once; HREC_LIB selects a variant build."""
+"""Timing probe of hrec_dot_scores / hrec_dot_topk for 1-4 users (the GEMV,
+csrc/dot_gemv.hip) at BASELINE c4 (50M x 128 f32); HREC_LIB picks a variant."""
+import os
 import sys
 
 import torch
@@ -8,24 +8,31 @@ import torch
 sys.path.insert(0, "hybrid-als-twotower-recommender_amd")
 from src import _hrec as h  # noqa: E402
 
-N, d = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000, 128
+
+def t_ms(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000
 g = torch.Generator(device="cuda").manual_seed(0)
-V = torch.randn((N, d), device="cuda", generator=g)
-U = torch.randn((4, d), device="cuda", generator=g)
-for dt in (torch.float32, torch.bfloat16):
-    Vd = h.dot_operand(V, dt)
-    for B in (1, 2, 4):
-        Ud = h.dot_operand(U[:B].contiguous(), dt)
-        h.dot_topk(Ud, Vd, 5)
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(10):
-            h.dot_topk(Ud, Vd, 5)
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / 10
-        gb = N * d * Vd.element_size() / 1e9
-        print(f"{str(dt)[6:]:9s} B={B}: {ms:.3f} ms  {gb / ms:.2f} TB/s  frac {gb / ms / 8:.3f}", flush=True)
-    del Vd
+for d in (128, 64, 256):
+    n = N if d <= 128 else N // 2
+    V = torch.randn((n, d), device="cuda", generator=g)
+    U = torch.randn((4, d), device="cuda", generator=g)
+    for B in (1, 4):
+        Ub = U[:B].contiguous()
+        out = torch.empty((B, n), device="cuda")
+        ms = t_ms(lambda: h.dot_scores(Ub, V))
+        mk = t_ms(lambda: h.dot_topk(Ub, V, 5))
+        print(f"{os.path.basename(os.environ.get('HREC_LIB', 'default'))} d={d} B={B} N={n}: scores {ms:.3f} ms "
+              f"({n * d * 4 / ms / 1e6:.0f} GB/s)  topk5 {mk:.3f} ms ({n * d * 4 / mk / 1e6:.0f} GB/s)", flush=True)
+    del V
     torch.cuda.empty_cache()
