@@ -21,9 +21,9 @@
 // one structured buffer load per (tile, ks) — 16 rows x 64 contiguous bytes
 // per wave load, every byte of a row read once per call; the B operand is the
 // users: lane (g, c) holds user c's same chunk (zeros for c >= B). A wave owns
-// NT = 16 / KS tiles of 16 items at a time (NT x KS x 16 B = 256 B of item
-// operand per lane in flight), its loads issued before its MFMAs; the waves
-// of a CU overlap each other's loads with MFMAs.
+// NT = 8 / KS tiles of 16 items at a time (NT x KS x 16 B = 128 B of item
+// operand per lane), the next round's loads issued before this round's MFMAs
+// (two rounds in registers); the waves of a CU overlap each other's too.
 //
 // FILTER = false: out[b * ldo + j] = score of item row j * item_step.
 // FILTER = true:  append (score, j + idx_offset) to user b's list when score
@@ -40,6 +40,15 @@ constexpr int kGemvMaxB = 4;
 
 typedef float gemv_f4 __attribute__((ext_vector_type(4)));
 
+#ifndef HREC_GEMV_PIPE
+// 1 = the next round's loads issued before this round's MFMAs (with half the
+// tiles per round: the same registers). c4 one user, top-5 (50M x 128):
+// 4.34 -> 4.23 ms; 50M x 64: 2.50 -> 2.25 ms; 25M x 256 unchanged (4.33)
+#define HREC_GEMV_PIPE 1
+#endif
+#ifndef HREC_GEMV_NTDIV
+#define HREC_GEMV_NTDIV 2  // item tiles per wave round / this (with PIPE: two rounds' loads in registers)
+#endif
 #ifndef HREC_GEMV_NTX
 #define HREC_GEMV_NTX 1  // A/B builds: item tiles per wave round x this
 #endif
@@ -47,7 +56,8 @@ template <int DK>
 struct GemvShape {
   static constexpr int R = DK * 4;                  // row bytes (f32)
   static constexpr int KS = DK / 16;                // k steps of 16 (4 MFMAs each)
-  static constexpr int NT = (KS >= 16 ? 1 : 16 / KS) * HREC_GEMV_NTX;  // 16-item tiles per wave round
+  static constexpr int NT0 = (KS >= 16 ? 1 : 16 / KS) * HREC_GEMV_NTX / HREC_GEMV_NTDIV;
+  static constexpr int NT = NT0 < 1 ? 1 : NT0;  // 16-item tiles per wave round
   static constexpr int kItems = 16 * NT;            // items per wave round
 };
 
@@ -88,17 +98,33 @@ __global__ __launch_bounds__(kGemvThreads) void dot_gemv_kernel(
   const int64_t nw = (int64_t)gridDim.x * (kGemvThreads / 64);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool vec = !FILTER && (ldo & 3) == 0 && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-  for (int64_t rd = (int64_t)blockIdx.x * (kGemvThreads / 64) + wave; rd < n_rounds; rd += nw) {
-    const int64_t j0 = rd * S::kItems;
-    // one resource per round, based at its first row (rows past the matrix
-    // read as zeros; their scores are never reported)
-    const hrec_rsrc_t rs = rows_rsrc(V, j0 * item_step, S::R, n_rows);
-    gemv_f4 it[NT][KS];
+  // one resource per round, based at its first row (rows past the matrix
+  // read as zeros; their scores are never reported)
+  auto load_round = [&](int64_t rd, gemv_f4 (&it)[NT][KS]) {
+    const hrec_rsrc_t rs = rows_rsrc(V, rd * S::kItems * item_step, S::R, n_rows);
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         it[t][ks] = gemv_sbuf_load(rs, (int)((16 * t + c) * item_step), 64 * ks + 16 * g, 0, HREC_GEMV_AUX);
+  };
+  int64_t rd = (int64_t)blockIdx.x * (kGemvThreads / 64) + wave;
+#if HREC_GEMV_PIPE
+  gemv_f4 nx[NT][KS];  // the next round's items, loading during this round's MFMAs
+  if (rd < n_rounds) load_round(rd, nx);
+#endif
+  for (; rd < n_rounds; rd += nw) {
+    const int64_t j0 = rd * S::kItems;
+    gemv_f4 it[NT][KS];
+#if HREC_GEMV_PIPE
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) it[t][ks] = nx[t][ks];
+    if (rd + nw < n_rounds) load_round(rd + nw, nx);
+#else
+    load_round(rd, it);
+#endif
     gemv_f4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = gemv_f4{0.f, 0.f, 0.f, 0.f};
@@ -181,7 +207,7 @@ bool dot_gemv_applies(int B, int64_t step, int dk, int bf16) {
   if (bf16) return false;
   // a round's rows x step must stay within one 32-bit buffer offset (a round
   // is 16 KiB of rows at every dk: kItems * R = 16 NT * 4 dk)
-  const int64_t round_bytes = (int64_t)16384 * HREC_GEMV_NTX * step;
+  const int64_t round_bytes = (int64_t)16384 * HREC_GEMV_NTX * step;  // >= the real round (NTDIV shrinks it)
   return B >= 1 && B <= kGemvMaxB && (dk == 32 || dk == 64 || dk == 128 || dk == 256) &&
          round_bytes < ((int64_t)1 << 32);
 }
