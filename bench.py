@@ -311,6 +311,58 @@ def source_sha256(name):
         return hashlib.sha256(f.read()).hexdigest()
 
 
+# Counter evidence per bench line: the kernels a line's roofline is about
+# (name prefixes in the profile's per-kernel table) and the source they come
+# from; attached only when that source is the one profiled (sha256).
+COUNTER_KERNELS = [
+    ((), ["als_half_sweep_f64_kernel"], "als.hip"),
+    (("scoring",), ["als_bound_filter_kernel", "als_rescore_topk_kernel", "als_prune_"], "score.hip"),
+    (("hybrid_top5",), ["hx_"], "hybrid_exact.hip"),
+    (("ingest",), ["sort_downsweep_kernel", "sort_upsweep_kernel", "mark_", "codes_", "descent_kernel"],
+     "ingest.hip"),
+    (("tt_item_vectors_c4",), ["tt_item_forward_mfma_kernel<8, 8, true, false, 16, true>"], "tt_mfma.hip"),
+    (("tt_scoring_c4", "f32"), ["dot_res_kernel<false, 128, true"], "dot_topk.hip"),
+    (("tt_scoring_c4", "bf16"), ["dot_res_kernel<true, 128, true"], "dot_topk.hip"),
+    (("tt_scoring_c4", "f32_B1"), ["dot_gemv_kernel<128, true>"], "dot_gemv.hip"),
+    (("hybrid_top5_c5",), ["hyb_scores_kernel", "hp_", "dot_res_kernel<true, 256, true"], "hybrid_scores.hip"),
+    (("tt_train",), ["tt_item_forward_mfma_kernel<4, 4, true, true", "tt_bwd_", "adam_sparse_group4_kernel"],
+     "tt_mfma.hip"),
+    (("api_hybrid_call", "cold_user"), ["cold_"], "cold_start.hip"),
+    (("als_rank256",), ["als_half_sweep_wide_kernel"], "als_wide.hip"),
+]
+
+
+def attach_counters(line, pj, prof):
+    """roofline["counters"] of every line: per kernel of the line the trace
+    duration, the MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over every
+    SIMD's cycles), the effective clock and the HBM bytes per dispatch, from
+    the newest profiles/r*_prof_summary.json when it profiled this tree's
+    source of those kernels; otherwise null with the reason."""
+    table = pj.get("kernels") if pj else None
+    for path, prefixes, src in COUNTER_KERNELS:
+        node = line
+        for key in path:
+            node = node.get(key) if isinstance(node, dict) else None
+        if not isinstance(node, dict) or not isinstance(node.get("roofline"), dict):
+            continue
+        if not table:
+            node["roofline"]["counters"] = None
+            continue
+        fresh = pj.get("sources_sha256", {}).get(src) == source_sha256(src)
+        ks = {}
+        if fresh:
+            for name, e in sorted(table.items()):
+                if any(name.startswith(p) for p in prefixes):
+                    ks[name] = {k: e[k] for k in ("avg_ms", "mfma_busy_frac", "eff_clock_GHz",
+                                                  "hbm_bytes_per_dispatch_corrected") if k in e}
+        node["roofline"]["counters"] = {
+            "profile": os.path.relpath(prof, ROOT), "source": src, "source_matches_profile": fresh,
+            "kernels": ks if fresh else None,
+            "note": ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), reads low on "
+                     "dispatches < 0.3 ms; hbm bytes = FETCH_SIZE x 2 + WRITE_SIZE (KiB, gfx950 16-B-load "
+                     "correction); separate PMC passes, scripts/gpu_profile.sh")}
+
+
 def api_line(eng, n_users, n_items, k, reps, want_cpu):
     import contextlib
     import io
@@ -1331,6 +1383,7 @@ def main():
             "als_rank256": als256,
             "als_c3": als_c3,
         }
+        attach_counters(line, pj if world == 1 else {}, prof)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

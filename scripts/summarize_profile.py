@@ -180,8 +180,61 @@ def main(base):
                                 "indptr_from_sorted_kernel", "sort_upsweep_kernel",
                                 "sort_downsweep_kernel<true, false>", "sort_downsweep_kernel<false, true>"],
                                "prof_fetch_ing", "prof_write_ing")
+    res["kernels"] = per_kernel_counters(base, trace, wide)
     res["sources_sha256"] = source_hashes()
     print(json.dumps(res, indent=1))
+
+
+def kname(name):
+    return name.split("(")[0].replace("void ", "").replace("hrec::", "").strip()
+
+
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
+
+
+def per_kernel_counters(base, trace, wide):
+    """Every kernel of every pass, by template instantiation: trace average
+    duration, HBM bytes per dispatch (FETCH_SIZE x2 + WRITE_SIZE, KiB units,
+    gfx950 16-B-load correction) and the MFMA-busy fraction per dispatch:
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) (GRBM counts
+    every XCD's cycles; the MFMA counter every SIMD's busy cycles; reads low on
+    dispatches shorter than ~0.3 ms, MI355X_MICROARCH.md DVFS note), with the
+    effective clock GRBM_GUI_ACTIVE / 8 / trace duration."""
+    import collections
+
+    out = collections.defaultdict(dict)
+    dur = collections.defaultdict(list)
+    for r in trace + wide:
+        dur[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    for k, v in dur.items():
+        out[k]["launches_in_trace"] = len(v)
+        out[k]["avg_ms"] = sum(v) / len(v)
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for sub in glob.glob(os.path.join(base, "prof_*")):
+        if os.path.basename(sub).startswith(("prof_fetch", "prof_write", "prof_mfma")) and os.path.isdir(sub):
+            for r in rows(os.path.join(sub, "**", "*counter_collection.csv")):
+                vals[kname(r.get("Kernel_Name", ""))][r.get("Counter_Name")].append(
+                    ((sub, r.get("Dispatch_Id")), float(r["Counter_Value"])))
+    for k, cs in vals.items():
+        e = out[k]
+        f = [v for _, v in cs.get("FETCH_SIZE", [])]
+        w = [v for _, v in cs.get("WRITE_SIZE", [])]
+        if f:
+            e["FETCH_SIZE_KiB_avg"] = sum(f) / len(f)
+        if w:
+            e["WRITE_SIZE_KiB_avg"] = sum(w) / len(w)
+        if f and w:
+            e["hbm_bytes_per_dispatch_corrected"] = 1024 * (2 * e["FETCH_SIZE_KiB_avg"] + e["WRITE_SIZE_KiB_avg"])
+        mb = dict(cs.get("SQ_VALU_MFMA_BUSY_CYCLES", []))
+        gr = dict(cs.get("GRBM_GUI_ACTIVE", []))
+        fr = [mb[d] / (gr[d] / 8 * N_SIMD) for d in mb if d in gr and gr[d] > 0]
+        if fr:
+            e["mfma_busy_frac"] = sum(fr) / len(fr)
+            e["mfma_busy_dispatches"] = len(fr)
+            g = [v for v in gr.values()]
+            if e.get("avg_ms"):
+                e["eff_clock_GHz"] = sum(g) / len(g) / 8 / (e["avg_ms"] * 1e6)
+    return dict(out)
 
 
 if __name__ == "__main__":
