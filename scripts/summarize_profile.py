@@ -210,11 +210,13 @@ def per_kernel_counters(base, trace, wide):
         out[k]["launches_in_trace"] = len(v)
         out[k]["avg_ms"] = sum(v) / len(v)
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    grids = collections.defaultdict(dict)  # kernel -> (pass, dispatch) -> grid size
     for sub in glob.glob(os.path.join(base, "prof_*")):
         if os.path.basename(sub).startswith(("prof_fetch", "prof_write", "prof_mfma")) and os.path.isdir(sub):
             for r in rows(os.path.join(sub, "**", "*counter_collection.csv")):
-                vals[kname(r.get("Kernel_Name", ""))][r.get("Counter_Name")].append(
-                    ((sub, r.get("Dispatch_Id")), float(r["Counter_Value"])))
+                kn = kname(r.get("Kernel_Name", ""))
+                vals[kn][r.get("Counter_Name")].append(((sub, r.get("Dispatch_Id")), float(r["Counter_Value"])))
+                grids[kn][(sub, r.get("Dispatch_Id"))] = int(r.get("Grid_Size") or 0)
     for k, cs in vals.items():
         e = out[k]
         f = [v for _, v in cs.get("FETCH_SIZE", [])]
@@ -227,13 +229,24 @@ def per_kernel_counters(base, trace, wide):
             e["hbm_bytes_per_dispatch_corrected"] = 1024 * (2 * e["FETCH_SIZE_KiB_avg"] + e["WRITE_SIZE_KiB_avg"])
         mb = dict(cs.get("SQ_VALU_MFMA_BUSY_CYCLES", []))
         gr = dict(cs.get("GRBM_GUI_ACTIVE", []))
-        fr = [mb[d] / (gr[d] / 8 * N_SIMD) for d in mb if d in gr and gr[d] > 0]
-        if fr:
-            e["mfma_busy_frac"] = sum(fr) / len(fr)
-            e["mfma_busy_dispatches"] = len(fr)
-            g = [v for v in gr.values()]
+        ds = [d for d in mb if d in gr and gr[d] > 0]
+        if ds:
+            # time-weighted (sum of busy cycles over sum of SIMD cycles): the
+            # long dispatches dominate; per launch shape (grid size) as well,
+            # since one kernel serves batches of 1 and of 1024 users
+            e["mfma_busy_frac"] = sum(mb[d] for d in ds) / sum(gr[d] / 8 * N_SIMD for d in ds)
+            e["mfma_busy_dispatches"] = len(ds)
+            by = collections.defaultdict(list)
+            for d in ds:
+                by[grids[k].get(d, 0)].append(d)
+            if len(by) > 1:
+                e["mfma_busy_by_grid"] = {
+                    str(gsz): {"dispatches": len(dd), "mfma_busy_frac":
+                               sum(mb[d] for d in dd) / sum(gr[d] / 8 * N_SIMD for d in dd),
+                               "grbm_cycles_per_xcd_avg": sum(gr[d] for d in dd) / len(dd) / 8}
+                    for gsz, dd in sorted(by.items())}
             if e.get("avg_ms"):
-                e["eff_clock_GHz"] = sum(g) / len(g) / 8 / (e["avg_ms"] * 1e6)
+                e["eff_clock_GHz"] = sum(gr[d] for d in ds) / len(ds) / 8 / (e["avg_ms"] * 1e6)
     return dict(out)
 
 
