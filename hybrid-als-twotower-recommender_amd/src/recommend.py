@@ -68,6 +68,26 @@ class DeviceOps:
     topk_keyed = staticmethod(_hrec.topk_keyed)
 
 
+# Batch shapes whose workspaces a recommender keeps (one per shape
+# ever seen grew device memory without bound for callers that vary the batch).
+WORKSPACE_CACHE = 4
+
+
+def _lru_get(cache, key):
+    """cache: a dict in insertion order = recency order."""
+    v = cache.pop(key, None)
+    if v is not None:
+        cache[key] = v
+    return v
+
+
+def _lru_put(cache, key, value):
+    cache[key] = value
+    while len(cache) > WORKSPACE_CACHE:
+        cache.pop(next(iter(cache)))
+    return value
+
+
 class ShardedRecommender:
     """precision "exact": JVM-exact ALS scores (Spark's f32 mul/add chain) and
     f32 two-tower Dot — the reference's numerics. For top_k <= 8, batches of
@@ -137,12 +157,12 @@ class ShardedRecommender:
         B = int(user_rows.shape[0])
         dev = user_vecs.device
         if self.n_local > 0:
-            # one workspace per batch shape, reused across batches
-            cache = self.__dict__.setdefault("_prune", {})
-            hp = cache.get((B, int(top_k), tuple(user_vecs.shape)))
+            # one workspace per batch shape, reused across batches (a few shapes kept)
+            key = (B, int(top_k), tuple(user_vecs.shape))
+            hp = _lru_get(self.__dict__.setdefault("_prune", {}), key)
             if hp is None:
-                hp = cache[(B, int(top_k), tuple(user_vecs.shape))] = o.hybrid_prune(
-                    self.U, user_rows, user_vecs, self.V_op, self.iv_op, top_k)
+                hp = _lru_put(self._prune, key, o.hybrid_prune(self.U, user_rows, user_vecs, self.V_op, self.iv_op,
+                                                               top_k))
             else:
                 hp.rebind(user_rows, user_vecs)
             if self.world == 1:  # one shard: both phases in one call (no C2 between them)
@@ -173,10 +193,10 @@ class ShardedRecommender:
         B = int(user_rows.shape[0])
         dev = user_vecs.device
         if self.n_local > 0:
-            cache = self.__dict__.setdefault("_hx", {})
-            hx = cache.get((B, int(top_k)))
+            key = (B, int(top_k))
+            hx = _lru_get(self.__dict__.setdefault("_hx", {}), key)
             if hx is None:
-                hx = cache[(B, int(top_k))] = o.hybrid_exact(self.U, user_rows, user_vecs, self.exact_items, top_k)
+                hx = _lru_put(self._hx, key, o.hybrid_exact(self.U, user_rows, user_vecs, self.exact_items, top_k))
             else:
                 hx.rebind(user_rows, user_vecs)
             self.last_exact = hx

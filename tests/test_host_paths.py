@@ -142,3 +142,17 @@ def test_fast_columns_lookup_rules():
     assert tt._fast_columns(pd.concat([df, df[["price"]]], axis=1)) is None
     assert tt._fast_columns(df["itemId"].to_numpy()) is None   # a plain id array: no column lookups
     assert tt._fast_columns({"itemId": df["itemId"]}) is None
+
+
+def test_recommender_workspace_cache_is_bounded():
+    """the per-batch-shape workspaces of ShardedRecommender stay a
+    small LRU (a caller sweeping batch sizes does not grow device memory)."""
+    from src import recommend as rc
+
+    cache = {}
+    for b in range(10):
+        assert rc._lru_get(cache, b) is None
+        rc._lru_put(cache, b, object())
+        rc._lru_get(cache, 0)  # keep shape 0 in use
+    assert len(cache) == rc.WORKSPACE_CACHE
+    assert 0 in cache and 9 in cache and 1 not in cache
