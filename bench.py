@@ -902,7 +902,8 @@ def main():
                    "items": n_items, "top_k": 5, "dtype": "f32 (JVM-exact, no FMA) behind a bf16 bound",
                    "kernel": "hrec_als_score_topk_pruned (bf16 wave-tile maxima of 32768 items -> a sample bound; "
                              "bf16 matrix-core bound filter over every pair; JVM-exact chain over the kept pairs + "
-                             "stable top-k in one block per user)",
+                             "stable top-k in one block per user; an overflow resolved on the device by the gated "
+                             "exact top-k, so a call needs no host read)",
                    "fused_ms_per_batch": fu_s * 1e3, "fused_pairs_per_s": B * n_items / fu_s,
                    "pruned_equals_fused": same,
                    "pairs_per_user": {"bound_kept_mean": float(kept[0].float().mean()),

@@ -1858,6 +1858,106 @@ __global__ __launch_bounds__(256) void als_rescore_topk_kernel(const float* __re
   }
 }
 
+// The exact fallback of the pruned top-k for kk <= 8, on the device: when
+// *gate != 0 (a user overflowed a list or had no finite bound), every user's
+// stable top-kk of the JVM chain over ALL items — the chain of
+// als_rescore_topk_kernel (and of the fused path), one block per user, a
+// sorted list of KK per thread, then wave and block merges by arg-best rounds
+// (ties -> smaller item, NaN last). An unknown user (row < 0) gets the
+// pruned path's answer for it, no candidates: (0, -1) entries. Gate 0:
+// every block returns after one load (no host round trip decides the
+// fallback).
+template <int KK>
+__global__ __launch_bounds__(256) void als_exact_topk_kernel(const float* __restrict__ U, int kp,
+                                                             const int64_t* __restrict__ user_rows, int k,
+                                                             const float* __restrict__ V, int64_t ldv, int64_t N,
+                                                             int kk, const int* __restrict__ gate,
+                                                             int64_t* __restrict__ out_idx,
+                                                             float* __restrict__ out_val) {
+#pragma clang fp contract(off)
+  if (*gate == 0) return;  // block-uniform
+  __shared__ __attribute__((aligned(16))) float su[kScoreKMax];
+  __shared__ float s_v[4 * KK];
+  __shared__ int64_t s_i[4 * KK];
+  const int b = blockIdx.x;
+  const int64_t r = user_rows[b];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (r < 0) {  // block-uniform
+    for (int q = threadIdx.x; q < kk; q += blockDim.x) {
+      out_val[(int64_t)b * kk + q] = 0.f;
+      out_idx[(int64_t)b * kk + q] = -1;
+    }
+    return;
+  }
+  for (int c = threadIdx.x; c < kp; c += blockDim.x) su[c] = c < k ? U[r * kp + c] : 0.f;
+  __syncthreads();
+  float lv[KK];
+  int64_t li[KK];
+#pragma unroll
+  for (int q = 0; q < KK; ++q) {
+    lv[q] = 0.f;
+    li[q] = INT64_MAX;
+  }
+  const int kr = (k + 3) & ~3;
+  const bool vec = (ldv & 3) == 0 && ((uintptr_t)V & 15) == 0;
+  for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+    float acc = 0.f;
+    const float* v = V + j * ldv;
+    int c = 0;
+    if (vec) {
+      for (; c + 4 <= k; c += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(v + c);
+        acc = acc + su[c] * x.x;
+        acc = acc + su[c + 1] * x.y;
+        acc = acc + su[c + 2] * x.z;
+        acc = acc + su[c + 3] * x.w;
+      }
+    }
+    for (; c < k; ++c) acc = acc + su[c] * v[c];
+    for (; c < kr; ++c) acc = acc + 0.f * 0.f;
+    float xv = acc;
+    int64_t xi = j;
+#pragma unroll
+    for (int q = 0; q < KK; ++q) {
+      const bool sw = li[q] == INT64_MAX || better(xv, xi, lv[q], li[q]);
+      const float tv = lv[q];
+      const int64_t ti = li[q];
+      lv[q] = sw ? xv : tv;
+      li[q] = sw ? xi : ti;
+      xv = sw ? tv : xv;
+      xi = sw ? ti : xi;
+    }
+  }
+  // each wave's best kk -> LDS
+  for (int q = 0; q < kk; ++q) {
+    const KV<float> x = wave_best(KV<float>{lv[0], li[0]});
+    if (lane == 0) {
+      s_v[w * KK + q] = x.v;
+      s_i[w * KK + q] = x.i;
+    }
+    if (x.i != INT64_MAX && li[0] == x.i) {
+#pragma unroll
+      for (int e = 0; e + 1 < KK; ++e) {
+        lv[e] = lv[e + 1];
+        li[e] = li[e + 1];
+      }
+      li[KK - 1] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+  KV<float> m{0.f, INT64_MAX};
+  if (lane < 4 * KK && lane % KK < kk) m = KV<float>{s_v[lane], s_i[lane]};
+  for (int q = 0; q < kk; ++q) {
+    const KV<float> x = wave_best(m);
+    if (lane == 0) {
+      out_val[(int64_t)b * kk + q] = x.i == INT64_MAX ? 0.f : x.v;
+      out_idx[(int64_t)b * kk + q] = x.i == INT64_MAX ? -1 : x.i;
+    }
+    if (x.i != INT64_MAX && m.i == x.i) m.i = INT64_MAX;
+  }
+}
+
 template <bool MAXONLY>
 static int bound_filter_launch(int dk, dim3 grid, hipStream_t s, const uint16_t* uop, int n_users,
                                const uint16_t* items, int64_t N, const float* thr2, int cap, int64_t* pre_i,
@@ -2005,11 +2105,26 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
   HREC_REQUIRE(((uintptr_t)items_bf16 & 255) == 0, "als_score_topk_pruned: items_bf16 must be 256-B aligned");
   const size_t need = hrec_als_score_topk_pruned_workspace_bytes(n_users, n_items, top_k, k);
   HREC_REQUIRE(workspace_bytes >= need, "als_score_topk_pruned: workspace %zu < %zu", workspace_bytes, need);
-  if (n_items <= kSample)  // small: the fused path scores everything anyway
-    return hrec_als_score_topk(user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp, top_k,
-                               out_idx, out_val, overflow, workspace, workspace_bytes, stream);
   hipStream_t s = as_stream(stream);
   const int kk = (int)(top_k < n_items ? top_k : n_items);
+  // kk <= 8: a set *overflow is resolved here, on the device (the gated
+  // exact top-k over every item), so the result is always exact
+  auto exact_fallback = [&]() {
+    if (kk > 8) return (int)HREC_OK;
+#define HREC_EXT(KK)                                                                                             \
+  hipLaunchKernelGGL(als_exact_topk_kernel<KK>, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp,        \
+                     user_rows, k, item_factors, ld_v, n_items, kk, overflow, out_idx, out_val)
+    if (kk <= 2) HREC_EXT(2);
+    else if (kk <= 4) HREC_EXT(4);
+    else HREC_EXT(8);
+#undef HREC_EXT
+    return check_launch("als_exact_topk_kernel");
+  };
+  if (n_items <= kSample) {  // small: the fused path scores everything anyway
+    const int rc = hrec_als_score_topk(user_factors, user_rows, n_users, item_factors_t, ld_items, n_items, k, kp,
+                                       top_k, out_idx, out_val, overflow, workspace, workspace_bytes, stream);
+    return rc ? rc : exact_fallback();
+  }
   const int dk = prune_dk(k);
   const PruneWs w = prune_layout((char*)workspace, n_users, n_items, kk, dk);
   const int64_t S = n_items < kPruneSample ? n_items : kPruneSample;
@@ -2065,7 +2180,8 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
     else if (kk <= 4) HREC_RTK(4);
     else HREC_RTK(8);
 #undef HREC_RTK
-    return check_launch("als_rescore_topk_kernel");
+    rc = check_launch("als_rescore_topk_kernel");
+    return rc ? rc : exact_fallback();
   }
   hipLaunchKernelGGL(als_rescore_kernel, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp, user_rows,
                      n_users, k, item_factors, ld_v, w.pi, w.pn, kCap, w.tau, kk, w.cv, w.ci, w.cn, overflow);

@@ -427,9 +427,10 @@ def als_score_topk_pruned(user_factors, user_rows, item_factors_t, item_factors,
     """als_score_topk with the bf16 matrix-core bound in front of the exact
     chain (hrec_als_score_topk_pruned): the same (ids, scores). item_factors
     is the row-major copy of item_factors_t, items_bf16 from als_items_bf16.
-    workspace (uint8 device, optional) is reused when large enough; the
-    overflow flag falls back to the full score matrix + top-k as
-    als_score_topk does."""
+    workspace (uint8 device, optional) is reused when large enough. For
+    top_k <= 8 an overflow is resolved on the device inside the call (no
+    host read); above, the overflow flag falls back to the full score matrix
+    + top-k as als_score_topk does (check_overflow)."""
     kp = user_factors.shape[1]
     B = user_rows.numel()
     kk = min(int(top_k), int(n_items))
@@ -449,7 +450,7 @@ def als_score_topk_pruned(user_factors, user_rows, item_factors_t, item_factors,
         _dev(items_bf16, torch.uint8, "items_bf16"), n_items, int(k), kp, kk,
         _dev(out_i, torch.int64, "out_idx"), _dev(out_v, torch.float32, "out_val"),
         _dev(flag, torch.int32, "overflow"), _dev(ws, torch.uint8, "ws"), ws.numel(), _stream()))
-    if check_overflow and int(flag.item()) != 0:
+    if check_overflow and kk > 8 and int(flag.item()) != 0:
         scores = als_score(user_factors, user_rows, item_factors_t, None, n_items, k)
         return topk(scores, kk)
     return out_i, out_v

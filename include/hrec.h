@@ -42,7 +42,8 @@ extern "C" {
  *    replaces them); hrec_dot_topk's +inf bound admits scores >= +inf.
  * 4: the RCCL exchange steps (hrec_comm_*, hrec_allgather, hrec_allreduce_minmax).
  * 6: hrec_als_score_topk_pruned_counts, hrec_cold_fallback*; the pruned ALS
- *    bound is 2^-7 + 2^-13. */
+ *    bound is 2^-7 + 2^-13 and its top_k <= 8 results are exact without a
+ *    host-side fallback. */
 #define HREC_ABI_VERSION 6
 
 #define HREC_OK 0
@@ -205,7 +206,11 @@ int hrec_als_score_topk(const float* user_factors, const int64_t* user_rows,
  * same stable top-k. *overflow is also set when a bound is not finite (a
  * non-finite factor), when the bf16 filter's list overflows, or when a known
  * user ends with fewer than min(top_k, n_items) candidates (a bound slip:
- * never short or padded ids). items_bf16: hrec_als_items_bf16 of
+ * never short or padded ids). For min(top_k, n_items) <= 8 a set *overflow
+ * is resolved in the same call, on the device (a gated exact top-k of the
+ * JVM chain over every item, no host round trip): the outputs are then
+ * always exact and *overflow only reports that the fallback ran; above 8 the
+ * caller falls back as for hrec_als_score_topk. items_bf16: hrec_als_items_bf16 of
  * item_factors (row-major [n_items, ld_v], the same values as
  * item_factors_t), 256-B aligned; it is built once per item matrix.
  * hrec_als_score_topk_pruned_counts copies the last call's diagnostics from

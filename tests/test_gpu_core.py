@@ -413,7 +413,8 @@ def test_als_score_topk_overflow_flag(device):
     (100_003, 64, 64, 40, 5, "normal"), (100_000, 64, 64, 17, 10, "quant"), (30_000, 16, 16, 9, 1, "normal"),
     (50_000, 100, 128, 12, 100, "normal"), (40_000, 200, 256, 8, 8, "scaled"), (3000, 64, 64, 5, 5, "normal"),
     (60_000, 64, 64, 10, 5, "unknown"), (60_000, 64, 64, 10, 5, "nan_item"), (60_000, 64, 64, 10, 5, "const"),
-    (3000, 16, 16, 4, 1, "round_up"), (40_000, 16, 16, 4, 1, "round_up"), (40_000, 64, 64, 6, 3, "round_up")])
+    (3000, 16, 16, 4, 1, "round_up"), (40_000, 16, 16, 4, 1, "round_up"), (40_000, 64, 64, 6, 3, "round_up"),
+    (60_000, 64, 64, 10, 8, "const"), (60_000, 64, 64, 10, 3, "nan_item")])
 def test_als_score_topk_pruned_matches_fused(device, n_items, k, kp, B, top_k, case):
     """hrec_als_score_topk_pruned (bf16 matrix-core bound, exact chain only
     for the pairs it keeps) returns the fused path's (ids, scores) bit for
@@ -461,17 +462,23 @@ def test_als_score_topk_pruned_matches_fused(device, n_items, k, kp, B, top_k, c
                                      overflow_out=flag_p)
     fi, fv = h.als_score_topk(dU, users, Vt, n_items, k, top_k, check_overflow=False, overflow_out=flag_f)
     fp, ff = int(flag_p.item()), int(flag_f.item())
+    known = rows >= 0
+    full = oals.score_matrix(U[known, :k], V[:, :k])
+    exp_i = _np_stable_topk(full, min(top_k, n_items))
     if case in ("nan_item", "const"):
         assert fp == 1
     else:
         assert fp == ff == 0, (fp, ff)
         np.testing.assert_array_equal(pi.cpu().numpy(), fi.cpu().numpy())
         np.testing.assert_array_equal(pv.cpu().numpy().view(np.int32), fv.cpu().numpy().view(np.int32))
+    if min(top_k, n_items) <= 8:  # resolved on the device inside the call, whatever the flag says
+        np.testing.assert_array_equal(pi.cpu().numpy()[known], exp_i)
+        np.testing.assert_array_equal(pv.cpu().numpy()[known].view(np.int32),
+                                      np.take_along_axis(full, exp_i, 1).view(np.int32))
+        if not known.all():
+            assert (pi.cpu().numpy()[~known] == -1).all()
     # with the fallback resolved, both equal the full matrix's stable top-k
     pi, pv = h.als_score_topk_pruned(dU, users, Vt, dV, ops, n_items, k, top_k)
-    known = rows >= 0
-    full = oals.score_matrix(U[known, :k], V[:, :k])
-    exp_i = _np_stable_topk(full, min(top_k, n_items))
     got_i, got_v = pi.cpu().numpy()[known], pv.cpu().numpy()[known]
     np.testing.assert_array_equal(got_i, exp_i)
     np.testing.assert_array_equal(got_v.view(np.int32), np.take_along_axis(full, exp_i, 1).view(np.int32))
