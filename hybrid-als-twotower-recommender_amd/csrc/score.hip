@@ -1401,9 +1401,11 @@ __global__ __launch_bounds__(256) void als_items_bf16_kernel(const float* __rest
 __global__ __launch_bounds__(256) void als_prune_user_kernel(const float* __restrict__ U, int kp,
                                                              const int64_t* __restrict__ user_rows, int n_users,
                                                              int k, int dk, const float* __restrict__ max_norm,
-                                                             uint16_t* __restrict__ uop, double* __restrict__ err) {
+                                                             uint16_t* __restrict__ uop, double* __restrict__ err,
+                                                             int* __restrict__ overflow) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = 0;  // the call's first kernel (no memset launch)
   if (b >= n_users) return;  // wave-uniform
   const int64_t r = user_rows[b];
   double ss = 0.0;
@@ -1869,9 +1871,9 @@ __global__ __launch_bounds__(256) void als_rescore_topk_kernel(const float* __re
 // fallback).
 template <int KK>
 __global__ __launch_bounds__(256) void als_exact_topk_kernel(const float* __restrict__ U, int kp,
-                                                             const int64_t* __restrict__ user_rows, int k,
-                                                             const float* __restrict__ V, int64_t ldv, int64_t N,
-                                                             int kk, const int* __restrict__ gate,
+                                                             const int64_t* __restrict__ user_rows, int n_users,
+                                                             int k, const float* __restrict__ V, int64_t ldv,
+                                                             int64_t N, int kk, const int* __restrict__ gate,
                                                              int64_t* __restrict__ out_idx,
                                                              float* __restrict__ out_val) {
 #pragma clang fp contract(off)
@@ -1879,82 +1881,85 @@ __global__ __launch_bounds__(256) void als_exact_topk_kernel(const float* __rest
   __shared__ __attribute__((aligned(16))) float su[kScoreKMax];
   __shared__ float s_v[4 * KK];
   __shared__ int64_t s_i[4 * KK];
-  const int b = blockIdx.x;
-  const int64_t r = user_rows[b];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (r < 0) {  // block-uniform
-    for (int q = threadIdx.x; q < kk; q += blockDim.x) {
-      out_val[(int64_t)b * kk + q] = 0.f;
-      out_idx[(int64_t)b * kk + q] = -1;
-    }
-    return;
-  }
-  for (int c = threadIdx.x; c < kp; c += blockDim.x) su[c] = c < k ? U[r * kp + c] : 0.f;
-  __syncthreads();
-  float lv[KK];
-  int64_t li[KK];
-#pragma unroll
-  for (int q = 0; q < KK; ++q) {
-    lv[q] = 0.f;
-    li[q] = INT64_MAX;
-  }
   const int kr = (k + 3) & ~3;
   const bool vec = (ldv & 3) == 0 && ((uintptr_t)V & 15) == 0;
-  for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
-    float acc = 0.f;
-    const float* v = V + j * ldv;
-    int c = 0;
-    if (vec) {
-      for (; c + 4 <= k; c += 4) {
-        const float4 x = *reinterpret_cast<const float4*>(v + c);
-        acc = acc + su[c] * x.x;
-        acc = acc + su[c + 1] * x.y;
-        acc = acc + su[c + 2] * x.z;
-        acc = acc + su[c + 3] * x.w;
+  for (int b = blockIdx.x; b < n_users; b += gridDim.x) {  // block-uniform trip count
+    const int64_t r = user_rows[b];
+    if (r < 0) {
+      for (int q = threadIdx.x; q < kk; q += blockDim.x) {
+        out_val[(int64_t)b * kk + q] = 0.f;
+        out_idx[(int64_t)b * kk + q] = -1;
       }
+      continue;
     }
-    for (; c < k; ++c) acc = acc + su[c] * v[c];
-    for (; c < kr; ++c) acc = acc + 0.f * 0.f;
-    float xv = acc;
-    int64_t xi = j;
+    __syncthreads();  // the previous user's readers of su / s_v are done
+    for (int c = threadIdx.x; c < kp; c += blockDim.x) su[c] = c < k ? U[r * kp + c] : 0.f;
+    __syncthreads();
+    float lv[KK];
+    int64_t li[KK];
 #pragma unroll
     for (int q = 0; q < KK; ++q) {
-      const bool sw = li[q] == INT64_MAX || better(xv, xi, lv[q], li[q]);
-      const float tv = lv[q];
-      const int64_t ti = li[q];
-      lv[q] = sw ? xv : tv;
-      li[q] = sw ? xi : ti;
-      xv = sw ? tv : xv;
-      xi = sw ? ti : xi;
+      lv[q] = 0.f;
+      li[q] = INT64_MAX;
     }
-  }
-  // each wave's best kk -> LDS
-  for (int q = 0; q < kk; ++q) {
-    const KV<float> x = wave_best(KV<float>{lv[0], li[0]});
-    if (lane == 0) {
-      s_v[w * KK + q] = x.v;
-      s_i[w * KK + q] = x.i;
-    }
-    if (x.i != INT64_MAX && li[0] == x.i) {
-#pragma unroll
-      for (int e = 0; e + 1 < KK; ++e) {
-        lv[e] = lv[e + 1];
-        li[e] = li[e + 1];
+    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+      float acc = 0.f;
+      const float* v = V + j * ldv;
+      int c = 0;
+      if (vec) {
+        for (; c + 4 <= k; c += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(v + c);
+          acc = acc + su[c] * x.x;
+          acc = acc + su[c + 1] * x.y;
+          acc = acc + su[c + 2] * x.z;
+          acc = acc + su[c + 3] * x.w;
+        }
       }
-      li[KK - 1] = INT64_MAX;
+      for (; c < k; ++c) acc = acc + su[c] * v[c];
+      for (; c < kr; ++c) acc = acc + 0.f * 0.f;
+      float xv = acc;
+      int64_t xi = j;
+#pragma unroll
+      for (int q = 0; q < KK; ++q) {
+        const bool sw = li[q] == INT64_MAX || better(xv, xi, lv[q], li[q]);
+        const float tv = lv[q];
+        const int64_t ti = li[q];
+        lv[q] = sw ? xv : tv;
+        li[q] = sw ? xi : ti;
+        xv = sw ? tv : xv;
+        xi = sw ? ti : xi;
+      }
     }
-  }
-  __syncthreads();
-  if (w != 0) return;
-  KV<float> m{0.f, INT64_MAX};
-  if (lane < 4 * KK && lane % KK < kk) m = KV<float>{s_v[lane], s_i[lane]};
-  for (int q = 0; q < kk; ++q) {
-    const KV<float> x = wave_best(m);
-    if (lane == 0) {
-      out_val[(int64_t)b * kk + q] = x.i == INT64_MAX ? 0.f : x.v;
-      out_idx[(int64_t)b * kk + q] = x.i == INT64_MAX ? -1 : x.i;
+    // each wave's best kk -> LDS, then wave 0 merges the four lists
+    for (int q = 0; q < kk; ++q) {
+      const KV<float> x = wave_best(KV<float>{lv[0], li[0]});
+      if (lane == 0) {
+        s_v[w * KK + q] = x.v;
+        s_i[w * KK + q] = x.i;
+      }
+      if (x.i != INT64_MAX && li[0] == x.i) {
+#pragma unroll
+        for (int e = 0; e + 1 < KK; ++e) {
+          lv[e] = lv[e + 1];
+          li[e] = li[e + 1];
+        }
+        li[KK - 1] = INT64_MAX;
+      }
     }
-    if (x.i != INT64_MAX && m.i == x.i) m.i = INT64_MAX;
+    __syncthreads();
+    if (w == 0) {
+      KV<float> m{0.f, INT64_MAX};
+      if (lane < 4 * KK && lane % KK < kk) m = KV<float>{s_v[lane], s_i[lane]};
+      for (int q = 0; q < kk; ++q) {
+        const KV<float> x = wave_best(m);
+        if (lane == 0) {
+          out_val[(int64_t)b * kk + q] = x.i == INT64_MAX ? 0.f : x.v;
+          out_idx[(int64_t)b * kk + q] = x.i == INT64_MAX ? -1 : x.i;
+        }
+        if (x.i != INT64_MAX && m.i == x.i) m.i = INT64_MAX;
+      }
+    }
   }
 }
 
@@ -2112,8 +2117,9 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
   auto exact_fallback = [&]() {
     if (kk > 8) return (int)HREC_OK;
 #define HREC_EXT(KK)                                                                                             \
-  hipLaunchKernelGGL(als_exact_topk_kernel<KK>, dim3((unsigned)n_users), dim3(256), 0, s, user_factors, kp,        \
-                     user_rows, k, item_factors, ld_v, n_items, kk, overflow, out_idx, out_val)
+  hipLaunchKernelGGL(als_exact_topk_kernel<KK>, dim3((unsigned)(n_users < 512 ? n_users : 512)), dim3(256), 0, s,  \
+                     user_factors, kp, user_rows, n_users, k, item_factors, ld_v, n_items, kk, overflow, out_idx,     \
+                     out_val)
     if (kk <= 2) HREC_EXT(2);
     else if (kk <= 4) HREC_EXT(4);
     else HREC_EXT(8);
@@ -2130,10 +2136,9 @@ extern "C" int hrec_als_score_topk_pruned(const float* user_factors, const int64
   const int64_t S = n_items < kPruneSample ? n_items : kPruneSample;
   const float* max_norm = reinterpret_cast<const float*>(static_cast<const char*>(items_bf16) +
                                                          hrec_als_items_bf16_bytes(n_items, k) - 256);
-  if (hipMemsetAsync(overflow, 0, sizeof(int), s) != hipSuccess) return check_launch("score_topk_pruned memset");
-  // 1) bf16 user operands and E_b; the sample's bf16 scores; its bound
+  // 1) bf16 user operands and E_b (and *overflow = 0); the sample's bf16 scores; its bound
   hipLaunchKernelGGL(als_prune_user_kernel, dim3((unsigned)((n_users + 3) / 4)), dim3(256), 0, s, user_factors, kp,
-                     user_rows, n_users, k, dk, max_norm, w.uop, w.err);
+                     user_rows, n_users, k, dk, max_norm, w.uop, w.err, overflow);
   int rc = check_launch("als_prune_user_kernel");
   if (rc) return rc;
   if (kk <= 64) {
