@@ -113,8 +113,9 @@ __global__ __launch_bounds__(128) void hx_user_ops_kernel(const float* __restric
                                                           const int64_t* __restrict__ rows, int64_t n_rows, int ka,
                                                           const float* __restrict__ T, int64_t ldt, int kt, int B,
                                                           int dk, uint16_t* __restrict__ uop, float* __restrict__ uf,
-                                                          int* __restrict__ uok) {
+                                                          int* __restrict__ uok, int* __restrict__ flag) {
   const int b = blockIdx.x, m = blockIdx.y;
+  if (b == 0 && m == 0 && threadIdx.x < 2) flag[threadIdx.x] = 0;  // the flag + pair total (no reset launch)
   int64_t r = b;
   bool bad = false;
   if (m == 0 && rows) {
@@ -1184,14 +1185,16 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   const int G = (int)((N + kHxGrp - 1) / kHxGrp);
   const char* items = static_cast<const char*>(x->prepared);
   {
-    hipLaunchKernelGGL(hx_reset_kernel, dim3(1), dim3(64), 0, s, w.flag, 2, mode == 1);
-    const int rc = check_launch("hx_reset_kernel");
-    if (rc) return rc;
+    if (mode == 1) {  // otherwise hx_user_ops_kernel resets both
+      hipLaunchKernelGGL(hx_reset_kernel, dim3(1), dim3(64), 0, s, w.flag, 2, 1);
+      const int rc = check_launch("hx_reset_kernel");
+      if (rc) return rc;
+    }
   }
   if (mode != 1) {
     hipLaunchKernelGGL(hx_user_ops_kernel, dim3((unsigned)B, 2), dim3(128), 0, s, x->als_users, x->als_ld,
                        x->als_rows, x->n_als_rows, x->als_width, x->tt_users, x->tt_ld, x->tt_width, B, dk, w.uop,
-                       w.uf, w.uok);
+                       w.uf, w.uok, w.flag);
     int rc = check_launch("hx_user_ops_kernel");
     if (rc) return rc;
 #define HREC_HX_STATS(DK)                                                                                        \
