@@ -324,6 +324,7 @@ COUNTER_KERNELS = [
     (("tt_scoring_c4", "f32"), ["dot_res_kernel<false, 128, true"], "dot_topk.hip"),
     (("tt_scoring_c4", "bf16"), ["dot_res_kernel<true, 128, true"], "dot_topk.hip"),
     (("tt_scoring_c4", "f32_B1"), ["dot_gemv_kernel<128, true>"], "dot_gemv.hip"),
+    (("tt_scoring_c4", "bf16_B1"), ["dot_res_kernel<true, 128, true"], "dot_topk.hip"),
     (("hybrid_top5_c5",), ["hyb_scores_kernel", "hp_", "dot_res_kernel<true, 256, true"], "hybrid_scores.hip"),
     (("tt_train",), ["tt_item_forward_mfma_kernel<4, 4, true, true", "tt_bwd_", "adam_sparse_group4_kernel"],
      "tt_mfma.hip"),
@@ -353,14 +354,15 @@ def attach_counters(line, pj, prof):
         if fresh:
             for name, e in sorted(table.items()):
                 if any(name.startswith(p) for p in prefixes):
-                    ks[name] = {k: e[k] for k in ("avg_ms", "mfma_busy_frac", "eff_clock_GHz",
+                    ks[name] = {k: e[k] for k in ("avg_ms", "mfma_busy_frac", "mfma_busy_by_grid", "eff_clock_GHz",
                                                   "hbm_bytes_per_dispatch_corrected") if k in e}
         node["roofline"]["counters"] = {
             "profile": os.path.relpath(prof, ROOT), "source": src, "source_matches_profile": fresh,
             "kernels": ks if fresh else None,
-            "note": ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), reads low on "
-                     "dispatches < 0.3 ms; hbm bytes = FETCH_SIZE x 2 + WRITE_SIZE (KiB, gfx950 16-B-load "
-                     "correction); separate PMC passes, scripts/gpu_profile.sh")}
+            "note": ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), time-weighted "
+                     "over the kernel's dispatches (mfma_busy_by_grid: per launch shape, e.g. the 1-user and the "
+                     "1024-user c4 batches), reads low on dispatches < 0.3 ms; hbm bytes = FETCH_SIZE x 2 + "
+                     "WRITE_SIZE (KiB, gfx950 16-B-load correction); separate PMC passes, scripts/gpu_profile.sh")}
 
 
 def api_line(eng, n_users, n_items, k, reps, want_cpu):
