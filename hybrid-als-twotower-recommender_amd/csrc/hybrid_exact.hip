@@ -364,10 +364,11 @@ constexpr int kHxQueued = 0;  // live pairs queued for 2b, candidates ranked in 
 constexpr int kHxEvery = 1;   // no usable bound: 2c scores every group
 constexpr int kHxNaN = 2;     // a model without any number: every fused score NaN
 constexpr int kHxSlots = 8;  // a pair's best exact candidates kept (>= top_k)
-// pairs a user may queue: a quarter of the shard's groups within [512, 8192]
-// (the live-group list sits in 2a's LDS); more: kHxEvery
+// the live-group list in 2a's LDS holds 2 x this many groups (a quarter of
+// the shard's groups within [512, 8192]); the queue holds B x this many pairs
+// (a user with more live groups writes them window by window; a user the
+// queue has no room for: kHxEvery)
 __host__ __device__ inline int hx_pair_cap(int G) { return G / 8 < 512 ? 512 : (G / 8 > 8192 ? 8192 : G / 8); }
-
 struct HxArgs {
   int ka, kt, B;
   const float* Vat;  // ALS item factors transposed: item j, column c at Vat[c * lda + j]
@@ -393,6 +394,7 @@ struct HxArgs {
   int* flag;    // set when a user rescored every group
   HxRec* rec;   // [B]
   int pair_cap;
+  int pair_capacity;  // B * pair_cap: the queue's entries
   int4* pairs;  // [B * pair_cap] (user, group A, group B)
   int* pair_total;
   double* cv;   // [pair][kHxSlots] a pair's best exact fused scores
@@ -702,11 +704,11 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
   // (any order: the results do not depend on it), then dealt to the waves
   // two at a time, round robin (the fallback when the list overflows)
   auto sweep = [&](auto pred, auto pair) {
-    for (int w0 = 0; w0 < G; w0 += kList) {
-      const int w1e = G - w0 < kList ? G : w0 + kList;
+    for (int g0 = 0; g0 < G; g0 += kList) {
+      const int g1 = G - g0 < kList ? G : g0 + kList;
       if (tid == 0) s_n = 0;
       __syncthreads();
-      for (int g = w0 + tid; g < w1e; g += kHxThreads2)
+      for (int g = g0 + tid; g < g1; g += kHxThreads2)
         if (pred(g)) s_list[atomicAdd(&s_n, 1)] = g;
       __syncthreads();
       const int n = s_n;
@@ -906,7 +908,30 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
   }
   __syncthreads();
   const int n_live = s_n;
-  if (n_live > cap2) {  // too many: 2c scores every group
+  // the user's queue range (contiguous; reserved against the queue's
+  // capacity); more live groups than the LDS list holds: filled window by
+  // window (below), each window's odd group pairs with an empty slot, so the
+  // range covers (n_live + windows) / 2 entries and the unused ones stay
+  // empty pairs. No room: 2c scores every group.
+  const bool big = n_live > cap2;
+  const int np = big ? (n_live + (G + cap2 - 1) / cap2 + 1) / 2 : (n_live + 1) / 2;
+  // (an atomicAdd, not a CAS loop: a thousand blocks retrying one CAS cost
+  // 1.1 ms at B = 1024; a reservation that passes the capacity fills its
+  // part below it with empty pairs, 2b reads min(total, capacity) entries)
+  __shared__ int s_base, s_hole0, s_hole1;
+  if (tid == 0) {
+    const int cap = a.pair_capacity;
+    int base = 0, h0 = 0, h1 = 0;
+    if (np) {
+      base = *(volatile int*)a.pair_total > cap - np ? cap : atomicAdd(a.pair_total, np);
+      if (base > cap - np) h0 = base < cap ? base : cap, h1 = cap, base = -1;
+    }
+    s_base = base, s_hole0 = h0, s_hole1 = h1;
+  }
+  __syncthreads();
+  const int base = s_base;
+  if (base < 0) {
+    for (int q = s_hole0 + tid; q < s_hole1; q += kHxThreads2) a.pairs[q] = make_int4(b, -1, -1, 0);
     if (tid == 0) {
       r.state = kHxEvery;
       r.tau = -INFINITY;
@@ -915,13 +940,30 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
     }
     return;
   }
-  const int np = (n_live + 1) / 2;
-  __shared__ int s_base;
-  if (tid == 0) s_base = np ? atomicAdd(a.pair_total, np) : 0;
-  __syncthreads();
-  const int base = s_base;
-  for (int q = tid; q < np; q += kHxThreads2)
-    a.pairs[base + q] = make_int4(b, s_glist[2 * q], 2 * q + 1 < n_live ? s_glist[2 * q + 1] : -1, 0);
+  if (!big) {
+    for (int q = tid; q < np; q += kHxThreads2)
+      a.pairs[base + q] = make_int4(b, s_glist[2 * q], 2 * q + 1 < n_live ? s_glist[2 * q + 1] : -1, 0);
+  } else {
+    // windows of cap2 groups: at most cap2 live ones each, paired in LDS
+    // and appended to the range (the rescoring runs on every CU in 2b,
+    // not on this user's one block in 2c)
+    __shared__ int s_w;
+    int written = 0;
+    for (int g0 = 0; g0 < G; g0 += cap2) {
+      const int g1 = G - g0 < cap2 ? G : g0 + cap2;
+      __syncthreads();
+      if (tid == 0) s_w = 0;
+      __syncthreads();
+      for (int g = g0 + tid; g < g1; g += kHxThreads2)
+        if (ub_of(g) >= tau) s_glist[atomicAdd(&s_w, 1)] = g;
+      __syncthreads();
+      const int nw = s_w, pw = (nw + 1) / 2;
+      for (int q = tid; q < pw; q += kHxThreads2)
+        a.pairs[base + written + q] = make_int4(b, s_glist[2 * q], 2 * q + 1 < nw ? s_glist[2 * q + 1] : -1, 0);
+      written += pw;
+    }
+    for (int q = written + tid; q < np; q += kHxThreads2) a.pairs[base + q] = make_int4(b, -1, -1, 0);
+  }
   if (tid == 0) {
     r.state = kHxQueued;
     r.tau = tau;
@@ -951,7 +993,8 @@ __global__ __launch_bounds__(256) void hx_pairs_kernel(HxArgs a) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int ka = FULL ? DK : a.ka, kt = FULL ? DK : a.kt;
-  const int total = *(volatile const int*)a.pair_total;  // final: 2a has completed
+  const int filled = *(volatile const int*)a.pair_total;  // final: 2a has completed
+  const int total = filled < a.pair_capacity ? filled : a.pair_capacity;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), n_waves = gridDim.x * 4;
 #ifdef HREC_HX_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -1227,6 +1270,7 @@ static int hx_run(const hrec_hybrid_batch* x, int mode, float* als_mm, float* tt
   a.idx_offset = idx_offset, a.out_idx = out_idx, a.out_val = out_val;
   a.counts = w.counts, a.flag = w.flag;
   a.pair_cap = hx_pair_cap(G);
+  a.pair_capacity = (int)((int64_t)B * a.pair_cap < 0x7fffffff ? (int64_t)B * a.pair_cap : 0x7fffffff);
   a.rec = w.rec, a.pairs = w.pairs, a.pair_total = w.flag + 1;
   a.cv = w.cv, a.ci = w.ci, a.pc = w.pc;
   const bool full = x->als_width == dk && x->tt_width == dk;

@@ -173,3 +173,35 @@ def test_recommender_exact_paths_agree(device):
         g = cap()
         assert torch.equal(g[0], b[0]) and torch.equal(g[1], b[1])
     assert not pr.last_exact.counts()[2]
+
+
+@pytest.mark.parametrize("B", [8, 40])
+def test_hybrid_exact_many_live_groups(device, B):
+    """The first half of the items nearly tie at the top for every user (the
+    two-tower vectors along one direction, the ALS side flat), the second
+    half scores far below: every user keeps about half of the groups live,
+    more than 2a's LDS list holds (> 2 x pair cap). Their pairs are written
+    window by window into the shared queue while it has room; the users it
+    has no room for rescore every group in 2c. Both give the materialised
+    path's bits."""
+    h = _h()
+    rng = np.random.default_rng(B)
+    N, ka, kt = 100_003, 64, 64
+    U, V, _, _, rows = _case(device, B, N, ka, kt, 77, same_items=True)
+    e = rng.normal(size=kt)
+    sign = np.where(np.arange(N) < N // 2, 1.0, -1.0)[:, None]
+    iv = sign * e + 1e-4 * rng.normal(size=(N, kt))
+    uv = e + 0.01 * rng.normal(size=(B, kt))
+    iv = torch.as_tensor(iv.astype(np.float32), device=device)
+    uv = torch.as_tensor(uv.astype(np.float32), device=device)
+    Vt = h.transpose(V)
+    items = h.HybridExactItems(Vt, N, ka, iv)
+    G = -(-N // 32)
+    for wins in (True, False):
+        ei, ev, ea, et = _materialised(h, U, rows, Vt, N, ka, uv, iv, wins, 5)
+        hx = h.HybridExact(U, rows, uv, items, 5)
+        li, lv, la, lt = hx.local(wins)
+        assert torch.equal(li, ei) and torch.equal(lv, ev)
+        assert torch.equal(la, ea) and torch.equal(lt, et)
+        n_live = hx.counts()[1].cpu().numpy()
+        assert ((n_live > 1024) & (n_live < G)).any(), n_live  # the windowed queue path ran
