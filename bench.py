@@ -1080,10 +1080,11 @@ def main():
         vals = csr.values
 
         def run_ingest():
-            _, urow = _hrec.encode_ids(uid, (u0, u0 + u_per - 1))
-            iu, irow = _hrec.encode_ids(iid, (0, n_items - 1))
-            a = _hrec.coo_to_csr(urow, irow, vals, u_per, alias=True)  # grouped by user: the codes are the CSR
-            b = _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()))
+            _, urow, u_ord = _hrec.encode_ids(uid, (u0, u0 + u_per - 1), order=True)
+            iu, irow, i_ord = _hrec.encode_ids(iid, (0, n_items - 1), order=True)
+            # grouped by user: the codes are the CSR (its order read by the marking pass)
+            a = _hrec.coo_to_csr(urow, irow, vals, u_per, alias=True, rows_in_order=u_ord)
+            b = _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()), rows_in_order=i_ord)
             return a, b
 
         run_ingest()

@@ -82,10 +82,39 @@ __device__ __forceinline__ void load_id_pair(const int64_t* __restrict__ ids, in
   }
 }
 
+// The input order, read by the marking passes for free: 1 when ids[2p] >
+// ids[2p + 1] or ids[2p + 1] > ids[2p + 2] (a = ids[2p] - lo, b = ids[2p + 1]
+// - lo; ids[2p + 2] is the lane above's a — lanes hold consecutive pairs — or,
+// on the wave's last lane, a load). The caller ORs the waves' results into
+// *desc: ids non-decreasing <=> codes non-decreasing (the code map is monotone).
+__device__ __forceinline__ bool pair_descends(int64_t n, int64_t p, int64_t a, int64_t b, int64_t above_a,
+                                              int64_t edge, int64_t lo) {
+  bool d = 2 * p + 1 < n && a > b;
+  if (2 * p + 2 < n) d |= b > (((threadIdx.x & 63) < 63) ? above_a : edge - lo);
+  return d;
+}
+// x of the lane above (DPP wave_shl:1 — VALU moves, no LDS traffic beside
+// the marking pass's LDS atomics); lane 63 keeps its own
+__device__ __forceinline__ int64_t from_lane_above(int64_t x) {
+  const int lo = __builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(x >> 32), (int)(x >> 32), 0x130, 0xf, 0xf, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// ids[2p + 2] of the wave's last lane (p = lane 0's p + 63), a wave-uniform
+// address: a scalar load beside the pair loads (no vector memory instruction
+// for one lane), 0 past the end
+__device__ __forceinline__ int64_t edge_id(const int64_t* __restrict__ ids, int64_t n, int64_t p, bool want) {
+  const int64_t q = 2 * ((int64_t)__builtin_amdgcn_readfirstlane((int)(p & 0xffffffff)) |
+                         ((int64_t)__builtin_amdgcn_readfirstlane((int)(p >> 32)) << 32)) + 2 * 63 + 2;
+  return (want && q < n) ? ids[q] : 0;
+}
+
 __global__ __launch_bounds__(256) void mark_present_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
-                                                           int64_t span, int32_t* __restrict__ present) {
+                                                           int64_t span, int32_t* __restrict__ present,
+                                                           int32_t* __restrict__ desc) {
   const bool vec = ((uintptr_t)ids & 15) == 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  bool dsc = false, found = false;
   for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
     int64_t v[4];
     load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
@@ -94,12 +123,20 @@ __global__ __launch_bounds__(256) void mark_present_kernel(const int64_t* __rest
     } else {
       v[2] = v[3] = -1;
     }
+    const int64_t e0 = edge_id(ids, n, p0, desc && !found), e2 = edge_id(ids, n, p0 + stride, desc && !found);
+    if (desc && !found) {  // a wave stops checking at its first descent (unsorted ids: the first pairs)
+      const int64_t up0 = from_lane_above(v[0]), up2 = from_lane_above(v[2]);
+      dsc |= pair_descends(n, p0, v[0], v[1], up0, e0, lo);
+      if (p0 + stride < np) dsc |= pair_descends(n, p0 + stride, v[2], v[3], up2, e2, lo);
+      found = __any(dsc);
+    }
     // every writer stores the same value; a read first keeps the repeats of
     // a hot id (an item rated ~5000 times) from hammering its line with stores
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (v[u] >= 0 && v[u] < span && present[v[u]] == 0) present[v[u]] = 1;
   }
+  if (desc && __ballot(dsc) && (threadIdx.x & 63) == 0) atomicOr(desc, 1);
 }
 
 __global__ __launch_bounds__(256) void codes_from_rank_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
@@ -149,13 +186,15 @@ constexpr int64_t kBitsSpan = (int64_t)1 << 19;  // bitmap 64 KB + prefixes 64 K
 constexpr unsigned kBitsBlocks = 1024;
 
 __global__ __launch_bounds__(256) void mark_bits_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
-                                                        int64_t span, uint32_t* __restrict__ bits) {
+                                                        int64_t span, uint32_t* __restrict__ bits,
+                                                        int32_t* __restrict__ desc) {
   extern __shared__ uint32_t lb[];
   const int nw = (int)((span + 31) >> 5);
   for (int q = threadIdx.x; q < nw; q += 256) lb[q] = 0u;
   __syncthreads();
   const bool vec = ((uintptr_t)ids & 15) == 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  bool dsc = false, found = false;
   for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
     int64_t v[4];
     load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
@@ -164,10 +203,18 @@ __global__ __launch_bounds__(256) void mark_bits_kernel(const int64_t* __restric
     } else {
       v[2] = v[3] = -1;
     }
+    const int64_t e0 = edge_id(ids, n, p0, desc && !found), e2 = edge_id(ids, n, p0 + stride, desc && !found);
+    if (desc && !found) {  // a wave stops checking at its first descent (unsorted ids: the first pairs)
+      const int64_t up0 = from_lane_above(v[0]), up2 = from_lane_above(v[2]);
+      dsc |= pair_descends(n, p0, v[0], v[1], up0, e0, lo);
+      if (p0 + stride < np) dsc |= pair_descends(n, p0 + stride, v[2], v[3], up2, e2, lo);
+      found = __any(dsc);
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (v[u] >= 0 && v[u] < span) atomicOr(&lb[v[u] >> 5], 1u << (v[u] & 31));
   }
+  if (desc && __ballot(dsc) && (threadIdx.x & 63) == 0) atomicOr(desc, 1);
   __syncthreads();
   for (int q = threadIdx.x; q < nw; q += 256)
     if (lb[q]) atomicOr(&bits[q], lb[q]);
@@ -284,30 +331,73 @@ __global__ __launch_bounds__(256) void indptr_from_sorted_kernel(const int32_t* 
 
 // indptr[r] = min(first[r], first[r + 1], ...) from the end: rows without
 // entries take the next row's start (first[] holds each present key's first
-// position, nnz elsewhere; indptr[n_rows] = nnz). One block: chunks of the
-// rows per thread, a block min-scan of the chunk minima, then each chunk.
-__global__ __launch_bounds__(1024) void indptr_suffix_min_kernel(unsigned long long* __restrict__ first,
-                                                                 int64_t n_rows) {
-  __shared__ unsigned long long cm[1024];
-  const int t = threadIdx.x;
-  const int64_t per = (n_rows + 1 + 1023) / 1024;
-  const int64_t r0 = t * per, r1 = r0 + per < n_rows + 1 ? r0 + per : n_rows + 1;
-  unsigned long long m = ~0ull;
-  for (int64_t r = r1 - 1; r >= r0; --r) m = first[r] < m ? first[r] : m;
-  cm[t] = m;
+// position, nnz elsewhere; indptr[n_rows] = nnz). Tiles of kMinTile rows:
+// the tiles' minima (one block each), then per tile the minimum of the tiles
+// after it and a suffix min of its rows (a thread's 8 rows in registers, a
+// wave / block suffix scan of the threads' minima).
+constexpr int kMinThreads = 1024, kMinPer = 8, kMinTile = kMinThreads * kMinPer;
+
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+
+// block-wide min over kMinThreads values; every thread gets the result
+__device__ __forceinline__ unsigned long long block_min64(unsigned long long m, unsigned long long* sh) {
+  for (int off = 32; off >= 1; off >>= 1) m = umin64(m, __shfl_xor(m, off, 64));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __syncthreads();
-  // inclusive suffix min over the chunk minima (Hillis-Steele)
-  for (int off = 1; off < 1024; off <<= 1) {
-    const unsigned long long o = t + off < 1024 ? cm[t + off] : ~0ull;
-    __syncthreads();
-    cm[t] = o < cm[t] ? o : cm[t];
-    __syncthreads();
+  if (lane == 0) sh[w] = m;
+  __syncthreads();
+  m = ~0ull;
+  for (int q = 0; q < kMinThreads / 64; ++q) m = umin64(m, sh[q]);
+  return m;
+}
+
+__global__ __launch_bounds__(kMinThreads) void indptr_tile_min_kernel(const unsigned long long* __restrict__ first,
+                                                                      int64_t n, unsigned long long* __restrict__ tmin) {
+  __shared__ unsigned long long sh[kMinThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kMinTile;
+  unsigned long long m = ~0ull;
+#pragma unroll
+  for (int e = 0; e < kMinPer; ++e) {
+    const int64_t r = base + (int64_t)e * kMinThreads + threadIdx.x;
+    if (r < n) m = umin64(m, first[r]);
   }
-  unsigned long long run = t + 1 < 1024 ? cm[t + 1] : ~0ull;  // the rows after this chunk
-  for (int64_t r = r1 - 1; r >= r0; --r) {
-    run = first[r] < run ? first[r] : run;
-    first[r] = run;
+  m = block_min64(m, sh);
+  if (threadIdx.x == 0) tmin[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(kMinThreads) void indptr_suffix_min_kernel(unsigned long long* __restrict__ first,
+                                                                        int64_t n,
+                                                                        const unsigned long long* __restrict__ tmin,
+                                                                        int64_t n_tiles) {
+  __shared__ unsigned long long sh[kMinThreads / 64];
+  // the tiles after this one
+  unsigned long long carry = ~0ull;
+  for (int64_t t = blockIdx.x + 1 + threadIdx.x; t < n_tiles; t += kMinThreads) carry = umin64(carry, tmin[t]);
+  carry = block_min64(carry, sh);
+  // thread t: rows base + 8t .. 8t + 7
+  const int64_t r0 = (int64_t)blockIdx.x * kMinTile + (int64_t)threadIdx.x * kMinPer;
+  unsigned long long v[kMinPer];
+#pragma unroll
+  for (int e = 0; e < kMinPer; ++e) v[e] = r0 + e < n ? first[r0 + e] : ~0ull;
+#pragma unroll
+  for (int e = kMinPer - 2; e >= 0; --e) v[e] = umin64(v[e], v[e + 1]);
+  // suffix min over the threads above (lanes, then waves)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long x = v[0];
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_down(x, off, 64);
+    if (lane + off < 64) x = umin64(x, y);
   }
+  __syncthreads();
+  if (lane == 0) sh[w] = x;  // the wave's minimum
+  __syncthreads();
+  unsigned long long after = carry;
+  for (int q = w + 1; q < kMinThreads / 64; ++q) after = umin64(after, sh[q]);
+  const unsigned long long up = __shfl_down(x, 1, 64);  // the lanes above within the wave
+  if (lane < 63) after = umin64(after, up);
+#pragma unroll
+  for (int e = 0; e < kMinPer; ++e)
+    if (r0 + e < n) first[r0 + e] = umin64(v[e], after);
 }
 
 __global__ __launch_bounds__(256) void fill_u64_kernel(unsigned long long* __restrict__ x, int64_t n,
@@ -337,24 +427,85 @@ __global__ __launch_bounds__(256) void fill_u64_kernel(unsigned long long* __res
 //      coalesced run at the (digit, tile) offset: a stable scatter with
 //      per-block ranks. The last pass writes indices / values unpacked; the
 //      first reads cols / values unpacked.
-constexpr int kSortThreads = 512, kSortIPT = 16, kSortTile = kSortThreads * kSortIPT;  // 8192 entries
+#ifndef HREC_SORT_IPT
+#define HREC_SORT_IPT 20
+#endif
+#ifndef HREC_SORT_BPC
+#define HREC_SORT_BPC 1
+#endif
+#ifndef HREC_SORT_NT
+#define HREC_SORT_NT 0
+#endif
+#ifndef HREC_SORT_NTL
+#define HREC_SORT_NTL 0
+#endif
+template <typename T>
+__device__ __forceinline__ void sort_st(T* p, T v) {
+  if constexpr (HREC_SORT_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <typename T>
+__device__ __forceinline__ T sort_ld(const T* p) {
+  if constexpr (HREC_SORT_NTL) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+constexpr int kSortThreads = 512, kSortIPT = HREC_SORT_IPT, kSortTile = kSortThreads * kSortIPT;  // 10240 entries
 constexpr int kSortMaxBits = 10;
+static_assert(kSortIPT % 4 == 0, "the upsweep's 16-B key loads");
+
+// Persistent blocks (4 per CU) walk the tiles; the next tile's keys are
+// loaded (16-B loads where aligned) before this tile's LDS histogram.
+constexpr int kUpBlocksPerCU = 4;
 
 __global__ __launch_bounds__(kSortThreads) void sort_upsweep_kernel(const int32_t* __restrict__ keys, int64_t n,
                                                                     int shift, int bits, int64_t n_tiles,
                                                                     uint32_t* __restrict__ counts) {
   __shared__ uint32_t h[1 << kSortMaxBits];
+  constexpr int NV = kSortIPT / 4;  // 16-B loads per thread and tile
   const int R = 1 << bits;
-  for (int d = threadIdx.x; d < R; d += kSortThreads) h[d] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-#pragma unroll 8
-  for (int e = 0; e < kSortIPT; ++e) {
-    const int64_t i = base + (int64_t)e * kSortThreads + threadIdx.x;
-    if (i < n) atomicAdd(&h[((uint32_t)keys[i] >> shift) & (uint32_t)(R - 1)], 1u);
+  const uint32_t dmask = (uint32_t)(R - 1);
+  const bool vec = ((uintptr_t)keys & 15) == 0;
+  int4 cur[NV], nxt[NV];
+  auto load = [&](int64_t tile, int4* k) {
+    const int64_t base = tile * kSortTile;
+    if (tile >= n_tiles) return;
+    if (vec && base + kSortTile <= n) {
+#pragma unroll
+      for (int e = 0; e < NV; ++e)
+        k[e] = *reinterpret_cast<const int4*>(keys + base + 4 * ((int64_t)e * kSortThreads + threadIdx.x));
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        const int64_t i = base + 4 * ((int64_t)e * kSortThreads + threadIdx.x);
+        k[e].x = i < n ? keys[i] : -1;
+        k[e].y = i + 1 < n ? keys[i + 1] : -1;
+        k[e].z = i + 2 < n ? keys[i + 2] : -1;
+        k[e].w = i + 3 < n ? keys[i + 3] : -1;
+      }
+    }
+  };
+  int64_t tile = blockIdx.x;
+  load(tile, cur);
+  for (; tile < n_tiles; tile += gridDim.x) {
+    load(tile + gridDim.x, nxt);
+    for (int d = threadIdx.x; d < R; d += kSortThreads) h[d] = 0;
+    __syncthreads();
+    const int64_t base = tile * kSortTile;
+    const bool full = base + kSortTile <= n;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+      const int64_t i = base + 4 * ((int64_t)e * kSortThreads + threadIdx.x);
+      const int32_t kv[4] = {cur[e].x, cur[e].y, cur[e].z, cur[e].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (full || i + q < n) atomicAdd(&h[((uint32_t)kv[q] >> shift) & dmask], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < R; d += kSortThreads) counts[tile * R + d] = h[d];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < NV; ++e) cur[e] = nxt[e];
   }
-  __syncthreads();
-  for (int d = threadIdx.x; d < R; d += kSortThreads) counts[(int64_t)blockIdx.x * R + d] = h[d];
 }
 
 // counts [tile][digit] (tile-major: every access below reads or writes whole
@@ -381,11 +532,17 @@ __global__ __launch_bounds__(1024) void sort_colscan_top_kernel(uint32_t* __rest
   __shared__ uint32_t wsum[16];
   const int d = threadIdx.x;  // R <= 1024 = blockDim
   uint32_t run = 0;
-  if (d < R)
-    for (int64_t c = 0; c < n_chunks; ++c) {
-      const uint32_t v = csum[c * R + d];
-      csum[c * R + d] = run;
-      run += v;
+  if (d < R)  // 8 loads in flight per step (not one dependent load per chunk)
+    for (int64_t c0 = 0; c0 < n_chunks; c0 += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = c0 + j < n_chunks ? csum[(c0 + j) * R + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < n_chunks) {
+          csum[(c0 + j) * R + d] = run;
+          run += v[j];
+        }
     }
   // exclusive scan of the digit totals
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -402,8 +559,17 @@ __global__ __launch_bounds__(1024) void sort_colscan_top_kernel(uint32_t* __rest
   for (int q = 0; q < w; ++q) base += wsum[q];
   tot[d] = base;
   __syncthreads();
-  if (d < R)
-    for (int64_t c = 0; c < n_chunks; ++c) csum[c * R + d] += tot[d];
+  if (d < R) {
+    const uint32_t t = tot[d];
+    for (int64_t c0 = 0; c0 < n_chunks; c0 += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = c0 + j < n_chunks ? csum[(c0 + j) * R + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < n_chunks) csum[(c0 + j) * R + d] = v[j] + t;
+    }
+  }
 }
 
 __global__ __launch_bounds__(512) void sort_colscan_apply_kernel(uint32_t* __restrict__ cnt, int64_t n_tiles, int R,
@@ -412,11 +578,16 @@ __global__ __launch_bounds__(512) void sort_colscan_apply_kernel(uint32_t* __res
   const int64_t t1 = t0 + kScanTiles < n_tiles ? t0 + kScanTiles : n_tiles;
   for (int d = threadIdx.x; d < R; d += 512) {
     uint32_t run = csum[(int64_t)blockIdx.x * R + d];
-#pragma unroll 8
-    for (int64_t t = t0; t < t1; ++t) {
-      const uint32_t v = cnt[t * R + d];
-      cnt[t * R + d] = run;
-      run += v;
+    for (int64_t tb = t0; tb < t1; tb += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = tb + j < t1 ? cnt[(tb + j) * R + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (tb + j < t1) {
+          cnt[(tb + j) * R + d] = run;
+          run += v[j];
+        }
     }
   }
 }
@@ -454,11 +625,11 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
       key[r] = 0;
       pay[r] = 0;
       if (tile < n_tiles && i < n) {
-        key[r] = keys_in[i];
+        key[r] = sort_ld(keys_in + i);
         if constexpr (FIRST) {
-          pay[r] = (uint64_t)(uint32_t)cols_in[i] | ((uint64_t)__float_as_uint(vals_in[i]) << 32);
+          pay[r] = (uint64_t)(uint32_t)sort_ld(cols_in + i) | ((uint64_t)__float_as_uint(sort_ld(vals_in + i)) << 32);
         } else {
-          pay[r] = pay_in[i];
+          pay[r] = sort_ld(pay_in + i);
         }
       }
     }
@@ -571,15 +742,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
       const uint32_t pos = goff[dg] + ((uint32_t)q - wh[0][dg]);
       const uint64_t pv = sp[q];
       if (!LAST || imin == nullptr) {
-        keys_out[pos] = k;
+        sort_st(keys_out + pos, k);
       } else if (((uint32_t)q == wh[0][dg] || sk[q - 1] != k) && (uint32_t)k < (uint64_t)imin_n) {
         atomicMin(&imin[(uint32_t)k], (unsigned long long)pos);  // the run's first entry of key k
       }
       if constexpr (LAST) {
-        idx_out[pos] = (int32_t)(uint32_t)pv;
-        val_out[pos] = __uint_as_float((uint32_t)(pv >> 32));
+        sort_st(idx_out + pos, (int32_t)(uint32_t)pv);
+        sort_st(val_out + pos, __uint_as_float((uint32_t)(pv >> 32)));
       } else {
-        pay_out[pos] = pv;
+        sort_st(pay_out + pos, pv);
       }
     }
     __syncthreads();
@@ -587,7 +758,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_downsweep_kernel(
 }
 
 // *flag = 1 if some x[i] > x[i + 1] (the caller zeroes it first)
-__global__ __launch_bounds__(256) void descent_kernel(const int32_t* __restrict__ x, int64_t n, int32_t* __restrict__ flag) {
+template <typename T>
+__global__ __launch_bounds__(256) void descent_kernel(const T* __restrict__ x, int64_t n, int32_t* __restrict__ flag) {
   bool d = false;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 + 1 < n; i0 += kStreamUnroll * stride) {
@@ -651,7 +823,12 @@ struct CsrWs {
   CsrWs(int64_t nnz, int bits) {
     passes = (bits + kSortMaxBits - 1) / kSortMaxBits;
     if (passes < 1) passes = 1;
-    for (int p = 0; p < passes; ++p) digit[p] = bits / passes + (p < bits % passes ? 1 : 0);
+#ifndef HREC_SORT_WIDE_LAST
+#define HREC_SORT_WIDE_LAST 1
+#endif
+    // the wider digits first (HREC_SORT_WIDE_LAST=1: last)
+    for (int p = 0; p < passes; ++p)
+      digit[p] = bits / passes + ((HREC_SORT_WIDE_LAST ? p >= passes - bits % passes : p < bits % passes) ? 1 : 0);
     n_tiles = (nnz + kSortTile - 1) / kSortTile;
     int maxd = 0;
     for (int p = 0; p < passes; ++p) maxd = digit[p] > maxd ? digit[p] : maxd;
@@ -713,11 +890,11 @@ int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, in
   uint64_t* pbuf[2] = {reinterpret_cast<uint64_t*>(w + L.pa), reinterpret_cast<uint64_t*>(w + L.pb)};
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
   uint32_t* sums = reinterpret_cast<uint32_t*>(w + L.sums);
-  const unsigned nt = (unsigned)L.n_tiles;
   // downsweep: persistent, one block per CU (its tile takes 118 KB of LDS)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const unsigned nd = (unsigned)(L.n_tiles < cus ? L.n_tiles : cus);
+  const int64_t nd_max = (int64_t)HREC_SORT_BPC * cus;
+  const unsigned nd = (unsigned)(L.n_tiles < nd_max ? L.n_tiles : nd_max);
   const int32_t* kin = keys;
   const uint64_t* pin = nullptr;
   int shift = 0;
@@ -725,7 +902,9 @@ int csr_sort_run(const int32_t* keys, const int32_t* cols, const float* vals, in
     const int db = L.digit[p];
     const int R = 1 << db;
     const int64_t n_chunks = (L.n_tiles + kScanTiles - 1) / kScanTiles;
-    hipLaunchKernelGGL(sort_upsweep_kernel, dim3(nt), dim3(kSortThreads), 0, s, kin, nnz, shift, db, L.n_tiles, cnt);
+    const int64_t nu_max = (int64_t)kUpBlocksPerCU * cus;
+    hipLaunchKernelGGL(sort_upsweep_kernel, dim3((unsigned)(L.n_tiles < nu_max ? L.n_tiles : nu_max)),
+                       dim3(kSortThreads), 0, s, kin, nnz, shift, db, L.n_tiles, cnt);
     hipLaunchKernelGGL(sort_colsum_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
     hipLaunchKernelGGL(sort_colscan_top_kernel, dim3(1), dim3(1024), 0, s, sums, n_chunks, R);
     hipLaunchKernelGGL(sort_colscan_apply_kernel, dim3((unsigned)n_chunks), dim3(512), 0, s, cnt, L.n_tiles, R, sums);
@@ -788,12 +967,15 @@ extern "C" size_t hrec_encode_ids_workspace_bytes(int64_t n) {
   return EncodeWs(n).total;
 }
 
-extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi, int64_t* uniq,
-                               int64_t* n_uniq, int32_t* codes, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi, int64_t* uniq,
+                                  int64_t* n_uniq, int32_t* codes, int32_t* descending, void* ws, size_t ws_bytes,
+                                  void* stream) {
   HREC_REQUIRE(n >= 0 && n < 0x7fffffffll, "encode_ids: n=%lld out of range [0, 2^31-1)", (long long)n);
   HREC_REQUIRE(n_uniq, "encode_ids: null n_uniq");
   HREC_REQUIRE(id_lo <= id_hi, "encode_ids: id_lo > id_hi");
   hipStream_t s = as_stream(stream);
+  if (descending && hipMemsetAsync(descending, 0, sizeof(int32_t), s) != hipSuccess)
+    return check_launch("encode_ids: memset");
   if (n == 0) {
     if (hipMemsetAsync(n_uniq, 0, sizeof(int64_t), s) != hipSuccess) return check_launch("encode_ids: memset");
     return HREC_OK;
@@ -820,7 +1002,8 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
     if (hipMemsetAsync(bits, 0, (size_t)nw * sizeof(uint32_t), s) != hipSuccess)
       return check_launch("encode_ids: memset");
     const unsigned gb = g < kBitsBlocks ? g : kBitsBlocks;
-    hipLaunchKernelGGL(mark_bits_kernel, dim3(gb), dim3(256), (size_t)nw * 4, s, ids, n, id_lo, span, bits);
+    hipLaunchKernelGGL(mark_bits_kernel, dim3(gb), dim3(256), (size_t)nw * 4, s, ids, n, id_lo, span, bits,
+                       descending);
     hipLaunchKernelGGL(bits_prefix_kernel, dim3(1), dim3(1024), 0, s, bits, nw, pre, n_uniq);
     const auto kfn = codes_bits_kernel;
     if (!allow_max_lds(kfn)) return check_launch("encode_ids: LDS attribute");
@@ -832,7 +1015,7 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
     // dense range: the span-long tables fit the flag / incl buffers (n entries each)
     if (hipMemsetAsync(flag, 0, (size_t)span * sizeof(int32_t), s) != hipSuccess)
       return check_launch("encode_ids: memset");
-    hipLaunchKernelGGL(mark_present_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, flag);
+    hipLaunchKernelGGL(mark_present_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, flag, descending);
     const int rc = scan_run<int32_t>(flag, incl, span, false, temp, s);
     if (rc) return rc;
     hipLaunchKernelGGL(codes_from_rank_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, incl, codes);
@@ -840,6 +1023,8 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
                        n_uniq);
     return check_launch("encode_ids: dense");
   }
+  if (descending && n > 1)  // the sorting paths: one more pass over the ids
+    hipLaunchKernelGGL(descent_kernel<int64_t>, dim3(g), dim3(256), 0, s, ids, n, descending);
   hipLaunchKernelGGL(iota_i32_kernel, dim3(g), dim3(256), 0, s, pos, n);
   if (span32) {
     // (id - lo) as 32-bit keys, sorted with their positions by the in-tree
@@ -892,6 +1077,11 @@ extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int
   return check_launch("encode_ids");
 }
 
+extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi, int64_t* uniq,
+                               int64_t* n_uniq, int32_t* codes, void* ws, size_t ws_bytes, void* stream) {
+  return hrec_encode_ids_ex(ids, n, id_lo, id_hi, uniq, n_uniq, codes, nullptr, ws, ws_bytes, stream);
+}
+
 extern "C" size_t hrec_minmax_i64_workspace_bytes(int64_t n) { return n > 0 ? 256 : 0; }
 
 extern "C" int hrec_minmax_i64(const int64_t* x, int64_t n, int64_t* out, void* ws, size_t ws_bytes,
@@ -905,7 +1095,7 @@ extern "C" int hrec_minmax_i64(const int64_t* x, int64_t n, int64_t* out, void* 
 
 extern "C" size_t hrec_coo_to_csr_workspace_bytes(int64_t nnz, int64_t n_rows) {
   if (nnz <= 0 || nnz >= 0x7fffffffll || n_rows <= 0 || n_rows >= 0x7fffffffll) return 0;
-  return CsrWs(nnz, bits_for(n_rows)).total;
+  return CsrWs(nnz, bits_for(n_rows)).total + align256(8 * (size_t)((n_rows + 1 + kMinTile - 1) / kMinTile));
 }
 
 extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const float* vals, int64_t nnz,
@@ -924,7 +1114,8 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   HREC_REQUIRE(rows && cols && vals && indices && values && ws, "coo_to_csr: null pointer");
   const int bits = bits_for(n_rows);
   const CsrWs L(nnz, bits);
-  HREC_REQUIRE(ws_bytes >= L.total, "coo_to_csr: workspace %zu < %zu bytes", ws_bytes, L.total);
+  const size_t need = hrec_coo_to_csr_workspace_bytes(nnz, n_rows);
+  HREC_REQUIRE(ws_bytes >= need, "coo_to_csr: workspace %zu < %zu bytes", ws_bytes, need);
   // indptr: every row's first position (atomicMin in the last pass, nnz for
   // rows without entries), then a suffix min fills the empty rows
   unsigned long long* first = reinterpret_cast<unsigned long long*>(indptr);
@@ -933,7 +1124,12 @@ extern "C" int hrec_coo_to_csr(const int32_t* rows, const int32_t* cols, const f
   const int32_t* kin = nullptr;
   int rc = csr_sort_run(rows, cols, vals, nnz, bits, ws, indices, values, &kin, s, first, n_rows);
   if (rc) return rc;
-  hipLaunchKernelGGL(indptr_suffix_min_kernel, dim3(1), dim3(1024), 0, s, first, n_rows);
+  const int64_t n_min_tiles = (n_rows + 1 + kMinTile - 1) / kMinTile;
+  unsigned long long* tmin = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + L.total);
+  hipLaunchKernelGGL(indptr_tile_min_kernel, dim3((unsigned)n_min_tiles), dim3(kMinThreads), 0, s, first, n_rows + 1,
+                     tmin);
+  hipLaunchKernelGGL(indptr_suffix_min_kernel, dim3((unsigned)n_min_tiles), dim3(kMinThreads), 0, s, first,
+                     n_rows + 1, tmin, n_min_tiles);
   return check_launch("coo_to_csr");
 }
 
@@ -943,7 +1139,7 @@ extern "C" int hrec_rows_descending_pairs(const int32_t* rows, int64_t n, int32_
   if (hipMemsetAsync(out, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("rows_descending_pairs: memset");
   if (n < 2) return HREC_OK;
   HREC_REQUIRE(rows, "rows_descending_pairs: null rows");
-  hipLaunchKernelGGL(descent_kernel, dim3(grid_for(n)), dim3(256), 0, s, rows, n, out);
+  hipLaunchKernelGGL(descent_kernel<int32_t>, dim3(grid_for(n)), dim3(256), 0, s, rows, n, out);
   return check_launch("descent_kernel");
 }
 

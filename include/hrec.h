@@ -43,8 +43,9 @@ extern "C" {
  * 4: the RCCL exchange steps (hrec_comm_*, hrec_allgather, hrec_allreduce_minmax).
  * 6: hrec_als_score_topk_pruned_counts, hrec_cold_fallback*; the pruned ALS
  *    bound is 2^-7 + 2^-13 and its top_k <= 8 results are exact without a
- *    host-side fallback. */
-#define HREC_ABI_VERSION 6
+ *    host-side fallback.
+ * 7: hrec_encode_ids_ex (the ids' order from the marking pass). */
+#define HREC_ABI_VERSION 7
 
 #define HREC_OK 0
 #define HREC_E_INVALID (-1) /* bad argument (shape, null pointer, range) */
@@ -99,6 +100,15 @@ size_t hrec_encode_ids_workspace_bytes(int64_t n);
 int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi,
                     int64_t* uniq, int64_t* n_uniq, int32_t* codes,
                     void* workspace, size_t workspace_bytes, void* stream);
+/* The same, plus *descending (device int32, may be null) = 1 if some
+ * ids[i] > ids[i+1], else 0 — hrec_rows_descending_pairs of the codes
+ * (the code map is monotone), read by the dense paths' marking pass instead
+ * of a pass over the codes: ratings grouped by user go straight to
+ * hrec_coo_to_csr_sorted. */
+int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi,
+                       int64_t* uniq, int64_t* n_uniq, int32_t* codes,
+                       int32_t* descending, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /* hrec_coo_to_csr: (rows[nnz], cols[nnz], vals[nnz]) with 0 <= rows < n_rows
  * -> indptr[n_rows+1], indices[nnz], values[nnz]; rows ascending, the entries

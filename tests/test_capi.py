@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared if not hasattr(lib, n)]
     assert not missing, missing
     lib.hrec_abi_version.restype = ctypes.c_int
-    assert lib.hrec_abi_version() == 6
+    assert lib.hrec_abi_version() == 7
 
 
 def test_python_binding_covers_the_header():

@@ -57,6 +57,33 @@ def test_encode_ids_dense_path_unaligned_views(device):
     np.testing.assert_array_equal(codes.cpu().numpy(), exp_c.astype(np.int32))
 
 
+@pytest.mark.parametrize("n,lo,hi", [(2, 0, 1), (3, 0, 2), (1000, 0, 50), (200001, 0, 150000), (600_000, 0, 550_000),
+                                     (5000, 0, 10 ** 6), (65537, 10 ** 12, 10 ** 12 + 7),
+                                     (100000, -(2 ** 31), 2 ** 31)])
+def test_encode_ids_order_flag(device, n, lo, hi):
+    """encode_ids(order=True): the ids' order read by the marking pass (dense
+    bitmap, dense table) or a descent pass (sorting paths) equals numpy's
+    all(ids[:-1] <= ids[1:]) — sorted ids, one descent at every lane / wave /
+    block boundary position of the pairs, unsorted — with the same codes."""
+    h = _hrec()
+    rng = np.random.default_rng(n + 1)
+    base = np.sort(rng.integers(lo, hi, n, dtype=np.int64))
+    cases = [base, rng.permutation(base)]
+    for pos in (0, 1, 2, 126, 127, 128, 511, 512, 2 * 256 * 4 - 1, n // 2, n - 2):
+        if 0 <= pos < n - 1 and base[pos] != base[pos + 1]:
+            x = base.copy()
+            x[pos], x[pos + 1] = x[pos + 1], x[pos]
+            cases.append(x)
+    for ids in cases:
+        d_ids = torch.as_tensor(ids, device=device)
+        exp_u, exp_c = np.unique(ids, return_inverse=True)
+        for r in ((lo, hi), None):
+            uniq, codes, in_order = h.encode_ids(d_ids, r, order=True)
+            assert in_order == bool(np.all(ids[:-1] <= ids[1:]))
+            np.testing.assert_array_equal(uniq.cpu().numpy(), exp_u)
+            np.testing.assert_array_equal(codes.cpu().numpy(), exp_c.astype(np.int32))
+
+
 def test_encode_ids_empty(device):
     h = _hrec()
     uniq, codes = h.encode_ids(torch.zeros(0, dtype=torch.int64, device=device))
