@@ -1095,9 +1095,10 @@ def main():
         gs = time.perf_counter() - g0
         ok = bool(torch.equal(out[0][0], csr.indptr) and torch.equal(out[0][1], csr.indices))
         ingest = {"ratings_per_s": csr.nnz / gs, "ms": gs * 1e3, "ratings": csr.nnz,
-                  "steps": ("encode user ids + encode item ids (presence bitmap + rank) + CSR (rows grouped by "
-                            "user: the item codes and ratings ARE the CSR, indptr from the row codes) + CSC "
-                            "(2-pass stable radix sort, each row's start by atomicMin in the last pass)"),
+                  "steps": ("encode user ids + encode item ids (presence table / bitmap + rank; the ids' order "
+                            "read by the marking pass) + CSR (rows grouped by user: the item codes and ratings ARE "
+                            "the CSR, indptr from the row codes) + CSC (2-pass stable radix sort, 10240-entry "
+                            "tiles, each row's start by atomicMin in the last pass)"),
                   "csr_matches_generator": ok,
                   # algorithmic bytes per rating: read user id, item id (int64) + rating (f32) = 20 B; write
                   # both id codes (2 x int32) + the CSC column/value arrays (int32 + f32) = 16 B (the CSR's
