@@ -408,8 +408,8 @@ __global__ __launch_bounds__(256) void fill_u64_kernel(unsigned long long* __res
 // ---------------------------------------------------------------- CSR build
 // Stable LSD radix sort of the row codes carrying (col, rating), written for
 // this shape: dense codes < n_rows, so ceil(bits / 10) passes of <= 10-bit
-// digits (c2's CSC: 100k item codes = 17 bits = 2 passes of 9 + 8 bits).
-// Per pass:
+// digits (c2's CSC: 100k item codes = 17 bits = 2 passes of 8 + 9 bits, the
+// wider digit last). Per pass:
 //   1. upsweep: per tile of kSortTile entries, the digit histogram (LDS
 //      atomics) -> counts[tile][digit];
 //   2. a column scan of the tile-major counts (sort_colsum / colscan_*): the
@@ -417,8 +417,7 @@ __global__ __launch_bounds__(256) void fill_u64_kernel(unsigned long long* __res
 //      input order;
 //   3. downsweep (persistent, one block per CU; the next tile's entries load
 //      while a tile is written out): each wave takes a contiguous 1/8 of the
-//      block's tile into
-//      registers and ranks its entries among its own same-digit entries in
+//      block's tile into registers and ranks its entries among its own same-digit entries in
 //      input order (per 64-entry round: the lanes below with the same digit,
 //      from `bits` ballots, plus the wave's running per-digit count in LDS —
 //      no block barriers); one scan over (digit, wave) turns the per-wave
