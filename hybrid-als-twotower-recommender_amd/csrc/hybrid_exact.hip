@@ -70,6 +70,9 @@ constexpr int kHxThreads1 = 256;
 constexpr int kHxThreads2 = 512;
 constexpr int kHxStatsLds = 8192;  // group records a phase-2 block keeps in LDS (128 KiB)
 
+#ifndef HREC_HX_NSP_MAX
+#define HREC_HX_NSP_MAX 8  // seed pairs scanned beside the extremes' pairs (mode 2), at most
+#endif
 #ifndef HREC_HX_UB64
 // phase-1 users per tile at DK 64: 256 = one 512-thread block per CU (139 KB
 // of LDS, 2 waves per SIMD), every item fragment read once per 256-user
@@ -831,7 +834,8 @@ __global__ __launch_bounds__(kHxThreads2) void hx_pre_kernel(HxArgs a) {
     if (n <= cap2) {
       // work items: the seed pairs (waves 0..nsp-1), then the extremes' pairs
       const int n_ext = (n + 1) / 2;
-      const int nsp = kSeeds ? (n_ext >= 4 ? 4 : 8 - n_ext) : 0;
+      const int nsp0 = kSeeds ? (n_ext >= 4 ? 4 : 8 - n_ext) : 0;
+      const int nsp = nsp0 < HREC_HX_NSP_MAX ? nsp0 : HREC_HX_NSP_MAX;
       for (int it = wv; it < nsp + n_ext; it += 8) {
         if (it < nsp) {
           seed_scan(it);
