@@ -1080,10 +1080,10 @@ def main():
         vals = csr.values
 
         def run_ingest():
-            _, urow, u_ord = _hrec.encode_ids(uid, (u0, u0 + u_per - 1), order=True)
-            iu, irow, i_ord = _hrec.encode_ids(iid, (0, n_items - 1), order=True)
+            _, urow, u_ord, u_ptr = _hrec.encode_ids(uid, (u0, u0 + u_per - 1), order=True)
+            iu, irow, i_ord, _ = _hrec.encode_ids(iid, (0, n_items - 1), order=True)
             # grouped by user: the codes are the CSR (its order read by the marking pass)
-            a = _hrec.coo_to_csr(urow, irow, vals, u_per, alias=True, rows_in_order=u_ord)
+            a = _hrec.coo_to_csr(urow, irow, vals, u_per, alias=True, rows_in_order=u_ord, indptr=u_ptr)
             b = _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()), rows_in_order=i_ord)
             return a, b
 

@@ -109,6 +109,32 @@ __device__ __forceinline__ int64_t edge_id(const int64_t* __restrict__ ids, int6
   return (want && q < n) ? ids[q] : 0;
 }
 
+// x of the lane below (DPP wave_shr:1); lane 0 keeps its own
+__device__ __forceinline__ int32_t from_lane_below(int32_t x) {
+  return __builtin_amdgcn_update_dpp(x, x, 0x138, 0xf, 0xf, false);
+}
+// Row starts of codes in input order (the code kernels, when the ids are
+// non-decreasing: a CSR with rows = codes needs no pass over the codes).
+// Pair p holds codes a (position 2p), b (2p + 1); prev = the code at 2p - 1
+// (-1 at the start). Codes of sorted ids are dense and non-decreasing, so the
+// first position of every code gets written, and the last entry closes the
+// array: starts[n_uniq] = n.
+__device__ __forceinline__ void pair_starts(int64_t n, int64_t p, int32_t a, int32_t b, int32_t prev,
+                                            int64_t* __restrict__ starts) {
+  if (a >= 0 && a != prev) starts[a] = 2 * p;
+  if (2 * p + 1 < n) {
+    if (b >= 0 && b != a) starts[b] = 2 * p + 1;
+    if (2 * p + 2 == n && b >= 0) starts[b + 1] = n;
+  } else if (a >= 0) {
+    starts[a + 1] = n;  // 2p = n - 1
+  }
+}
+// the lane-0 position before pair p (wave-uniform: p of lane 0 - 1 ... as 2p - 1)
+__device__ __forceinline__ int64_t wave_prev_pos(int64_t p) {
+  return 2 * ((int64_t)__builtin_amdgcn_readfirstlane((int)(p & 0xffffffff)) |
+              ((int64_t)__builtin_amdgcn_readfirstlane((int)(p >> 32)) << 32)) - 1;
+}
+
 __global__ __launch_bounds__(256) void mark_present_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
                                                            int64_t span, int32_t* __restrict__ present,
                                                            int32_t* __restrict__ desc) {
@@ -141,9 +167,15 @@ __global__ __launch_bounds__(256) void mark_present_kernel(const int64_t* __rest
 
 __global__ __launch_bounds__(256) void codes_from_rank_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
                                                               int64_t span, const int32_t* __restrict__ incl,
-                                                              int32_t* __restrict__ codes) {
+                                                              int32_t* __restrict__ codes,
+                                                              const int32_t* __restrict__ desc,
+                                                              int64_t* __restrict__ starts) {
   const bool vec = ((uintptr_t)ids & 15) == 0, vst = ((uintptr_t)codes & 7) == 0;
+  const bool st = starts != nullptr && *desc == 0;  // the marking pass found the ids in order
   const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
+  auto code = [&](int64_t v) -> int32_t {  // out-of-range ids (a caller error) -> -1
+    return (v >= 0 && v < span) ? incl[v] - 1 : -1;
+  };
   for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < np; p0 += 2 * stride) {
     int64_t v[4];
     load_id_pair(ids, n, p0, lo, vec, v[0], v[1]);
@@ -152,13 +184,23 @@ __global__ __launch_bounds__(256) void codes_from_rank_kernel(const int64_t* __r
     } else {
       v[2] = v[3] = -1;
     }
+    int32_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[u] = code(v[u]);
+    if (st) {  // the code before each pair: the lane below's, or on lane 0 a scalar lookup
+      const int64_t q0 = wave_prev_pos(p0), q2 = wave_prev_pos(p0 + stride);
+      const int32_t e0 = q0 >= 0 && q0 < n ? code(ids[q0] - lo) : -1;
+      const int32_t e2 = q2 >= 0 && q2 < n ? code(ids[q2] - lo) : -1;
+      int32_t b0 = from_lane_below(c[1]), b2 = from_lane_below(c[3]);
+      if ((threadIdx.x & 63) == 0) b0 = e0, b2 = e2;
+      pair_starts(n, p0, c[0], c[1], b0, starts);
+      if (p0 + stride < np) pair_starts(n, p0 + stride, c[2], c[3], b2, starts);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int64_t p = p0 + h * stride;
       if (p >= np) break;
-      // out-of-range ids (a caller error) -> -1
-      const int32_t c0 = (v[2 * h] >= 0 && v[2 * h] < span) ? incl[v[2 * h]] - 1 : -1;
-      const int32_t c1 = (v[2 * h + 1] >= 0 && v[2 * h + 1] < span) ? incl[v[2 * h + 1]] - 1 : -1;
+      const int32_t c0 = c[2 * h], c1 = c[2 * h + 1];
       if (vst && 2 * p + 1 < n) {
         *reinterpret_cast<int2*>(codes + 2 * p) = make_int2(c0, c1);
       } else {
@@ -252,7 +294,9 @@ __global__ __launch_bounds__(1024) void bits_prefix_kernel(const uint32_t* __res
 __global__ __launch_bounds__(256) void codes_bits_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t lo,
                                                          int64_t span, const uint32_t* __restrict__ bits,
                                                          const uint32_t* __restrict__ pre,
-                                                         int32_t* __restrict__ codes) {
+                                                         int32_t* __restrict__ codes,
+                                                         const int32_t* __restrict__ desc,
+                                                         int64_t* __restrict__ starts) {
   extern __shared__ uint32_t lb[];
   const int nw = (int)((span + 31) >> 5);
   uint32_t* lp = lb + nw;
@@ -262,6 +306,7 @@ __global__ __launch_bounds__(256) void codes_bits_kernel(const int64_t* __restri
   }
   __syncthreads();
   const bool vec = ((uintptr_t)ids & 15) == 0, vst = ((uintptr_t)codes & 7) == 0;
+  const bool st = starts != nullptr && *desc == 0;  // the marking pass found the ids in order
   const int64_t stride = (int64_t)gridDim.x * blockDim.x, np = (n + 1) / 2;
   auto code = [&](int64_t v) -> int32_t {
     if (v < 0 || v >= span) return -1;  // out of range (a caller error)
@@ -276,11 +321,23 @@ __global__ __launch_bounds__(256) void codes_bits_kernel(const int64_t* __restri
     } else {
       v[2] = v[3] = -1;
     }
+    int32_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[u] = code(v[u]);
+    if (st) {  // as codes_from_rank_kernel
+      const int64_t q0 = wave_prev_pos(p0), q2 = wave_prev_pos(p0 + stride);
+      const int32_t e0 = q0 >= 0 && q0 < n ? code(ids[q0] - lo) : -1;
+      const int32_t e2 = q2 >= 0 && q2 < n ? code(ids[q2] - lo) : -1;
+      int32_t b0 = from_lane_below(c[1]), b2 = from_lane_below(c[3]);
+      if ((threadIdx.x & 63) == 0) b0 = e0, b2 = e2;
+      pair_starts(n, p0, c[0], c[1], b0, starts);
+      if (p0 + stride < np) pair_starts(n, p0 + stride, c[2], c[3], b2, starts);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int64_t p = p0 + h * stride;
       if (p >= np) break;
-      const int32_t c0 = code(v[2 * h]), c1 = code(v[2 * h + 1]);
+      const int32_t c0 = c[2 * h], c1 = c[2 * h + 1];
       if (vst && 2 * p + 1 < n) {
         *reinterpret_cast<int2*>(codes + 2 * p) = make_int2(c0, c1);
       } else {
@@ -297,6 +354,20 @@ __global__ __launch_bounds__(256) void uniq_bits_kernel(const uint32_t* __restri
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < span; v += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t wd = bits[v >> 5];
     if ((wd >> (v & 31)) & 1u) uniq[pre[v >> 5] + (uint32_t)__popc(wd & ((1u << (v & 31)) - 1u))] = v + lo;
+  }
+}
+
+// Row starts of the codes (the sorting paths of hrec_encode_ids_ex; skipped
+// unless the ids were found in order): as pair_starts, one position a thread.
+__global__ __launch_bounds__(256) void code_starts_kernel(const int32_t* __restrict__ codes, int64_t n,
+                                                          const int32_t* __restrict__ desc,
+                                                          int64_t* __restrict__ starts) {
+  if (*desc != 0) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = codes[i];
+    if (c < 0) continue;
+    if (i == 0 || codes[i - 1] != c) starts[c] = i;
+    if (i == n - 1) starts[c + 1] = n;
   }
 }
 
@@ -967,16 +1038,19 @@ extern "C" size_t hrec_encode_ids_workspace_bytes(int64_t n) {
 }
 
 extern "C" int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi, int64_t* uniq,
-                                  int64_t* n_uniq, int32_t* codes, int32_t* descending, void* ws, size_t ws_bytes,
-                                  void* stream) {
+                                  int64_t* n_uniq, int32_t* codes, int32_t* descending, int64_t* starts,
+                                  void* ws, size_t ws_bytes, void* stream) {
   HREC_REQUIRE(n >= 0 && n < 0x7fffffffll, "encode_ids: n=%lld out of range [0, 2^31-1)", (long long)n);
   HREC_REQUIRE(n_uniq, "encode_ids: null n_uniq");
   HREC_REQUIRE(id_lo <= id_hi, "encode_ids: id_lo > id_hi");
+  HREC_REQUIRE(!starts || descending, "encode_ids: starts needs the descending flag");
   hipStream_t s = as_stream(stream);
   if (descending && hipMemsetAsync(descending, 0, sizeof(int32_t), s) != hipSuccess)
     return check_launch("encode_ids: memset");
   if (n == 0) {
     if (hipMemsetAsync(n_uniq, 0, sizeof(int64_t), s) != hipSuccess) return check_launch("encode_ids: memset");
+    if (starts && hipMemsetAsync(starts, 0, sizeof(int64_t), s) != hipSuccess)
+      return check_launch("encode_ids: memset");
     return HREC_OK;
   }
   HREC_REQUIRE(ids && uniq && codes && ws, "encode_ids: null pointer");
@@ -1006,7 +1080,8 @@ extern "C" int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, 
     hipLaunchKernelGGL(bits_prefix_kernel, dim3(1), dim3(1024), 0, s, bits, nw, pre, n_uniq);
     const auto kfn = codes_bits_kernel;
     if (!allow_max_lds(kfn)) return check_launch("encode_ids: LDS attribute");
-    hipLaunchKernelGGL(kfn, dim3(gb), dim3(256), (size_t)nw * 8, s, ids, n, id_lo, span, bits, pre, codes);
+    hipLaunchKernelGGL(kfn, dim3(gb), dim3(256), (size_t)nw * 8, s, ids, n, id_lo, span, bits, pre, codes, descending,
+                       starts);
     hipLaunchKernelGGL(uniq_bits_kernel, dim3(grid_for(span)), dim3(256), 0, s, bits, pre, span, id_lo, uniq);
     return check_launch("encode_ids: dense bitmap");
   }
@@ -1017,7 +1092,8 @@ extern "C" int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, 
     hipLaunchKernelGGL(mark_present_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, flag, descending);
     const int rc = scan_run<int32_t>(flag, incl, span, false, temp, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(codes_from_rank_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, incl, codes);
+    hipLaunchKernelGGL(codes_from_rank_kernel, dim3(g), dim3(256), 0, s, ids, n, id_lo, span, incl, codes, descending,
+                       starts);
     hipLaunchKernelGGL(uniq_from_rank_kernel, dim3(grid_for(span)), dim3(256), 0, s, flag, incl, span, id_lo, uniq,
                        n_uniq);
     return check_launch("encode_ids: dense");
@@ -1073,12 +1149,13 @@ extern "C" int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, 
     hipLaunchKernelGGL(scatter_codes_kernel<int64_t>, dim3(g), dim3(256), 0, s, keys, (int64_t)0, pos2, flag, incl,
                        n, codes, uniq, n_uniq);
   }
+  if (starts) hipLaunchKernelGGL(code_starts_kernel, dim3(g), dim3(256), 0, s, codes, n, descending, starts);
   return check_launch("encode_ids");
 }
 
 extern "C" int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi, int64_t* uniq,
                                int64_t* n_uniq, int32_t* codes, void* ws, size_t ws_bytes, void* stream) {
-  return hrec_encode_ids_ex(ids, n, id_lo, id_hi, uniq, n_uniq, codes, nullptr, ws, ws_bytes, stream);
+  return hrec_encode_ids_ex(ids, n, id_lo, id_hi, uniq, n_uniq, codes, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 extern "C" size_t hrec_minmax_i64_workspace_bytes(int64_t n) { return n > 0 ? 256 : 0; }

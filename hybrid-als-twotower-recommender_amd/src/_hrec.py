@@ -31,7 +31,7 @@ _SIGNATURES = {
     "hrec_exclusive_scan_i64": (_c_i32, [_vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "hrec_encode_ids_workspace_bytes": (_c_sz, [_c_i64]),
     "hrec_encode_ids": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
-    "hrec_encode_ids_ex": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "hrec_encode_ids_ex": (_c_i32, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "hrec_minmax_i64_workspace_bytes": (_c_sz, [_c_i64]),
     "hrec_minmax_i64": (_c_i32, [_vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "hrec_coo_to_csr_workspace_bytes": (_c_sz, [_c_i64, _c_i64]),
@@ -258,40 +258,55 @@ def encode_ids(ids, id_range=None, order=False):
     """numpy.unique(ids, return_inverse=True) on the device: ids int64[n] ->
     (sorted distinct ids int64[m], codes int32[n]). id_range = (lo, hi) with
     lo <= ids <= hi if known; else it is measured on the device first.
-    order=True appends whether ids (hence codes) are non-decreasing — read by
-    the marking pass (hrec_encode_ids_ex), for coo_to_csr's rows_in_order."""
+    order=True appends whether ids (hence codes) are non-decreasing and, when
+    they are, the row pointer of rows = codes (int64[m + 1]; else None) — both
+    read by the marking / code passes (hrec_encode_ids_ex), for coo_to_csr's
+    rows_in_order / indptr."""
     n = ids.numel()
     dev = ids.device
     uniq = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     codes = torch.empty(n, dtype=torch.int32, device=dev)
     n_uniq = torch.zeros(1, dtype=torch.int64, device=dev)
     if n == 0:
-        return (uniq[:0], codes, True) if order else (uniq[:0], codes)
+        return (uniq[:0], codes, True, torch.zeros(1, dtype=torch.int64, device=dev)) if order else (uniq[:0], codes)
     lo, hi = minmax_i64(ids) if id_range is None else (int(id_range[0]), int(id_range[1]))
     ws = torch.empty(max(int(lib().hrec_encode_ids_workspace_bytes(n)), 16), dtype=torch.uint8, device=dev)
-    desc = torch.zeros(1, dtype=torch.int32, device=dev) if order else None
+    desc = starts = None
+    if order:
+        desc = torch.zeros(1, dtype=torch.int32, device=dev)
+        starts = torch.empty(min(n, hi - lo + 1) + 1, dtype=torch.int64, device=dev)
     _check("hrec_encode_ids_ex", lib().hrec_encode_ids_ex(
         _dev(ids, torch.int64, "ids"), n, lo, hi, _dev(uniq, torch.int64, "uniq"),
         _dev(n_uniq, torch.int64, "n_uniq"), _dev(codes, torch.int32, "codes"),
-        _dev(desc, torch.int32, "descending") if order else None, _dev(ws, torch.uint8, "ws"),
+        _dev(desc, torch.int32, "descending") if order else None,
+        _dev(starts, torch.int64, "starts") if order else None, _dev(ws, torch.uint8, "ws"),
         ws.numel(), _stream()))
     if order:
         m, d = torch.cat([n_uniq, desc.to(torch.int64)]).tolist()  # one host read
-        return uniq[:m], codes, d == 0
+        return uniq[:m], codes, d == 0, (starts[: m + 1] if d == 0 else None)
     return uniq[: int(n_uniq.item())], codes
 
 
-def coo_to_csr(rows, cols, vals, n_rows, alias=False, rows_in_order=None):
+def coo_to_csr(rows, cols, vals, n_rows, alias=False, rows_in_order=None, indptr=None):
     """(indptr int64[n_rows+1], indices int32[nnz], values f32[nnz]) of the COO
     (rows, cols, vals), rows ascending, a row's entries in input order.
     alias=True: when rows are already in order the returned indices / values
     ARE cols / vals (no copy) — for callers that do not modify either after.
     rows_in_order: whether rows is non-decreasing, when the caller knows it
-    (encode_ids(..., order=True)); None checks on the device."""
+    (encode_ids(..., order=True)); None checks on the device. indptr: the
+    row pointer encode_ids(..., order=True) returned for rows in order (with
+    alias=True nothing runs on the device)."""
     nnz = rows.numel()
     dev = rows.device
     if cols.numel() != nnz or vals.numel() != nnz:
         raise HrecError("coo_to_csr: rows, cols and vals must have the same length")
+    if indptr is not None and rows_in_order and alias:
+        if indptr.numel() > n_rows + 1:
+            raise HrecError("coo_to_csr: indptr has more than n_rows + 1 entries")
+        if indptr.numel() < n_rows + 1:  # rows past the last code: empty (they end at nnz)
+            indptr = torch.cat([indptr, torch.full((n_rows + 1 - indptr.numel(),), nnz, dtype=torch.int64,
+                                                   device=dev)])
+        return indptr, cols, vals
     indptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
     # rows already in order (e.g. ratings grouped by user): no sort needed
     if rows_in_order is None:

@@ -187,14 +187,15 @@ def _int_ids(col, name):
     return a
 
 
-def build_csr(rows, cols, vals, n_rows, n_cols, alias=False, rows_in_order=None):
+def build_csr(rows, cols, vals, n_rows, n_cols, alias=False, rows_in_order=None, indptr=None):
     """Device CSR of COO ratings (hrec_coo_to_csr): rows ascending, a row's
     entries in input order; duplicate (u, i) ratings stay separate terms, as
     in Spark. rows/cols int32, vals f32, all device tensors. alias: rows
     already in order hand back cols / vals themselves (no copy);
-    rows_in_order: the rows' order when known (else checked on the device)."""
+    rows_in_order / indptr: the rows' order and row pointer when known (from
+    encode_ids(..., order=True); else checked / built on the device)."""
     indptr, indices, values = _hrec.coo_to_csr(rows, cols, vals, int(n_rows), alias=alias,
-                                               rows_in_order=rows_in_order)
+                                               rows_in_order=rows_in_order, indptr=indptr)
     return DeviceCSR(indptr, indices, values, 0, int(n_rows), int(n_cols))
 
 
@@ -285,11 +286,12 @@ class ALSModel:
             ratings = torch.as_tensor(ratings_h).to(dev)
             # ingest on the device (§8(f) row 1): dense codes + CSR (users) / CSC (items)
             rng = (lambda a: (int(a.min()), int(a.max())) if a.size else None)
-            user_ids_t, urow, u_ord = _hrec.encode_ids(users, rng(users_h), order=True)
-            item_ids_t, irow, i_ord = _hrec.encode_ids(items, rng(items_h), order=True)
+            user_ids_t, urow, u_ord, u_ptr = _hrec.encode_ids(users, rng(users_h), order=True)
+            item_ids_t, irow, i_ord, _ = _hrec.encode_ids(items, rng(items_h), order=True)
             user_ids, item_ids = user_ids_t.cpu().numpy(), item_ids_t.cpu().numpy()
             n_u, n_i = len(user_ids), len(item_ids)
-            csr = build_csr(urow, irow, ratings, n_u, n_i, alias=True, rows_in_order=u_ord)  # grouped: no copy
+            # ratings grouped by user: the row pointer came with the codes, the CSR is the input (no pass)
+            csr = build_csr(urow, irow, ratings, n_u, n_i, alias=True, rows_in_order=u_ord, indptr=u_ptr)
             csc = build_csr(irow, urow, ratings, n_i, n_u, rows_in_order=i_ord)
             del urow, irow, ratings, users, items, user_ids_t, item_ids_t
         if track:

@@ -103,11 +103,14 @@ int hrec_encode_ids(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi,
 /* The same, plus *descending (device int32, may be null) = 1 if some
  * ids[i] > ids[i+1], else 0 — hrec_rows_descending_pairs of the codes
  * (the code map is monotone), read by the dense paths' marking pass instead
- * of a pass over the codes: ratings grouped by user go straight to
- * hrec_coo_to_csr_sorted. */
+ * of a pass over the codes — and, when descending is 0, starts[0..n_uniq]
+ * (may be null; room for min(n, id_hi - id_lo + 1) + 1 entries) = the CSR
+ * row pointer of rows = codes, written by the code pass: ratings grouped by
+ * user need neither hrec_rows_descending_pairs nor hrec_coo_to_csr_sorted
+ * (the CSR is (starts, item codes, ratings)). starts needs descending. */
 int hrec_encode_ids_ex(const int64_t* ids, int64_t n, int64_t id_lo, int64_t id_hi,
                        int64_t* uniq, int64_t* n_uniq, int32_t* codes,
-                       int32_t* descending, void* workspace,
+                       int32_t* descending, int64_t* starts, void* workspace,
                        size_t workspace_bytes, void* stream);
 
 /* hrec_coo_to_csr: (rows[nnz], cols[nnz], vals[nnz]) with 0 <= rows < n_rows

@@ -44,11 +44,11 @@ def main():
     vals = csr.values
     nnz = int(csr.nnz)
     print("nnz", nnz)
-    t, (_, urow, u_ord) = ev(lambda: _hrec.encode_ids(uid, (0, a.users - 1), order=True))
+    t, (_, urow, u_ord, u_ptr) = ev(lambda: _hrec.encode_ids(uid, (0, a.users - 1), order=True))
     print("encode users ms %.3f  (%.1f GB/s at 12 B/rating)" % (t, 12 * nnz / t / 1e6))
-    t, (iu, irow, i_ord) = ev(lambda: _hrec.encode_ids(iid, (0, a.items - 1), order=True))
+    t, (iu, irow, i_ord, _) = ev(lambda: _hrec.encode_ids(iid, (0, a.items - 1), order=True))
     print("encode items ms %.3f" % t)
-    t, _ = ev(lambda: _hrec.coo_to_csr(urow, irow, vals, a.users, alias=True, rows_in_order=u_ord))
+    t, _ = ev(lambda: _hrec.coo_to_csr(urow, irow, vals, a.users, alias=True, rows_in_order=u_ord, indptr=u_ptr))
     print("csr (sorted rows, the codes aliased) ms %.3f" % t)
     t, out = ev(lambda: _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()), rows_in_order=i_ord))
     print("csc (stable sort) ms %.3f  (%.1f GB/s at 20 B/rating)" % (t, 20 * nnz / t / 1e6))

@@ -27,12 +27,12 @@ ORDER = os.environ.get("ORDER", "1") == "1"  # 0: the order from a separate desc
 
 def run():
     if ORDER:
-        _, urow, u_ord = _hrec.encode_ids(uid, (0, n_users - 1), order=True)
-        iu, irow, i_ord = _hrec.encode_ids(iid, (0, n_items - 1), order=True)
+        _, urow, u_ord, u_ptr = _hrec.encode_ids(uid, (0, n_users - 1), order=True)
+        iu, irow, i_ord, _ = _hrec.encode_ids(iid, (0, n_items - 1), order=True)
     else:
-        (_, urow), (iu, irow), u_ord, i_ord = (_hrec.encode_ids(uid, (0, n_users - 1)),
-                                               _hrec.encode_ids(iid, (0, n_items - 1)), None, None)
-    a = _hrec.coo_to_csr(urow, irow, vals, n_users, alias=True, rows_in_order=u_ord)
+        (_, urow), (iu, irow), u_ord, i_ord, u_ptr = (_hrec.encode_ids(uid, (0, n_users - 1)),
+                                                      _hrec.encode_ids(iid, (0, n_items - 1)), None, None, None)
+    a = _hrec.coo_to_csr(urow, irow, vals, n_users, alias=True, rows_in_order=u_ord, indptr=u_ptr)
     b = _hrec.coo_to_csr(irow, urow, vals, int(iu.numel()), rows_in_order=i_ord)
     return a, b
 

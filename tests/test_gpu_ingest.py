@@ -64,7 +64,9 @@ def test_encode_ids_order_flag(device, n, lo, hi):
     """encode_ids(order=True): the ids' order read by the marking pass (dense
     bitmap, dense table) or a descent pass (sorting paths) equals numpy's
     all(ids[:-1] <= ids[1:]) — sorted ids, one descent at every lane / wave /
-    block boundary position of the pairs, unsorted — with the same codes."""
+    block boundary position of the pairs, unsorted — with the same codes; for
+    ids in order the row pointer written by the code pass equals the stable
+    argsort CSR's indptr, and coo_to_csr(indptr=...) hands it back."""
     h = _hrec()
     rng = np.random.default_rng(n + 1)
     base = np.sort(rng.integers(lo, hi, n, dtype=np.int64))
@@ -78,10 +80,21 @@ def test_encode_ids_order_flag(device, n, lo, hi):
         d_ids = torch.as_tensor(ids, device=device)
         exp_u, exp_c = np.unique(ids, return_inverse=True)
         for r in ((lo, hi), None):
-            uniq, codes, in_order = h.encode_ids(d_ids, r, order=True)
+            uniq, codes, in_order, starts = h.encode_ids(d_ids, r, order=True)
             assert in_order == bool(np.all(ids[:-1] <= ids[1:]))
             np.testing.assert_array_equal(uniq.cpu().numpy(), exp_u)
             np.testing.assert_array_equal(codes.cpu().numpy(), exp_c.astype(np.int32))
+            assert (starts is not None) == in_order
+            if in_order:
+                exp_ptr = np.concatenate([[0], np.cumsum(np.bincount(exp_c, minlength=len(exp_u)))])
+                np.testing.assert_array_equal(starts.cpu().numpy(), exp_ptr)
+                vals = torch.arange(n, dtype=torch.float32, device=device)
+                ip, ix, iv = h.coo_to_csr(codes, codes, vals, len(exp_u), alias=True, rows_in_order=True,
+                                          indptr=starts)
+                assert ip is starts and ix is codes and iv is vals
+                ip, _, _ = h.coo_to_csr(codes, codes, vals, len(exp_u) + 3, alias=True, rows_in_order=True,
+                                        indptr=starts)  # rows past the last code: empty
+                np.testing.assert_array_equal(ip.cpu().numpy(), np.concatenate([exp_ptr, [n, n, n]]))
 
 
 def test_encode_ids_empty(device):
