@@ -70,6 +70,9 @@ constexpr int kHxThreads1 = 256;
 constexpr int kHxThreads2 = 512;
 constexpr int kHxStatsLds = 8192;  // group records a phase-2 block keeps in LDS (128 KiB)
 
+#ifndef HREC_HX_SCAN_BATCH
+#define HREC_HX_SCAN_BATCH 64  // item columns whose loads a full-width DK-64 phase-2 scan issues at once
+#endif
 #ifndef HREC_HX_NSP_MAX
 #define HREC_HX_NSP_MAX 8  // seed pairs scanned beside the extremes' pairs (mode 2), at most
 #endif
@@ -434,17 +437,22 @@ struct HxWave {
     const float* pa = a.Vat + jj;
     const float* pt = a.Vtt + jj;
     const int n = ka > kt ? ka : kt;
+    // columns per batch of loads: all 64 at once for full-width DK 64 (one
+    // memory round trip per scan instead of two: c2 batch 0.1025 -> 0.0984 ms,
+    // 2b 26.1 -> 23.2 us); 32 elsewhere (64 spills in hx_pre's DK 128 / partial
+    // width kernels)
+    constexpr int NB = (FULL && DK == 64) ? HREC_HX_SCAN_BATCH : 32;
     float s = 0.f, t = 0.f;
-    for (int c0 = 0; c0 < n; c0 += 32) {
-      float va[32], vt[32];
+    for (int c0 = 0; c0 < n; c0 += NB) {
+      float va[NB], vt[NB];
 #pragma unroll
-      for (int q = 0; q < 32; ++q) {
+      for (int q = 0; q < NB; ++q) {
         va[q] = (FULL || c0 + q < ka) ? pa[(int64_t)(c0 + q) * a.lda] : 0.f;
         vt[q] = (FULL || c0 + q < kt) ? pt[(int64_t)(c0 + q) * a.ldtt] : 0.f;
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int q = 0; q < 32; q += 4) {
+      for (int q = 0; q < NB; q += 4) {
         const float4 u = *reinterpret_cast<const float4*>(sua + c0 + q);
         const float4 w = *reinterpret_cast<const float4*>(sut + c0 + q);
         float p = u.x * va[q];
